@@ -1,0 +1,82 @@
+# mdfx native build: gfx950 HIP kernels (hipcc), host runtime (g++), pybind11 module, CLIs, tests.
+#
+#   make -j8            -> mpi_cuda_process_amd/lib/libmdfx.so, mpi_cuda_process_amd/_mdfx*.so,
+#                          build/bin/{mdfx,mdf,life,mdfx_tests}
+#   make clean
+#
+# Everything is built in-tree so the shared objects travel with the repository snapshot to the GPU
+# box (no JIT cache, no site-packages install).
+
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX_HOST  ?= g++
+ARCH      ?= gfx950
+PYTHON    ?= python3
+
+PKG       := mpi_cuda_process_amd
+LIBDIR    := $(PKG)/lib
+OBJ       := build/obj
+BIN       := build/bin
+
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+PY_EXT    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-function
+HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
+HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -fopenmp
+
+KERNEL_SRC := $(wildcard csrc/kernels/*.hip)
+HOST_SRC   := $(wildcard csrc/core/*.cpp) $(wildcard csrc/cpu/*.cpp) $(wildcard csrc/comm/*.cpp) \
+              $(wildcard csrc/engine/*.cpp) $(wildcard csrc/io/*.cpp)
+KERNEL_OBJ := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(KERNEL_SRC))
+HOST_OBJ   := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(HOST_SRC))
+HEADERS    := $(wildcard csrc/include/mdfx/*.hpp) $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/app/*.hpp)
+
+LIB        := $(LIBDIR)/libmdfx.so
+PYMOD      := $(PKG)/_mdfx$(PY_EXT)
+APPS       := $(BIN)/mdfx $(BIN)/mdf $(BIN)/life
+TESTS      := $(BIN)/mdfx_tests
+
+LINK_ROCM  := -L$(ROCM)/lib -lamdhip64 -lrccl -lgomp -lpthread -ldl
+
+.PHONY: all lib pymod apps tests clean
+all: lib pymod
+
+lib: $(LIB)
+pymod: $(PYMOD)
+apps: $(APPS)
+tests: $(TESTS)
+
+$(OBJ)/%.o: csrc/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX_HOST) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(KERNEL_OBJ) $(HOST_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ $(LINK_ROCM) -Wl,-soname,libmdfx.so -Wl,-rpath,$(ROCM)/lib
+
+$(PYMOD): csrc/python/bindings.cpp $(LIB) $(HEADERS)
+	$(CXX_HOST) $(HOSTFLAGS) -fvisibility=hidden -I$(PY_INC) -I$(PYBIND_INC) -shared -o $@ $< \
+	  -L$(LIBDIR) -lmdfx -Wl,-rpath,'$$ORIGIN/lib'
+
+$(OBJ)/app/%.o: csrc/app/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX_HOST) $(HOSTFLAGS) -c $< -o $@
+
+$(BIN)/%: $(OBJ)/app/%_main.o $(OBJ)/app/cli_common.o $(LIB)
+	@mkdir -p $(BIN)
+	$(CXX_HOST) -o $@ $< $(OBJ)/app/cli_common.o -L$(LIBDIR) -lmdfx $(LINK_ROCM) \
+	  -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,$(ROCM)/lib
+
+$(TESTS): csrc/tests/test_main.cpp $(LIB) $(HEADERS)
+	@mkdir -p $(BIN)
+	$(CXX_HOST) $(HOSTFLAGS) -o $@ $< -L$(LIBDIR) -lmdfx $(LINK_ROCM) \
+	  -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,$(ROCM)/lib
+
+clean:
+	rm -rf build $(LIB) $(PYMOD)

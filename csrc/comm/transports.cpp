@@ -1,0 +1,158 @@
+// In-process halo transports (host memcpy, HIP loopback / peer copies) and the host-callback
+// transport used by the Python layer (torch.distributed: gloo on CPU, or NCCL=RCCL on GPU).
+//
+// Reference parity: MDF_kernel.cu:167-169,180-183 exchanged the cut row one float per MPI message
+// through pageable host memory after a full-grid D2H copy (D5, D12) and rank 1 addressed itself
+// (D3). Here a neighbour pair is derived from the slab index only (rank +- 1), a face is one
+// contiguous span, and copies stay on the device.
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <map>
+
+#include "mdfx/runtime.hpp"
+
+namespace mdfx {
+
+#define HIPC(x)                                                                          \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) ::mdfx::throw_error(__FILE__, __LINE__, std::string("HIP: ") + #x + " -> " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+class InProcessBase : public Transport {
+ public:
+  void setup(const std::vector<LocalSlab>& locals, int nranks) override {
+    locals_ = locals;
+    nranks_ = nranks;
+    by_rank_.clear();
+    for (size_t i = 0; i < locals_.size(); ++i) by_rank_[locals_[i].rank] = (int)i;
+    for (auto& s : locals_)
+      for (int side = 0; side < 2; ++side) {
+        const HaloSpan h = halo_span(s, 0, side, nranks_);
+        MDFX_CHECK(h.peer < 0 || by_rank_.count(h.peer),
+                   format("%s transport needs every rank in this process (rank %d has remote neighbour %d)",
+                          name(), s.rank, h.peer));
+      }
+  }
+  double allreduce_sum(double v) override { return v; }
+  double allreduce_max(double v) override { return v; }
+  void barrier() override {}
+
+ protected:
+  const LocalSlab& peer_slab(int rank) const { return locals_[by_rank_.at(rank)]; }
+  std::vector<LocalSlab> locals_;
+  std::map<int, int> by_rank_;
+  int nranks_ = 1;
+};
+
+class HostTransport final : public InProcessBase {
+ public:
+  const char* name() const override { return "host"; }
+  void exchange(int b) override {
+    for (auto& q : locals_)
+      for (int side = 0; side < 2; ++side) {
+        const HaloSpan hq = halo_span(q, b, side, nranks_);
+        if (hq.peer < 0) continue;
+        const HaloSpan hp = halo_span(peer_slab(hq.peer), b, 1 - side, nranks_);
+        std::memcpy(hq.recv, hp.send, hq.bytes);
+      }
+  }
+};
+
+class LoopbackTransport final : public InProcessBase {
+ public:
+  ~LoopbackTransport() override {
+    for (size_t i = 0; i < ev_.size(); ++i) locals_[i].be->destroy_event(ev_[i]);
+  }
+  const char* name() const override { return "loopback"; }
+  void setup(const std::vector<LocalSlab>& locals, int nranks) override {
+    InProcessBase::setup(locals, nranks);
+    for (auto& s : locals_) {
+      MDFX_CHECK(s.be->kind() == DeviceKind::HIP, "loopback transport needs HIP backends");
+      ev_.push_back(s.be->create_event());
+    }
+    // enable peer access between distinct devices that neighbour each other
+    for (auto& s : locals_)
+      for (int side = 0; side < 2; ++side) {
+        const HaloSpan h = halo_span(s, 0, side, nranks_);
+        if (h.peer < 0) continue;
+        const int pd = peer_slab(h.peer).be->device();
+        if (pd == s.be->device()) continue;
+        int can = 0;
+        HIPC(hipDeviceCanAccessPeer(&can, s.be->device(), pd));
+        if (can) {
+          s.be->activate();
+          const hipError_t e = hipDeviceEnablePeerAccess(pd, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            MDFX_FAIL(std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+          (void)hipGetLastError();
+        }
+      }
+  }
+  void exchange(int b) override {
+    // pull: each receiver waits for its neighbour's boundary kernel, then copies the face
+    for (size_t i = 0; i < locals_.size(); ++i) {
+      const LocalSlab& q = locals_[i];
+      for (int side = 0; side < 2; ++side) {
+        const HaloSpan hq = halo_span(q, b, side, nranks_);
+        if (hq.peer < 0) continue;
+        const LocalSlab& p = peer_slab(hq.peer);
+        const HaloSpan hp = halo_span(p, b, 1 - side, nranks_);
+        q.be->wait(q.halo_stream, p.bnd_event);
+        q.be->activate();
+        if (p.be->device() == q.be->device())
+          HIPC(hipMemcpyAsync(hq.recv, hp.send, hq.bytes, hipMemcpyDeviceToDevice, (hipStream_t)q.halo_stream));
+        else
+          HIPC(hipMemcpyPeerAsync(hq.recv, q.be->device(), hp.send, p.be->device(), hq.bytes,
+                                  (hipStream_t)q.halo_stream));
+      }
+      q.be->record(ev_[i], q.halo_stream);
+    }
+    // a sender may not overwrite its faces until its neighbours have pulled them
+    for (size_t i = 0; i < locals_.size(); ++i) {
+      const LocalSlab& p = locals_[i];
+      for (int side = 0; side < 2; ++side) {
+        const HaloSpan hp = halo_span(p, b, side, nranks_);
+        if (hp.peer < 0) continue;
+        p.be->wait(p.halo_stream, ev_[by_rank_.at(hp.peer)]);
+      }
+    }
+  }
+
+ private:
+  std::vector<void*> ev_;
+};
+
+class CallbackTransport final : public Transport {
+ public:
+  explicit CallbackTransport(CallbackFns f) : f_(std::move(f)) {}
+  const char* name() const override { return "callback"; }
+  void setup(const std::vector<LocalSlab>&, int) override {}
+  void exchange(int b) override {
+    if (f_.exchange) f_.exchange(b);
+  }
+  double allreduce_sum(double v) override { return f_.allreduce_sum ? f_.allreduce_sum(v) : v; }
+  double allreduce_max(double v) override { return f_.allreduce_max ? f_.allreduce_max(v) : v; }
+  void barrier() override {
+    if (f_.barrier) f_.barrier();
+  }
+  bool in_process_only() const override { return false; }
+
+ private:
+  CallbackFns f_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_host_transport() { return std::unique_ptr<Transport>(new HostTransport()); }
+std::unique_ptr<Transport> make_loopback_transport() {
+  return std::unique_ptr<Transport>(new LoopbackTransport());
+}
+std::unique_ptr<Transport> make_callback_transport(CallbackFns fns) {
+  return std::unique_ptr<Transport>(new CallbackTransport(std::move(fns)));
+}
+
+}  // namespace mdfx

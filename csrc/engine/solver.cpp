@@ -1,0 +1,474 @@
+// mdfx engine implementation (see solver.hpp for the schedule).
+#include "mdfx/solver.hpp"
+
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <sys/stat.h>
+#include <thread>
+
+namespace mdfx {
+
+#define HIPC(x)                                                                          \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) ::mdfx::throw_error(__FILE__, __LINE__, std::string("HIP: ") + #x + " -> " + hipGetErrorString(e_)); \
+  } while (0)
+
+Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<int> local_ranks,
+               std::vector<std::unique_ptr<Backend>> backends, std::unique_ptr<Transport> transport,
+               SolverOptions opt)
+    : spec_(spec), global_(global), nranks_(nranks), decomp_(global.nz, nranks),
+      transport_(std::move(transport)), opt_(opt) {
+  MDFX_CHECK(!local_ranks.empty(), "a process must own at least one slab");
+  MDFX_CHECK(local_ranks.size() == backends.size(), "one backend per local slab");
+  MDFX_CHECK(transport_ != nullptr, "transport required");
+  if (stencil_is_2d(spec_.kind))
+    MDFX_CHECK(global_.ny == 1, "2D stencils store an h x w grid as nx=w, ny=1, nz=h");
+  else
+    MDFX_CHECK(global_.ny >= 1, "bad ny");
+  if (spec_.kind == StencilKind::Life) MDFX_CHECK(spec_.dtype == DType::U8, "life cells are u8");
+  if (spec_.kind != StencilKind::Life)
+    MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
+  const int halo = 1;
+  for (size_t i = 0; i < local_ranks.size(); ++i) {
+    const int r = local_ranks[i];
+    MDFX_CHECK(r >= 0 && r < nranks, format("local rank %d outside [0,%d)", r, nranks));
+    Slab s;
+    s.rank = r;
+    s.be = std::move(backends[i]);
+    s.lay = FieldLayout::make(global_, decomp_.z0(r), decomp_.z1(r), halo, spec_.dtype);
+    MDFX_CHECK(s.lay.nzl() >= 1, "every slab needs at least one plane");
+    const size_t bytes = s.lay.bytes();
+    s.buf[0] = s.be->alloc(bytes);
+    s.buf[1] = s.be->alloc(bytes);
+    s.be->memset(s.buf[0], 0, bytes, nullptr);
+    s.be->memset(s.buf[1], 0, bytes, nullptr);
+    s.hs = s.be->create_stream(1);
+    s.cs = s.be->create_stream(0);
+    s.ev_bnd = s.be->create_event();
+    s.ev_int = s.be->create_event();
+    s.resid = (double*)s.be->alloc(2 * sizeof(double));
+    // regions (storage planes); owned = [halo, halo + nzl)
+    const int64_t ob = halo, oe = halo + s.lay.nzl();
+    const bool has_lo = r > 0, has_hi = r + 1 < nranks;
+    s.lo_b = ob;
+    s.lo_e = has_lo ? ob + 1 : ob;
+    s.hi_e = oe;
+    s.hi_b = has_hi ? std::max(oe - 1, s.lo_e) : oe;
+    s.in_b = s.lo_e;
+    s.in_e = s.hi_b;
+    slabs_.push_back(std::move(s));
+  }
+  for (auto& s : slabs_) s.be->sync_device();
+  std::vector<LocalSlab> ls;
+  for (auto& s : slabs_) {
+    LocalSlab l;
+    l.rank = s.rank;
+    l.be = s.be.get();
+    l.halo_stream = s.hs;
+    l.bnd_event = s.ev_bnd;
+    l.lay = s.lay;
+    l.buf[0] = s.buf[0];
+    l.buf[1] = s.buf[1];
+    ls.push_back(l);
+  }
+  transport_->setup(ls, nranks_);
+}
+
+Solver::~Solver() {
+  try {
+    sync_all();
+  } catch (...) {
+  }
+  destroy_graph();
+  transport_.reset();  // communicators before the memory they reference
+  for (auto& s : slabs_) {
+    s.be->release(s.buf[0]);
+    s.be->release(s.buf[1]);
+    s.be->release(s.resid);
+    s.be->destroy_event(s.ev_bnd);
+    s.be->destroy_event(s.ev_int);
+    s.be->destroy_stream(s.hs);
+    s.be->destroy_stream(s.cs);
+  }
+}
+
+void Solver::set_options(const SolverOptions& o) {
+  if (o.graph != opt_.graph || o.overlap != opt_.overlap) destroy_graph();
+  opt_ = o;
+}
+
+void Solver::init(const InitSpec& is) {
+  destroy_graph();
+  for (auto& s : slabs_) {
+    s.be->init(is, s.lay, s.buf[0], s.hs);
+    s.be->init(is, s.lay, s.buf[1], s.hs);
+  }
+  sync_all();
+  cur_ = 0;
+  stats_ = StepStats();
+  ghosts_dirty_ = false;  // ghosts are generated from the global index too
+}
+
+void Solver::sync_all() {
+  for (auto& s : slabs_) {
+    s.be->activate();
+    s.be->sync_stream(s.hs);
+    s.be->sync_stream(s.cs);
+  }
+}
+
+void Solver::synchronize() {
+  if (opt_.timeout_s <= 0 || slabs_[0].be->kind() != DeviceKind::HIP) {
+    sync_all();
+    transport_->check();
+    return;
+  }
+  // watchdog: poll the streams and RCCL's async error state instead of blocking forever (the
+  // reference hangs in MPI_Send).
+  const auto t0 = std::chrono::steady_clock::now();
+  for (auto& s : slabs_) {
+    s.be->activate();
+    for (void* st : {s.hs, s.cs}) {
+      for (;;) {
+        const hipError_t q = hipStreamQuery((hipStream_t)st);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIPC(q);
+        transport_->check();
+        const double el =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > opt_.timeout_s)
+          MDFX_FAIL(format("watchdog: step stream of rank %d not done after %.1f s", s.rank, el));
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
+    }
+  }
+}
+
+void Solver::exchange_ghosts() {
+  destroy_graph();
+  // make the current buffer's owned planes visible to the exchange (ordered on the halo stream)
+  for (auto& s : slabs_) {
+    s.be->wait(s.hs, s.ev_int);
+    s.be->record(s.ev_bnd, s.hs);
+  }
+  transport_->exchange(cur_);
+  sync_all();
+  ghosts_dirty_ = false;
+}
+
+void Solver::step(bool want_resid) {
+  const int nb = 1 - cur_;
+  for (auto& s : slabs_) {
+    s.be->activate();
+    s.be->trace_push("mdfx.step");
+    RegionArgs a;
+    a.in = s.buf[cur_];
+    a.out = s.buf[nb];
+    a.lay = s.lay;
+    if (want_resid) {
+      s.be->memset(s.resid, 0, sizeof(double), s.hs);
+      s.be->memset(s.resid + 1, 0, sizeof(double), opt_.overlap ? s.cs : s.hs);
+    }
+    // halo stream: boundary planes of this step, after the previous interior sweep
+    s.be->wait(s.hs, s.ev_int);
+    a.resid = want_resid ? s.resid : nullptr;
+    if (s.lo_e > s.lo_b) {
+      a.lz_begin = s.lo_b;
+      a.lz_end = s.lo_e;
+      s.be->stencil(spec_, a, s.hs);
+    }
+    if (s.hi_e > s.hi_b) {
+      a.lz_begin = s.hi_b;
+      a.lz_end = s.hi_e;
+      s.be->stencil(spec_, a, s.hs);
+    }
+    if (opt_.sync_debug) s.be->sync_device();
+    // compute stream: interior, after the previous step's boundary kernels
+    void* is = opt_.overlap ? s.cs : s.hs;
+    if (opt_.overlap) s.be->wait(s.cs, s.ev_bnd);
+    if (s.in_e > s.in_b) {
+      a.lz_begin = s.in_b;
+      a.lz_end = s.in_e;
+      a.resid = want_resid ? s.resid + 1 : nullptr;
+      s.be->stencil(spec_, a, is);
+    }
+    s.be->record(s.ev_bnd, s.hs);
+    s.be->record(s.ev_int, is);
+    if (opt_.sync_debug) s.be->sync_device();
+    s.be->trace_pop();
+  }
+  if (!slabs_.empty()) slabs_[0].be->trace_push("mdfx.exchange");
+  transport_->exchange(nb);
+  if (!slabs_.empty()) slabs_[0].be->trace_pop();
+  if (opt_.sync_debug) sync_all();
+  cur_ = nb;
+  ++stats_.steps;
+  if (want_resid) finish_residual();
+}
+
+void Solver::finish_residual() {
+  sync_all();
+  double local = 0.0;
+  for (auto& s : slabs_) {
+    double h[2] = {0, 0};
+    s.be->copy(h, s.resid, 2 * sizeof(double), CopyKind::D2H, s.hs);
+    s.be->sync_stream(s.hs);
+    local += h[0] + h[1];
+  }
+  const double g = transport_->allreduce_sum(local);
+  stats_.last_residual = std::sqrt(g);
+  stats_.residual_step = stats_.steps;
+  if (!std::isfinite(stats_.last_residual))
+    MDFX_FAIL(format("non-finite residual at step %lld: the solution diverged (unstable coefficient?)",
+                     (long long)stats_.steps));
+}
+
+void Solver::run(int64_t steps) {
+  MDFX_CHECK(steps >= 0, "negative step count");
+  if (ghosts_dirty_) exchange_ghosts();
+  transport_->check();
+  const bool hip = slabs_[0].be->kind() == DeviceKind::HIP;
+  int64_t done = 0;
+  while (done < steps) {
+    const int64_t k = stats_.steps + 1;
+    const bool res = opt_.residual_every > 0 && (k % opt_.residual_every == 0);
+    // graph replay for plain (non-residual, non-debug) stretches of >= 2 steps
+    if (opt_.graph && hip && !res && !opt_.sync_debug) {
+      int64_t plain = steps - done;
+      if (opt_.residual_every > 0) {
+        const int64_t next_res = ((stats_.steps / opt_.residual_every) + 1) * opt_.residual_every;
+        plain = std::min<int64_t>(plain, next_res - stats_.steps - 1);
+      }
+      const int64_t pairs = plain / 2;
+      if (pairs > 0) {
+        run_graph(pairs);
+        done += 2 * pairs;
+        continue;
+      }
+    }
+    step(res);
+    ++done;
+  }
+}
+
+// ---- hipGraph replay of a 2-step cycle --------------------------------------------------------
+// Captured from the halo stream of slab 0; every other stream joins the capture through event
+// waits (fork) and is joined back at the end, so the replay carries exactly the eager schedule's
+// dependencies. The captured cycle starts at buffer `graph_parity_`.
+void Solver::destroy_graph() {
+  if (graph_exec_) {
+    (void)hipGraphExecDestroy((hipGraphExec_t)graph_exec_);
+    graph_exec_ = nullptr;
+  }
+  graph_parity_ = -1;
+}
+
+void Solver::run_graph(int64_t pairs) {
+  if (!graph_exec_ || graph_parity_ != cur_) {
+    destroy_graph();
+    Slab& o = slabs_[0];
+    o.be->activate();
+    hipStream_t origin = (hipStream_t)o.hs;
+    std::vector<hipEvent_t> fork(slabs_.size() * 2), join(slabs_.size() * 2);
+    for (auto& e : fork) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : join) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPC(hipStreamBeginCapture(origin, hipStreamCaptureModeRelaxed));
+    HIPC(hipEventRecord(fork[0], origin));
+    size_t k = 0;
+    for (auto& s : slabs_) {
+      s.be->activate();
+      for (void* st : {s.hs, s.cs}) {
+        if (st != (void*)origin) HIPC(hipStreamWaitEvent((hipStream_t)st, fork[0], 0));
+        ++k;
+      }
+    }
+    // every event the captured steps wait on must itself be recorded inside the capture
+    for (auto& s : slabs_) {
+      s.be->activate();
+      s.be->record(s.ev_bnd, s.hs);
+      s.be->record(s.ev_int, s.cs);
+    }
+    const int64_t saved = stats_.steps;
+    step(false);
+    step(false);
+    stats_.steps = saved;  // replay accounts for them
+    k = 0;
+    for (auto& s : slabs_) {
+      s.be->activate();
+      for (void* st : {s.hs, s.cs}) {
+        if (st != (void*)origin) {
+          HIPC(hipEventRecord(join[k], (hipStream_t)st));
+          o.be->activate();
+          HIPC(hipStreamWaitEvent(origin, join[k], 0));
+          s.be->activate();
+        }
+        ++k;
+      }
+    }
+    o.be->activate();
+    hipGraph_t g;
+    HIPC(hipStreamEndCapture(origin, &g));
+    hipGraphExec_t ex;
+    HIPC(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    HIPC(hipGraphDestroy(g));
+    for (auto& e : fork) (void)hipEventDestroy(e);
+    for (auto& e : join) (void)hipEventDestroy(e);
+    graph_exec_ = ex;
+    graph_parity_ = cur_;  // step() x2 leaves cur_ unchanged
+  }
+  Slab& o = slabs_[0];
+  o.be->activate();
+  for (int64_t i = 0; i < pairs; ++i) HIPC(hipGraphLaunch((hipGraphExec_t)graph_exec_, (hipStream_t)o.hs));
+  // later eager work on the other streams must follow the replay
+  HIPC(hipEventRecord((hipEvent_t)o.ev_bnd, (hipStream_t)o.hs));
+  for (auto& s : slabs_) {
+    s.be->activate();
+    if (s.cs != o.hs) HIPC(hipStreamWaitEvent((hipStream_t)s.cs, (hipEvent_t)o.ev_bnd, 0));
+    if (s.hs != o.hs) HIPC(hipStreamWaitEvent((hipStream_t)s.hs, (hipEvent_t)o.ev_bnd, 0));
+  }
+  // re-establish per-slab events for the next eager step
+  for (auto& s : slabs_) {
+    s.be->activate();
+    s.be->record(s.ev_bnd, s.hs);
+    s.be->record(s.ev_int, s.cs);
+  }
+  stats_.steps += 2 * pairs;
+}
+
+// ---- host I/O ----------------------------------------------------------------------------------
+
+void Solver::read_owned(int i, void* host) {
+  Slab& s = slabs_[i];
+  sync_all();
+  const FieldLayout& l = s.lay;
+  const size_t es = l.esize();
+  std::vector<char> stage((size_t)l.nzl() * l.plane_bytes());
+  s.be->copy(stage.data(), (char*)s.buf[cur_] + (size_t)l.halo * l.plane_bytes(), stage.size(),
+             CopyKind::D2H, s.hs);
+  s.be->sync_stream(s.hs);
+  char* dst = (char*)host;
+  for (int64_t z = 0; z < l.nzl(); ++z)
+    for (int64_t y = 0; y < l.global.ny; ++y) {
+      std::memcpy(dst, stage.data() + ((size_t)z * l.plane + (size_t)y * l.pitch) * es,
+                  (size_t)l.global.nx * es);
+      dst += (size_t)l.global.nx * es;
+    }
+}
+
+void Solver::write_owned(int i, const void* host) {
+  destroy_graph();
+  Slab& s = slabs_[i];
+  sync_all();
+  const FieldLayout& l = s.lay;
+  const size_t es = l.esize();
+  std::vector<char> stage((size_t)l.nzl() * l.plane_bytes(), 0);
+  const char* src = (const char*)host;
+  for (int64_t z = 0; z < l.nzl(); ++z)
+    for (int64_t y = 0; y < l.global.ny; ++y) {
+      std::memcpy(stage.data() + ((size_t)z * l.plane + (size_t)y * l.pitch) * es, src,
+                  (size_t)l.global.nx * es);
+      src += (size_t)l.global.nx * es;
+    }
+  s.be->copy((char*)s.buf[cur_] + (size_t)l.halo * l.plane_bytes(), stage.data(), stage.size(),
+             CopyKind::H2D, s.hs);
+  s.be->sync_stream(s.hs);
+  ghosts_dirty_ = true;
+}
+
+static void mkdir_p(const std::string& d) {
+  std::string cur;
+  for (size_t i = 0; i < d.size(); ++i) {
+    cur.push_back(d[i]);
+    if (d[i] == '/' || i + 1 == d.size()) ::mkdir(cur.c_str(), 0755);
+  }
+}
+
+void Solver::save_checkpoint(const std::string& dir) {
+  mkdir_p(dir);
+  for (int i = 0; i < num_local(); ++i) {
+    const FieldLayout& l = slabs_[i].lay;
+    std::vector<char> data((size_t)l.owned_cells() * l.esize());
+    read_owned(i, data.data());
+    const std::string base = dir + "/slab_" + std::to_string(slabs_[i].rank);
+    {
+      std::ofstream f(base + ".bin", std::ios::binary);
+      MDFX_CHECK(f.good(), "cannot write " + base + ".bin");
+      f.write(data.data(), (std::streamsize)data.size());
+    }
+    std::ofstream j(base + ".json");
+    j << "{\"format\": \"mdfx-slab-v1\", \"stencil\": \"" << stencil_name(spec_.kind) << "\", \"dtype\": \""
+      << dtype_name(spec_.dtype) << "\", \"nx\": " << global_.nx << ", \"ny\": " << global_.ny
+      << ", \"nz\": " << global_.nz << ", \"z0\": " << l.z0 << ", \"z1\": " << l.z1
+      << ", \"rank\": " << slabs_[i].rank << ", \"nranks\": " << nranks_
+      << ", \"step\": " << stats_.steps << "}\n";
+  }
+}
+
+static bool json_int(const std::string& s, const std::string& key, long long& out) {
+  const std::string k = "\"" + key + "\":";
+  size_t p = s.find(k);
+  if (p == std::string::npos) return false;
+  p += k.size();
+  out = std::atoll(s.c_str() + p);
+  return true;
+}
+
+void Solver::load_checkpoint(const std::string& dir) {
+  // discover slabs written by any decomposition: slab_<r>.json for r = 0.. until missing
+  struct F {
+    long long z0, z1, step;
+    std::string bin;
+  };
+  std::vector<F> files;
+  for (int r = 0;; ++r) {
+    const std::string base = dir + "/slab_" + std::to_string(r);
+    std::ifstream j(base + ".json");
+    if (!j.good()) break;
+    std::stringstream ss;
+    ss << j.rdbuf();
+    const std::string js = ss.str();
+    F f;
+    long long nx = 0, ny = 0, nz = 0;
+    MDFX_CHECK(json_int(js, "z0", f.z0) && json_int(js, "z1", f.z1) && json_int(js, "step", f.step) &&
+                   json_int(js, "nx", nx) && json_int(js, "ny", ny) && json_int(js, "nz", nz),
+               "malformed checkpoint header " + base + ".json");
+    MDFX_CHECK(nx == global_.nx && ny == global_.ny && nz == global_.nz,
+               "checkpoint grid does not match the solver grid");
+    MDFX_CHECK(js.find(std::string("\"dtype\": \"") + dtype_name(spec_.dtype) + "\"") != std::string::npos,
+               "checkpoint dtype does not match");
+    f.bin = base + ".bin";
+    files.push_back(f);
+  }
+  MDFX_CHECK(!files.empty(), "no checkpoint slabs in " + dir);
+  for (int i = 0; i < num_local(); ++i) {
+    const FieldLayout& l = slabs_[i].lay;
+    const size_t pb = (size_t)global_.nx * global_.ny * l.esize();  // dense plane bytes
+    std::vector<char> data((size_t)l.nzl() * pb);
+    for (int64_t z = l.z0; z < l.z1; ++z) {
+      bool found = false;
+      for (auto& f : files)
+        if (z >= f.z0 && z < f.z1) {
+          std::ifstream in(f.bin, std::ios::binary);
+          in.seekg((std::streamoff)((z - f.z0) * pb));
+          in.read(data.data() + (size_t)(z - l.z0) * pb, (std::streamsize)pb);
+          MDFX_CHECK(in.good(), "short read in " + f.bin);
+          found = true;
+          break;
+        }
+      MDFX_CHECK(found, format("checkpoint is missing plane %lld", (long long)z));
+    }
+    write_owned(i, data.data());
+    stats_.steps = files[0].step;
+  }
+  // owned planes of buffer 1 are stale but are fully rewritten by the next step
+  exchange_ghosts();
+}
+
+}  // namespace mdfx

@@ -1,0 +1,80 @@
+// mdfx — stencil / init / reduction kernels: one interface, two implementations
+// (hand-written gfx950 HIP in csrc/kernels/*.hip, and the CPU oracle in csrc/cpu/cpu_kernels.cpp).
+//
+// Reference parity:
+//   run_mdf      MDF_kernel.cu:10-22   -> StencilKind::Jacobi5
+//   game_of_life kernel.cu:10-68       -> StencilKind::Life
+//   middle_kernel / border_kernel (MDF_kernel.cu:24-70, kernel.cu:70-113) -> a *region* launch:
+//   one kernel computes a plane range [lz_begin, lz_end) of the slab. Unlike the reference, a
+//   region launch writes only its own planes (fixes the cross-stream write race D6) and every
+//   boundary cell is handled explicitly (fixes the unsigned-wrap OOB reads D8 and the floored
+//   grid D10).
+//   create_universe MDF_kernel.cu:88-99 / kernel.cu:131-146 -> InitSpec.
+#pragma once
+
+#include "mdfx/grid.hpp"
+
+namespace mdfx {
+
+// One region update: out[planes lz_begin..lz_end) = stencil(in). Cells on the global boundary
+// (x, y or z equal to 0 or n-1) are Dirichlet: copied through unchanged.
+struct RegionArgs {
+  const void* in = nullptr;
+  void* out = nullptr;
+  FieldLayout lay;
+  int64_t lz_begin = 0, lz_end = 0;  // storage planes to write
+  double* resid = nullptr;           // optional accumulator of sum((out-in)^2) over the region
+};
+
+enum class InitKind : int {
+  Constant = 0,   // every cell = value
+  Dirichlet = 1,  // global-boundary cells = edge, interior = interior (MDF_kernel.cu:88-99)
+  Random = 2,     // uniform [lo, hi) from a counter-based hash of (seed, global index)
+  LifeRandom = 3, // U8: alive with probability `density` off the frame, frame dead (kernel.cu:131-146)
+};
+
+struct InitSpec {
+  InitKind kind = InitKind::Random;
+  uint64_t seed = 1;
+  double lo = 0.0, hi = 1.0;
+  double value = 0.0;
+  double edge = 100.0, interior = 0.0;
+  double density = 0.15;
+};
+
+// Counter-based generator shared by host and device: value depends only on (seed, global linear
+// index gx + nx*(gy + ny*gz)), so any decomposition produces the same grid.
+#if defined(__HIPCC__)
+#define MDFX_HD __host__ __device__
+#else
+#define MDFX_HD
+#endif
+MDFX_HD inline uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+MDFX_HD inline double hash_unit(uint64_t seed, uint64_t gidx) {
+  const uint64_t h = mix64(gidx * 0x9E3779B97F4A7C15ull + mix64(seed + 0x632BE59BD9B4E019ull));
+  return (double)(h >> 11) * (1.0 / 9007199254740992.0);  // [0,1) with 53 bits
+}
+
+// ---- HIP (gfx950) -------------------------------------------------------------------------
+// `stream` is a hipStream_t. All launches are asynchronous.
+void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream);
+void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* stream);
+// Variant selection for kernel A/B benchmarking and tests: "auto", "naive", "tuned".
+void hip_set_kernel_variant(const char* name);
+const char* hip_kernel_variant();
+
+// ---- CPU oracle / CPU backend ----------------------------------------------------------------
+void cpu_stencil(const StencilSpec& spec, const RegionArgs& a);
+void cpu_init(const InitSpec& init, const FieldLayout& lay, void* buf);
+// Reproduce the reference's intended GoL initial grid with glibc rand() seeded by `seed` (the
+// reference never seeds: seed 1). Fills a dense h*w int8 host array in global row-major order.
+void cpu_life_compat_init(uint8_t* grid, int64_t h, int64_t w, double density, unsigned seed);
+
+}  // namespace mdfx

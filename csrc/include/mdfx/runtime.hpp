@@ -1,0 +1,104 @@
+// mdfx runtime: device backends (HIP / CPU) and halo transports.
+//
+// Reference parity:
+//   CUDA runtime calls (MDF_kernel.cu:114-121,141-144,161,171,175,177,226-231; layer L0) ->
+//   Backend, with RAII ownership and every call checked (D18).
+//   MPI p2p halo loops (MDF_kernel.cu:167-169,180-183, one 4-byte message per cell, D5) ->
+//   Transport::exchange: one whole-plane message per neighbour per step, device-resident, on a
+//   dedicated halo stream.
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "mdfx/kernels.hpp"
+
+namespace mdfx {
+
+enum class CopyKind : int { H2D = 0, D2H = 1, D2D = 2, H2H = 3 };
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual DeviceKind kind() const = 0;
+  virtual int device() const = 0;  // HIP ordinal; -1 for CPU
+  virtual void activate() const {}
+  virtual void* alloc(size_t bytes) = 0;
+  virtual void release(void* p) = 0;
+  virtual void* create_stream(int priority) = 0;  // priority: 0 normal, 1 high
+  virtual void destroy_stream(void* s) = 0;
+  virtual void* create_event() = 0;
+  virtual void destroy_event(void* e) = 0;
+  virtual void record(void* ev, void* stream) = 0;
+  virtual void wait(void* stream, void* ev) = 0;
+  virtual void sync_stream(void* stream) = 0;
+  virtual void sync_device() = 0;
+  virtual void memset(void* p, int v, size_t n, void* stream) = 0;
+  virtual void copy(void* dst, const void* src, size_t n, CopyKind k, void* stream) = 0;
+  virtual void stencil(const StencilSpec& s, const RegionArgs& a, void* stream) = 0;
+  virtual void init(const InitSpec& s, const FieldLayout& l, void* buf, void* stream) = 0;
+  virtual void trace_push(const char*) {}
+  virtual void trace_pop() {}
+};
+
+std::unique_ptr<Backend> make_cpu_backend();
+std::unique_ptr<Backend> make_hip_backend(int device);
+int hip_device_count();
+
+// What a transport needs to know about one subdomain owned by this process.
+struct LocalSlab {
+  int rank = 0;               // global subdomain index (0..nranks-1)
+  Backend* be = nullptr;
+  void* halo_stream = nullptr;
+  void* bnd_event = nullptr;  // recorded right after this step's boundary kernel(s)
+  FieldLayout lay;
+  void* buf[2] = {nullptr, nullptr};
+};
+
+// Byte ranges of one side of a halo exchange for buffer b.
+struct HaloSpan {
+  int peer = -1;            // neighbouring subdomain, -1 if none (global boundary)
+  void* send = nullptr;     // first/last `halo` owned planes
+  void* recv = nullptr;     // ghost planes
+  size_t bytes = 0;
+};
+HaloSpan halo_span(const LocalSlab& s, int b, int side /*0 = lo, 1 = hi*/, int nranks);
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual const char* name() const = 0;
+  virtual void setup(const std::vector<LocalSlab>& locals, int nranks) = 0;
+  // Enqueue the exchange of buffer b (just written by the boundary kernels) on every local
+  // slab's halo stream. On return, work later enqueued on a halo stream sees the ghosts, and
+  // the sent planes may be overwritten by later work on the sender's halo stream.
+  virtual void exchange(int b) = 0;
+  // Blocking host-side reductions across all processes.
+  virtual double allreduce_sum(double v) = 0;
+  virtual double allreduce_max(double v) = 0;
+  virtual void barrier() = 0;
+  virtual bool in_process_only() const { return true; }  // every rank lives in this process
+  // Optional async-error poll (RCCL); throws if a peer failed.
+  virtual void check() {}
+};
+
+// CPU, all subdomains in this process: memcpy.
+std::unique_ptr<Transport> make_host_transport();
+// HIP, all subdomains in this process (one or several devices): D2D / peer copies with
+// event ordering. Used for multi-rank testing on one GPU (RCCL refuses two ranks on one GPU).
+std::unique_ptr<Transport> make_loopback_transport();
+// RCCL send/recv over xGMI. `unique_id` is the 128-byte ncclUniqueId shared by all processes.
+std::unique_ptr<Transport> make_rccl_transport(const std::string& unique_id);
+std::string rccl_unique_id();
+// Host callbacks (the Python layer plugs torch.distributed in here, e.g. gloo on CPU).
+struct CallbackFns {
+  std::function<void(int)> exchange;
+  std::function<double(double)> allreduce_sum;
+  std::function<double(double)> allreduce_max;
+  std::function<void()> barrier;
+};
+std::unique_ptr<Transport> make_callback_transport(CallbackFns fns);
+
+}  // namespace mdfx

@@ -1,0 +1,115 @@
+// mdfx engine: the overlapped, double-buffered time-step scheduler.
+//
+// Reference parity: the per-rank generation loops of MDF_kernel.cu:155-222 / kernel.cu:202-269
+// (C12/C13). The reference launched middle_kernel and border_kernel on two streams but then
+// serialised everything with cudaDeviceSynchronize (MDF_kernel.cu:175), raced the two streams on
+// d_new_univ (D6) and d_univ (D7), and never swapped buffers (D1). Here, per step and per slab:
+//
+//   halo stream (high priority):  wait(interior t-1) -> boundary planes (cur -> nxt)
+//                                 -> record(bnd) -> exchange faces of nxt (RCCL / loopback)
+//   compute stream:               wait(boundary t-1) -> interior planes (cur -> nxt)
+//                                 -> record(int)
+//   swap(cur, nxt)
+//
+// so the interior sweep of step t overlaps the boundary kernel and the halo exchange of step t
+// (and the exchange may run on into step t+1's interior). No host synchronisation inside the loop.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "mdfx/runtime.hpp"
+
+namespace mdfx {
+
+struct SolverOptions {
+  bool overlap = true;        // interior || (boundary + exchange) on two streams
+  bool sync_debug = false;    // device-synchronise after every phase (race differential tests)
+  int residual_every = 0;     // compute the global L2 update norm every k steps (0 = never)
+  bool graph = false;         // replay a captured 2-step cycle as a hipGraph (HIP only)
+  double timeout_s = 0.0;     // watchdog for synchronize(): abort instead of hanging (0 = off)
+};
+
+struct StepStats {
+  int64_t steps = 0;
+  double last_residual = -1.0;  // sqrt(sum over the grid of (u_new - u_old)^2), -1 if never
+  int64_t residual_step = -1;
+};
+
+class Solver {
+ public:
+  // local_ranks[i] is the global slab index owned by backends[i] in this process.
+  Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<int> local_ranks,
+         std::vector<std::unique_ptr<Backend>> backends, std::unique_ptr<Transport> transport,
+         SolverOptions opt = SolverOptions());
+  ~Solver();
+  Solver(const Solver&) = delete;
+  Solver& operator=(const Solver&) = delete;
+
+  void init(const InitSpec& s);
+  void run(int64_t steps);
+  void synchronize();
+  // Refresh ghost planes of the current buffer (after write_owned / resume).
+  void exchange_ghosts();
+
+  const StencilSpec& spec() const { return spec_; }
+  const Extent3& global() const { return global_; }
+  int nranks() const { return nranks_; }
+  int num_local() const { return (int)slabs_.size(); }
+  int local_rank(int i) const { return slabs_[i].rank; }
+  const FieldLayout& layout(int i) const { return slabs_[i].lay; }
+  Backend& backend(int i) { return *slabs_[i].be; }
+  Transport& transport() { return *transport_; }
+  const SolverOptions& options() const { return opt_; }
+  void set_options(const SolverOptions& o);
+  int current_index() const { return cur_; }
+  void* buffer(int i, int b) { return slabs_[i].buf[b]; }
+  void* current(int i) { return slabs_[i].buf[cur_]; }
+  void* halo_stream(int i) { return slabs_[i].hs; }
+  void* compute_stream(int i) { return slabs_[i].cs; }
+  const StepStats& stats() const { return stats_; }
+  int64_t owned_cells_global() const { return global_.cells(); }
+
+  // Dense copies of the owned planes (nx*ny*nzl elements, x fastest, no pitch / ghosts).
+  void read_owned(int i, void* host) ;
+  void write_owned(int i, const void* host);
+  // Checkpoint: every process writes its slabs as <dir>/slab_<rank>.bin + .json; resume reads any
+  // decomposition (files are in global plane order).
+  void save_checkpoint(const std::string& dir);
+  void load_checkpoint(const std::string& dir);
+
+ private:
+  struct Slab {
+    int rank = 0;
+    std::unique_ptr<Backend> be;
+    FieldLayout lay;
+    void* buf[2] = {nullptr, nullptr};
+    void* hs = nullptr;  // halo stream
+    void* cs = nullptr;  // compute stream
+    void* ev_bnd = nullptr;
+    void* ev_int = nullptr;
+    double* resid = nullptr;  // 2 accumulators (halo-stream kernels, compute-stream kernels)
+    int64_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0, in_b = 0, in_e = 0;  // storage-plane regions
+  };
+  void step(bool want_resid);
+  void sync_all();
+  void finish_residual();
+  void run_graph(int64_t pairs);
+  void destroy_graph();
+
+  StencilSpec spec_;
+  Extent3 global_;
+  int nranks_;
+  SlabDecomposition decomp_;
+  std::vector<Slab> slabs_;
+  std::unique_ptr<Transport> transport_;
+  SolverOptions opt_;
+  int cur_ = 0;
+  StepStats stats_;
+  bool ghosts_dirty_ = false;
+  void* graph_exec_ = nullptr;  // hipGraphExec_t for the 2-step cycle starting at buffer 0
+  int graph_parity_ = -1;
+};
+
+}  // namespace mdfx

@@ -1,0 +1,161 @@
+// Device-side field initialisation and the stencil dispatcher (variant selection + geometry).
+//
+// Reference parity: create_universe (MDF_kernel.cu:88-99, kernel.cu:131-146) built the grid on the
+// host and shipped it over PCIe every generation (D12); here the initial condition is generated
+// in place on the device from the *global* cell index, so every decomposition yields the same grid
+// and no host copy is needed.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "kcommon.hpp"
+#include "mdfx/kernels.hpp"
+
+namespace mdfx {
+namespace dev {
+
+void naive_launch(const StencilSpec& spec, const Geo& g, const void* in, void* out, double* resid,
+                  hipStream_t s);
+template <class T>
+void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
+template <class T>
+void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
+template <class T>
+void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
+                  hipStream_t s);
+void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s);
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return std::atoi(v);
+}
+
+struct InitArgs {
+  int kind;
+  uint64_t seed;
+  double lo, hi, value, edge, interior, density;
+  int dims;
+};
+
+template <class T>
+__global__ __launch_bounds__(256) void init_kernel(T* __restrict__ buf, Geo g, InitArgs a) {
+  const int64_t n = g.pitch * g.ny * g.lz_max;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = i % g.pitch, t = i / g.pitch, y = t % g.ny, lz = t / g.ny;
+    const int64_t gz = lz + g.gz_off;
+    double v = 0.0;
+    if (x < g.nx && gz >= 0 && gz < g.gnz) {
+      const bool bnd = x == 0 || x == g.nx - 1 || gz == 0 || gz == g.gnz - 1 ||
+                       (a.dims == 3 && (y == 0 || y == g.ny - 1));
+      const uint64_t gidx = (uint64_t)x + (uint64_t)g.nx * ((uint64_t)y + (uint64_t)g.ny * (uint64_t)gz);
+      switch (a.kind) {
+        case 0: v = a.value; break;
+        case 1: v = bnd ? a.edge : a.interior; break;
+        case 2: v = fma(a.hi - a.lo, hash_unit(a.seed, gidx), a.lo); break;
+        default: v = (!bnd && hash_unit(a.seed, gidx) < a.density) ? 1.0 : 0.0; break;
+      }
+    }
+    buf[lz * g.plane + y * g.pitch + x] = (T)v;
+  }
+}
+
+static Geo make_geo(const FieldLayout& lay, int64_t lz_begin, int64_t lz_end) {
+  Geo g;
+  g.pitch = lay.pitch;
+  g.plane = lay.plane;
+  g.nx = lay.global.nx;
+  g.ny = lay.global.ny;
+  g.gnz = lay.global.nz;
+  g.lz_begin = lz_begin;
+  g.lz_end = lz_end;
+  g.gz_off = lay.z0 - lay.halo;
+  g.lz_max = lay.planes();
+  return g;
+}
+
+static std::mutex g_variant_mu;
+static std::string g_variant = "auto";
+
+}  // namespace dev
+
+void hip_set_kernel_variant(const char* name) {
+  std::lock_guard<std::mutex> lk(dev::g_variant_mu);
+  const std::string v = name ? name : "auto";
+  MDFX_CHECK(v == "auto" || v == "naive" || v == "tuned", "unknown kernel variant " + v);
+  dev::g_variant = v;
+}
+
+const char* hip_kernel_variant() {
+  std::lock_guard<std::mutex> lk(dev::g_variant_mu);
+  return dev::g_variant.c_str();
+}
+
+void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* stream) {
+  const dev::Geo g = dev::make_geo(lay, 0, lay.planes());
+  dev::InitArgs a{(int)init.kind, init.seed, init.lo,       init.hi,  init.value,
+                  init.edge,      init.interior, init.density, lay.global.ny == 1 ? 2 : 3};
+  const int64_t n = lay.pitch * lay.global.ny * lay.planes();
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 256 * 64);
+  hipStream_t s = (hipStream_t)stream;
+  switch (lay.dtype) {
+    case DType::F32:
+      hipLaunchKernelGGL(dev::init_kernel<float>, dim3(grid), dim3(256), 0, s, (float*)buf, g, a);
+      break;
+    case DType::F64:
+      hipLaunchKernelGGL(dev::init_kernel<double>, dim3(grid), dim3(256), 0, s, (double*)buf, g, a);
+      break;
+    case DType::U8:
+      hipLaunchKernelGGL(dev::init_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, (uint8_t*)buf, g, a);
+      break;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) MDFX_FAIL(std::string("init launch failed: ") + hipGetErrorString(e));
+}
+
+void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
+  if (a.lz_end <= a.lz_begin) return;
+  MDFX_CHECK(a.lz_begin >= a.lay.halo && a.lz_end <= a.lay.halo + a.lay.nzl(),
+             "region must lie inside the owned planes");
+  const dev::Geo g = dev::make_geo(a.lay, a.lz_begin, a.lz_end);
+  hipStream_t s = (hipStream_t)stream;
+  std::string variant;
+  {
+    std::lock_guard<std::mutex> lk(dev::g_variant_mu);
+    variant = dev::g_variant;
+  }
+  if (variant == "naive") {
+    dev::naive_launch(spec, g, a.in, a.out, a.resid, s);
+  } else {
+    switch (spec.kind) {
+      case StencilKind::Heat7:
+        if (spec.dtype == DType::F32)
+          dev::launch_heat7<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
+        else
+          dev::launch_heat7<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
+        break;
+      case StencilKind::Jacobi5:
+        if (spec.dtype == DType::F32)
+          dev::launch_jacobi5<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
+        else
+          dev::launch_jacobi5<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
+        break;
+      case StencilKind::Box27:
+        if (spec.dtype == DType::F32)
+          dev::launch_box27<float>(g, (const float*)a.in, (float*)a.out, spec.coef, a.resid, s);
+        else
+          dev::launch_box27<double>(g, (const double*)a.in, (double*)a.out, spec.coef, a.resid, s);
+        break;
+      case StencilKind::Life:
+        dev::launch_life(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
+        break;
+    }
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) MDFX_FAIL(std::string("stencil launch failed: ") + hipGetErrorString(e));
+}
+
+}  // namespace mdfx

@@ -1,0 +1,324 @@
+// Tuned gfx950 kernels for the 3D 7-point heat/Jacobi stencil (headline benchmark) and the 2D
+// 5-point MDF stencil.
+//
+// heat7_zw: 2.5D blocking. A 256-thread block = 4 waves arranged WXN (along x) x WYN (along y).
+// Every lane owns one 16-byte vector (4 fp32 / 2 fp64) of RY consecutive rows and marches along z
+// through `zc` planes, keeping planes z-1, z, z+1 of its rows in registers (no re-read of the
+// z-neighbours: each input byte crosses HBM once per chunk). In-plane neighbours:
+//   x +-1   : lane shuffles (ds_bpermute), the wave-segment edge from the neighbouring wave
+//             through a 2-deep LDS ring, and the block edge from one scalar global load;
+//   y +-1   : the lane's own registers except the top / bottom halo row (2 vector loads / plane).
+// Plane z+2 (own rows) and the halo rows / edges of z+1 are prefetched one iteration ahead so a
+// wave keeps ~RY+2 KiB of loads in flight. Stores are non-temporal (the next sweep reads the
+// output after ~8 GiB of other traffic: keeping it in L2/MALL only evicts useful lines).
+// Block->tile order is XCD-aware so vertically adjacent tiles (sharing halo rows) share an L2.
+//
+// Measured (bench/micro/stencil7_variants.hip, 1024^3 fp32, one MI355X): the RY=4, 4-waves-in-x
+// form ran 698 GCells/s = 5.59 TB/s at 8 B/cell vs 509 for the one-cell-per-lane kernel.
+//
+// Reference parity: replaces run_mdf + middle_kernel/border_kernel (MDF_kernel.cu:10-70): the
+// "region" is [lz_begin, lz_end), so the same kernel serves the interior and the boundary planes.
+#include <algorithm>
+
+#include "kcommon.hpp"
+#include "mdfx/kernels.hpp"
+#include "mdfx/stencil_math.hpp"
+
+namespace mdfx {
+namespace dev {
+
+template <class V, class T>
+__device__ __forceinline__ V vsplat(T v) {
+  V r;
+#pragma unroll
+  for (int e = 0; e < (int)(sizeof(V) / sizeof(T)); ++e) r[e] = v;
+  return r;
+}
+
+template <class T, int RY, int WXN, bool RES>
+__global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __restrict__ out, Geo g,
+                                                T r, int zc, int XT, int YT,
+                                                double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  constexpr int N = VT<T>::N;
+  constexpr int WYN = 4 / WXN;
+  constexpr int WX = 64 * N;
+  __shared__ T edge[2][4][RY][2];
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int xt = t % XT;
+  const int yt = (t / XT) % YT;
+  const int zt = t / (XT * YT);
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int wx = w % WXN, wy = w / WXN;
+  const int64_t x = ((int64_t)xt * WXN + wx) * WX + (int64_t)lane * N;
+  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
+  const int64_t lzs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t lze = min(g.lz_end, lzs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const T* ib = in + y0 * pitch + x;
+  T* ob = out + y0 * pitch + x;
+
+  auto ld = [&](int64_t lz, int i) -> V {
+    V v = vsplat<V>(T(0));
+    const int64_t y = y0 + i;
+    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny)
+      v = *(const V*)(ib + lz * plane + (int64_t)i * pitch);
+    return v;
+  };
+  auto ldl = [&](int64_t lz, int i) -> T {
+    const int64_t y = y0 + i;
+    if (wx == 0 && lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max && y < g.ny)
+      return ib[lz * plane + (int64_t)i * pitch - 1];
+    return T(0);
+  };
+  auto ldr = [&](int64_t lz, int i) -> T {
+    const int64_t y = y0 + i;
+    if (wx == WXN - 1 && lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max && y < g.ny)
+      return ib[lz * plane + (int64_t)i * pitch + N];
+    return T(0);
+  };
+
+  V P[RY], C[RY], Nx[RY];
+  T EL[RY], ER[RY];
+#pragma unroll
+  for (int i = 0; i < RY; ++i) {
+    P[i] = ld(lzs - 1, i);
+    C[i] = ld(lzs, i);
+    Nx[i] = ld(lzs + 1, i);
+    EL[i] = ldl(lzs, i);
+    ER[i] = ldr(lzs, i);
+  }
+  V HL = ld(lzs, -1), HH = ld(lzs, RY);
+  double acc = 0.0;
+  int buf = 0;
+  for (int64_t lz = lzs; lz < lze; ++lz) {
+    V NN[RY];
+    T ELN[RY], ERN[RY];
+#pragma unroll
+    for (int i = 0; i < RY; ++i) {
+      NN[i] = ld(lz + 2, i);
+      ELN[i] = ldl(lz + 1, i);
+      ERN[i] = ldr(lz + 1, i);
+    }
+    const V HLN = ld(lz + 1, -1), HHN = ld(lz + 1, RY);
+    if (WXN > 1) {
+      if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < RY; ++i) edge[buf][w][i][0] = C[i][0];
+      }
+      if (lane == 63) {
+#pragma unroll
+        for (int i = 0; i < RY; ++i) edge[buf][w][i][1] = C[i][N - 1];
+      }
+      __syncthreads();
+    }
+    const int64_t gz = lz + g.gz_off;
+    const bool zb = (gz == 0 || gz == g.gnz - 1);
+#pragma unroll
+    for (int i = 0; i < RY; ++i) {
+      const int64_t y = y0 + i;
+      if (y >= g.ny) break;
+      const V c = C[i];
+      V o = c;
+      T l = __shfl_up(c[N - 1], 1, 64);
+      T rr = __shfl_down(c[0], 1, 64);
+      if (lane == 0) l = (WXN > 1 && wx > 0) ? edge[buf][w - 1][i][1] : EL[i];
+      if (lane == 63) rr = (WXN > 1 && wx < WXN - 1) ? edge[buf][w + 1][i][0] : ER[i];
+      if (!zb && y != 0 && y != g.ny - 1) {
+        const V ym = i > 0 ? C[i - 1] : HL;
+        const V yp = i < RY - 1 ? C[i + 1] : HH;
+        const V zm = P[i], zp = Nx[i];
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const T xm = e == 0 ? l : c[e - 1];
+          const T xp = e == N - 1 ? rr : c[e + 1];
+          const T v = sm::heat7<T>(c[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
+          const int64_t xe = x + e;
+          o[e] = (xe == 0 || xe >= g.nx - 1) ? c[e] : v;
+        }
+      }
+      if (xin) {
+        store_nt((V*)(ob + lz * plane + (int64_t)i * pitch), o);
+        if (RES) {
+#pragma unroll
+          for (int e = 0; e < N; ++e)
+            if (x + e < g.nx) {
+              const double d = (double)o[e] - (double)c[e];
+              acc += d * d;
+            }
+        }
+      }
+    }
+    buf ^= 1;
+#pragma unroll
+    for (int i = 0; i < RY; ++i) {
+      P[i] = C[i];
+      C[i] = Nx[i];
+      Nx[i] = NN[i];
+      EL[i] = ELN[i];
+      ER[i] = ERN[i];
+    }
+    HL = HLN;
+    HH = HHN;
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+// 2D 5-point: rows are planes (ny == 1). Each wave is an independent task (x segment of 64*N
+// values, zc rows); block = 4 tasks. Wave-edge x neighbours come from scalar global loads.
+template <class T, bool RES>
+__global__ __launch_bounds__(256) void jacobi5_wave(const T* __restrict__ in, T* __restrict__ out,
+                                                    Geo g, T r, int zc, int XT, int ntasks,
+                                                    double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  const int lane = threadIdx.x & 63;
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;  // wave-uniform; no block barriers in this kernel
+  const int xt = task % XT, zt = task / XT;
+  const int64_t x = (int64_t)xt * WX + (int64_t)lane * N;
+  const int64_t lzs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t lze = min(g.lz_end, lzs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t plane = g.plane;
+  auto ld = [&](int64_t lz) -> V {
+    V v = vsplat<V>(T(0));
+    if (xin && lz >= 0 && lz < g.lz_max) v = *(const V*)(in + lz * plane + x);
+    return v;
+  };
+  auto ldl = [&](int64_t lz) -> T {
+    if (lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max) return in[lz * plane + x - 1];
+    return T(0);
+  };
+  auto ldr = [&](int64_t lz) -> T {
+    if (lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max) return in[lz * plane + x + N];
+    return T(0);
+  };
+  V P = ld(lzs - 1), C = ld(lzs), Nx = ld(lzs + 1);
+  T EL = ldl(lzs), ER = ldr(lzs);
+  double acc = 0.0;
+  for (int64_t lz = lzs; lz < lze; ++lz) {
+    const V NN = ld(lz + 2);
+    const T ELN = ldl(lz + 1), ERN = ldr(lz + 1);
+    const int64_t gz = lz + g.gz_off;
+    const V c = C;
+    V o = c;
+    T l = __shfl_up(c[N - 1], 1, 64);
+    T rr = __shfl_down(c[0], 1, 64);
+    if (lane == 0) l = EL;
+    if (lane == 63) rr = ER;
+    if (gz != 0 && gz != g.gnz - 1) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const T xm = e == 0 ? l : c[e - 1];
+        const T xp = e == N - 1 ? rr : c[e + 1];
+        const T v = sm::jacobi5<T>(c[e], xm, xp, P[e], Nx[e], r);
+        const int64_t xe = x + e;
+        o[e] = (xe == 0 || xe >= g.nx - 1) ? c[e] : v;
+      }
+    }
+    if (xin) {
+      store_nt((V*)(out + lz * plane + x), o);
+      if (RES) {
+#pragma unroll
+        for (int e = 0; e < N; ++e)
+          if (x + e < g.nx) {
+            const double d = (double)o[e] - (double)c[e];
+            acc += d * d;
+          }
+      }
+    }
+    P = C;
+    C = Nx;
+    Nx = NN;
+    EL = ELN;
+    ER = ERN;
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+// ---- launch helpers ---------------------------------------------------------------------------
+
+// Pick the z-chunk so the grid has >= ~8 blocks per CU (2048) without chunks so short that the
+// 2 extra planes each chunk re-reads dominate.
+int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target) {
+  if (planes <= 0) return 1;
+  int64_t chunks = (blocks_target + columns - 1) / std::max<int64_t>(columns, 1);
+  chunks = std::max<int64_t>(chunks, 1);
+  int64_t zc = (planes + chunks - 1) / chunks;
+  zc = std::max<int64_t>(zc, 8);
+  zc = std::min<int64_t>(zc, zc_max);
+  return (int)std::max<int64_t>(zc, 1);
+}
+
+int env_int(const char* name, int dflt);
+
+template <class T, int RY, int WXN>
+static void launch_heat7_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  constexpr int WYN = 4 / WXN;
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int XT = (int)((g.nx + WXN * WX - 1) / (WXN * WX));
+  const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, 2048);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const dim3 grd((unsigned)((int64_t)XT * YT * ZT)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((heat7_zw<T, RY, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, resid);
+  else
+    hipLaunchKernelGGL((heat7_zw<T, RY, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, resid);
+}
+
+template <class T, int RY>
+static void launch_heat7_ry(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int WX = 64 * VT<T>::N;
+  // waves along x only as far as the row is wide; the rest stack along y.
+  if (g.nx > 2 * WX)
+    launch_heat7_t<T, RY, 4>(g, in, out, r, resid, s);
+  else if (g.nx > WX)
+    launch_heat7_t<T, RY, 2>(g, in, out, r, resid, s);
+  else
+    launch_heat7_t<T, RY, 1>(g, in, out, r, resid, s);
+}
+
+template <class T>
+void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  int ry = env_int("MDFX_RY", 0);
+  if (ry <= 0) ry = sizeof(T) == 4 ? 4 : 4;
+  if (g.ny < 8) ry = 1;
+  switch (ry) {
+    case 1: launch_heat7_ry<T, 1>(g, in, out, r, resid, s); break;
+    case 2: launch_heat7_ry<T, 2>(g, in, out, r, resid, s); break;
+    default: launch_heat7_ry<T, 4>(g, in, out, r, resid, s); break;
+  }
+}
+template void launch_heat7<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
+template void launch_heat7<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
+
+template <class T>
+void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  const int64_t planes = g.lz_end - g.lz_begin;
+  if (planes <= 0) return;
+  constexpr int WX = 64 * VT<T>::N;
+  const int XT = (int)((g.nx + WX - 1) / WX);
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const int ntasks = XT * ZT;
+  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((jacobi5_wave<T, true>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+  else
+    hipLaunchKernelGGL((jacobi5_wave<T, false>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+}
+template void launch_jacobi5<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
+template void launch_jacobi5<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
+
+}  // namespace dev
+}  // namespace mdfx

@@ -1,0 +1,427 @@
+// pybind11 bindings: module `_mdfx` (built in-tree into mpi_cuda_process_amd/).
+//
+// Deliberately torch-header-free (fast builds, no ABI coupling): tensors cross the boundary as raw
+// pointers checked by the Python layer, and device memory owned by the engine is exported
+// zero-copy through DLPack capsules (torch.from_dlpack).
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "mdfx/solver.hpp"
+
+namespace py = pybind11;
+using namespace mdfx;
+
+namespace {
+
+// ---- minimal DLPack ABI (v0.8 "dltensor" capsule) -------------------------------------------
+struct DLDevice {
+  int32_t device_type;  // kDLCPU = 1, kDLROCM = 10
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code;  // 0 int, 1 uint, 2 float
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+struct DLCtx {
+  std::vector<int64_t> shape, strides;
+};
+
+void dl_deleter(DLManagedTensor* t) {
+  delete (DLCtx*)t->manager_ctx;
+  delete t;
+}
+
+py::capsule make_dlpack(void* data, int device, DType dt, std::vector<int64_t> shape,
+                        std::vector<int64_t> strides) {
+  auto* ctx = new DLCtx{std::move(shape), std::move(strides)};
+  auto* t = new DLManagedTensor();
+  t->dl_tensor.data = data;
+  t->dl_tensor.device = DLDevice{device < 0 ? 1 : 10, device < 0 ? 0 : device};
+  t->dl_tensor.ndim = (int32_t)ctx->shape.size();
+  switch (dt) {
+    case DType::F32: t->dl_tensor.dtype = DLDataType{2, 32, 1}; break;
+    case DType::F64: t->dl_tensor.dtype = DLDataType{2, 64, 1}; break;
+    case DType::U8: t->dl_tensor.dtype = DLDataType{1, 8, 1}; break;
+  }
+  t->dl_tensor.shape = ctx->shape.data();
+  t->dl_tensor.strides = ctx->strides.data();
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = ctx;
+  t->deleter = dl_deleter;
+  return py::capsule(t, "dltensor", [](PyObject* cap) {
+    // only delete if the consumer never took ownership (name still "dltensor")
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* m = (DLManagedTensor*)PyCapsule_GetPointer(cap, "dltensor");
+      if (m && m->deleter) m->deleter(m);
+    }
+  });
+}
+
+StencilSpec make_spec(const std::string& kind, const std::string& dtype, double r, double c0,
+                      double c1, double c2, double c3) {
+  StencilSpec s;
+  s.kind = stencil_from_name(kind);
+  s.dtype = dtype_from_name(dtype);
+  s.coef.r = r;
+  s.coef.c0 = c0;
+  s.coef.c1 = c1;
+  s.coef.c2 = c2;
+  s.coef.c3 = c3;
+  return s;
+}
+
+InitSpec make_init(const std::string& kind, uint64_t seed, double lo, double hi, double value,
+                   double edge, double interior, double density) {
+  InitSpec s;
+  if (kind == "constant")
+    s.kind = InitKind::Constant;
+  else if (kind == "dirichlet")
+    s.kind = InitKind::Dirichlet;
+  else if (kind == "random")
+    s.kind = InitKind::Random;
+  else if (kind == "life" || kind == "life_random")
+    s.kind = InitKind::LifeRandom;
+  else
+    throw Error("unknown init kind '" + kind + "' (constant|dirichlet|random|life)");
+  s.seed = seed;
+  s.lo = lo;
+  s.hi = hi;
+  s.value = value;
+  s.edge = edge;
+  s.interior = interior;
+  s.density = density;
+  return s;
+}
+
+py::dict layout_dict(const FieldLayout& l) {
+  py::dict d;
+  d["nx"] = l.global.nx;
+  d["ny"] = l.global.ny;
+  d["nz"] = l.global.nz;
+  d["z0"] = l.z0;
+  d["z1"] = l.z1;
+  d["halo"] = l.halo;
+  d["pitch"] = l.pitch;
+  d["plane"] = l.plane;
+  d["planes"] = l.planes();
+  d["nzl"] = l.nzl();
+  d["bytes"] = l.bytes();
+  d["esize"] = l.esize();
+  d["dtype"] = dtype_name(l.dtype);
+  return d;
+}
+
+py::dtype np_dtype(DType t) {
+  switch (t) {
+    case DType::F32: return py::dtype::of<float>();
+    case DType::F64: return py::dtype::of<double>();
+    case DType::U8: return py::dtype::of<uint8_t>();
+  }
+  return py::dtype::of<float>();
+}
+
+class PySolver {
+ public:
+  PySolver(const std::string& kind, const std::string& dtype, int64_t nx, int64_t ny, int64_t nz,
+           int nranks, std::vector<int> local_ranks, std::vector<int> devices,
+           const std::string& transport, py::bytes unique_id, py::object callbacks, bool overlap,
+           bool sync_debug, int residual_every, bool graph, double timeout_s, double r, double c0,
+           double c1, double c2, double c3) {
+    const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3);
+    if (devices.size() == 1 && local_ranks.size() > 1) devices.assign(local_ranks.size(), devices[0]);
+    if (devices.size() != local_ranks.size())
+      throw Error("devices must have one entry per local rank (or a single entry)");
+    std::vector<std::unique_ptr<Backend>> bes;
+    for (int d : devices) bes.push_back(d < 0 ? make_cpu_backend() : make_hip_backend(d));
+    std::unique_ptr<Transport> tr;
+    if (transport == "host") {
+      tr = make_host_transport();
+    } else if (transport == "loopback") {
+      tr = make_loopback_transport();
+    } else if (transport == "rccl") {
+      tr = make_rccl_transport(std::string(unique_id));
+    } else if (transport == "callback") {
+      if (callbacks.is_none()) throw Error("callback transport needs callbacks");
+      py::dict cb = callbacks.cast<py::dict>();
+      CallbackFns f;
+      // callables may be released from a thread that does not hold the GIL (close() releases it)
+      auto keep = [](py::object o) {
+        return std::shared_ptr<py::object>(new py::object(std::move(o)), [](py::object* q) {
+          py::gil_scoped_acquire g;
+          delete q;
+        });
+      };
+      // keep the Python callables alive inside the std::functions; re-acquire the GIL, run()
+      // releases it.
+      auto ex = keep(cb["exchange"]);
+      f.exchange = [ex](int b) {
+        py::gil_scoped_acquire g;
+        (*ex)(b);
+      };
+      if (cb.contains("allreduce_sum")) {
+        auto ar = keep(cb["allreduce_sum"]);
+        f.allreduce_sum = [ar](double v) {
+          py::gil_scoped_acquire g;
+          return (*ar)(v).cast<double>();
+        };
+      }
+      if (cb.contains("allreduce_max")) {
+        auto am = keep(cb["allreduce_max"]);
+        f.allreduce_max = [am](double v) {
+          py::gil_scoped_acquire g;
+          return (*am)(v).cast<double>();
+        };
+      }
+      if (cb.contains("barrier")) {
+        auto ba = keep(cb["barrier"]);
+        f.barrier = [ba]() {
+          py::gil_scoped_acquire g;
+          (*ba)();
+        };
+      }
+      tr = make_callback_transport(std::move(f));
+    } else {
+      throw Error("unknown transport '" + transport + "' (host|loopback|rccl|callback)");
+    }
+    SolverOptions o;
+    o.overlap = overlap;
+    o.sync_debug = sync_debug;
+    o.residual_every = residual_every;
+    o.graph = graph;
+    o.timeout_s = timeout_s;
+    py::gil_scoped_release nogil;  // RCCL comm init may block on peers
+    s_.reset(new Solver(spec, Extent3{nx, ny, nz}, nranks, std::move(local_ranks), std::move(bes),
+                        std::move(tr), o));
+  }
+
+  Solver& s() { return *s_; }
+  void close() {
+    py::gil_scoped_release nogil;
+    s_.reset();
+  }
+  Solver& chk() {
+    if (!s_) throw Error("solver is closed");
+    return *s_;
+  }
+
+  std::unique_ptr<Solver> s_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_mdfx, m) {
+  m.doc() = "mdfx: MI355X-native multi-GPU finite-difference stencil engine (native core)";
+  py::register_exception<Error>(m, "MdfxError", PyExc_RuntimeError);
+
+  m.def("hip_device_count", &hip_device_count);
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("set_kernel_variant", [](const std::string& v) { hip_set_kernel_variant(v.c_str()); });
+  m.def("kernel_variant", []() { return std::string(hip_kernel_variant()); });
+  m.def("layout", [](int64_t nx, int64_t ny, int64_t nz, int64_t z0, int64_t z1, int halo,
+                     const std::string& dtype) {
+    return layout_dict(FieldLayout::make(Extent3{nx, ny, nz}, z0, z1, halo, dtype_from_name(dtype)));
+  }, py::arg("nx"), py::arg("ny"), py::arg("nz"), py::arg("z0"), py::arg("z1"), py::arg("halo") = 1,
+        py::arg("dtype") = "f32");
+  m.def("slab_bounds", [](int64_t nz, int parts) {
+    SlabDecomposition d(nz, parts);
+    std::vector<std::pair<int64_t, int64_t>> out;
+    for (int p = 0; p < parts; ++p) out.emplace_back(d.z0(p), d.z1(p));
+    return out;
+  });
+
+  // Kernel-level entry: one region update on caller-owned memory (torch tensors in the tests).
+  m.def(
+      "stencil",
+      [](const std::string& kind, const std::string& dtype, uintptr_t in, uintptr_t out, int64_t nx,
+         int64_t ny, int64_t nz, int64_t z0, int64_t z1, int halo, int64_t lz_begin, int64_t lz_end,
+         int device, uintptr_t stream, uintptr_t resid, double r, double c0, double c1, double c2,
+         double c3) {
+        RegionArgs a;
+        a.in = (const void*)in;
+        a.out = (void*)out;
+        a.lay = FieldLayout::make(Extent3{nx, ny, nz}, z0, z1, halo, dtype_from_name(dtype));
+        a.lz_begin = lz_begin;
+        a.lz_end = lz_end;
+        a.resid = (double*)resid;
+        const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3);
+        if (device < 0)
+          cpu_stencil(spec, a);
+        else
+          hip_stencil(spec, a, (void*)stream);
+      },
+      py::arg("kind"), py::arg("dtype"), py::arg("in_ptr"), py::arg("out_ptr"), py::arg("nx"),
+      py::arg("ny"), py::arg("nz"), py::arg("z0"), py::arg("z1"), py::arg("halo"),
+      py::arg("lz_begin"), py::arg("lz_end"), py::arg("device"), py::arg("stream") = 0,
+      py::arg("resid_ptr") = 0, py::arg("r") = -1.0, py::arg("c0") = 0.25, py::arg("c1") = 0.05,
+      py::arg("c2") = 0.025, py::arg("c3") = 3.0 / 160.0);
+  m.def(
+      "init_field",
+      [](const std::string& kind, const std::string& dtype, uintptr_t buf, int64_t nx, int64_t ny,
+         int64_t nz, int64_t z0, int64_t z1, int halo, int device, uintptr_t stream, uint64_t seed,
+         double lo, double hi, double value, double edge, double interior, double density) {
+        const FieldLayout l = FieldLayout::make(Extent3{nx, ny, nz}, z0, z1, halo, dtype_from_name(dtype));
+        const InitSpec s = make_init(kind, seed, lo, hi, value, edge, interior, density);
+        if (device < 0)
+          cpu_init(s, l, (void*)buf);
+        else
+          hip_init(s, l, (void*)buf, (void*)stream);
+      },
+      py::arg("kind"), py::arg("dtype"), py::arg("buf_ptr"), py::arg("nx"), py::arg("ny"),
+      py::arg("nz"), py::arg("z0"), py::arg("z1"), py::arg("halo"), py::arg("device"),
+      py::arg("stream") = 0, py::arg("seed") = 1, py::arg("lo") = 0.0, py::arg("hi") = 1.0,
+      py::arg("value") = 0.0, py::arg("edge") = 100.0, py::arg("interior") = 0.0,
+      py::arg("density") = 0.15);
+  m.def("life_compat_init", [](int64_t h, int64_t w, double density, unsigned seed) {
+    py::array_t<uint8_t> a({h, w});
+    cpu_life_compat_init(a.mutable_data(), h, w, density, seed);
+    return a;
+  }, py::arg("h"), py::arg("w"), py::arg("density") = 0.15, py::arg("seed") = 1);
+
+  py::class_<PySolver>(m, "Solver")
+      .def(py::init<const std::string&, const std::string&, int64_t, int64_t, int64_t, int,
+                    std::vector<int>, std::vector<int>, const std::string&, py::bytes, py::object,
+                    bool, bool, int, bool, double, double, double, double, double, double>(),
+           py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ny"), py::arg("nz"),
+           py::arg("nranks"), py::arg("local_ranks"), py::arg("devices"), py::arg("transport"),
+           py::arg("unique_id") = py::bytes(""), py::arg("callbacks") = py::none(),
+           py::arg("overlap") = true, py::arg("sync_debug") = false, py::arg("residual_every") = 0,
+           py::arg("graph") = false, py::arg("timeout_s") = 0.0, py::arg("r") = -1.0,
+           py::arg("c0") = 0.25, py::arg("c1") = 0.05, py::arg("c2") = 0.025,
+           py::arg("c3") = 3.0 / 160.0)
+      .def("close", &PySolver::close)
+      .def("init",
+           [](PySolver& p, const std::string& kind, uint64_t seed, double lo, double hi, double value,
+              double edge, double interior, double density) {
+             const InitSpec s = make_init(kind, seed, lo, hi, value, edge, interior, density);
+             py::gil_scoped_release nogil;
+             p.chk().init(s);
+           },
+           py::arg("kind") = "random", py::arg("seed") = 1, py::arg("lo") = 0.0, py::arg("hi") = 1.0,
+           py::arg("value") = 0.0, py::arg("edge") = 100.0, py::arg("interior") = 0.0,
+           py::arg("density") = 0.15)
+      .def("run",
+           [](PySolver& p, int64_t steps) {
+             py::gil_scoped_release nogil;
+             p.chk().run(steps);
+           })
+      .def("synchronize",
+           [](PySolver& p) {
+             py::gil_scoped_release nogil;
+             p.chk().synchronize();
+           })
+      .def("exchange_ghosts",
+           [](PySolver& p) {
+             py::gil_scoped_release nogil;
+             p.chk().exchange_ghosts();
+           })
+      .def("set_options",
+           [](PySolver& p, bool overlap, bool sync_debug, int residual_every, bool graph,
+              double timeout_s) {
+             SolverOptions o;
+             o.overlap = overlap;
+             o.sync_debug = sync_debug;
+             o.residual_every = residual_every;
+             o.graph = graph;
+             o.timeout_s = timeout_s;
+             p.chk().set_options(o);
+           },
+           py::arg("overlap") = true, py::arg("sync_debug") = false, py::arg("residual_every") = 0,
+           py::arg("graph") = false, py::arg("timeout_s") = 0.0)
+      .def_property_readonly("num_local", [](PySolver& p) { return p.chk().num_local(); })
+      .def_property_readonly("nranks", [](PySolver& p) { return p.chk().nranks(); })
+      .def_property_readonly("steps", [](PySolver& p) { return p.chk().stats().steps; })
+      .def_property_readonly("residual", [](PySolver& p) { return p.chk().stats().last_residual; })
+      .def_property_readonly("residual_step", [](PySolver& p) { return p.chk().stats().residual_step; })
+      .def_property_readonly("current_index", [](PySolver& p) { return p.chk().current_index(); })
+      .def_property_readonly("transport_name", [](PySolver& p) { return std::string(p.chk().transport().name()); })
+      .def("local_rank", [](PySolver& p, int i) { return p.chk().local_rank(i); })
+      .def("layout", [](PySolver& p, int i) { return layout_dict(p.chk().layout(i)); })
+      .def("device", [](PySolver& p, int i) { return p.chk().backend(i).device(); })
+      .def("buffer_ptr", [](PySolver& p, int i, int b) { return (uintptr_t)p.chk().buffer(i, b); })
+      .def("halo_stream", [](PySolver& p, int i) { return (uintptr_t)p.chk().halo_stream(i); })
+      .def("compute_stream", [](PySolver& p, int i) { return (uintptr_t)p.chk().compute_stream(i); })
+      .def("halo_spans",
+           [](PySolver& p, int i, int b) {
+             Solver& s = p.chk();
+             LocalSlab ls;
+             ls.rank = s.local_rank(i);
+             ls.lay = s.layout(i);
+             ls.buf[0] = s.buffer(i, 0);
+             ls.buf[1] = s.buffer(i, 1);
+             py::list out;
+             for (int side = 0; side < 2; ++side) {
+               const HaloSpan h = halo_span(ls, b, side, s.nranks());
+               py::dict d;
+               d["side"] = side;
+               d["peer"] = h.peer;
+               d["send"] = (uintptr_t)h.send;
+               d["recv"] = (uintptr_t)h.recv;
+               d["bytes"] = h.bytes;
+               out.append(d);
+             }
+             return out;
+           })
+      .def("view",
+           [](PySolver& p, int i, int b) {
+             Solver& s = p.chk();
+             const FieldLayout& l = s.layout(i);
+             return make_dlpack(s.buffer(i, b), s.backend(i).device(), l.dtype,
+                                {l.planes(), l.global.ny, l.pitch}, {l.plane, l.pitch, 1});
+           })
+      .def("bytes_view",
+           [](PySolver& p, int i, uintptr_t ptr, int64_t nbytes) {
+             Solver& s = p.chk();
+             return make_dlpack((void*)ptr, s.backend(i).device(), DType::U8, {nbytes}, {1});
+           })
+      .def("read_owned",
+           [](PySolver& p, int i) {
+             Solver& s = p.chk();
+             const FieldLayout& l = s.layout(i);
+             py::array a(np_dtype(l.dtype), std::vector<int64_t>{l.nzl(), l.global.ny, l.global.nx});
+             void* dst = a.mutable_data();
+             {
+               py::gil_scoped_release nogil;
+               s.read_owned(i, dst);
+             }
+             return a;
+           })
+      .def("write_owned",
+           [](PySolver& p, int i, py::array a) {
+             Solver& s = p.chk();
+             const FieldLayout& l = s.layout(i);
+             if ((size_t)a.nbytes() != (size_t)l.owned_cells() * l.esize())
+               throw Error("write_owned: array size does not match the slab");
+             py::array c = py::array::ensure(a, py::array::c_style);
+             const void* src = c.data();
+             py::gil_scoped_release nogil;
+             s.write_owned(i, src);
+           })
+      .def("save_checkpoint",
+           [](PySolver& p, const std::string& d) {
+             py::gil_scoped_release nogil;
+             p.chk().save_checkpoint(d);
+           })
+      .def("load_checkpoint", [](PySolver& p, const std::string& d) {
+        py::gil_scoped_release nogil;
+        p.chk().load_checkpoint(d);
+      });
+}

@@ -1,0 +1,206 @@
+"""High-level simulation API over the native engine (``mdfx::Solver``).
+
+:class:`Simulation` owns one native solver and picks the device backend and the halo transport:
+
+=================  ==============================================================================
+mode               slabs / transport
+=================  ==============================================================================
+single             1 slab (P = 1), no exchange
+virtual            P slabs in this process: ``host`` (CPU memcpy) or ``loopback`` (HIP D2D / peer
+                   copies, possibly over several GPUs) — how multi-rank runs are tested on one GPU
+distributed        one slab per torch.distributed rank (torchrun / mpirun): ``rccl`` (native
+                   ncclSend/ncclRecv on the engine's halo stream, unique id broadcast over the
+                   control group) or ``torch`` (torch.distributed p2p through a callback: gloo on
+                   CPU, nccl = RCCL on GPU)
+=================  ==============================================================================
+
+Reference parity: the reference's ``main`` (MDF_kernel.cu:101-236 / kernel.cu:148-283) is this
+object with P = 2 fixed, MPI host-staged halos, and no swap.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ._native import hip_available, native
+from .models import InitCondition, Problem
+from .ops import TORCH_DTYPE
+from .parallel.decomp import slab_bounds
+from .parallel.dist import TorchP2PTransport, broadcast_bytes, is_distributed
+
+
+class Simulation:
+    def __init__(self, problem: Problem, *, device: str = "auto", ranks: Optional[int] = None,
+                 devices: Optional[Sequence[int]] = None, transport: str = "auto",
+                 distributed: Optional[bool] = None, overlap: bool = True, sync_debug: bool = False,
+                 residual_every: int = 0, graph: bool = False, timeout_s: float = 0.0,
+                 group=None):
+        self.problem = problem
+        if device == "auto":
+            device = "hip" if hip_available() else "cpu"
+        if device not in ("hip", "cpu"):
+            raise ValueError("device must be 'hip', 'cpu' or 'auto'")
+        self.device = device
+        if distributed is None:
+            distributed = is_distributed() and ranks is None
+        self.distributed = bool(distributed)
+        self._torch_transport = None
+        self.group = group
+
+        if self.distributed:
+            world = dist.get_world_size(group)
+            rank = dist.get_rank(group)
+            nranks, local_ranks = world, [rank]
+            if device == "hip":
+                ndev = torch.cuda.device_count()
+                local = int(__import__("os").environ.get("LOCAL_RANK", rank))
+                dev_list = [devices[0] if devices else local % ndev]
+            else:
+                dev_list = [-1]
+            if transport == "auto":
+                transport = "rccl" if device == "hip" else "torch"
+            if transport == "rccl":
+                if device != "hip":
+                    raise ValueError("rccl transport needs HIP devices")
+                torch.cuda.set_device(dev_list[0])
+                uid = native().rccl_unique_id() if rank == 0 else None
+                uid = broadcast_bytes(uid, src=0, group=group)
+                args = dict(transport="rccl", unique_id=uid)
+            elif transport == "torch":
+                p2p_group = group
+                if device == "hip":
+                    torch.cuda.set_device(dev_list[0])
+                    p2p_group = dist.new_group(backend="nccl") if group is None else group
+                self._torch_transport = TorchP2PTransport(p2p_group)
+                args = dict(transport="callback", callbacks=self._torch_transport.callbacks())
+            else:
+                raise ValueError("distributed transport must be rccl|torch|auto")
+        else:
+            nranks = ranks or 1
+            local_ranks = list(range(nranks))
+            if device == "hip":
+                dev_list = list(devices) if devices else [torch.cuda.current_device()]
+                if len(dev_list) == 1:
+                    dev_list = dev_list * nranks
+                if len(dev_list) != nranks:
+                    raise ValueError("devices must list one device per rank")
+            else:
+                dev_list = [-1] * nranks
+            if transport == "auto":
+                transport = "loopback" if device == "hip" else "host"
+            if transport not in ("loopback", "host", "rccl"):
+                raise ValueError("in-process transport must be loopback|host|rccl")
+            args = dict(transport=transport)
+            if transport == "rccl":  # one process driving several GPUs
+                args["unique_id"] = native().rccl_unique_id()
+
+        self.nranks = nranks
+        self._s = native().Solver(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
+                                  nranks, local_ranks, dev_list, overlap=overlap,
+                                  sync_debug=sync_debug, residual_every=residual_every, graph=graph,
+                                  timeout_s=timeout_s, **problem.coef_kwargs(), **args)
+        if self._torch_transport is not None:
+            self._torch_transport.solver = self._s
+        self.transport = self._s.transport_name if self._torch_transport is None else "torch"
+        self.bounds = slab_bounds(problem.nz, nranks)
+
+    # ---- lifecycle -------------------------------------------------------------------------
+    def close(self):
+        if self._s is not None:
+            self._s.close()
+            self._s = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+        return False
+
+    @property
+    def native(self):
+        return self._s
+
+    # ---- state -----------------------------------------------------------------------------
+    def init(self, init: Optional[InitCondition] = None) -> "Simulation":
+        ic = init or self.problem.init
+        if ic.kind == "compat":
+            # reference GoL grid: glibc rand() Bernoulli(density) in global row-major order
+            g = native().life_compat_init(self.problem.nz, self.problem.nx, ic.density, ic.seed)
+            self._s.init("constant", value=0.0)
+            for i in range(self._s.num_local):
+                lay = self._s.layout(i)
+                self._s.write_owned(i, np.ascontiguousarray(g[lay["z0"]:lay["z1"]]).reshape(-1, 1, self.problem.nx))
+            return self
+        self._s.init(ic.kind, seed=ic.seed, lo=ic.lo, hi=ic.hi, value=ic.value, edge=ic.edge,
+                     interior=ic.interior, density=ic.density)
+        return self
+
+    def run(self, steps: int) -> "Simulation":
+        self._s.run(int(steps))
+        return self
+
+    def synchronize(self):
+        self._s.synchronize()
+
+    def set_options(self, **kw):
+        self._s.set_options(**kw)
+
+    @property
+    def steps(self) -> int:
+        return self._s.steps
+
+    @property
+    def residual(self) -> float:
+        return self._s.residual
+
+    @property
+    def num_local(self) -> int:
+        return self._s.num_local
+
+    def layout(self, i: int = 0) -> dict:
+        return self._s.layout(i)
+
+    def read_local(self, i: int = 0) -> np.ndarray:
+        """Owned planes of local slab i as a dense (nzl, ny, nx) numpy array."""
+        return self._s.read_owned(i)
+
+    def write_local(self, i: int, a: np.ndarray):
+        self._s.write_owned(i, np.ascontiguousarray(a))
+
+    def view(self, i: int = 0, current: bool = True) -> torch.Tensor:
+        """Zero-copy torch view (planes, ny, pitch) of a slab buffer (ghosts included)."""
+        b = self._s.current_index if current else 1 - self._s.current_index
+        t = torch.from_dlpack(self._s.view(i, b))
+        t._mdfx_owner = self  # keep the engine alive while the view is
+        return t
+
+    def gather(self) -> np.ndarray:
+        """The whole global grid (nz, ny, nx) as numpy, on every caller.
+
+        In-process: concatenation of the local slabs. Distributed: all_gather_object over the
+        control group (debug / test sized grids only).
+        """
+        parts = [self.read_local(i) for i in range(self.num_local)]
+        if self.distributed:
+            allp: List = [None] * dist.get_world_size(self.group)
+            dist.all_gather_object(allp, parts[0], group=self.group)
+            parts = allp
+        return np.concatenate(parts, axis=0)
+
+    def save_checkpoint(self, path: str):
+        self._s.save_checkpoint(path)
+
+    def load_checkpoint(self, path: str):
+        self._s.load_checkpoint(path)
+
+    @property
+    def torch_dtype(self):
+        return TORCH_DTYPE[self.problem.dtype]
+
+
+__all__ = ["Simulation"]

@@ -1,0 +1,129 @@
+"""Process bootstrap over torch.distributed and the torch point-to-point halo transport.
+
+One process per GPU (``torchrun --nproc-per-node N`` or ``mpirun -np N``): the process's rank is
+its slab index, its device is ``LOCAL_RANK % device_count``. The control plane (unique-id
+broadcast, barriers, max-over-ranks timing) runs on a gloo process group; the data plane is either
+the native RCCL transport (ncclSend/ncclRecv over xGMI on the engine's halo stream) or
+:class:`TorchP2PTransport` (torch.distributed isend/irecv, e.g. gloo for CPU tests).
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    launched: bool = False  # started by torchrun / mpirun
+
+
+def detect_env() -> DistEnv:
+    """Rank / size from torchrun (RANK/WORLD_SIZE), MPICH hydra (PMI_*) or Open MPI (OMPI_*)."""
+    e = os.environ
+    for rk, ws, lr in (("RANK", "WORLD_SIZE", "LOCAL_RANK"),
+                       ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"),
+                       ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID")):
+        if rk in e and ws in e:
+            rank, world = int(e[rk]), int(e[ws])
+            local = int(e.get(lr, rank))
+            return DistEnv(rank, world, local, True)
+    return DistEnv()
+
+
+def is_distributed() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def init_distributed(backend: str = "gloo", timeout_s: float = 600.0) -> DistEnv:
+    """Initialise the default process group from the launcher environment (idempotent)."""
+    env = detect_env()
+    if not dist.is_initialized() and env.world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(env.rank))
+        os.environ.setdefault("WORLD_SIZE", str(env.world))
+        dist.init_process_group(backend=backend, rank=env.rank, world_size=env.world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    if dist.is_initialized():
+        env.rank, env.world = dist.get_rank(), dist.get_world_size()
+    return env
+
+
+def broadcast_bytes(data: Optional[bytes], src: int = 0, group=None) -> bytes:
+    """Broadcast a byte string (e.g. the 128-byte ncclUniqueId) from ``src`` over a CPU group."""
+    obj = [data]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    return obj[0]
+
+
+class TorchP2PTransport:
+    """Halo exchange through torch.distributed point-to-point ops (callback transport).
+
+    The native engine calls :meth:`exchange` with the index of the buffer just written; faces are
+    exported zero-copy from the engine (DLPack) and exchanged with ``isend``/``irecv``. On a HIP
+    field the ops are issued on the slab's halo stream, so they stay ordered with the engine's
+    kernels exactly like the native transports.
+    """
+
+    def __init__(self, group=None):
+        self.group = group
+        self.solver = None  # set by the Simulation once the native solver exists
+
+    def callbacks(self) -> dict:
+        return {"exchange": self.exchange, "allreduce_sum": self.allreduce_sum,
+                "allreduce_max": self.allreduce_max, "barrier": self.barrier}
+
+    def _bytes(self, ptr: int, n: int) -> torch.Tensor:
+        return torch.from_dlpack(self.solver.bytes_view(0, ptr, n))
+
+    def exchange(self, b: int) -> None:
+        s = self.solver
+        spans = [sp for sp in s.halo_spans(0, b) if sp["peer"] >= 0]
+        if not spans:
+            return
+        dev = s.device(0)
+        ctx = torch.cuda.stream(torch.cuda.ExternalStream(s.halo_stream(0))) if dev >= 0 else _null()
+        with ctx:
+            ops = []
+            for sp in spans:
+                recv = self._bytes(sp["recv"], sp["bytes"])
+                send = self._bytes(sp["send"], sp["bytes"])
+                ops.append(dist.P2POp(dist.irecv, recv, sp["peer"], self.group))
+                ops.append(dist.P2POp(dist.isend, send, sp["peer"], self.group))
+            if dev >= 0:
+                # one NCCL (= RCCL) group for all faces: no pairwise ordering hazards
+                reqs = dist.batch_isend_irecv(ops)
+            else:
+                reqs = [op.op(op.tensor, op.peer, op.group) for op in ops]
+            for r in reqs:
+                r.wait()
+
+    def allreduce_sum(self, v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return float(t.item())
+
+    def allreduce_max(self, v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def barrier(self) -> None:
+        dist.barrier(group=self.group)
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU-box session: tests, smoke, bench, profile. Each GPU step has its own time limit and the
+# chain stops at the first failure (gpurun guidance: never retry a failing GPU step).
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+step() { local t=$1; shift; echo "== $* (limit ${t}s)"; timeout -k 10 "$t" "$@"; local rc=$?; echo "== rc=$rc"; return $rc; }
+MODE=${1:-all}
+if [[ $MODE == all || $MODE == test ]]; then
+  step 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -50 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -5 gpurun_out/pytest_gpu.log
+fi
+if [[ $MODE == all || $MODE == smoke ]]; then
+  step 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+fi
+if [[ $MODE == all || $MODE == bench ]]; then
+  step 300 python bench.py > gpurun_out/bench_n1.json 2> gpurun_out/bench_n1.err || { cat gpurun_out/bench_n1.err; exit 1; }
+  cat gpurun_out/bench_n1.json
+fi

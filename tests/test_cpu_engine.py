@@ -1,0 +1,246 @@
+"""CPU tier (T1 of SURVEY §4.3): slab math, CPU oracle vs PyTorch, engine invariants.
+
+The native engine runs the same scheduler on the CPU backend (host transport), so decomposition
+invariance, overlap/serialised equivalence, residuals and checkpoint re-decomposition are all
+covered here without a GPU.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mpi_cuda_process_amd as m
+from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, init_field, reference)
+from mpi_cuda_process_amd.parallel.decomp import neighbors, owner, slab_bounds
+
+
+# ---- slab decomposition --------------------------------------------------------------------
+@pytest.mark.parametrize("nz,parts", [(10, 1), (10, 3), (7, 7), (1024, 8), (1025, 8), (13, 4)])
+def test_slab_bounds_cover_and_match_native(mdfx, nz, parts):
+    b = slab_bounds(nz, parts)
+    assert b[0][0] == 0 and b[-1][1] == nz
+    assert all(b[i][1] == b[i + 1][0] for i in range(parts - 1))
+    sizes = [e - s for s, e in b]
+    assert max(sizes) - min(sizes) <= 1
+    assert [tuple(x) for x in mdfx.native().slab_bounds(nz, parts)] == b
+    for z in range(nz):
+        p = owner(z, nz, parts)
+        assert b[p][0] <= z < b[p][1]
+
+
+def test_slab_bounds_errors():
+    with pytest.raises(ValueError):
+        slab_bounds(3, 4)
+    with pytest.raises(ValueError):
+        slab_bounds(3, 0)
+    assert neighbors(0, 3) == (-1, 1) and neighbors(2, 3) == (1, -1)
+
+
+def test_layout_pitch_alignment(mdfx):
+    for dt, es in (("f32", 4), ("f64", 8), ("u8", 1)):
+        d = mdfx.native().layout(100, 3, 10, 2, 5, 1, dt)
+        assert d["pitch"] * es % 256 == 0 and d["pitch"] >= 100
+        assert d["planes"] == 3 + 2 and d["plane"] == d["pitch"] * 3
+
+
+# ---- CPU oracle kernels vs plain PyTorch -----------------------------------------------------
+PROBS = [m.heat3d(nx=23, ny=17, nz=13), m.heat3d(nx=19, ny=11, nz=9, dtype="f64"),
+         m.box27(nx=21, ny=15, nz=11), m.box27(nx=12, ny=9, nz=8, dtype="f64"), m.mdf2d(h=29, w=31),
+         m.mdf2d(h=17, w=40, dtype="f64"), m.life2d(h=33, w=41)]
+
+
+def _ids(p):
+    return p.describe().replace(" ", "_")
+
+
+@pytest.mark.parametrize("prob", PROBS, ids=_ids)
+def test_cpu_kernel_vs_torch_reference(mdfx, prob):
+    lay = FieldLayout.make(prob)
+    a, b = alloc_field(lay), alloc_field(lay)
+    init_field(prob, lay, a)
+    apply_stencil(prob, lay, a, b)
+    u = a[lay.owned, :, : lay.nx]
+    got = b[lay.owned, :, : lay.nx]
+    ref = reference.step(prob.kind, u.double() if prob.dtype != "u8" else u, **prob.coef_kwargs())
+    if prob.dtype == "u8":
+        assert torch.equal(got, ref)
+    else:
+        assert (got.double() - ref).abs().max().item() < (2e-6 if prob.dtype == "f32" else 1e-13)
+
+
+def test_dirichlet_boundary_held(mdfx):
+    prob = m.mdf2d(h=16, w=16)
+    with m.Simulation(prob, device="cpu", ranks=2) as sim:
+        sim.init()
+        sim.run(25)
+        g = sim.gather()[:, 0, :]
+    assert (g[0] == 100).all() and (g[-1] == 100).all() and (g[:, 0] == 100).all() and (g[:, -1] == 100).all()
+    assert 0 < g[8, 8] < 100  # heat diffused into the interior (the reference never advanced: D1)
+
+
+def test_mdf_matches_reference_formula(mdfx):
+    """u' = u + 0.25 (E + W + N + S - 4u) with edges 100 / interior 0 (MDF_kernel.cu:20, :88-99)."""
+    prob = m.mdf2d(h=9, w=11)
+    with m.Simulation(prob, device="cpu") as sim:
+        sim.init()
+        u = sim.gather()[:, 0, :].astype(np.float64)
+        sim.run(1)
+        got = sim.gather()[:, 0, :]
+    want = u.copy()
+    want[1:-1, 1:-1] = u[1:-1, 1:-1] + 0.25 * (u[1:-1, 2:] + u[1:-1, :-2] + u[:-2, 1:-1] + u[2:, 1:-1]
+                                               - 4 * u[1:-1, 1:-1])
+    assert np.abs(got - want).max() < 1e-4
+
+
+def test_life_blinker_and_glider(mdfx):
+    prob = m.life2d(h=12, w=12)
+    board = np.zeros((12, 1, 12), np.uint8)
+    board[5, 0, 4:7] = 1  # blinker
+    with m.Simulation(prob, device="cpu", ranks=3) as sim:
+        sim.init(m.InitCondition(kind="constant", value=0))
+        for i in range(3):
+            lay = sim.layout(i)
+            sim.write_local(i, board[lay["z0"]:lay["z1"]])
+        sim.run(1)
+        g = sim.gather()[:, 0, :]
+        assert g[4:7, 5].tolist() == [1, 1, 1] and g.sum() == 3
+        sim.run(1)
+        g = sim.gather()[:, 0, :]
+        assert g[5, 4:7].tolist() == [1, 1, 1] and g.sum() == 3
+
+
+def test_life_compat_init_is_glibc_rand(mdfx):
+    import ctypes
+
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(1)
+    h, w = 6, 7
+    want = np.zeros((h, w), np.uint8)
+    for i in range(h):
+        for j in range(w):
+            if i in (0, h - 1) or j in (0, w - 1):
+                continue
+            rp = np.float32(libc.rand()) / np.float32(2147483647)
+            want[i, j] = 0 if rp > np.float32(0.15) else 1
+    got = mdfx.native().life_compat_init(h, w, 0.15, 1)
+    assert np.array_equal(got, want)
+
+
+# ---- engine invariants on the CPU backend ----------------------------------------------------
+@pytest.mark.parametrize("prob", PROBS, ids=_ids)
+def test_decomposition_invariance_cpu(mdfx, prob):
+    def run(p):
+        with m.Simulation(prob, device="cpu", ranks=p) as sim:
+            sim.init()
+            sim.run(5)
+            return sim.gather()
+
+    base = run(1)
+    for p in (2, 3, min(5, prob.nz)):
+        assert np.array_equal(base, run(p)), p
+
+
+def test_overlap_flag_and_sync_debug_equivalent(mdfx):
+    prob = m.heat3d(nx=20, ny=10, nz=12)
+    outs = []
+    for kw in (dict(overlap=True), dict(overlap=False), dict(sync_debug=True)):
+        with m.Simulation(prob, device="cpu", ranks=4, **kw) as sim:
+            sim.init()
+            sim.run(6)
+            outs.append(sim.gather())
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+
+
+def test_residual_cpu(mdfx):
+    prob = m.heat3d(nx=16, ny=12, nz=10)
+    with m.Simulation(prob, device="cpu", ranks=2, residual_every=2) as sim:
+        sim.init()
+        sim.run(1)
+        assert sim.residual < 0
+        a = sim.gather()
+        sim.run(1)
+        b = sim.gather()
+        assert sim.native.residual_step == 2
+        want = float(np.sqrt(((b.astype(np.float64) - a) ** 2).sum()))
+        assert abs(sim.residual - want) < 1e-9 * max(1, want)
+
+
+def test_residual_decreases_for_jacobi(mdfx):
+    prob = m.mdf2d(h=32, w=32)
+    with m.Simulation(prob, device="cpu", residual_every=10) as sim:
+        sim.init()
+        res = []
+        for _ in range(5):
+            sim.run(10)
+            res.append(sim.residual)
+    assert all(res[i + 1] < res[i] for i in range(4))
+
+
+def test_divergence_raises(mdfx):
+    prob = m.heat3d(nx=12, ny=12, nz=12, r=10.0)  # unstable explicit step
+    with m.Simulation(prob, device="cpu", residual_every=5) as sim:
+        sim.init(m.InitCondition(kind="random", lo=-1e30, hi=1e30))
+        with pytest.raises(RuntimeError, match="non-finite"):
+            sim.run(400)
+
+
+def test_checkpoint_roundtrip_redecompose(mdfx, tmp_path):
+    prob = m.box27(nx=14, ny=9, nz=15)
+    with m.Simulation(prob, device="cpu", ranks=1) as sim:
+        sim.init()
+        sim.run(7)
+        ref = sim.gather()
+    with m.Simulation(prob, device="cpu", ranks=3) as sim:
+        sim.init()
+        sim.run(4)
+        sim.save_checkpoint(str(tmp_path / "ck"))
+    hdr = json.load(open(os.path.join(tmp_path, "ck", "slab_1.json")))
+    assert hdr["step"] == 4 and hdr["nranks"] == 3 and hdr["format"] == "mdfx-slab-v1"
+    with m.Simulation(prob, device="cpu", ranks=4) as sim:
+        sim.load_checkpoint(str(tmp_path / "ck"))
+        sim.run(3)
+        assert np.array_equal(ref, sim.gather())
+
+
+def test_checkpoint_mismatch_rejected(mdfx, tmp_path):
+    with m.Simulation(m.heat3d(n=8), device="cpu") as sim:
+        sim.init()
+        sim.save_checkpoint(str(tmp_path / "ck"))
+    with m.Simulation(m.heat3d(n=9), device="cpu") as sim:
+        with pytest.raises(RuntimeError, match="does not match"):
+            sim.load_checkpoint(str(tmp_path / "ck"))
+
+
+def test_write_owned_refreshes_ghosts(mdfx):
+    prob = m.heat3d(nx=10, ny=8, nz=9)
+    rng = np.random.default_rng(0)
+    u = rng.random((9, 8, 10), dtype=np.float32)
+    with m.Simulation(prob, device="cpu", ranks=3) as sim:
+        sim.init(m.InitCondition(kind="constant", value=0))
+        for i in range(3):
+            lay = sim.layout(i)
+            sim.write_local(i, u[lay["z0"]:lay["z1"]])
+        sim.run(2)
+        got = sim.gather()
+    ref = reference.run("heat7", torch.from_numpy(u).double(), 2).numpy()
+    assert np.abs(got - ref).max() < 1e-5
+
+
+def test_bad_configs_rejected(mdfx):
+    with pytest.raises(ValueError):
+        m.Problem("life", 8, 1, 8, dtype="f32")
+    with pytest.raises(ValueError):
+        m.Problem("heat7", 8, 8, 8, dtype="u8")
+    with pytest.raises(RuntimeError):
+        m.Simulation(m.heat3d(n=4), device="cpu", ranks=5)  # more ranks than planes
+
+
+def test_kernel_region_outside_owned_rejected(mdfx):
+    prob = m.heat3d(nx=8, ny=8, nz=8)
+    lay = FieldLayout.make(prob)
+    a, b = alloc_field(lay), alloc_field(lay)
+    with pytest.raises(ValueError):
+        apply_stencil(prob, lay, a, b, 0, 3)

@@ -1,0 +1,110 @@
+"""Multi-process path on the CPU: one process per slab over torch.distributed (gloo), halo
+exchange through the torch p2p callback transport, max-over-ranks timing — the same engine code
+the GPU bench drives with RCCL. World size 2 and 3, rendezvous on 127.0.0.1.
+"""
+
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import numpy as np
+import torch.distributed as dist
+import mpi_cuda_process_amd as m
+from mpi_cuda_process_amd.parallel.dist import init_distributed
+env = init_distributed("gloo")
+prob = %(prob)s
+with m.Simulation(prob, device="cpu", distributed=True, transport="torch", residual_every=3) as sim:
+    sim.init()
+    sim.run(7)
+    g = sim.gather()
+    if env.rank == 0:
+        np.save(%(out)r, g)
+        json.dump({"residual": sim.residual, "transport": sim.transport, "nranks": sim.nranks},
+                  open(%(out)r + ".json", "w"))
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(world, prob_src, out):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", WORKER % dict(root=ROOT, prob=prob_src, out=out)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(o.decode())
+        assert p.returncode == 0, "\n".join(outs)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("prob_src", ["m.heat3d(nx=18, ny=10, nz=11)", "m.mdf2d(h=20, w=24)",
+                                      "m.life2d(h=19, w=30)"])
+def test_gloo_multiprocess_matches_single(mdfx, tmp_path, world, prob_src):
+    import mpi_cuda_process_amd as m
+
+    out = str(tmp_path / "g.npy")
+    _launch(world, prob_src, out)
+    got = np.load(out)
+    prob = eval(prob_src)
+    with m.Simulation(prob, device="cpu", residual_every=3) as sim:
+        sim.init()
+        sim.run(7)
+        ref = sim.gather()
+        ref_res = sim.residual
+    assert np.array_equal(got, ref)
+    import json
+
+    meta = json.load(open(out + ".json"))
+    assert meta["transport"] == "torch" and meta["nranks"] == world
+    assert abs(meta["residual"] - ref_res) < 1e-9 * max(1.0, ref_res)
+
+
+def test_bench_multiprocess_cpu_json(mdfx, tmp_path):
+    """bench.py under a 2-process launch on CPU prints ONE JSON line from rank 0."""
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu",
+                                       "--gpus", "2", "--n", "24", "--steps", "2", "--warmup", "1"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e.decode()
+    lines = [l for l in outs[0][0].decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and not [l for l in outs[1][0].decode().splitlines() if l.startswith("{")]
+    import json
+
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in rec
+    assert rec["steps"] == 2 and rec["value"] > 0 and rec["config"]["grid"] == [24, 24, 24]
