@@ -41,7 +41,7 @@ TESTS      := $(BIN)/mdfx_tests
 LINK_ROCM  := -L$(ROCM)/lib -lamdhip64 -lrccl -lgomp -lpthread -ldl
 
 .PHONY: all lib pymod apps tests clean
-all: lib pymod
+all: lib pymod apps tests
 
 lib: $(LIB)
 pymod: $(PYMOD)

@@ -1,0 +1,100 @@
+// Native unit tests (no framework dependency): slab math, layout, CPU oracle invariants,
+// decomposition invariance through the engine on the CPU backend, GPU engine when a device exists.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "mdfx/solver.hpp"
+
+using namespace mdfx;
+
+static int g_fail = 0;
+#define EXPECT(c)                                                        \
+  do {                                                                   \
+    if (!(c)) {                                                          \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c);  \
+      ++g_fail;                                                          \
+    }                                                                    \
+  } while (0)
+
+static void test_slab() {
+  for (int64_t nz : {7, 8, 1025, 33})
+    for (int p : {1, 2, 3, 7}) {
+      SlabDecomposition d(nz, p);
+      EXPECT(d.z0(0) == 0 && d.z1(p - 1) == nz);
+      for (int i = 0; i < p; ++i) {
+        EXPECT(d.size(i) >= nz / p && d.size(i) <= nz / p + 1);
+        for (int64_t z = d.z0(i); z < d.z1(i); ++z) EXPECT(d.owner(z) == i);
+      }
+    }
+  bool threw = false;
+  try {
+    SlabDecomposition d(3, 4);
+  } catch (const Error&) {
+    threw = true;
+  }
+  EXPECT(threw);
+}
+
+static void test_layout() {
+  FieldLayout l = FieldLayout::make(Extent3{100, 7, 20}, 5, 9, 1, DType::F32);
+  EXPECT(l.pitch == 128 && l.plane == 128 * 7 && l.planes() == 6);
+  EXPECT(l.lz(5) == 1 && l.gz(1) == 5);
+  FieldLayout d = FieldLayout::make(Extent3{100, 1, 20}, 0, 20, 1, DType::F64);
+  EXPECT(d.pitch * 8 % 256 == 0);
+}
+
+static std::vector<char> run_engine(StencilKind k, DType dt, Extent3 g, int P, int steps, bool gpu) {
+  StencilSpec s;
+  s.kind = k;
+  s.dtype = dt;
+  std::vector<int> ranks;
+  std::vector<std::unique_ptr<Backend>> bes;
+  for (int r = 0; r < P; ++r) {
+    ranks.push_back(r);
+    bes.push_back(gpu ? make_hip_backend(0) : make_cpu_backend());
+  }
+  Solver sol(s, g, P, ranks, std::move(bes), gpu ? make_loopback_transport() : make_host_transport());
+  InitSpec is;
+  is.kind = k == StencilKind::Life ? InitKind::LifeRandom : InitKind::Random;
+  sol.init(is);
+  sol.run(steps);
+  std::vector<char> out;
+  for (int i = 0; i < P; ++i) {
+    const FieldLayout& l = sol.layout(i);
+    std::vector<char> b((size_t)l.owned_cells() * l.esize());
+    sol.read_owned(i, b.data());
+    out.insert(out.end(), b.begin(), b.end());
+  }
+  return out;
+}
+
+static void test_invariance(bool gpu) {
+  struct C {
+    StencilKind k;
+    DType d;
+    Extent3 g;
+  } cs[] = {{StencilKind::Heat7, DType::F32, {20, 9, 11}},
+            {StencilKind::Box27, DType::F64, {13, 8, 9}},
+            {StencilKind::Jacobi5, DType::F32, {30, 1, 17}},
+            {StencilKind::Life, DType::U8, {40, 1, 21}}};
+  for (auto& c : cs) {
+    const auto base = run_engine(c.k, c.d, c.g, 1, 5, gpu);
+    for (int p : {2, 3, 4}) EXPECT(run_engine(c.k, c.d, c.g, p, 5, gpu) == base);
+    if (gpu) EXPECT(run_engine(c.k, c.d, c.g, 1, 5, false) == base);  // GPU == CPU oracle
+  }
+}
+
+int main() {
+  test_slab();
+  test_layout();
+  test_invariance(false);
+  if (hip_device_count() > 0) test_invariance(true);
+  if (g_fail) {
+    std::fprintf(stderr, "%d failure(s)\n", g_fail);
+    return 1;
+  }
+  std::printf("mdfx_tests: all passed%s\n", hip_device_count() > 0 ? " (cpu + gpu)" : " (cpu)");
+  return 0;
+}
