@@ -1,5 +1,9 @@
 // mdfx core: error helpers, enum names, layout and slab decomposition math.
+#include <csignal>
 #include <cstdarg>
+#include <cstdlib>
+#include <execinfo.h>
+#include <unistd.h>
 #include <cstdio>
 #include <string>
 
@@ -7,6 +11,29 @@
 #include "mdfx/grid.hpp"
 
 namespace mdfx {
+
+namespace {
+// MDFX_SEGV_BACKTRACE=1: print the native stack on a crash (host-side debugging on the GPU box,
+// where debuggers are not available).
+void segv_handler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "\n[mdfx] fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+struct SegvInstaller {
+  SegvInstaller() {
+    const char* v = std::getenv("MDFX_SEGV_BACKTRACE");
+    if (v && *v == '1') {
+      signal(SIGSEGV, segv_handler);
+      signal(SIGABRT, segv_handler);
+    }
+  }
+} g_segv_installer;
+}  // namespace
 
 void throw_error(const char* file, int line, const std::string& msg) {
   const char* base = file;

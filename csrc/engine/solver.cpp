@@ -316,7 +316,7 @@ void Solver::run_graph(int64_t pairs) {
     hipGraph_t g;
     HIPC(hipStreamEndCapture(origin, &g));
     hipGraphExec_t ex;
-    HIPC(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    HIPC(hipGraphInstantiateWithFlags(&ex, g, 0));
     HIPC(hipGraphDestroy(g));
     for (auto& e : fork) (void)hipEventDestroy(e);
     for (auto& e : join) (void)hipEventDestroy(e);

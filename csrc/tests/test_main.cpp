@@ -86,11 +86,51 @@ static void test_invariance(bool gpu) {
   }
 }
 
+static void test_graph() {
+  // eager vs hipGraph replay, loopback with 3 slabs on device 0
+  for (int P : {1, 3}) {
+    std::vector<std::vector<char>> outs;
+    for (bool graph : {false, true}) {
+      std::fprintf(stderr, "[graph probe] P=%d graph=%d: build\n", P, (int)graph);
+      StencilSpec s;
+      s.kind = StencilKind::Heat7;
+      std::vector<int> ranks;
+      std::vector<std::unique_ptr<Backend>> bes;
+      for (int r = 0; r < P; ++r) {
+        ranks.push_back(r);
+        bes.push_back(make_hip_backend(0));
+      }
+      SolverOptions o;
+      o.graph = graph;
+      Solver sol(s, Extent3{64, 16, 20}, P, ranks, std::move(bes), make_loopback_transport(), o);
+      InitSpec is;
+      sol.init(is);
+      std::fprintf(stderr, "[graph probe] run\n");
+      sol.run(6);
+      std::fprintf(stderr, "[graph probe] sync\n");
+      sol.synchronize();
+      std::vector<char> out;
+      for (int i = 0; i < P; ++i) {
+        const FieldLayout& l = sol.layout(i);
+        std::vector<char> b((size_t)l.owned_cells() * l.esize());
+        sol.read_owned(i, b.data());
+        out.insert(out.end(), b.begin(), b.end());
+      }
+      outs.push_back(out);
+      std::fprintf(stderr, "[graph probe] done\n");
+    }
+    EXPECT(outs[0] == outs[1]);
+  }
+}
+
 int main() {
   test_slab();
   test_layout();
   test_invariance(false);
-  if (hip_device_count() > 0) test_invariance(true);
+  if (hip_device_count() > 0) {
+    test_invariance(true);
+    test_graph();
+  }
   if (g_fail) {
     std::fprintf(stderr, "%d failure(s)\n", g_fail);
     return 1;

@@ -7,13 +7,14 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 step() { local t=$1; shift; echo "== $* (limit ${t}s)"; timeout -k 10 "$t" "$@"; local rc=$?; echo "== rc=$rc"; return $rc; }
 MODE=${1:-all}
-if [[ $MODE == all || $MODE == test ]]; then
-  step 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -50 gpurun_out/pytest_gpu.log; exit 1; }
-  tail -5 gpurun_out/pytest_gpu.log
-fi
+export MDFX_SEGV_BACKTRACE=1
 if [[ $MODE == all || $MODE == native ]]; then
   step 300 ./build/bin/mdfx_tests || exit 1
   step 300 ./build/bin/mdfx --stencil 7 --n 512 --steps 20 --warmup 5 --residual-every 10 || exit 1
+fi
+if [[ $MODE == all || $MODE == test ]]; then
+  step 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -50 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -5 gpurun_out/pytest_gpu.log
 fi
 if [[ $MODE == all || $MODE == smoke ]]; then
   step 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
