@@ -28,8 +28,13 @@ struct SegvInstaller {
   SegvInstaller() {
     const char* v = std::getenv("MDFX_SEGV_BACKTRACE");
     if (v && *v == '1') {
-      signal(SIGSEGV, segv_handler);
-      signal(SIGABRT, segv_handler);
+      void* warm[4];
+      (void)backtrace(warm, 4);  // load the unwinder now, not inside the handler
+      struct sigaction sa {};
+      sa.sa_handler = segv_handler;
+      sa.sa_flags = SA_RESETHAND | SA_NODEFER;
+      sigaction(SIGSEGV, &sa, nullptr);
+      sigaction(SIGABRT, &sa, nullptr);
     }
   }
 } g_segv_installer;

@@ -6,6 +6,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -239,8 +240,12 @@ void Solver::run(int64_t steps) {
   while (done < steps) {
     const int64_t k = stats_.steps + 1;
     const bool res = opt_.residual_every > 0 && (k % opt_.residual_every == 0);
-    // graph replay for plain (non-residual, non-debug) stretches of >= 2 steps
-    if (opt_.graph && hip && !res && !opt_.sync_debug) {
+    // graph replay for plain (non-residual, non-debug) stretches of >= 2 steps. Restricted to one
+    // slab per process (the production layout: one rank per GPU): the ROCm 7.0 HIP runtime that
+    // PyTorch bundles crashes in hipStreamEndCapture on the multi-slab loopback capture (the same
+    // capture replays correctly under ROCm 7.2: csrc/tests/test_main.cpp test_graph), so several
+    // slabs in one process always run eagerly.
+    if (opt_.graph && hip && !res && !opt_.sync_debug && slabs_.size() == 1) {
       int64_t plain = steps - done;
       if (opt_.residual_every > 0) {
         const int64_t next_res = ((stats_.steps / opt_.residual_every) + 1) * opt_.residual_every;
@@ -270,8 +275,21 @@ void Solver::destroy_graph() {
   graph_parity_ = -1;
 }
 
+static bool graph_debug() {
+  static const bool on = [] {
+    const char* v = std::getenv("MDFX_DEBUG_GRAPH");
+    return v && *v == '1';
+  }();
+  return on;
+}
+#define GDBG(msg)                                                 \
+  do {                                                            \
+    if (graph_debug()) std::fprintf(stderr, "[mdfx graph] %s\n", msg); \
+  } while (0)
+
 void Solver::run_graph(int64_t pairs) {
   if (!graph_exec_ || graph_parity_ != cur_) {
+    GDBG("capture begin");
     destroy_graph();
     Slab& o = slabs_[0];
     o.be->activate();
@@ -296,8 +314,10 @@ void Solver::run_graph(int64_t pairs) {
       s.be->record(s.ev_int, s.cs);
     }
     const int64_t saved = stats_.steps;
+    GDBG("capture: steps");
     step(false);
     step(false);
+    GDBG("capture: join");
     stats_.steps = saved;  // replay accounts for them
     k = 0;
     for (auto& s : slabs_) {
@@ -314,7 +334,9 @@ void Solver::run_graph(int64_t pairs) {
     }
     o.be->activate();
     hipGraph_t g;
+    GDBG("capture: end");
     HIPC(hipStreamEndCapture(origin, &g));
+    GDBG("instantiate");
     hipGraphExec_t ex;
     HIPC(hipGraphInstantiateWithFlags(&ex, g, 0));
     HIPC(hipGraphDestroy(g));
@@ -322,7 +344,9 @@ void Solver::run_graph(int64_t pairs) {
     for (auto& e : join) (void)hipEventDestroy(e);
     graph_exec_ = ex;
     graph_parity_ = cur_;  // step() x2 leaves cur_ unchanged
+    GDBG("instantiated");
   }
+  GDBG("launch");
   Slab& o = slabs_[0];
   o.be->activate();
   for (int64_t i = 0; i < pairs; ++i) HIPC(hipGraphLaunch((hipGraphExec_t)graph_exec_, (hipStream_t)o.hs));
@@ -340,6 +364,7 @@ void Solver::run_graph(int64_t pairs) {
     s.be->record(s.ev_int, s.cs);
   }
   stats_.steps += 2 * pairs;
+  GDBG("replayed");
 }
 
 // ---- host I/O ----------------------------------------------------------------------------------
