@@ -23,3 +23,8 @@ if [[ $MODE == all || $MODE == bench ]]; then
   step 300 python bench.py > gpurun_out/bench_n1.json 2> gpurun_out/bench_n1.err || { cat gpurun_out/bench_n1.err; exit 1; }
   cat gpurun_out/bench_n1.json
 fi
+if [[ $MODE == all || $MODE == profile ]]; then
+  R=$(pwd)
+  (cd /tmp && export TMPDIR=/tmp && step 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python "$R/bench.py" --steps 20 --warmup 5 > "$R/gpurun_out/prof_bench.log" 2>&1) || { tail -20 gpurun_out/prof_bench.log; exit 1; }
+  find gpurun_out/prof -name "*stats*" | head
+fi
