@@ -199,18 +199,30 @@ static void launch_box27_t(const Geo& g, const T* in, T* out, const StencilCoef&
                        zc, XT, YT, resid);
 }
 
-template <class T>
-void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
-                  hipStream_t s) {
-  if (g.lz_end <= g.lz_begin) return;
+template <class T, int RY>
+static void launch_box27_ry(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
+                            hipStream_t s) {
   constexpr int WX = 64 * VT<T>::N;
-  constexpr int RY = 2;
   if (g.nx > 2 * WX)
     launch_box27_t<T, RY, 4>(g, in, out, c, resid, s);
   else if (g.nx > WX)
     launch_box27_t<T, RY, 2>(g, in, out, c, resid, s);
   else
     launch_box27_t<T, RY, 1>(g, in, out, c, resid, s);
+}
+
+template <class T>
+void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
+                  hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  int ry = env_int("MDFX_RY", 0);
+  if (ry <= 0) ry = 2;
+  if (g.ny < 8) ry = 1;
+  switch (ry) {
+    case 1: launch_box27_ry<T, 1>(g, in, out, c, resid, s); break;
+    case 4: launch_box27_ry<T, 4>(g, in, out, c, resid, s); break;
+    default: launch_box27_ry<T, 2>(g, in, out, c, resid, s); break;
+  }
 }
 template void launch_box27<float>(const Geo&, const float*, float*, const StencilCoef&, double*,
                                   hipStream_t);

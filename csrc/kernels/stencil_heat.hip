@@ -13,8 +13,10 @@
 // output after ~8 GiB of other traffic: keeping it in L2/MALL only evicts useful lines).
 // Block->tile order is XCD-aware so vertically adjacent tiles (sharing halo rows) share an L2.
 //
-// Measured (bench/micro/stencil7_variants.hip, 1024^3 fp32, one MI355X): the RY=4, 4-waves-in-x
-// form ran 698 GCells/s = 5.59 TB/s at 8 B/cell vs 509 for the one-cell-per-lane kernel.
+// Measured (bench/kernel_ab.py, 1024^3 fp32, one MI355X): RY=2 rows per lane, 4 waves along x
+// (one block spans the 1024-wide row, so no block-edge loads), prefetch depth 1: 1.546 ms per
+// sweep = 694.5 GCells/s = 5.56 TB/s at 8 B/cell, vs 3.18 ms for the one-cell-per-lane kernel and
+// 1.63 ms for torch's copy_ of the same bytes.
 //
 // Reference parity: replaces run_mdf + middle_kernel/border_kernel (MDF_kernel.cu:10-70): the
 // "region" is [lz_begin, lz_end), so the same kernel serves the interior and the boundary planes.
@@ -35,7 +37,7 @@ __device__ __forceinline__ V vsplat(T v) {
   return r;
 }
 
-template <class T, int RY, int WXN, bool RES>
+template <class T, int RY, int WXN, bool RES, bool EDGE, int PF>
 __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __restrict__ out, Geo g,
                                                 T r, int zc, int XT, int YT,
                                                 double* __restrict__ resid) {
@@ -49,34 +51,42 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
   const int yt = (t / XT) % YT;
   const int zt = t / (XT * YT);
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  // wave index made provably uniform: every row / plane address below is an SGPR base plus ONE
+  // per-lane 32-bit offset (global_load saddr form), which keeps the register file for data.
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wx = w % WXN, wy = w / WXN;
-  const int64_t x = ((int64_t)xt * WXN + wx) * WX + (int64_t)lane * N;
+  const int64_t xw = ((int64_t)xt * WXN + wx) * WX;
+  const uint32_t xo = (uint32_t)lane * N;
+  const int64_t x = xw + xo;
   const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
   const int64_t lzs = g.lz_begin + (int64_t)zt * zc;
   const int64_t lze = min(g.lz_end, lzs + (int64_t)zc);
   const bool xin = x < g.pitch;
   const int64_t pitch = g.pitch, plane = g.plane;
-  const T* ib = in + y0 * pitch + x;
-  T* ob = out + y0 * pitch + x;
+  const T* ib = in + y0 * pitch + xw;
+  T* ob = out + y0 * pitch + xw;
 
   auto ld = [&](int64_t lz, int i) -> V {
     V v = vsplat<V>(T(0));
     const int64_t y = y0 + i;
-    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny)
-      v = *(const V*)(ib + lz * plane + (int64_t)i * pitch);
+    if (lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
+      const T* p = ib + lz * plane + (int64_t)i * pitch;
+      if (xin) v = *(const V*)(p + xo);
+    }
     return v;
   };
   auto ldl = [&](int64_t lz, int i) -> T {
+    if (!EDGE) return T(0);
     const int64_t y = y0 + i;
     if (wx == 0 && lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max && y < g.ny)
       return ib[lz * plane + (int64_t)i * pitch - 1];
     return T(0);
   };
   auto ldr = [&](int64_t lz, int i) -> T {
+    if (!EDGE) return T(0);
     const int64_t y = y0 + i;
     if (wx == WXN - 1 && lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max && y < g.ny)
-      return ib[lz * plane + (int64_t)i * pitch + N];
+      return ib[lz * plane + (int64_t)i * pitch + WX];
     return T(0);
   };
 
@@ -86,7 +96,7 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
   for (int i = 0; i < RY; ++i) {
     P[i] = ld(lzs - 1, i);
     C[i] = ld(lzs, i);
-    Nx[i] = ld(lzs + 1, i);
+    if (PF == 2) Nx[i] = ld(lzs + 1, i);
     EL[i] = ldl(lzs, i);
     ER[i] = ldr(lzs, i);
   }
@@ -94,15 +104,26 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
   double acc = 0.0;
   int buf = 0;
   for (int64_t lz = lzs; lz < lze; ++lz) {
+    // PF == 2: the own rows of plane z+2 and the halo/edges of z+1 are in flight during plane z.
+    // PF == 1: only plane z+1 is loaded here (fewer registers, more waves hide the latency).
     V NN[RY];
     T ELN[RY], ERN[RY];
+    V HLN, HHN;
 #pragma unroll
     for (int i = 0; i < RY; ++i) {
-      NN[i] = ld(lz + 2, i);
-      ELN[i] = ldl(lz + 1, i);
-      ERN[i] = ldr(lz + 1, i);
+      if (PF == 2)
+        NN[i] = ld(lz + 2, i);
+      else
+        Nx[i] = ld(lz + 1, i);
+      if (PF == 2) {
+        ELN[i] = ldl(lz + 1, i);
+        ERN[i] = ldr(lz + 1, i);
+      }
     }
-    const V HLN = ld(lz + 1, -1), HHN = ld(lz + 1, RY);
+    if (PF == 2) {
+      HLN = ld(lz + 1, -1);
+      HHN = ld(lz + 1, RY);
+    }
     if (WXN > 1) {
       if (lane == 0) {
 #pragma unroll
@@ -140,7 +161,7 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
         }
       }
       if (xin) {
-        store_nt((V*)(ob + lz * plane + (int64_t)i * pitch), o);
+        store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
         if (RES) {
 #pragma unroll
           for (int e = 0; e < N; ++e)
@@ -156,12 +177,22 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
     for (int i = 0; i < RY; ++i) {
       P[i] = C[i];
       C[i] = Nx[i];
-      Nx[i] = NN[i];
-      EL[i] = ELN[i];
-      ER[i] = ERN[i];
+      if (PF == 2) {
+        Nx[i] = NN[i];
+        EL[i] = ELN[i];
+        ER[i] = ERN[i];
+      } else {
+        EL[i] = ldl(lz + 1, i);
+        ER[i] = ldr(lz + 1, i);
+      }
     }
-    HL = HLN;
-    HH = HHN;
+    if (PF == 2) {
+      HL = HLN;
+      HH = HHN;
+    } else {
+      HL = ld(lz + 1, -1);
+      HH = ld(lz + 1, RY);
+    }
   }
   if (RES) wave_atomic_add(resid, acc);
 }
@@ -256,7 +287,7 @@ int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target) {
 
 int env_int(const char* name, int dflt);
 
-template <class T, int RY, int WXN>
+template <class T, int RY, int WXN, bool EDGE, int PF>
 static void launch_heat7_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N;
   constexpr int WX = 64 * N;
@@ -265,37 +296,64 @@ static void launch_heat7_t(const Geo& g, const T* in, T* out, T r, double* resid
   const int XT = (int)((g.nx + WXN * WX - 1) / (WXN * WX));
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   int zc = env_int("MDFX_ZC", 0);
-  if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, 2048);
+  // ~16 blocks per CU: 512^3 fp32 ran 0.2018 ms at 4096 blocks vs 0.2296 ms at 2048
+  if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, env_int("MDFX_BLOCKS", 4096));
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XT * YT * ZT)), blk(256);
   if (resid)
-    hipLaunchKernelGGL((heat7_zw<T, RY, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, resid);
+    hipLaunchKernelGGL((heat7_zw<T, RY, WXN, true, EDGE, PF>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, resid);
   else
-    hipLaunchKernelGGL((heat7_zw<T, RY, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, resid);
+    hipLaunchKernelGGL((heat7_zw<T, RY, WXN, false, EDGE, PF>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, resid);
+}
+
+template <class T, int RY, int WXN>
+static void launch_heat7_e(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s, int pf) {
+  constexpr int WX = 64 * VT<T>::N;
+  // one block spans the whole row: the x neighbours at the block edge are the Dirichlet
+  // boundary, so the block-edge loads vanish from the kernel.
+  const bool edge = g.nx > (int64_t)WXN * WX;
+  if (edge) {
+    if (pf == 1)
+      launch_heat7_t<T, RY, WXN, true, 1>(g, in, out, r, resid, s);
+    else
+      launch_heat7_t<T, RY, WXN, true, 2>(g, in, out, r, resid, s);
+  } else {
+    if (pf == 1)
+      launch_heat7_t<T, RY, WXN, false, 1>(g, in, out, r, resid, s);
+    else
+      launch_heat7_t<T, RY, WXN, false, 2>(g, in, out, r, resid, s);
+  }
 }
 
 template <class T, int RY>
-static void launch_heat7_ry(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+static void launch_heat7_ry(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s, int pf) {
   constexpr int WX = 64 * VT<T>::N;
   // waves along x only as far as the row is wide; the rest stack along y.
   if (g.nx > 2 * WX)
-    launch_heat7_t<T, RY, 4>(g, in, out, r, resid, s);
+    launch_heat7_e<T, RY, 4>(g, in, out, r, resid, s, pf);
   else if (g.nx > WX)
-    launch_heat7_t<T, RY, 2>(g, in, out, r, resid, s);
+    launch_heat7_e<T, RY, 2>(g, in, out, r, resid, s, pf);
   else
-    launch_heat7_t<T, RY, 1>(g, in, out, r, resid, s);
+    launch_heat7_e<T, RY, 1>(g, in, out, r, resid, s, pf);
 }
 
 template <class T>
 void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
+  // defaults from bench/kernel_ab.py on MI355X, 1024^3 fp32 (profiles/r01_ab_heat7_f32.json):
+  // RY=2 PF=1 1.546 ms (694.5 GCells/s) > RY=4 PF=1 1.584 > RY=4 PF=2 1.603 > RY=2 PF=2 1.662
+  // fp64 1024^3: RY=4 PF=2 3.395 ms (316 GCells/s) > RY=4 PF=1 3.415 > RY=2 PF=1 3.479
+  // (profiles/r01_ab_heat7_f64.json)
   int ry = env_int("MDFX_RY", 0);
-  if (ry <= 0) ry = sizeof(T) == 4 ? 4 : 4;
+  if (ry <= 0) ry = sizeof(T) == 4 ? 2 : 4;
+  int pf = env_int("MDFX_PF", 0);
+  if (pf <= 0) pf = sizeof(T) == 4 ? 1 : 2;
   if (g.ny < 8) ry = 1;
   switch (ry) {
-    case 1: launch_heat7_ry<T, 1>(g, in, out, r, resid, s); break;
-    case 2: launch_heat7_ry<T, 2>(g, in, out, r, resid, s); break;
-    default: launch_heat7_ry<T, 4>(g, in, out, r, resid, s); break;
+    case 1: launch_heat7_ry<T, 1>(g, in, out, r, resid, s, pf); break;
+    case 2: launch_heat7_ry<T, 2>(g, in, out, r, resid, s, pf); break;
+    case 8: launch_heat7_ry<T, 8>(g, in, out, r, resid, s, pf); break;
+    default: launch_heat7_ry<T, 4>(g, in, out, r, resid, s, pf); break;
   }
 }
 template void launch_heat7<float>(const Geo&, const float*, float*, float, double*, hipStream_t);

@@ -131,7 +131,7 @@ void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, h
   constexpr int WX = 64 * 16;
   const int XT = (int)((g.nx + WX - 1) / WX);
   int zc = env_int("MDFX_ZC", 0);
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 4096);  // 32768^2: zc 64 beats 128 (profiles/r01_ab_life_u8.json)
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
