@@ -9,8 +9,11 @@ slab-decomposed over N MI355X GPUs (one process per GPU, RCCL halo exchange over
 The grid is fixed as N grows (strong scaling, the BASELINE.json config "3D 7-pt Jacobi 1024^3 fp32
 slab-decomposed across 8xMI355X"). Data is synthetic: a uniform random initial grid generated on
 the device from a counter-based hash of the global cell index (seed 1). Every timed step is a full
-Jacobi sweep of every cell (boundary planes + halo exchange + interior), nothing is skipped or
-cached. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
+Jacobi update of every cell (boundary planes + halo exchange + interior), nothing is skipped or
+cached. By default two consecutive Jacobi steps are fused into one pass over memory (temporal
+blocking, --temporal 2; bitwise identical to two single steps, tests/test_gpu_temporal.py): every
+step is still computed in full, the fused kernel just keeps u^{t+1} on chip. --temporal 1 measures
+one sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
 torch.cuda.synchronize() on both sides; the slowest rank's time is reported. GCells/s =
 nx*ny*nz*K / t / 1e9 for the whole job. Rank 0 prints one JSON line.
 """
@@ -47,6 +50,9 @@ def parse():
     p.add_argument("--virtual-ranks", type=int, default=0,
                    help="split the grid into P slabs inside ONE process (loopback transport)")
     p.add_argument("--graph", action="store_true", help="replay 2-step cycles as hipGraphs")
+    p.add_argument("--temporal", type=int, default=0,
+                   help="time steps fused per memory sweep (temporal blocking); 0 = 2 where a fused "
+                        "kernel exists (3D 7-pt, row <= one block), else 1")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
@@ -81,8 +87,14 @@ def main():
     else:
         prob = life2d(h=nz, w=nx)
 
+    temporal = a.temporal
+    if temporal <= 0:
+        temporal = 1
+        if a.stencil == "heat7" and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx,
+                                                                              prob.ny, prob.nz, 2, 2)):
+            temporal = 2
     kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap, graph=a.graph,
-              residual_every=a.residual_every, timeout_s=900.0 if hip else 0.0)
+              residual_every=a.residual_every, timeout_s=900.0 if hip else 0.0, temporal=temporal)
     if env:
         sim = Simulation(prob, distributed=True, transport=a.transport, **kw)
     else:
@@ -153,6 +165,7 @@ def main():
                 "kernel_variant": native().kernel_variant(),
                 "graph": a.graph,
                 "overlap": not a.no_overlap,
+                "temporal_block": temporal,
             },
             "per_gpu_gcells": round(gcells / max(nproc, 1), 3),
             "effective_hbm_TBps_per_gpu": round(gcells * bpc / 1e3 / max(nproc, 1), 3),

@@ -23,18 +23,21 @@ import mpi_cuda_process_amd as m  # noqa: E402
 from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, init_field,  # noqa: E402
                                       set_kernel_variant)
 
-KEYS = {"RY": "MDFX_RY", "PF": "MDFX_PF", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS"}
+KEYS = {"RY": "MDFX_RY", "PF": "MDFX_PF", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
+        "TBPF": "MDFX_TB_PF"}
 
 
 def parse_variant(s):
-    fam, env = "tuned", {}
+    fam, env, steps = "tuned", {}, 1
     for part in filter(None, s.split(",")):
         k, v = part.split("=")
         if k == "FAM":
             fam = v
+        elif k == "STEPS":
+            steps = int(v)
         else:
             env[KEYS[k]] = v
-    return fam, env
+    return fam, env, steps
 
 
 def apply_env(env):
@@ -65,25 +68,37 @@ def main():
         prob = m.mdf2d(h=nz, w=nx, dtype=a.dtype)
     else:
         prob = m.life2d(h=nz, w=nx)
-    lay = FieldLayout.make(prob)
+    variants = [v for v in a.variants.split(";") if v]
+    max_steps = max(parse_variant(v)[2] for v in variants)
+    lay = FieldLayout.make(prob, halo=max_steps)
     A = alloc_field(lay, "cuda")
     B = alloc_field(lay, "cuda")
     R = alloc_field(lay, "cuda")
     init_field(prob, lay, A)
     init_field(prob, lay, B)
     set_kernel_variant("naive")
+    refs = {1: R}
     apply_stencil(prob, lay, A, R)
+    if max_steps > 1:  # k naive single steps; the fused sweep must match them bitwise
+        R2 = alloc_field(lay, "cuda")
+        cur = R
+        for k in range(2, max_steps + 1):
+            nxt = alloc_field(lay, "cuda")
+            nxt.copy_(cur)
+            apply_stencil(prob, lay, cur, nxt)
+            refs[k] = nxt
+            cur = nxt
+        del R2
     torch.cuda.synchronize()
-    variants = [v for v in a.variants.split(";") if v]
     ok = {}
     for v in variants:
-        fam, env = parse_variant(v)
+        fam, env, steps = parse_variant(v)
         apply_env(env)
         set_kernel_variant(fam)
         B.zero_()
-        apply_stencil(prob, lay, A, B)
+        apply_stencil(prob, lay, A, B, steps=steps)
         torch.cuda.synchronize()
-        ok[v] = bool(torch.equal(B[lay.owned, :, :nx], R[lay.owned, :, :nx]))
+        ok[v] = bool(torch.equal(B[lay.owned, :, :nx], refs[steps][lay.owned, :, :nx]))
     # copy roof with the same bytes (one read + one write of the field)
     times = {v: [] for v in variants}
     copy_t = []
@@ -97,16 +112,16 @@ def main():
         copy_t.append(e0.elapsed_time(e1) / a.iters)
         init_field(prob, lay, A)
         for v in variants:
-            fam, env = parse_variant(v)
+            fam, env, steps = parse_variant(v)
             apply_env(env)
             set_kernel_variant(fam)
-            apply_stencil(prob, lay, A, B)
+            apply_stencil(prob, lay, A, B, steps=steps)
             e0.record()
             for i in range(a.iters):
-                apply_stencil(prob, lay, A if i % 2 == 0 else B, B if i % 2 == 0 else A)
+                apply_stencil(prob, lay, A if i % 2 == 0 else B, B if i % 2 == 0 else A, steps=steps)
             e1.record()
             torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1) / a.iters)
+            times[v].append(e0.elapsed_time(e1) / a.iters / steps)  # per time step
     set_kernel_variant("auto")
     apply_env({})
     cells = prob.cells
@@ -114,6 +129,7 @@ def main():
     cbest = min(copy_t)
     out = {"problem": prob.describe(), "copy_ms": cbest, "copy_TBps": lay.planes * lay.plane * (bpc // 2) * 2 / cbest / 1e9,
            "variants": []}
+    print("(times are per time step; fused variants divide the sweep time by STEPS)")
     print("%-28s %9s %9s %10s %8s %s" % ("variant", "best ms", "med ms", "GCells/s", "%copy", "bitwise"))
     print("%-28s %9.4f %9s %10.1f %8s" % ("torch copy_ (roof)", cbest, "", cells / cbest / 1e6, "100"))
     for v in variants:

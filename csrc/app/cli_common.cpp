@@ -36,6 +36,7 @@ struct Opts {
   int64_t ckpt_every = 0;
   std::string ckpt_dir = "mdfx_ckpt", resume;
   bool compat = false;
+  int temporal = 1;
 };
 
 void usage(const char* prog) {
@@ -57,7 +58,8 @@ void usage(const char* prog) {
       "  --checkpoint-every K --checkpoint-dir D ; --resume D\n"
       "  --print                   dump the final grid like the reference's print_array\n"
       "  --json                    one JSON metrics line ; --verbose per-rank detail ; --quiet\n"
-      "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n",
+      "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n"
+      "  --temporal 1|2            time steps fused per memory sweep (2: 3D 7-pt, rows <= one block)\n",
       prog);
 }
 
@@ -113,6 +115,7 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--variant") o.variant = need(i);
     else if (a == "--timeout") o.timeout = std::atof(need(i));
     else if (a == "--compat") o.compat = true;
+    else if (a == "--temporal") o.temporal = std::atoi(need(i));
     else MDFX_FAIL("unknown option " + a + " (try --help)");
   }
   return o;
@@ -255,6 +258,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     so.residual_every = o.residual_every;
     so.graph = o.graph;
     so.timeout_s = o.timeout;
+    so.temporal = o.temporal;
     Solver solver(spec, g, nranks, local_ranks, std::move(bes), std::move(tr), so);
 
     // ---- initial condition ----------------------------------------------------------------

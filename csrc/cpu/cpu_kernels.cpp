@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "mdfx/kernels.hpp"
 #include "mdfx/stencil_math.hpp"
@@ -140,10 +141,37 @@ void life_cpu(const uint8_t* in, uint8_t* out, const Pl& g, int64_t lb, int64_t 
 
 }  // namespace
 
+static void cpu_region(const StencilSpec& spec, const RegionArgs& a);
+
 void cpu_stencil(const StencilSpec& spec, const RegionArgs& a) {
   if (a.lz_end <= a.lz_begin) return;
   MDFX_CHECK(a.lz_begin >= a.lay.halo && a.lz_end <= a.lay.halo + a.lay.nzl(),
              "region must lie inside the owned planes");
+  if (a.steps == 1) {
+    cpu_region(spec, a);
+    return;
+  }
+  // fused k-step sweep = k single steps through a scratch copy, widening the first steps by the
+  // planes the later ones read (the device kernel computes exactly these values on chip)
+  const int k = a.steps;
+  MDFX_CHECK(k >= 1 && a.lay.halo >= k, "fused steps need halo >= steps");
+  std::vector<char> tmp[2];
+  tmp[0].assign(a.lay.bytes(), 0);
+  tmp[1].assign(a.lay.bytes(), 0);
+  std::memcpy(tmp[0].data(), a.in, a.lay.bytes());
+  for (int s = 1; s <= k; ++s) {
+    RegionArgs b = a;
+    b.in = tmp[(s - 1) & 1].data();
+    b.out = s == k ? a.out : (void*)tmp[s & 1].data();
+    b.lz_begin = a.lz_begin - (k - s);
+    b.lz_end = a.lz_end + (k - s);
+    b.resid = s == k ? a.resid : nullptr;
+    if (s < k) std::memcpy(tmp[s & 1].data(), tmp[(s - 1) & 1].data(), a.lay.bytes());
+    cpu_region(spec, b);
+  }
+}
+
+static void cpu_region(const StencilSpec& spec, const RegionArgs& a) {
   const Pl g = pl_of(a.lay);
   switch (spec.kind) {
     case StencilKind::Heat7:

@@ -36,7 +36,8 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   if (spec_.kind == StencilKind::Life) MDFX_CHECK(spec_.dtype == DType::U8, "life cells are u8");
   if (spec_.kind != StencilKind::Life)
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
-  const int halo = 1;
+  MDFX_CHECK(opt_.temporal == 1 || opt_.temporal == 2, "temporal blocking depth must be 1 or 2");
+  const int halo = opt_.temporal;
   for (size_t i = 0; i < local_ranks.size(); ++i) {
     const int r = local_ranks[i];
     MDFX_CHECK(r >= 0 && r < nranks, format("local rank %d outside [0,%d)", r, nranks));
@@ -55,13 +56,20 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.ev_bnd = s.be->create_event();
     s.ev_int = s.be->create_event();
     s.resid = (double*)s.be->alloc(2 * sizeof(double));
-    // regions (storage planes); owned = [halo, halo + nzl)
+    if (opt_.temporal > 1 && s.be->kind() == DeviceKind::HIP)
+      MDFX_CHECK(hip_supports_steps(spec_, s.lay, opt_.temporal),
+                 format("no fused %d-step kernel for %s %s with nx=%lld (temporal blocking needs heat7 and a row "
+                        "one block wide: nx <= 1024 fp32 / 512 fp64)",
+                        opt_.temporal, stencil_name(spec_.kind), dtype_name(spec_.dtype), (long long)global_.nx));
+    // regions (storage planes); owned = [halo, halo + nzl). The boundary regions are the `halo`
+    // planes at each end that the exchange sends: they are computed on the halo stream so the
+    // exchange can follow them in stream order; everything else is interior.
     const int64_t ob = halo, oe = halo + s.lay.nzl();
     const bool has_lo = r > 0, has_hi = r + 1 < nranks;
     s.lo_b = ob;
-    s.lo_e = has_lo ? ob + 1 : ob;
+    s.lo_e = has_lo ? std::min(ob + halo, oe) : ob;
     s.hi_e = oe;
-    s.hi_b = has_hi ? std::max(oe - 1, s.lo_e) : oe;
+    s.hi_b = has_hi ? std::max(oe - halo, s.lo_e) : oe;
     s.in_b = s.lo_e;
     s.in_e = s.hi_b;
     slabs_.push_back(std::move(s));
@@ -164,7 +172,7 @@ void Solver::exchange_ghosts() {
   ghosts_dirty_ = false;
 }
 
-void Solver::step(bool want_resid) {
+void Solver::step(bool want_resid, int k) {
   const int nb = 1 - cur_;
   for (auto& s : slabs_) {
     s.be->activate();
@@ -173,6 +181,7 @@ void Solver::step(bool want_resid) {
     a.in = s.buf[cur_];
     a.out = s.buf[nb];
     a.lay = s.lay;
+    a.steps = k;
     if (want_resid) {
       s.be->memset(s.resid, 0, sizeof(double), s.hs);
       s.be->memset(s.resid + 1, 0, sizeof(double), opt_.overlap ? s.cs : s.hs);
@@ -210,7 +219,7 @@ void Solver::step(bool want_resid) {
   if (!slabs_.empty()) slabs_[0].be->trace_pop();
   if (opt_.sync_debug) sync_all();
   cur_ = nb;
-  ++stats_.steps;
+  stats_.steps += k;
   if (want_resid) finish_residual();
 }
 
@@ -236,30 +245,32 @@ void Solver::run(int64_t steps) {
   if (ghosts_dirty_) exchange_ghosts();
   transport_->check();
   const bool hip = slabs_[0].be->kind() == DeviceKind::HIP;
+  const int T = opt_.temporal;
   int64_t done = 0;
   while (done < steps) {
-    const int64_t k = stats_.steps + 1;
-    const bool res = opt_.residual_every > 0 && (k % opt_.residual_every == 0);
-    // graph replay for plain (non-residual, non-debug) stretches of >= 2 steps. Restricted to one
+    // time steps until the next residual evaluation (inclusive), unbounded if none
+    int64_t to_res = steps - done + 1;
+    if (opt_.residual_every > 0)
+      to_res = ((stats_.steps / opt_.residual_every) + 1) * opt_.residual_every - stats_.steps;
+    // a fused sweep may not jump over a residual step: shorter stretches use single steps
+    const int k = (T > 1 && steps - done >= T && to_res >= T) ? T : 1;
+    const bool res = (to_res == k);
+    // graph replay for plain (non-residual, non-debug) stretches of >= 2 sweeps. Restricted to one
     // slab per process (the production layout: one rank per GPU): the ROCm 7.0 HIP runtime that
     // PyTorch bundles crashes in hipStreamEndCapture on the multi-slab loopback capture (the same
     // capture replays correctly under ROCm 7.2: csrc/tests/test_main.cpp test_graph), so several
     // slabs in one process always run eagerly.
     if (opt_.graph && hip && !res && !opt_.sync_debug && slabs_.size() == 1) {
-      int64_t plain = steps - done;
-      if (opt_.residual_every > 0) {
-        const int64_t next_res = ((stats_.steps / opt_.residual_every) + 1) * opt_.residual_every;
-        plain = std::min<int64_t>(plain, next_res - stats_.steps - 1);
-      }
-      const int64_t pairs = plain / 2;
+      const int64_t plain = std::min<int64_t>(steps - done, to_res - 1);
+      const int64_t pairs = plain / (2 * k);
       if (pairs > 0) {
-        run_graph(pairs);
-        done += 2 * pairs;
+        run_graph(pairs, k);
+        done += 2 * k * pairs;
         continue;
       }
     }
-    step(res);
-    ++done;
+    step(res, k);
+    done += k;
   }
 }
 
@@ -287,8 +298,8 @@ static bool graph_debug() {
     if (graph_debug()) std::fprintf(stderr, "[mdfx graph] %s\n", msg); \
   } while (0)
 
-void Solver::run_graph(int64_t pairs) {
-  if (!graph_exec_ || graph_parity_ != cur_) {
+void Solver::run_graph(int64_t pairs, int k) {
+  if (!graph_exec_ || graph_parity_ != cur_ || graph_k_ != k) {
     GDBG("capture begin");
     destroy_graph();
     Slab& o = slabs_[0];
@@ -315,8 +326,8 @@ void Solver::run_graph(int64_t pairs) {
     }
     const int64_t saved = stats_.steps;
     GDBG("capture: steps");
-    step(false);
-    step(false);
+    step(false, k);
+    step(false, k);
     GDBG("capture: join");
     stats_.steps = saved;  // replay accounts for them
     k = 0;
@@ -344,6 +355,7 @@ void Solver::run_graph(int64_t pairs) {
     for (auto& e : join) (void)hipEventDestroy(e);
     graph_exec_ = ex;
     graph_parity_ = cur_;  // step() x2 leaves cur_ unchanged
+    graph_k_ = k;
     GDBG("instantiated");
   }
   GDBG("launch");
@@ -363,7 +375,7 @@ void Solver::run_graph(int64_t pairs) {
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
   }
-  stats_.steps += 2 * pairs;
+  stats_.steps += 2 * (int64_t)k * pairs;
   GDBG("replayed");
 }
 

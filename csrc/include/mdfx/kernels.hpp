@@ -24,7 +24,13 @@ struct RegionArgs {
   FieldLayout lay;
   int64_t lz_begin = 0, lz_end = 0;  // storage planes to write
   double* resid = nullptr;           // optional accumulator of sum((out-in)^2) over the region
+  // Time steps fused into this sweep (temporal blocking). 2 needs lay.halo >= 2 and reads
+  // in[lz_begin-2, lz_end+2); the residual then covers the second step only.
+  int steps = 1;
 };
+
+// Whether a fused multi-step sweep is implemented for this stencil / grid on the device.
+bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps);
 
 enum class InitKind : int {
   Constant = 0,   // every cell = value

@@ -29,6 +29,10 @@ struct SolverOptions {
   int residual_every = 0;     // compute the global L2 update norm every k steps (0 = never)
   bool graph = false;         // replay a captured 2-step cycle as a hipGraph (HIP only)
   double timeout_s = 0.0;     // watchdog for synchronize(): abort instead of hanging (0 = off)
+  // Temporal blocking: time steps fused per sweep over memory (1 or 2). With 2 the slabs keep two
+  // ghost planes per side, exchanged once per fused step, and every sweep reads u^t once and writes
+  // u^{t+2} once (bitwise identical to two single steps). Fixed at construction.
+  int temporal = 1;
 };
 
 struct StepStats {
@@ -92,10 +96,10 @@ class Solver {
     double* resid = nullptr;  // 2 accumulators (halo-stream kernels, compute-stream kernels)
     int64_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0, in_b = 0, in_e = 0;  // storage-plane regions
   };
-  void step(bool want_resid);
+  void step(bool want_resid, int k);
   void sync_all();
   void finish_residual();
-  void run_graph(int64_t pairs);
+  void run_graph(int64_t pairs, int k);
   void destroy_graph();
 
   StencilSpec spec_;
@@ -110,6 +114,7 @@ class Solver {
   bool ghosts_dirty_ = false;
   void* graph_exec_ = nullptr;  // hipGraphExec_t for the 2-step cycle starting at buffer 0
   int graph_parity_ = -1;
+  int graph_k_ = 0;
 };
 
 }  // namespace mdfx

@@ -26,6 +26,10 @@ template <class T>
 void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
                   hipStream_t s);
 void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s);
+template <class T>
+void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
+template <class T>
+bool heat7_tb2_supported(const Geo& g);
 
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -116,12 +120,31 @@ void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* str
   if (e != hipSuccess) MDFX_FAIL(std::string("init launch failed: ") + hipGetErrorString(e));
 }
 
+bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps) {
+  if (steps == 1) return true;
+  if (steps != 2 || spec.kind != StencilKind::Heat7 || lay.halo < 2) return false;
+  const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
+  return spec.dtype == DType::F32 ? dev::heat7_tb2_supported<float>(g) : dev::heat7_tb2_supported<double>(g);
+}
+
 void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   if (a.lz_end <= a.lz_begin) return;
   MDFX_CHECK(a.lz_begin >= a.lay.halo && a.lz_end <= a.lay.halo + a.lay.nzl(),
              "region must lie inside the owned planes");
   const dev::Geo g = dev::make_geo(a.lay, a.lz_begin, a.lz_end);
   hipStream_t s = (hipStream_t)stream;
+  if (a.steps != 1) {
+    MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),
+               format("no fused %d-step kernel for %s %s at nx=%lld (halo %d)", a.steps, stencil_name(spec.kind),
+                      dtype_name(spec.dtype), (long long)a.lay.global.nx, a.lay.halo));
+    if (spec.dtype == DType::F32)
+      dev::launch_heat7_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
+    else
+      dev::launch_heat7_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) MDFX_FAIL(std::string("stencil launch failed: ") + hipGetErrorString(e));
+    return;
+  }
   std::string variant;
   {
     std::lock_guard<std::mutex> lk(dev::g_variant_mu);

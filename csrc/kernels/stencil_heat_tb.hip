@@ -1,0 +1,238 @@
+// Temporally blocked 3D 7-point heat/Jacobi: TWO time steps per sweep over memory.
+//
+// The single-step kernels (stencil_heat.hip) already run at the HBM copy roof (1 read + 1 write
+// per cell per step). This kernel reads u^t once and writes u^{t+2} once, computing u^{t+1} on
+// chip, so a sweep advances two steps for the same HBM bytes.
+//
+// Geometry: one block = 4 waves along x covering the WHOLE row (nx <= 4 * 64 * N, i.e. 1024 fp32 /
+// 512 fp64), so the block's x edges are the Dirichlet boundary and no x halo is needed; RY rows
+// per lane; the block marches along z over `zc` output planes. Per z-iteration with u1 plane c:
+//   u1(c)   rows y0-1 .. y0+RY   from u0 planes c-1, c, c+1 (rows y0-2 .. y0+RY+1 of plane c)
+//   u2(c-1) rows y0   .. y0+RY-1 from u1 planes c-2, c-1, c
+// u0 planes are loaded once (RY+4 rows each: the y halo rows are L2 hits shared with the
+// neighbouring tiles, which the XCD-aware block order keeps on the same XCD); the one redundant u1
+// row above and below the tile is recomputed instead of exchanged. x neighbours come from lane
+// shuffles plus a 2-deep LDS ring for the 4 wave seams (one barrier per z-iteration).
+// The arithmetic is exactly two applications of sm::heat7 with the boundary held, so the result
+// is bitwise identical to two single steps (tests/test_gpu_temporal.py).
+//
+// Region contract: output storage planes [lz_begin, lz_end) need u0 valid on
+// [lz_begin - 2, lz_end + 2): the engine keeps 2 ghost planes (halo = 2) when temporal blocking is on.
+#include <algorithm>
+
+#include "kcommon.hpp"
+#include "mdfx/kernels.hpp"
+#include "mdfx/stencil_math.hpp"
+
+namespace mdfx {
+namespace dev {
+
+int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target);
+int env_int(const char* name, int dflt);
+
+template <class V, class T>
+__device__ __forceinline__ V vsplat_tb(T v) {
+  V r;
+#pragma unroll
+  for (int e = 0; e < (int)(sizeof(V) / sizeof(T)); ++e) r[e] = v;
+  return r;
+}
+
+template <class T, int RY, bool RES, int PF>
+__global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g,
+                                                 T r, int zc, int YT, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  constexpr int R0 = RY + 4;  // u0 rows y0-2 .. y0+RY+1
+  constexpr int R1 = RY + 2;  // u1 rows y0-1 .. y0+RY
+  __shared__ T edge[2][4][R1 + RY][2];
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int yt = t % YT;
+  const int zt = t / YT;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t xw = (int64_t)w * WX;
+  const uint32_t xo = (uint32_t)lane * N;
+  const int64_t x = xw + xo;
+  const int64_t y0 = (int64_t)yt * RY;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const T* ib = in + (y0 - 2) * pitch + xw;  // u0 row r of the window = y0 - 2 + r
+  T* ob = out + y0 * pitch + xw;
+
+  auto ld = [&](int64_t lz, int rr) -> V {
+    V v = vsplat_tb<V>(T(0));
+    const int64_t y = y0 - 2 + rr;
+    if (lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
+      const T* p = ib + lz * plane + (int64_t)rr * pitch;
+      if (xin) v = *(const V*)(p + xo);
+    }
+    return v;
+  };
+
+  V L0[R0], M0[R0], H0[R0];  // u0 planes c-1, c, c+1
+  V U1a[R1], U1b[R1];        // u1 planes c-2, c-1
+#pragma unroll
+  for (int k = 0; k < R0; ++k) {
+    L0[k] = ld(zs - 2, k);
+    M0[k] = ld(zs - 1, k);
+    H0[k] = ld(zs, k);
+  }
+#pragma unroll
+  for (int k = 0; k < R1; ++k) {
+    U1a[k] = vsplat_tb<V>(T(0));
+    U1b[k] = vsplat_tb<V>(T(0));
+  }
+  double acc = 0.0;
+  int buf = 0;
+  // c = u1 plane computed this iteration; u2 plane c-1 is produced from c >= zs + 1
+  for (int64_t c = zs - 1; c <= ze; ++c) {
+    V NX[R0];
+    if (PF) {
+#pragma unroll
+      for (int k = 0; k < R0; ++k) NX[k] = ld(c + 2, k);
+    }
+    // publish the wave-seam values: u0 plane c rows used for u1, u1 plane c-1 own rows for u2
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < R1; ++j) edge[buf][w][j][0] = M0[j + 1][0];
+#pragma unroll
+      for (int i = 0; i < RY; ++i) edge[buf][w][R1 + i][0] = U1b[i + 1][0];
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int j = 0; j < R1; ++j) edge[buf][w][j][1] = M0[j + 1][N - 1];
+#pragma unroll
+      for (int i = 0; i < RY; ++i) edge[buf][w][R1 + i][1] = U1b[i + 1][N - 1];
+    }
+    __syncthreads();
+
+    // ---- u1 at plane c ------------------------------------------------------------------
+    V U1c[R1];
+    {
+      const int64_t gz = c + g.gz_off;
+      const bool zb = (gz <= 0 || gz >= g.gnz - 1);
+#pragma unroll
+      for (int j = 0; j < R1; ++j) {
+        const int64_t y = y0 - 1 + j;
+        const V cc = M0[j + 1];
+        V o = cc;
+        T l = __shfl_up(cc[N - 1], 1, 64);
+        T rr = __shfl_down(cc[0], 1, 64);
+        if (lane == 0) l = w > 0 ? edge[buf][w - 1][j][1] : T(0);
+        if (lane == 63) rr = w < 3 ? edge[buf][w + 1][j][0] : T(0);
+        if (!zb && y > 0 && y < g.ny - 1) {
+          const V ym = M0[j], yp = M0[j + 2], zm = L0[j + 1], zp = H0[j + 1];
+#pragma unroll
+          for (int e = 0; e < N; ++e) {
+            const T xm = e == 0 ? l : cc[e - 1];
+            const T xp = e == N - 1 ? rr : cc[e + 1];
+            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
+            const int64_t xe = x + e;
+            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
+          }
+        }
+        U1c[j] = o;
+      }
+    }
+    // ---- u2 at plane c-1 ----------------------------------------------------------------
+    if (c >= zs + 1) {
+      const int64_t lz = c - 1;
+      const int64_t gz = lz + g.gz_off;
+      const bool zb = (gz == 0 || gz == g.gnz - 1);
+#pragma unroll
+      for (int i = 0; i < RY; ++i) {
+        const int64_t y = y0 + i;
+        if (y >= g.ny) break;
+        const V cc = U1b[i + 1];
+        V o = cc;
+        T l = __shfl_up(cc[N - 1], 1, 64);
+        T rr = __shfl_down(cc[0], 1, 64);
+        if (lane == 0) l = w > 0 ? edge[buf][w - 1][R1 + i][1] : T(0);
+        if (lane == 63) rr = w < 3 ? edge[buf][w + 1][R1 + i][0] : T(0);
+        if (!zb && y != 0 && y != g.ny - 1) {
+          const V ym = U1b[i], yp = U1b[i + 2], zm = U1a[i + 1], zp = U1c[i + 1];
+#pragma unroll
+          for (int e = 0; e < N; ++e) {
+            const T xm = e == 0 ? l : cc[e - 1];
+            const T xp = e == N - 1 ? rr : cc[e + 1];
+            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
+            const int64_t xe = x + e;
+            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
+          }
+        }
+        if (xin) {
+          store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
+          if (RES) {
+#pragma unroll
+            for (int e = 0; e < N; ++e)
+              if (x + e < g.nx) {
+                const double d = (double)o[e] - (double)cc[e];
+                acc += d * d;
+              }
+          }
+        }
+      }
+    }
+    buf ^= 1;
+#pragma unroll
+    for (int k = 0; k < R1; ++k) {
+      U1a[k] = U1b[k];
+      U1b[k] = U1c[k];
+    }
+#pragma unroll
+    for (int k = 0; k < R0; ++k) {
+      L0[k] = M0[k];
+      M0[k] = H0[k];
+      H0[k] = PF ? NX[k] : ld(c + 2, k);
+    }
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T>
+bool heat7_tb2_supported(const Geo& g) {
+  constexpr int WX = 64 * VT<T>::N;
+  return g.nx <= 4 * WX && g.pitch <= 4 * WX && g.ny >= 1;
+}
+template bool heat7_tb2_supported<float>(const Geo&);
+template bool heat7_tb2_supported<double>(const Geo&);
+
+template <class T, int RY, int PF>
+static void launch_tb2_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int YT = (int)((g.ny + RY - 1) / RY);
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = pick_zc(planes, YT, 128, env_int("MDFX_BLOCKS", 4096));
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((heat7_tb2<T, RY, true, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+  else
+    hipLaunchKernelGGL((heat7_tb2<T, RY, false, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+}
+
+template <class T>
+void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  int ry = env_int("MDFX_TB_RY", 0);
+  if (ry <= 0) ry = 2;
+  const int pf = env_int("MDFX_TB_PF", 0);
+  if (g.ny < 8) ry = 1;
+  switch (ry * 2 + (pf ? 1 : 0)) {
+    case 2: launch_tb2_t<T, 1, 0>(g, in, out, r, resid, s); break;
+    case 3: launch_tb2_t<T, 1, 1>(g, in, out, r, resid, s); break;
+    case 5: launch_tb2_t<T, 2, 1>(g, in, out, r, resid, s); break;
+    case 8: launch_tb2_t<T, 4, 0>(g, in, out, r, resid, s); break;
+    case 9: launch_tb2_t<T, 4, 1>(g, in, out, r, resid, s); break;
+    default: launch_tb2_t<T, 2, 0>(g, in, out, r, resid, s); break;
+  }
+}
+template void launch_heat7_tb2<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
+template void launch_heat7_tb2<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
+
+}  // namespace dev
+}  // namespace mdfx

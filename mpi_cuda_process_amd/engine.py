@@ -38,7 +38,7 @@ class Simulation:
                  devices: Optional[Sequence[int]] = None, transport: str = "auto",
                  distributed: Optional[bool] = None, overlap: bool = True, sync_debug: bool = False,
                  residual_every: int = 0, graph: bool = False, timeout_s: float = 0.0,
-                 group=None):
+                 temporal: int = 1, group=None):
         self.problem = problem
         if device == "auto":
             device = "hip" if hip_available() else "cpu"
@@ -102,7 +102,7 @@ class Simulation:
         self._s = native().Solver(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                   nranks, local_ranks, dev_list, overlap=overlap,
                                   sync_debug=sync_debug, residual_every=residual_every, graph=graph,
-                                  timeout_s=timeout_s, **problem.coef_kwargs(), **args)
+                                  timeout_s=timeout_s, temporal=temporal, **problem.coef_kwargs(), **args)
         if self._torch_transport is not None:
             self._torch_transport.solver = self._s
         self.transport = self._s.transport_name if self._torch_transport is None else "torch"
@@ -149,6 +149,10 @@ class Simulation:
 
     def set_options(self, **kw):
         self._s.set_options(**kw)
+
+    @property
+    def temporal(self) -> int:
+        return self._s.temporal
 
     @property
     def steps(self) -> int:

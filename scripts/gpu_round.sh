@@ -22,6 +22,10 @@ fi
 if [[ $MODE == all || $MODE == bench ]]; then
   step 300 python bench.py > gpurun_out/bench_n1.json 2> gpurun_out/bench_n1.err || { cat gpurun_out/bench_n1.err; exit 1; }
   cat gpurun_out/bench_n1.json
+  step 300 python bench.py --temporal 1 > gpurun_out/bench_n1_t1.json 2>> gpurun_out/bench_n1.err || exit 1
+  cat gpurun_out/bench_n1_t1.json
+  step 300 python bench.py --virtual-ranks 8 > gpurun_out/bench_v8.json 2>> gpurun_out/bench_n1.err || exit 1
+  cat gpurun_out/bench_v8.json
 fi
 if [[ $MODE == all || $MODE == profile ]]; then
   R=$(pwd)

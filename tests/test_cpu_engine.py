@@ -244,3 +244,55 @@ def test_kernel_region_outside_owned_rejected(mdfx):
     a, b = alloc_field(lay), alloc_field(lay)
     with pytest.raises(ValueError):
         apply_stencil(prob, lay, a, b, 0, 3)
+
+
+# ---- temporal blocking (2 fused steps per sweep, halo 2) ----------------------------------------
+@pytest.mark.parametrize("ranks", [1, 2, 3, 5])
+@pytest.mark.parametrize("steps", [1, 2, 7, 10])
+def test_temporal2_equals_single_steps_cpu(mdfx, ranks, steps):
+    prob = m.heat3d(nx=14, ny=11, nz=13)
+    with m.Simulation(prob, device="cpu") as sim:
+        sim.init()
+        sim.run(steps)
+        ref = sim.gather()
+    with m.Simulation(prob, device="cpu", ranks=ranks, temporal=2) as sim:
+        assert sim.temporal == 2 and sim.layout(0)["halo"] == 2
+        sim.init()
+        sim.run(steps)
+        assert sim.steps == steps
+        assert np.array_equal(ref, sim.gather())
+
+
+@pytest.mark.parametrize("every", [1, 2, 3, 4])
+def test_temporal2_residual_schedule(mdfx, every):
+    prob = m.heat3d(nx=12, ny=10, nz=11)
+    res = {}
+    for t in (1, 2):
+        with m.Simulation(prob, device="cpu", ranks=2, temporal=t, residual_every=every) as sim:
+            sim.init()
+            sim.run(9)
+            res[t] = (sim.residual, sim.native.residual_step, sim.gather())
+    assert res[1][1] == res[2][1] == (9 // every) * every
+    assert abs(res[1][0] - res[2][0]) <= 1e-9 * max(1.0, res[1][0])
+    assert np.array_equal(res[1][2], res[2][2])
+
+
+def test_temporal2_checkpoint_roundtrip(mdfx, tmp_path):
+    prob = m.heat3d(nx=12, ny=9, nz=16)
+    with m.Simulation(prob, device="cpu") as sim:
+        sim.init()
+        sim.run(9)
+        ref = sim.gather()
+    with m.Simulation(prob, device="cpu", ranks=3, temporal=2) as sim:
+        sim.init()
+        sim.run(4)
+        sim.save_checkpoint(str(tmp_path / "ck"))
+    with m.Simulation(prob, device="cpu", ranks=2, temporal=2) as sim:
+        sim.load_checkpoint(str(tmp_path / "ck"))
+        sim.run(5)
+        assert np.array_equal(ref, sim.gather())
+
+
+def test_temporal_depth_validated(mdfx):
+    with pytest.raises(RuntimeError):
+        m.Simulation(m.heat3d(n=8), device="cpu", temporal=3)
