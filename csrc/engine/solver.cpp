@@ -310,12 +310,12 @@ void Solver::run_graph(int64_t pairs, int k) {
     for (auto& e : join) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPC(hipStreamBeginCapture(origin, hipStreamCaptureModeRelaxed));
     HIPC(hipEventRecord(fork[0], origin));
-    size_t k = 0;
+    size_t ei = 0;
     for (auto& s : slabs_) {
       s.be->activate();
       for (void* st : {s.hs, s.cs}) {
         if (st != (void*)origin) HIPC(hipStreamWaitEvent((hipStream_t)st, fork[0], 0));
-        ++k;
+        ++ei;
       }
     }
     // every event the captured steps wait on must itself be recorded inside the capture
@@ -330,17 +330,17 @@ void Solver::run_graph(int64_t pairs, int k) {
     step(false, k);
     GDBG("capture: join");
     stats_.steps = saved;  // replay accounts for them
-    k = 0;
+    ei = 0;
     for (auto& s : slabs_) {
       s.be->activate();
       for (void* st : {s.hs, s.cs}) {
         if (st != (void*)origin) {
-          HIPC(hipEventRecord(join[k], (hipStream_t)st));
+          HIPC(hipEventRecord(join[ei], (hipStream_t)st));
           o.be->activate();
-          HIPC(hipStreamWaitEvent(origin, join[k], 0));
+          HIPC(hipStreamWaitEvent(origin, join[ei], 0));
           s.be->activate();
         }
-        ++k;
+        ++ei;
       }
     }
     o.be->activate();
