@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--nz", type=int, default=0)
     p.add_argument("--stencil", default="heat7", choices=["heat7", "box27", "jacobi5", "life"])
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "u8"])
-    p.add_argument("--transport", default="auto", help="auto|rccl|torch (distributed), loopback (1 process)")
+    p.add_argument("--transport", default="auto",
+                   help="auto|rccl|torch|staged (distributed), loopback (1 process)")
     p.add_argument("--virtual-ranks", type=int, default=0,
                    help="split the grid into P slabs inside ONE process (loopback transport)")
     p.add_argument("--graph", action="store_true", help="replay 2-step cycles as hipGraphs")
@@ -66,7 +67,8 @@ def main():
     from mpi_cuda_process_amd import Simulation, heat3d, box27, mdf2d, life2d, native
     from mpi_cuda_process_amd.parallel.dist import init_distributed
 
-    env = init_distributed("gloo") if int(os.environ.get("WORLD_SIZE", "1")) > 1 else None
+    force = os.environ.get("MDFX_FORCE_DIST", "") == "1"  # distributed path even at WORLD_SIZE 1 (tests)
+    env = init_distributed("gloo", force=force) if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or force) else None
     world = dist.get_world_size() if env else 1
     rank = dist.get_rank() if env else 0
     if env and a.gpus != world:
@@ -100,7 +102,8 @@ def main():
     else:
         vr = a.virtual_ranks or 1
         sim = Simulation(prob, ranks=vr, distributed=False,
-                         transport="auto" if a.transport in ("auto", "rccl", "torch") else a.transport, **kw)
+                         transport="auto" if a.transport in ("auto", "rccl", "torch", "staged") else a.transport,
+                         **kw)
     sim.init()
 
     def barrier():

@@ -70,15 +70,17 @@ class Simulation:
                 uid = native().rccl_unique_id() if rank == 0 else None
                 uid = broadcast_bytes(uid, src=0, group=group)
                 args = dict(transport="rccl", unique_id=uid)
-            elif transport == "torch":
+            elif transport in ("torch", "staged"):
                 p2p_group = group
+                staged = transport == "staged" and device == "hip"
                 if device == "hip":
                     torch.cuda.set_device(dev_list[0])
-                    p2p_group = dist.new_group(backend="nccl") if group is None else group
-                self._torch_transport = TorchP2PTransport(p2p_group)
+                    if not staged:
+                        p2p_group = dist.new_group(backend="nccl") if group is None else group
+                self._torch_transport = TorchP2PTransport(p2p_group, staged=staged)
                 args = dict(transport="callback", callbacks=self._torch_transport.callbacks())
             else:
-                raise ValueError("distributed transport must be rccl|torch|auto")
+                raise ValueError("distributed transport must be rccl|torch|staged|auto")
         else:
             nranks = ranks or 1
             local_ranks = list(range(nranks))

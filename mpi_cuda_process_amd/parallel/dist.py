@@ -43,10 +43,12 @@ def is_distributed() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
-def init_distributed(backend: str = "gloo", timeout_s: float = 600.0) -> DistEnv:
-    """Initialise the default process group from the launcher environment (idempotent)."""
+def init_distributed(backend: str = "gloo", timeout_s: float = 600.0, force: bool = False) -> DistEnv:
+    """Initialise the default process group from the launcher environment (idempotent).
+
+    ``force`` initialises it even for a single process (exercises the distributed code path)."""
     env = detect_env()
-    if not dist.is_initialized() and env.world > 1:
+    if not dist.is_initialized() and (env.world > 1 or force):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", str(env.rank))
@@ -74,8 +76,12 @@ class TorchP2PTransport:
     kernels exactly like the native transports.
     """
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, staged: bool = False):
         self.group = group
+        # staged: device faces travel through host memory over a CPU (gloo) group. Slow, but it
+        # lets several processes share ONE GPU and still run the real multi-process engine path
+        # (RCCL refuses two ranks on one device) — tests/test_gpu_multiprocess.py.
+        self.staged = staged
         self.solver = None  # set by the Simulation once the native solver exists
 
     def callbacks(self) -> dict:
@@ -91,6 +97,9 @@ class TorchP2PTransport:
         if not spans:
             return
         dev = s.device(0)
+        if dev >= 0 and self.staged:
+            self._exchange_staged(spans)
+            return
         ctx = torch.cuda.stream(torch.cuda.ExternalStream(s.halo_stream(0))) if dev >= 0 else _null()
         with ctx:
             ops = []
@@ -106,6 +115,24 @@ class TorchP2PTransport:
                 reqs = [op.op(op.tensor, op.peer, op.group) for op in ops]
             for r in reqs:
                 r.wait()
+
+    def _exchange_staged(self, spans) -> None:
+        s = self.solver
+        hs = torch.cuda.ExternalStream(s.halo_stream(0))
+        hs.synchronize()  # the boundary kernels that produced the faces are done
+        sends, recvs, reqs = [], [], []
+        for sp in spans:
+            sends.append(self._bytes(sp["send"], sp["bytes"]).cpu())
+            recvs.append(torch.empty(sp["bytes"], dtype=torch.uint8))
+        for sp, snd, rcv in zip(spans, sends, recvs):
+            reqs.append(dist.irecv(rcv, src=sp["peer"], group=self.group))
+            reqs.append(dist.isend(snd, dst=sp["peer"], group=self.group))
+        for r in reqs:
+            r.wait()
+        with torch.cuda.stream(hs):
+            for sp, rcv in zip(spans, recvs):
+                self._bytes(sp["recv"], sp["bytes"]).copy_(rcv, non_blocking=False)
+        hs.synchronize()
 
     def allreduce_sum(self, v: float) -> float:
         t = torch.tensor([v], dtype=torch.float64)
