@@ -80,6 +80,8 @@ def main():
     native().set_kernel_variant(a.variant)
 
     nx, ny, nz = a.nx or a.n, a.ny or a.n, a.nz or a.n
+    if a.stencil in ("jacobi5", "life"):
+        ny = 1  # 2D grids: nx = width, nz = height
     if a.stencil == "heat7":
         prob = heat3d(nx=nx, ny=ny, nz=nz, dtype=a.dtype)
     elif a.stencil == "box27":

@@ -38,12 +38,13 @@ __device__ __forceinline__ V vsplat_tb(T v) {
   return r;
 }
 
-template <class T, int RY, bool RES, int PF>
+template <class T, int RY, int WXN, bool RES, int PF>
 __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g,
                                                  T r, int zc, int YT, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   constexpr int N = VT<T>::N;
   constexpr int WX = 64 * N;
+  constexpr int WYN = 4 / WXN;  // narrow rows: wave groups stacked along y, each its own RY-row tile
   constexpr int R0 = RY + 4;  // u0 rows y0-2 .. y0+RY+1
   constexpr int R1 = RY + 2;  // u1 rows y0-1 .. y0+RY
   __shared__ T edge[2][4][R1 + RY][2];
@@ -52,10 +53,11 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
   const int zt = t / YT;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t xw = (int64_t)w * WX;
+  const int wx = w % WXN, wy = w / WXN;
+  const int64_t xw = (int64_t)wx * WX;
   const uint32_t xo = (uint32_t)lane * N;
   const int64_t x = xw + xo;
-  const int64_t y0 = (int64_t)yt * RY;
+  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
   const int64_t zs = g.lz_begin + (int64_t)zt * zc;
   const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
   const bool xin = x < g.pitch;
@@ -122,8 +124,8 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
         V o = cc;
         T l = __shfl_up(cc[N - 1], 1, 64);
         T rr = __shfl_down(cc[0], 1, 64);
-        if (lane == 0) l = w > 0 ? edge[buf][w - 1][j][1] : T(0);
-        if (lane == 63) rr = w < 3 ? edge[buf][w + 1][j][0] : T(0);
+        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][j][1] : T(0);
+        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][j][0] : T(0);
         if (!zb && y > 0 && y < g.ny - 1) {
           const V ym = M0[j], yp = M0[j + 2], zm = L0[j + 1], zp = H0[j + 1];
 #pragma unroll
@@ -151,8 +153,8 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
         V o = cc;
         T l = __shfl_up(cc[N - 1], 1, 64);
         T rr = __shfl_down(cc[0], 1, 64);
-        if (lane == 0) l = w > 0 ? edge[buf][w - 1][R1 + i][1] : T(0);
-        if (lane == 63) rr = w < 3 ? edge[buf][w + 1][R1 + i][0] : T(0);
+        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][R1 + i][1] : T(0);
+        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][R1 + i][0] : T(0);
         if (!zb && y != 0 && y != g.ny - 1) {
           const V ym = U1b[i], yp = U1b[i + 2], zm = U1a[i + 1], zp = U1c[i + 1];
 #pragma unroll
@@ -201,18 +203,32 @@ bool heat7_tb2_supported(const Geo& g) {
 template bool heat7_tb2_supported<float>(const Geo&);
 template bool heat7_tb2_supported<double>(const Geo&);
 
-template <class T, int RY, int PF>
-static void launch_tb2_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+template <class T, int RY, int WXN, int PF>
+static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int WYN = 4 / WXN;
   const int64_t planes = g.lz_end - g.lz_begin;
-  const int YT = (int)((g.ny + RY - 1) / RY);
+  const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   int zc = env_int("MDFX_ZC", 0);
   if (zc <= 0) zc = pick_zc(planes, YT, 128, env_int("MDFX_BLOCKS", 4096));
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
-    hipLaunchKernelGGL((heat7_tb2<T, RY, true, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, true, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
   else
-    hipLaunchKernelGGL((heat7_tb2<T, RY, false, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+}
+
+template <class T, int RY, int PF>
+static void launch_tb2_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int WX = 64 * VT<T>::N;
+  // as many waves along x as the row needs (the block must span the row), the rest along y:
+  // 512^3 fp32 otherwise leaves half of every block idle
+  if (g.pitch > 2 * WX)
+    launch_tb2_w<T, RY, 4, PF>(g, in, out, r, resid, s);
+  else if (g.pitch > WX)
+    launch_tb2_w<T, RY, 2, PF>(g, in, out, r, resid, s);
+  else
+    launch_tb2_w<T, RY, 1, PF>(g, in, out, r, resid, s);
 }
 
 template <class T>
