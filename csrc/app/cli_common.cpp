@@ -37,6 +37,7 @@ struct Opts {
   std::string ckpt_dir = "mdfx_ckpt", resume;
   bool compat = false;
   int temporal = 1;
+  bool profile = false;
 };
 
 void usage(const char* prog) {
@@ -59,7 +60,8 @@ void usage(const char* prog) {
       "  --print                   dump the final grid like the reference's print_array\n"
       "  --json                    one JSON metrics line ; --verbose per-rank detail ; --quiet\n"
       "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n"
-      "  --temporal 1|2            time steps fused per memory sweep (2: 3D 7-pt, rows <= one block)\n",
+      "  --temporal 1|2            time steps fused per memory sweep (2: 3D 7-pt, rows <= one block)\n"
+      "  --profile                 per-phase timing of rank 0 (boundary / interior / exchange)\n",
       prog);
 }
 
@@ -116,6 +118,7 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--timeout") o.timeout = std::atof(need(i));
     else if (a == "--compat") o.compat = true;
     else if (a == "--temporal") o.temporal = std::atoi(need(i));
+    else if (a == "--profile") o.profile = true;
     else MDFX_FAIL("unknown option " + a + " (try --help)");
   }
   return o;
@@ -316,6 +319,25 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     solver.transport().barrier();
 
     // ---- output ---------------------------------------------------------------------------
+    if (o.profile) {
+      // profiled separately from the timed loop (profiling syncs the host every sweep); every
+      // rank runs the extra steps, rank 0 reports its slab
+      SolverOptions po = solver.options();
+      po.profile = true;
+      solver.set_options(po);
+      solver.run(std::min<int64_t>(std::max<int64_t>(o.steps, 2), 50));
+      solver.synchronize();
+      const PhaseStats& ph = solver.phases();
+      const double n = ph.steps ? (double)ph.steps : 1.0;
+      if (root) std::fprintf(stderr,
+                   "profile (rank 0, %lld sweeps, per sweep): boundary %.4f ms | interior %.4f ms | "
+                   "exchange %.4f ms | step %.4f ms | overlap %.0f%%\n",
+                   (long long)ph.steps, ph.boundary_ms / n, ph.interior_ms / n, ph.exchange_ms / n,
+                   ph.step_ms / n,
+                   ph.step_ms > 0 ? 100.0 * (ph.boundary_ms + ph.exchange_ms + ph.interior_ms - ph.step_ms) /
+                                        std::max(1e-9, std::min(ph.boundary_ms + ph.exchange_ms, ph.interior_ms))
+                                  : 0.0);
+    }
     const double cells = (double)g.cells();
     const double gcs = dt > 0 ? cells * (double)o.steps / dt / 1e9 : 0.0;
     const int ngpu = hip ? (env.world > 1 ? env.world : (o.gpus ? o.gpus : 1)) : 0;

@@ -286,9 +286,13 @@ class TcpTransport final : public Transport {
         if (ev) pf.push_back({fd, ev, 0});
       }
       if (pf.empty()) break;
-      const int k = ::poll(pf.data(), pf.size(), 120000);
+      static const int timeout_ms = [] {
+        const char* v = std::getenv("MDFX_TCP_TIMEOUT_S");
+        return (int)(1000 * ((v && *v) ? std::atof(v) : 120.0));
+      }();
+      const int k = ::poll(pf.data(), pf.size(), timeout_ms);
       if (k < 0 && errno == EINTR) continue;
-      MDFX_CHECK(k > 0, "tcp halo exchange timed out (peer hung?)");
+      MDFX_CHECK(k > 0, format("tcp halo exchange timed out after %.1f s (peer hung?)", timeout_ms / 1000.0));
       for (auto& q : pf) {
         if (q.revents & (POLLERR | POLLHUP | POLLNVAL)) MDFX_FAIL("tcp halo peer closed the connection");
         for (auto& x : xs) {

@@ -11,7 +11,9 @@
 #include <fstream>
 #include <sstream>
 #include <sys/stat.h>
+#include <string>
 #include <thread>
+#include <vector>
 
 namespace mdfx {
 
@@ -75,6 +77,10 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     slabs_.push_back(std::move(s));
   }
   for (auto& s : slabs_) s.be->sync_device();
+  if (slabs_[0].be->kind() == DeviceKind::HIP) {
+    slabs_[0].be->activate();
+    for (auto& e : pev_) HIPC(hipEventCreate((hipEvent_t*)&e));
+  }
   std::vector<LocalSlab> ls;
   for (auto& s : slabs_) {
     LocalSlab l;
@@ -97,6 +103,8 @@ Solver::~Solver() {
   }
   destroy_graph();
   transport_.reset();  // communicators before the memory they reference
+  for (auto& e : pev_)
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
   for (auto& s : slabs_) {
     s.be->release(s.buf[0]);
     s.be->release(s.buf[1]);
@@ -174,7 +182,13 @@ void Solver::exchange_ghosts() {
 
 void Solver::step(bool want_resid, int k) {
   const int nb = 1 - cur_;
+  const bool prof = opt_.profile;
+  const bool prof_hip = prof && pev_[0] != nullptr;
+  using clk = std::chrono::steady_clock;
+  clk::time_point c0, c1, c2, c3;
+  if (prof && !prof_hip) c0 = clk::now();
   for (auto& s : slabs_) {
+    const bool p0 = prof_hip && &s == &slabs_[0];
     s.be->activate();
     s.be->trace_push("mdfx.step");
     RegionArgs a;
@@ -188,6 +202,7 @@ void Solver::step(bool want_resid, int k) {
     }
     // halo stream: boundary planes of this step, after the previous interior sweep
     s.be->wait(s.hs, s.ev_int);
+    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)s.hs));
     a.resid = want_resid ? s.resid : nullptr;
     if (s.lo_e > s.lo_b) {
       a.lz_begin = s.lo_b;
@@ -199,16 +214,21 @@ void Solver::step(bool want_resid, int k) {
       a.lz_end = s.hi_e;
       s.be->stencil(spec_, a, s.hs);
     }
+    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)s.hs));
     if (opt_.sync_debug) s.be->sync_device();
+    if (prof && !prof_hip && &s == &slabs_[0]) c1 = clk::now();
     // compute stream: interior, after the previous step's boundary kernels
     void* is = opt_.overlap ? s.cs : s.hs;
     if (opt_.overlap) s.be->wait(s.cs, s.ev_bnd);
+    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)is));
     if (s.in_e > s.in_b) {
       a.lz_begin = s.in_b;
       a.lz_end = s.in_e;
       a.resid = want_resid ? s.resid + 1 : nullptr;
       s.be->stencil(spec_, a, is);
     }
+    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[3], (hipStream_t)is));
+    if (prof && !prof_hip && &s == &slabs_[0]) c2 = clk::now();
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, is);
     if (opt_.sync_debug) s.be->sync_device();
@@ -217,6 +237,34 @@ void Solver::step(bool want_resid, int k) {
   if (!slabs_.empty()) slabs_[0].be->trace_push("mdfx.exchange");
   transport_->exchange(nb);
   if (!slabs_.empty()) slabs_[0].be->trace_pop();
+  if (prof_hip) {
+    Slab& s0 = slabs_[0];
+    s0.be->activate();
+    HIPC(hipEventRecord((hipEvent_t)pev_[4], (hipStream_t)s0.hs));
+    HIPC(hipEventSynchronize((hipEvent_t)pev_[4]));
+    HIPC(hipEventSynchronize((hipEvent_t)pev_[3]));
+    float b = 0, i = 0, x = 0, t1 = 0, t2 = 0;
+    HIPC(hipEventElapsedTime(&b, (hipEvent_t)pev_[0], (hipEvent_t)pev_[1]));
+    HIPC(hipEventElapsedTime(&i, (hipEvent_t)pev_[2], (hipEvent_t)pev_[3]));
+    HIPC(hipEventElapsedTime(&x, (hipEvent_t)pev_[1], (hipEvent_t)pev_[4]));
+    HIPC(hipEventElapsedTime(&t1, (hipEvent_t)pev_[0], (hipEvent_t)pev_[4]));
+    HIPC(hipEventElapsedTime(&t2, (hipEvent_t)pev_[0], (hipEvent_t)pev_[3]));
+    phases_.boundary_ms += b;
+    phases_.interior_ms += i;
+    phases_.exchange_ms += x;
+    phases_.step_ms += std::max(t1, t2);
+    ++phases_.steps;
+  } else if (prof) {
+    c3 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    phases_.boundary_ms += ms(c0, c1);
+    phases_.interior_ms += ms(c1, c2);
+    phases_.exchange_ms += ms(c2, c3);
+    phases_.step_ms += ms(c0, c3);
+    ++phases_.steps;
+  }
   if (opt_.sync_debug) sync_all();
   cur_ = nb;
   stats_.steps += k;
@@ -240,6 +288,69 @@ void Solver::finish_residual() {
                      (long long)stats_.steps));
 }
 
+// Fault injection for failure-detection tests: MDFX_FAULT=<kind>@<rank>:<step> with kind
+// exit (the process dies), hang (it stops responding) or nan (a NaN is written into its slab);
+// fires once, when the slab <rank> of this process reaches time step <step>.
+namespace {
+struct Fault {
+  std::string kind;
+  int rank = -1;
+  int64_t step = -1;
+  bool fired = false;
+};
+Fault& fault() {
+  static Fault f = [] {
+    Fault x;
+    const char* v = std::getenv("MDFX_FAULT");
+    if (v && *v) {
+      char kind[16] = {0};
+      long long st = -1;
+      int rk = -1;
+      if (std::sscanf(v, "%15[a-z]@%d:%lld", kind, &rk, &st) == 3) {
+        x.kind = kind;
+        x.rank = rk;
+        x.step = st;
+      }
+    }
+    return x;
+  }();
+  return f;
+}
+}  // namespace
+
+void Solver::maybe_inject_fault() {
+  Fault& f = fault();
+  if (f.fired || f.rank < 0 || stats_.steps < f.step) return;
+  for (int i = 0; i < num_local(); ++i) {
+    if (slabs_[i].rank != f.rank) continue;
+    f.fired = true;
+    std::fprintf(stderr, "[mdfx] injecting fault '%s' on rank %d at step %lld\n", f.kind.c_str(), f.rank,
+                 (long long)stats_.steps);
+    std::fflush(stderr);
+    if (f.kind == "exit") std::_Exit(42);
+    if (f.kind == "hang")
+      for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+    if (f.kind == "nan") {
+      Slab& s = slabs_[i];
+      sync_all();
+      const size_t es = s.lay.esize();
+      std::vector<char> v(es, 0);
+      if (spec_.dtype == DType::F32) {
+        const float q = std::nanf("");
+        std::memcpy(v.data(), &q, es);
+      } else if (spec_.dtype == DType::F64) {
+        const double q = std::nan("");
+        std::memcpy(v.data(), &q, es);
+      }
+      // an interior cell of the first owned plane (not on the Dirichlet frame)
+      const size_t off = ((size_t)s.lay.halo * s.lay.plane + (size_t)std::min<int64_t>(1, s.lay.global.ny - 1) * s.lay.pitch +
+                          (size_t)std::min<int64_t>(1, s.lay.global.nx - 1)) * es;
+      s.be->copy((char*)s.buf[cur_] + off, v.data(), es, CopyKind::H2D, s.hs);
+      s.be->sync_stream(s.hs);
+    }
+  }
+}
+
 void Solver::run(int64_t steps) {
   MDFX_CHECK(steps >= 0, "negative step count");
   if (ghosts_dirty_) exchange_ghosts();
@@ -260,9 +371,9 @@ void Solver::run(int64_t steps) {
     // PyTorch bundles crashes in hipStreamEndCapture on the multi-slab loopback capture (the same
     // capture replays correctly under ROCm 7.2: csrc/tests/test_main.cpp test_graph), so several
     // slabs in one process always run eagerly.
-    if (opt_.graph && hip && !res && !opt_.sync_debug && slabs_.size() == 1) {
+    if (opt_.graph && hip && !res && !opt_.sync_debug && !opt_.profile && slabs_.size() == 1) {
       const int64_t plain = std::min<int64_t>(steps - done, to_res - 1);
-      const int64_t pairs = plain / (2 * k);
+      const int64_t pairs = fault().rank >= 0 ? 0 : plain / (2 * k);
       if (pairs > 0) {
         run_graph(pairs, k);
         done += 2 * k * pairs;
@@ -271,6 +382,7 @@ void Solver::run(int64_t steps) {
     }
     step(res, k);
     done += k;
+    maybe_inject_fault();
   }
 }
 

@@ -33,6 +33,14 @@ struct SolverOptions {
   // ghost planes per side, exchanged once per fused step, and every sweep reads u^t once and writes
   // u^{t+2} once (bitwise identical to two single steps). Fixed at construction.
   int temporal = 1;
+  // Per-phase hipEvent timing of slab 0 (boundary / interior / exchange / whole step); syncs the
+  // host once per step, so it is a diagnostic mode, not a benchmark mode.
+  bool profile = false;
+};
+
+struct PhaseStats {
+  int64_t steps = 0;  // sweeps profiled
+  double boundary_ms = 0, interior_ms = 0, exchange_ms = 0, step_ms = 0;
 };
 
 struct StepStats {
@@ -73,6 +81,8 @@ class Solver {
   void* halo_stream(int i) { return slabs_[i].hs; }
   void* compute_stream(int i) { return slabs_[i].cs; }
   const StepStats& stats() const { return stats_; }
+  const PhaseStats& phases() const { return phases_; }
+  void reset_phases() { phases_ = PhaseStats(); }
   int64_t owned_cells_global() const { return global_.cells(); }
 
   // Dense copies of the owned planes (nx*ny*nzl elements, x fastest, no pitch / ghosts).
@@ -97,6 +107,7 @@ class Solver {
     int64_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0, in_b = 0, in_e = 0;  // storage-plane regions
   };
   void step(bool want_resid, int k);
+  void maybe_inject_fault();
   void sync_all();
   void finish_residual();
   void run_graph(int64_t pairs, int k);
@@ -111,6 +122,8 @@ class Solver {
   SolverOptions opt_;
   int cur_ = 0;
   StepStats stats_;
+  PhaseStats phases_;
+  void* pev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // timing events (slab 0)
   bool ghosts_dirty_ = false;
   void* graph_exec_ = nullptr;  // hipGraphExec_t for the 2-step cycle starting at buffer 0
   int graph_parity_ = -1;

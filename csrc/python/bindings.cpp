@@ -315,6 +315,18 @@ PYBIND11_MODULE(_mdfx, m) {
            py::arg("c0") = 0.25, py::arg("c1") = 0.05, py::arg("c2") = 0.025,
            py::arg("c3") = 3.0 / 160.0, py::arg("temporal") = 1)
       .def("close", &PySolver::close)
+      .def("phase_times",
+           [](PySolver& p) {
+             const PhaseStats& ph = p.chk().phases();
+             py::dict d;
+             d["sweeps"] = ph.steps;
+             d["boundary_ms"] = ph.boundary_ms;
+             d["interior_ms"] = ph.interior_ms;
+             d["exchange_ms"] = ph.exchange_ms;
+             d["step_ms"] = ph.step_ms;
+             return d;
+           })
+      .def("reset_phases", [](PySolver& p) { p.chk().reset_phases(); })
       .def("init",
            [](PySolver& p, const std::string& kind, uint64_t seed, double lo, double hi, double value,
               double edge, double interior, double density) {
@@ -342,8 +354,9 @@ PYBIND11_MODULE(_mdfx, m) {
            })
       .def("set_options",
            [](PySolver& p, bool overlap, bool sync_debug, int residual_every, bool graph,
-              double timeout_s) {
+              double timeout_s, bool profile) {
              SolverOptions o = p.chk().options();
+             o.profile = profile;
              o.overlap = overlap;
              o.sync_debug = sync_debug;
              o.residual_every = residual_every;
@@ -352,7 +365,7 @@ PYBIND11_MODULE(_mdfx, m) {
              p.chk().set_options(o);
            },
            py::arg("overlap") = true, py::arg("sync_debug") = false, py::arg("residual_every") = 0,
-           py::arg("graph") = false, py::arg("timeout_s") = 0.0)
+           py::arg("graph") = false, py::arg("timeout_s") = 0.0, py::arg("profile") = false)
       .def_property_readonly("num_local", [](PySolver& p) { return p.chk().num_local(); })
       .def_property_readonly("temporal", [](PySolver& p) { return p.chk().options().temporal; })
       .def_property_readonly("nranks", [](PySolver& p) { return p.chk().nranks(); })
