@@ -40,8 +40,8 @@ TESTS      := $(BIN)/mdfx_tests
 
 LINK_ROCM  := -L$(ROCM)/lib -lamdhip64 -lrccl -lgomp -lpthread -ldl
 
-.PHONY: all lib pymod apps tests clean
-all: lib pymod apps tests
+.PHONY: all lib pymod apps tests asan clean
+all: lib pymod apps tests asan
 
 lib: $(LIB)
 pymod: $(PYMOD)
@@ -77,6 +77,27 @@ $(TESTS): csrc/tests/test_main.cpp $(LIB) $(HEADERS)
 	@mkdir -p $(BIN)
 	$(CXX_HOST) $(HOSTFLAGS) -o $@ $< -L$(LIBDIR) -lmdfx $(LINK_ROCM) \
 	  -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -Wl,-rpath,$(ROCM)/lib
+
+# Host AddressSanitizer + UBSan build of the native tests (host code only: GPU sanitizers are not
+# available on the MI355X pool; on hipcc lines every -fsanitize= follows -Xarch_host).
+ASAN_DIR   := build/asan
+ASAN_HOST  := -fsanitize=address -fsanitize=undefined -fno-omit-frame-pointer -g
+ASAN_HIP   := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
+ASAN_KOBJ  := $(patsubst csrc/%.hip,$(ASAN_DIR)/%.o,$(KERNEL_SRC))
+ASAN_HOBJ  := $(patsubst csrc/%.cpp,$(ASAN_DIR)/%.o,$(HOST_SRC))
+asan: $(BIN)/mdfx_tests_asan
+
+$(ASAN_DIR)/%.o: csrc/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(ASAN_HIP) -O1 -c $< -o $@
+
+$(ASAN_DIR)/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX_HOST) $(HOSTFLAGS) $(ASAN_HOST) -O1 -c $< -o $@
+
+$(BIN)/mdfx_tests_asan: $(ASAN_DIR)/tests/test_main.o $(ASAN_KOBJ) $(ASAN_HOBJ)
+	@mkdir -p $(BIN)
+	$(CXX_HOST) $(ASAN_HOST) -o $@ $^ $(LINK_ROCM) -fopenmp -Wl,-rpath,$(ROCM)/lib
 
 clean:
 	rm -rf build $(LIB) $(PYMOD)

@@ -2,6 +2,7 @@
 #include "cli_common.hpp"
 
 #include <chrono>
+#include <csignal>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -391,6 +392,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     return 0;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "%s: error: %s\n", prog, e.what());
+    std::fflush(stderr);
     return 1;
   }
 }

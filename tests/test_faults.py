@@ -38,14 +38,32 @@ def test_dead_peer_is_an_error_not_a_hang():
     assert b"peer closed the connection" in p.stderr or b"peer gone" in p.stderr
 
 
-@pytest.mark.skipif(MPIEXEC is None, reason="no mpiexec in this image")
 def test_hung_peer_times_out():
-    p, dt = _run([MPIEXEC, "-np", "2", BIN, "--backend", "cpu", "--stencil", "5", "--h", "40", "--w", "40",
-                  "--steps", "20"],
-                 {"MDFX_FAULT": "hang@1:3", "MDFX_TCP_TIMEOUT_S": "2", "MDFX_PORT": str(34000 + os.getpid() % 700)},
-                 timeout=120)
-    assert p.returncode != 0 and dt < 100
-    assert b"timed out" in p.stderr
+    """Rank 1 stops responding: rank 0 must fail within the TCP timeout instead of waiting forever.
+    (Tearing down the hung rank is the launcher's job: torchrun does; the test kills it.)"""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, PMI_RANK=str(r), PMI_SIZE="2", MDFX_PORT=str(port), MDFX_FAULT="hang@1:3",
+                   MDFX_TCP_TIMEOUT_S="2", OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([BIN, "--backend", "cpu", "--stencil", "5", "--h", "40", "--w", "40",
+                                       "--steps", "20"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      cwd="/tmp"))
+    try:
+        t0 = time.time()
+        _, err = procs[0].communicate(timeout=60)
+        assert procs[0].returncode != 0 and time.time() - t0 < 60
+        assert b"timed out" in err
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
 
 
 def test_python_engine_nan_guard():

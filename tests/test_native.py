@@ -1,0 +1,32 @@
+"""Native unit tests (csrc/tests/test_main.cpp) as built, and under host AddressSanitizer +
+UndefinedBehaviorSanitizer (make asan; host code only — GPU sanitizers are not available on the
+MI355X pool). CPU tier: the GPU is hidden so the sanitizer run never touches a device."""
+
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "build", "bin")
+
+
+def _run(name, extra_env=None):
+    exe = os.path.join(BIN, name)
+    if not os.path.exists(exe):
+        pytest.fail("%s is not built (make -j8 all)" % name)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="", OMP_NUM_THREADS="4")
+    env.update(extra_env or {})
+    p = subprocess.run([exe], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=600)
+    assert p.returncode == 0, p.stderr.decode()[-4000:]
+    return p.stdout.decode() + p.stderr.decode()
+
+
+def test_native_unit_tests_cpu():
+    assert "all passed" in _run("mdfx_tests")
+
+
+def test_native_unit_tests_asan_ubsan():
+    out = _run("mdfx_tests_asan", {"ASAN_OPTIONS": "detect_leaks=0:abort_on_error=1",
+                                   "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
+    assert "all passed" in out and "runtime error" not in out
