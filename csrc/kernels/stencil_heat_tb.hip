@@ -209,7 +209,16 @@ static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   int zc = env_int("MDFX_ZC", 0);
-  if (zc <= 0) zc = pick_zc(planes, YT, 128, env_int("MDFX_BLOCKS", 4096));
+  if (zc <= 0) {
+    // Short z-chunks keep the tiles resident on an XCD at nearly the same z, so the u0 halo rows
+    // each tile shares with its y neighbours are still in that XCD's L2 when the neighbour reads
+    // them. 1024^3 fp32: zc 128 fetched 2.00x the field (FETCH_SIZE x2) at 1.026 ms/step, zc 32
+    // 1.25x at 0.964 ms/step (profiles/r01_tb2_zc_sweep.txt). Thin slabs trade a little of that for
+    // enough blocks to fill the chip.
+    zc = 32;
+    while (zc > 16 && (int64_t)YT * ((planes + zc - 1) / zc) < 1024) zc /= 2;
+    zc = (int)std::min<int64_t>(zc, std::max<int64_t>(planes, 1));
+  }
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
