@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (scripts/pmc_profile.sh) into one table per kernel.
+
+FETCH_SIZE / WRITE_SIZE are in KB; on gfx950 FETCH_SIZE counts half the bytes of a wide streaming
+read (MI355X_MICROARCH.md §HBM), so the 'fetch/field' column doubles it."""
+import collections
+import csv
+import glob
+import sys
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+field = float(sys.argv[2]) if len(sys.argv) > 2 else 1024 ** 3 * 4
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+dur = collections.defaultdict(list)
+for f in sorted(glob.glob(root + "/p*/run_counter_collection.csv")):
+    for row in csv.DictReader(open(f)):
+        k = row["Kernel_Name"]
+        if "mdfx" not in k:
+            continue
+        name = k.split("(")[0].replace("void mdfx::dev::", "")
+        agg[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+        dur[name].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
+print("%-44s %9s %11s %11s %8s %8s %9s" % ("kernel", "ms(prof)", "fetch/field", "write/field", "L2 hit", "LDSconf", "busy%"))
+for k, d in agg.items():
+    m = lambda c: sum(d[c]) / len(d[c]) if d.get(c) else float("nan")
+    fetch = 2 * m("FETCH_SIZE") * 1024 / field
+    write = m("WRITE_SIZE") * 1024 / field
+    hit = m("TCC_HIT_sum") / (m("TCC_HIT_sum") + m("TCC_MISS_sum"))
+    busy = 100 * m("SQ_ACTIVE_INST_ANY") / m("SQ_WAVE_CYCLES") if d.get("SQ_WAVE_CYCLES") else float("nan")
+    print("%-44s %9.3f %11.3f %11.3f %7.1f%% %8.0f %8.1f%%" % (k[:44], min(dur[k]), fetch, write, 100 * hit,
+                                                             m("SQ_LDS_BANK_CONFLICT"), busy))
