@@ -57,3 +57,39 @@ __device__ __forceinline__ void wave_atomic_add(double* dst, double v) {
 
 }  // namespace dev
 }  // namespace mdfx
+
+namespace mdfx {
+namespace dev {
+
+// Whole-wave lane shifts by one (lane i <- lane i-1 / lane i+1) with DPP wave_shr:1 / wave_shl:1:
+// a VALU move with a DPP modifier instead of a ds_bpermute through the LDS crossbar. The lane that
+// has no source (0 or 63) receives 0; callers overwrite it with the seam value.
+#ifndef MDFX_NO_DPP
+__device__ __forceinline__ int dpp_shr1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_shl1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, false); }
+__device__ __forceinline__ float lane_up1(float v) { return __int_as_float(dpp_shr1_i(__float_as_int(v))); }
+__device__ __forceinline__ float lane_down1(float v) { return __int_as_float(dpp_shl1_i(__float_as_int(v))); }
+__device__ __forceinline__ double lane_up1(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_shr1_i((int)(b & 0xffffffffll)), hi = dpp_shr1_i((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_down1(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_shl1_i((int)(b & 0xffffffffll)), hi = dpp_shl1_i((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+#else
+template <class T>
+__device__ __forceinline__ T lane_up1(T v) { return __shfl_up(v, 1, 64); }
+template <class T>
+__device__ __forceinline__ T lane_down1(T v) { return __shfl_down(v, 1, 64); }
+#endif
+// A/B twin of lane_up1 / lane_down1 through ds_bpermute (the __shfl path)
+template <class T>
+__device__ __forceinline__ T lane_up1_bp(T v) { return __shfl_up(v, 1, 64); }
+template <class T>
+__device__ __forceinline__ T lane_down1_bp(T v) { return __shfl_down(v, 1, 64); }
+
+}  // namespace dev
+}  // namespace mdfx

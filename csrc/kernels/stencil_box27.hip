@@ -102,8 +102,8 @@ __global__ __launch_bounds__(256) void box27_zw(const T* __restrict__ in, T* __r
     V H[RR];
 #pragma unroll
     for (int j = 0; j < RR; ++j) {
-      T l = __shfl_up(R[j][N - 1], 1, 64);
-      T rr = __shfl_down(R[j][0], 1, 64);
+      T l = lane_up1(R[j][N - 1]);
+      T rr = lane_down1(R[j][0]);
       if (lane == 0) l = (WXN > 1 && wx > 0) ? edge[buf][w - 1][j][1] : EL[j];
       if (lane == 63) rr = (WXN > 1 && wx < WXN - 1) ? edge[buf][w + 1][j][0] : ER[j];
 #pragma unroll

@@ -143,8 +143,8 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
       if (y >= g.ny) break;
       const V c = C[i];
       V o = c;
-      T l = __shfl_up(c[N - 1], 1, 64);
-      T rr = __shfl_down(c[0], 1, 64);
+      T l = lane_up1(c[N - 1]);
+      T rr = lane_down1(c[0]);
       if (lane == 0) l = (WXN > 1 && wx > 0) ? edge[buf][w - 1][i][1] : EL[i];
       if (lane == 63) rr = (WXN > 1 && wx < WXN - 1) ? edge[buf][w + 1][i][0] : ER[i];
       if (!zb && y != 0 && y != g.ny - 1) {
@@ -237,8 +237,8 @@ __global__ __launch_bounds__(256) void jacobi5_wave(const T* __restrict__ in, T*
     const int64_t gz = lz + g.gz_off;
     const V c = C;
     V o = c;
-    T l = __shfl_up(c[N - 1], 1, 64);
-    T rr = __shfl_down(c[0], 1, 64);
+    T l = lane_up1(c[N - 1]);
+    T rr = lane_down1(c[0]);
     if (lane == 0) l = EL;
     if (lane == 63) rr = ER;
     if (gz != 0 && gz != g.gnz - 1) {

@@ -38,7 +38,7 @@ __device__ __forceinline__ V vsplat_tb(T v) {
   return r;
 }
 
-template <class T, int RY, int WXN, bool RES, int PF>
+template <class T, int RY, int WXN, bool RES, int PF, bool BP = false>
 __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g,
                                                  T r, int zc, int YT, double* __restrict__ resid) {
   using V = typename VT<T>::type;
@@ -122,8 +122,8 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
         const int64_t y = y0 - 1 + j;
         const V cc = M0[j + 1];
         V o = cc;
-        T l = __shfl_up(cc[N - 1], 1, 64);
-        T rr = __shfl_down(cc[0], 1, 64);
+        T l = BP ? lane_up1_bp(cc[N - 1]) : lane_up1(cc[N - 1]);
+        T rr = BP ? lane_down1_bp(cc[0]) : lane_down1(cc[0]);
         if (lane == 0) l = wx > 0 ? edge[buf][w - 1][j][1] : T(0);
         if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][j][0] : T(0);
         if (!zb && y > 0 && y < g.ny - 1) {
@@ -151,8 +151,8 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
         if (y >= g.ny) break;
         const V cc = U1b[i + 1];
         V o = cc;
-        T l = __shfl_up(cc[N - 1], 1, 64);
-        T rr = __shfl_down(cc[0], 1, 64);
+        T l = BP ? lane_up1_bp(cc[N - 1]) : lane_up1(cc[N - 1]);
+        T rr = BP ? lane_down1_bp(cc[0]) : lane_down1(cc[0]);
         if (lane == 0) l = wx > 0 ? edge[buf][w - 1][R1 + i][1] : T(0);
         if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][R1 + i][0] : T(0);
         if (!zb && y != 0 && y != g.ny - 1) {
@@ -213,9 +213,10 @@ static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, 
     // Short z-chunks keep the tiles resident on an XCD at nearly the same z, so the u0 halo rows
     // each tile shares with its y neighbours are still in that XCD's L2 when the neighbour reads
     // them. 1024^3 fp32: zc 128 fetched 2.00x the field (FETCH_SIZE x2) at 1.026 ms/step, zc 32
-    // 1.25x at 0.964 ms/step (profiles/r01_tb2_zc_sweep.txt). Thin slabs trade a little of that for
-    // enough blocks to fill the chip.
-    zc = 32;
+    // 1.25x at 0.964 ms/step (profiles/r01_tb2_zc_sweep.txt); zc 64 0.930 vs zc 32 0.978 ms/step
+    // in one process (profiles/r01_tb2_dpp_zc.txt). Thin slabs trade a little of that for enough
+    // blocks to fill the chip.
+    zc = 64;
     while (zc > 16 && (int64_t)YT * ((planes + zc - 1) / zc) < 1024) zc /= 2;
     zc = (int)std::min<int64_t>(zc, std::max<int64_t>(planes, 1));
   }
@@ -223,6 +224,8 @@ static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
     hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, true, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+  else if (RY == 2 && env_int("MDFX_TB_BP", 0))  // A/B: neighbour lanes through ds_bpermute
+    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
   else
     hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
 }
