@@ -4,9 +4,12 @@
 // per cell per step). This kernel reads u^t once and writes u^{t+2} once, computing u^{t+1} on
 // chip, so a sweep advances two steps for the same HBM bytes.
 //
-// Geometry: one block = 4 waves along x covering the WHOLE row (nx <= 4 * 64 * N, i.e. 1024 fp32 /
-// 512 fp64), so the block's x edges are the Dirichlet boundary and no x halo is needed; RY rows
-// per lane; the block marches along z over `zc` output planes. Per z-iteration with u1 plane c:
+// Geometry: one block = 4 waves along x; RY rows per lane; the block marches along z over `zc`
+// output planes. Rows up to 4 * 64 * N wide (1024 fp32 / 512 fp64) are covered by ONE block, whose
+// x edges are then the Dirichlet boundary. Wider rows are cut into aligned x tiles of 4 * 64 * N
+// cells (2048^2 rows: exactly 2 tiles). A tile needs two u0 columns of each x neighbour: the edge
+// wave streams them (one 16-B vector per row, prefetched a plane ahead, L2 hits) through a small
+// LDS plane ring, and its seam lane recomputes the neighbour's u1 column from that ring. Per z-iteration with u1 plane c:
 //   u1(c)   rows y0-1 .. y0+RY   from u0 planes c-1, c, c+1 (rows y0-2 .. y0+RY+1 of plane c)
 //   u2(c-1) rows y0   .. y0+RY-1 from u1 planes c-2, c-1, c
 // u0 planes are loaded once (RY+4 rows each: the y halo rows are L2 hits shared with the
@@ -38,9 +41,9 @@ __device__ __forceinline__ V vsplat_tb(T v) {
   return r;
 }
 
-template <class T, int RY, int WXN, bool RES, int PF, bool BP = false>
-__global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g,
-                                                 T r, int zc, int YT, double* __restrict__ resid) {
+template <class T, int RY, int WXN, bool RES, int PF, bool BP = false, bool XT = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <= 2 ? 3 : 1))) void heat7_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g,
+                                                 T r, int zc, int YT, int XTn, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   constexpr int N = VT<T>::N;
   constexpr int WX = 64 * N;
@@ -48,15 +51,20 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
   constexpr int R0 = RY + 4;  // u0 rows y0-2 .. y0+RY+1
   constexpr int R1 = RY + 2;  // u1 rows y0-1 .. y0+RY
   __shared__ T edge[2][4][R1 + RY][2];
-  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const unsigned t0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int xt = XT ? t0 % XTn : 0;  // x tiles fastest: neighbours share their overlap vectors in L2
+  const unsigned t = XT ? t0 / XTn : t0;
   const int yt = t % YT;
   const int zt = t / YT;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wx = w % WXN, wy = w / WXN;
-  const int64_t xw = (int64_t)wx * WX;
+  constexpr int TW = WXN * WX;  // x tile width (XT implies WXN == 4)
+  const int64_t X0 = (int64_t)xt * TW;
+  const int64_t xw = X0 + (int64_t)wx * WX;
   const uint32_t xo = (uint32_t)lane * N;
   const int64_t x = xw + xo;
+  const bool hl = XT && X0 > 0, hr = XT && X0 + TW < g.pitch;  // neighbour tiles
   const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
   const int64_t zs = g.lz_begin + (int64_t)zt * zc;
   const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
@@ -74,6 +82,41 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
     }
     return v;
   };
+
+  // x-tiled rows: lanes 0..R0-1 of the edge wave stream the two u0 columns beyond the tile edge
+  // (one 16-B vector per row) into a 4-plane LDS ring; the seam lane computes the neighbour
+  // tile's u1 column from it. Only that one wave writes and reads its side of the ring.
+  __shared__ T hx[4][2][R0][2];  // [plane & 3][left/right][window row][adjacent column, next]
+  const bool hw = (hl && wx == 0) || (hr && wx == WXN - 1);
+  const int side = wx == 0 ? 0 : 1;
+  auto ldhv = [&](int64_t lz) -> V {
+    V v = vsplat_tb<V>(T(0));
+    const int64_t y = y0 - 2 + lane;
+    if (lane < R0 && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny)
+      v = *(const V*)(ib + lz * plane + (int64_t)lane * pitch + (side == 0 ? -N : WX));
+    return v;
+  };
+  auto puthv = [&](int64_t lz, V v) {
+    if (lane < R0) {
+      hx[lz & 3][side][lane][0] = side == 0 ? v[N - 1] : v[0];
+      hx[lz & 3][side][lane][1] = side == 0 ? v[N - 2] : v[1];
+    }
+  };
+  // u1 at the neighbour column of side sd, plane p, row y0 + i; `inner` = u0 of this tile's edge cell
+  auto u1h = [&](int64_t p, int sd, int i, T inner) -> T {
+    const int k = i + 2, sp = (int)(p & 3);
+    const T cc = hx[sp][sd][k][0];
+    const int64_t y = y0 + i, gz = p + g.gz_off, xh = sd == 0 ? X0 - 1 : X0 + TW;
+    if (gz <= 0 || gz >= g.gnz - 1 || y <= 0 || y >= g.ny - 1 || xh >= g.nx - 1) return cc;
+    const T out_ = hx[sp][sd][k][1];
+    return sm::heat7<T>(cc, sd == 0 ? out_ : inner, sd == 0 ? inner : out_, hx[sp][sd][k - 1][0],
+                        hx[sp][sd][k + 1][0], hx[(p - 1) & 3][sd][k][0], hx[(p + 1) & 3][sd][k][0], r);
+  };
+  V HV;
+  if (XT && hw) {
+    puthv(zs - 1, ldhv(zs - 1));
+    HV = ldhv(zs);
+  }
 
   V L0[R0], M0[R0], H0[R0];  // u0 planes c-1, c, c+1
   V U1a[R1], U1b[R1];        // u1 planes c-2, c-1
@@ -110,6 +153,10 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
 #pragma unroll
       for (int i = 0; i < RY; ++i) edge[buf][w][R1 + i][1] = U1b[i + 1][N - 1];
     }
+    if (XT && hw) {  // stream the next u0 halo columns into the ring (plane c+1 now, c+2 prefetched)
+      puthv(c + 1, HV);
+      HV = ldhv(c + 2);
+    }
     __syncthreads();
 
     // ---- u1 at plane c ------------------------------------------------------------------
@@ -124,8 +171,8 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
         V o = cc;
         T l = BP ? lane_up1_bp(cc[N - 1]) : lane_up1(cc[N - 1]);
         T rr = BP ? lane_down1_bp(cc[0]) : lane_down1(cc[0]);
-        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][j][1] : T(0);
-        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][j][0] : T(0);
+        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][j][1] : (hl ? hx[c & 3][0][j + 1][0] : T(0));
+        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][j][0] : (hr ? hx[c & 3][1][j + 1][0] : T(0));
         if (!zb && y > 0 && y < g.ny - 1) {
           const V ym = M0[j], yp = M0[j + 2], zm = L0[j + 1], zp = H0[j + 1];
 #pragma unroll
@@ -153,8 +200,8 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
         V o = cc;
         T l = BP ? lane_up1_bp(cc[N - 1]) : lane_up1(cc[N - 1]);
         T rr = BP ? lane_down1_bp(cc[0]) : lane_down1(cc[0]);
-        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][R1 + i][1] : T(0);
-        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][R1 + i][0] : T(0);
+        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][R1 + i][1] : (hl ? u1h(lz, 0, i, L0[i + 2][0]) : T(0));
+        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][R1 + i][0] : (hr ? u1h(lz, 1, i, L0[i + 2][N - 1]) : T(0));
         if (!zb && y != 0 && y != g.ny - 1) {
           const V ym = U1b[i], yp = U1b[i + 2], zm = U1a[i + 1], zp = U1c[i + 1];
 #pragma unroll
@@ -198,7 +245,8 @@ __global__ __launch_bounds__(256) void heat7_tb2(const T* __restrict__ in, T* __
 template <class T>
 bool heat7_tb2_supported(const Geo& g) {
   constexpr int WX = 64 * VT<T>::N;
-  return g.nx <= 4 * WX && g.pitch <= 4 * WX && g.ny >= 1;
+  (void)WX;  // any row width: rows wider than one block are x-tiled
+  return g.nx >= 1 && g.ny >= 1;
 }
 template bool heat7_tb2_supported<float>(const Geo&);
 template bool heat7_tb2_supported<double>(const Geo&);
@@ -206,6 +254,8 @@ template bool heat7_tb2_supported<double>(const Geo&);
 template <class T, int RY, int WXN, int PF>
 static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int WYN = 4 / WXN;
+  constexpr int N = VT<T>::N, WX = 64 * N;
+  const int XTn = g.pitch <= 4 * WX ? 1 : (int)((g.pitch + 4 * WX - 1) / (4 * WX));
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   int zc = env_int("MDFX_ZC", 0);
@@ -217,17 +267,22 @@ static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, 
     // in one process (profiles/r01_tb2_dpp_zc.txt). Thin slabs trade a little of that for enough
     // blocks to fill the chip.
     zc = 64;
-    while (zc > 16 && (int64_t)YT * ((planes + zc - 1) / zc) < 1024) zc /= 2;
+    while (zc > 16 && (int64_t)XTn * YT * ((planes + zc - 1) / zc) < 1024) zc /= 2;
     zc = (int)std::min<int64_t>(zc, std::max<int64_t>(planes, 1));
   }
   const int ZT = (int)((planes + zc - 1) / zc);
-  const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
-  if (resid)
-    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, true, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+  const dim3 grd((unsigned)((int64_t)XTn * YT * ZT)), blk(256);
+  if (XTn > 1) {
+    if (resid)
+      hipLaunchKernelGGL((heat7_tb2<T, RY, 4, true, PF, false, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
+    else
+      hipLaunchKernelGGL((heat7_tb2<T, RY, 4, false, PF, false, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
+  } else if (resid)
+    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, true, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
   else if (RY == 2 && env_int("MDFX_TB_BP", 0))  // A/B: neighbour lanes through ds_bpermute
-    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
   else
-    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
 }
 
 template <class T, int RY, int PF>

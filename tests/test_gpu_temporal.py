@@ -12,7 +12,10 @@ from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, i
 
 CASES = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=15),
          models.heat3d(nx=256, ny=9, nz=12), models.heat3d(nx=500, ny=21, nz=11, dtype="f64"),
-         models.heat3d(nx=64, ny=64, nz=9, r=0.1)]
+         models.heat3d(nx=64, ny=64, nz=9, r=0.1),
+         # rows wider than one block: overlapping x tiles (3 tiles f32, 3 tiles f64, a 2-tile remainder)
+         models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, ny=9, nz=9, dtype="f64"),
+         models.heat3d(nx=1030, ny=7, nz=8)]
 
 
 def _two_single_steps(prob, lay, src, device):
@@ -25,8 +28,9 @@ def _two_single_steps(prob, lay, src, device):
     apply_stencil(prob, lay, a, b)
     c = alloc_field(lay, device)
     c.copy_(b)
-    apply_stencil(prob, lay, b, c)
-    return c
+    res = torch.zeros((), dtype=torch.float64, device=device)
+    apply_stencil(prob, lay, b, c, resid=res)
+    return c, res
 
 
 @pytest.mark.parametrize("prob", CASES, ids=lambda p: p.describe().replace(" ", "_"))
@@ -41,7 +45,7 @@ def test_fused_two_steps_bitwise(hip, prob, tbry, monkeypatch):
     apply_stencil(prob, lay, src, fused, steps=2, resid=res)
     set_kernel_variant("naive")
     try:
-        ref = _two_single_steps(prob, lay, src, "cuda")
+        ref, ref_res = _two_single_steps(prob, lay, src, "cuda")
     finally:
         set_kernel_variant("auto")
     torch.cuda.synchronize()
@@ -52,7 +56,8 @@ def test_fused_two_steps_bitwise(hip, prob, tbry, monkeypatch):
     cpu_out = alloc_field(lay, "cpu")
     apply_stencil(prob, lay, cpu_src, cpu_out, steps=2)
     assert torch.equal(fused[o, :, :lay.nx].cpu(), cpu_out[o, :, :lay.nx])
-    assert res.item() > 0
+    # the fused residual is that of the second step (summation order differs)
+    assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
 def test_fused_region_on_a_slab_with_ghosts(hip):
@@ -105,6 +110,10 @@ def test_engine_temporal2_graph_and_residual(hip):
     assert np.array_equal(ref, got2)
 
 
-def test_engine_temporal2_unsupported_width_rejected(hip):
-    with pytest.raises(RuntimeError, match="fused"):
-        mm.Simulation(mm.heat3d(nx=2048, ny=8, nz=8), device="hip", temporal=2)
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_engine_temporal2_wide_rows(hip, dtype):
+    """2048-wide rows (the 2048^3 fp64 config's width) run x-tiled and stay bitwise."""
+    prob = mm.heat3d(nx=2048, ny=12, nz=20, dtype=dtype)
+    ref, _ = _sim(prob, 7, ranks=1)
+    got, _ = _sim(prob, 7, ranks=2, temporal=2)
+    assert np.array_equal(ref, got)
