@@ -1,0 +1,48 @@
+"""Static resource check of every gfx950 kernel in libmdfx.so (VGPR / LDS / occupancy
+checked in CI). Reads the AMDHSA metadata of the code objects; no GPU needed."""
+
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+from kernel_resources import kernel_resources  # noqa: E402
+
+LIB = os.path.join(ROOT, "mpi_cuda_process_amd", "lib", "libmdfx.so")
+
+
+@pytest.fixture(scope="module")
+def recs():
+    if not os.path.exists(LIB):
+        pytest.fail("libmdfx.so is not built (make -j8 all)")
+    r = kernel_resources(LIB)
+    assert len(r) > 50
+    return {x["name"].split("(")[0].replace("void ", ""): x for x in r}
+
+
+def test_no_kernel_spills_to_scratch(recs):
+    # VGPR spills go to scratch memory (HBM round trips inside the z-march). SGPR spills land in
+    # VGPR lanes (v_writelane / v_readlane) and are tolerated; profiles/r01_kernel_resources.txt
+    # lists them.
+    bad = [n for n, r in recs.items() if r.get("private_segment_fixed_size", 0) or r.get("vgpr_spill_count", 0)]
+    assert not bad, bad
+
+
+def test_lds_fits_with_many_blocks_per_cu(recs):
+    # 160 KiB LDS per CU: every kernel leaves room for >= 8 resident blocks
+    assert max(r.get("group_segment_fixed_size", 0) for r in recs.values()) <= 20 * 1024
+
+
+@pytest.mark.parametrize("name,min_waves", [
+    ("mdfx::dev::heat7_tb2<float, 2, 4, false, 1, false, false>", 3),   # headline fused sweep
+    ("mdfx::dev::heat7_tb2<float, 2, 4, false, 1, false, true>", 3),    # x-tiled rows
+    ("mdfx::dev::heat7_tb2<double, 2, 4, false, 1, false, true>", 3),
+    ("mdfx::dev::heat7_zw<float, 2, 4, false, false, 1>", 6),           # single-step default
+    ("mdfx::dev::box27_zw<float, 2, 4, false>", 4),
+])
+def test_default_kernels_keep_their_occupancy(recs, name, min_waves):
+    assert name in recs, sorted(k for k in recs if name.split("<")[0] in k)[:8]
+    assert recs[name]["waves_per_simd"] >= min_waves, recs[name]
