@@ -39,6 +39,8 @@ struct Opts {
   bool compat = false;
   int temporal = 1;
   bool profile = false;
+  int dim = 0;
+  std::string dump;
 };
 
 void usage(const char* prog) {
@@ -62,7 +64,10 @@ void usage(const char* prog) {
       "  --json                    one JSON metrics line ; --verbose per-rank detail ; --quiet\n"
       "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n"
       "  --temporal 1|2            time steps fused per memory sweep (2: 3D 7-pt, rows <= one block)\n"
-      "  --profile                 per-phase timing of rank 0 (boundary / interior / exchange)\n",
+      "  --profile                 per-phase timing of rank 0 (boundary / interior / exchange)\n"
+      "  --dim 2|3                 default stencil of that dimension (5 / 7) ; --bc V = --edge V ; --coef R = --r R\n"
+      "  --dump DIR                write the final grid (per-slab raw + JSON header, checkpoint format)\n"
+      "  --trace                   roctx ranges around every phase (rocprofv3 --marker-trace)\n",
       prog);
 }
 
@@ -96,10 +101,10 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--lo") o.lo = std::atof(need(i));
     else if (a == "--hi") o.hi = std::atof(need(i));
     else if (a == "--value") o.value = std::atof(need(i));
-    else if (a == "--edge") o.edge = std::atof(need(i));
+    else if (a == "--edge" || a == "--bc") o.edge = std::atof(need(i));
     else if (a == "--interior") o.interior = std::atof(need(i));
     else if (a == "--density") o.density = std::atof(need(i));
-    else if (a == "--r") o.r = std::atof(need(i));
+    else if (a == "--r" || a == "--coef") o.r = std::atof(need(i));
     else if (a == "--c0") o.c0 = std::atof(need(i));
     else if (a == "--c1") o.c1 = std::atof(need(i));
     else if (a == "--c2") o.c2 = std::atof(need(i));
@@ -120,6 +125,9 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--compat") o.compat = true;
     else if (a == "--temporal") o.temporal = std::atoi(need(i));
     else if (a == "--profile") o.profile = true;
+    else if (a == "--dim") o.dim = std::atoi(need(i));
+    else if (a == "--dump") o.dump = need(i);
+    else if (a == "--trace") setenv("MDFX_TRACE", "1", 1);
     else MDFX_FAIL("unknown option " + a + " (try --help)");
   }
   return o;
@@ -158,9 +166,11 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     std::unique_ptr<Rendezvous> rv;
     if (env.world > 1) rv.reset(new Rendezvous(env));
     const bool root = env.rank == 0;
-    if (o.stencil.empty()) o.stencil = default_stencil;
+    MDFX_CHECK(o.dim == 0 || o.dim == 2 || o.dim == 3, "--dim is 2 or 3");
+    if (o.stencil.empty()) o.stencil = o.dim == 3 ? "7" : (o.dim == 2 ? "5" : default_stencil);
     const StencilKind kind = stencil_from_name(o.stencil);
     const bool is2d = stencil_is_2d(kind);
+    MDFX_CHECK(o.dim == 0 || (o.dim == 2) == is2d, "--dim does not match --stencil " + o.stencil);
 
     // ---- reference dialogue (rank 0 reads, everyone receives) -----------------------------
     const bool sized = o.n || o.nx || o.ny || o.nz || o.h || o.w;
@@ -320,25 +330,6 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     solver.transport().barrier();
 
     // ---- output ---------------------------------------------------------------------------
-    if (o.profile) {
-      // profiled separately from the timed loop (profiling syncs the host every sweep); every
-      // rank runs the extra steps, rank 0 reports its slab
-      SolverOptions po = solver.options();
-      po.profile = true;
-      solver.set_options(po);
-      solver.run(std::min<int64_t>(std::max<int64_t>(o.steps, 2), 50));
-      solver.synchronize();
-      const PhaseStats& ph = solver.phases();
-      const double n = ph.steps ? (double)ph.steps : 1.0;
-      if (root) std::fprintf(stderr,
-                   "profile (rank 0, %lld sweeps, per sweep): boundary %.4f ms | interior %.4f ms | "
-                   "exchange %.4f ms | step %.4f ms | overlap %.0f%%\n",
-                   (long long)ph.steps, ph.boundary_ms / n, ph.interior_ms / n, ph.exchange_ms / n,
-                   ph.step_ms / n,
-                   ph.step_ms > 0 ? 100.0 * (ph.boundary_ms + ph.exchange_ms + ph.interior_ms - ph.step_ms) /
-                                        std::max(1e-9, std::min(ph.boundary_ms + ph.exchange_ms, ph.interior_ms))
-                                  : 0.0);
-    }
     const double cells = (double)g.cells();
     const double gcs = dt > 0 ? cells * (double)o.steps / dt / 1e9 : 0.0;
     const int ngpu = hip ? (env.world > 1 ? env.world : (o.gpus ? o.gpus : 1)) : 0;
@@ -371,14 +362,45 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
         else print_grid<double>(full, g.nx, g.ny, g.nz);
       }
     }
+    if (!o.dump.empty()) solver.save_checkpoint(o.dump);  // the state after --steps, before --profile
+    double ph_b = -1, ph_i = -1, ph_x = -1, ph_s = -1;
+    if (o.profile) {
+      // profiled separately from the timed loop (profiling syncs the host every sweep); every
+      // rank runs the extra steps, rank 0 reports its slab
+      SolverOptions po = solver.options();
+      po.profile = true;
+      solver.set_options(po);
+      solver.run(std::min<int64_t>(std::max<int64_t>(o.steps, 2), 50));
+      solver.synchronize();
+      const PhaseStats& ph = solver.phases();
+      const double n = ph.steps ? (double)ph.steps : 1.0;
+      ph_b = ph.boundary_ms / n;
+      ph_i = ph.interior_ms / n;
+      ph_x = ph.exchange_ms / n;
+      ph_s = ph.step_ms / n;
+      if (root) std::fprintf(stderr,
+                   "profile (rank 0, %lld sweeps, per sweep): boundary %.4f ms | interior %.4f ms | "
+                   "exchange %.4f ms | step %.4f ms | overlap %.0f%%\n",
+                   (long long)ph.steps, ph.boundary_ms / n, ph.interior_ms / n, ph.exchange_ms / n,
+                   ph.step_ms / n,
+                   ph.step_ms > 0 ? 100.0 * (ph.boundary_ms + ph.exchange_ms + ph.interior_ms - ph.step_ms) /
+                                        std::max(1e-9, std::min(ph.boundary_ms + ph.exchange_ms, ph.interior_ms))
+                                  : 0.0);
+    }
     if (root && o.json) {
+      std::string extra;
+      if (ph_s > 0)
+        extra = format(", \"phase_ms\": {\"boundary\": %.5f, \"interior\": %.5f, \"exchange\": %.5f, \"sweep\": %.5f}, "
+                       "\"halo_fraction\": %.4f",
+                       ph_b, ph_i, ph_x, ph_s, (ph_b + ph_x) / ph_s);
       std::printf(
           "{\"metric\": \"GCells/s\", \"value\": %.4f, \"unit\": \"GCells/s\", \"stencil\": \"%s\", \"dtype\": \"%s\", "
           "\"grid\": [%lld, %lld, %lld], \"steps\": %lld, \"seconds\": %.6f, \"ms_per_step\": %.4f, "
-          "\"ranks\": %d, \"n_gpus\": %d, \"transport\": \"%s\", \"overlap\": %s, \"graph\": %s, \"residual\": %.9g}\n",
+          "\"ranks\": %d, \"n_gpus\": %d, \"transport\": \"%s\", \"overlap\": %s, \"graph\": %s, \"residual\": %.9g, \"gcells_per_gpu\": %.4f%s}\n",
           gcs, stencil_name(kind), dtype_name(spec.dtype), (long long)g.nx, (long long)g.ny, (long long)g.nz,
           (long long)o.steps, dt, o.steps ? dt / o.steps * 1e3 : 0.0, nranks, ngpu, solver.transport().name(),
-          o.overlap ? "true" : "false", o.graph ? "true" : "false", solver.stats().last_residual);
+          o.overlap ? "true" : "false", o.graph ? "true" : "false", solver.stats().last_residual,
+          ngpu ? gcs / ngpu : gcs, extra.c_str());
     } else if (root && !o.compat && !o.quiet) {
       std::printf("mdfx: %s %lldx%lldx%lld %s | %d slab(s), %s transport, %s | %lld steps in %.4f s | "
                   "%.4f ms/step | %.2f GCells/s total, %.2f per GPU",

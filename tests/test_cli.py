@@ -122,3 +122,49 @@ def test_mpirun_heat7_json():
     single = run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--stencil", "7", "--n", "20", "--steps", "3",
                   "--json", "--residual-every", "3"])
     assert abs(json.loads(single.strip())["residual"] - rec["residual"]) < 1e-9 * rec["residual"]
+
+
+def _read_dump(d):
+    """Reassemble a --dump / checkpoint directory (per-slab raw + JSON header) into one array."""
+    metas = [json.load(open(os.path.join(d, f))) for f in sorted(os.listdir(d)) if f.endswith(".json")]
+    m0 = metas[0]
+    dt = {"f32": np.float32, "f64": np.float64, "u8": np.uint8}[m0["dtype"]]
+    out = np.zeros((m0["nz"], m0["ny"], m0["nx"]), dtype=dt)
+    for m in metas:
+        raw = np.fromfile(os.path.join(d, "slab_%d.bin" % m["rank"]), dtype=dt)
+        out[m["z0"]:m["z1"]] = raw.reshape(m["z1"] - m["z0"], m["ny"], m["nx"])
+    return out, metas
+
+
+def test_dump_dim_profile_json_matches_python_engine(tmp_path):
+    import mpi_cuda_process_amd as mm
+
+    d = str(tmp_path / "dump")
+    out = run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--dim", "3", "--n", "20", "--steps", "5", "--ranks",
+               "3", "--dump", d, "--json", "--profile", "--trace"])
+    rec = json.loads(out.strip().splitlines()[-1])
+    assert rec["stencil"] == "heat7" and "phase_ms" in rec and 0 <= rec["halo_fraction"] <= 1
+    assert rec["gcells_per_gpu"] > 0
+    got, metas = _read_dump(d)
+    assert len(metas) == 3 and all(m["step"] == 5 for m in metas)  # the dump precedes the profile steps
+    with mm.Simulation(mm.heat3d(n=20), device="cpu", ranks=2) as sim:
+        sim.init()
+        sim.run(5)
+        ref = sim.gather()
+    assert np.array_equal(got, ref.reshape(got.shape))
+
+
+def test_dim_bc_coef_aliases():
+    a = run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--dim", "2", "--h", "12", "--w", "14", "--steps", "3",
+             "--bc", "7", "--coef", "0.2", "--json"])
+    b = run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--stencil", "5", "--h", "12", "--w", "14", "--steps",
+             "3", "--edge", "7", "--r", "0.2", "--json"])
+    assert json.loads(a)["stencil"] == "jacobi5" == json.loads(b)["stencil"]
+    pa = run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--dim", "2", "--h", "12", "--w", "14", "--steps", "3",
+              "--bc", "1", "--coef", "0.2", "--print", "--quiet"])
+    pb = run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--stencil", "5", "--h", "12", "--w", "14", "--steps",
+              "3", "--edge", "1", "--r", "0.2", "--print", "--quiet"])
+    assert pa == pb and "0" in pa  # edges of value 1 print as '0'
+    p = subprocess.run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--dim", "2", "--stencil", "7"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    assert p.returncode != 0 and b"--dim" in p.stderr
