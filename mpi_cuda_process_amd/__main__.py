@@ -1,0 +1,141 @@
+"""Python command line over :class:`mpi_cuda_process_amd.Simulation`.
+
+    python -m mpi_cuda_process_amd --stencil 7 --n 256 --steps 100 --json
+    torchrun --nproc-per-node 2 --master-addr 127.0.0.1 -m mpi_cuda_process_amd --stencil 7 --n 512
+
+The native executables (build/bin/mdfx, mdf, life) are the reference-compatible entry points
+(stdin dialogue). This module is the same engine driven from Python, for launches
+through torchrun and for scripting; it prints the same JSON metrics line (--json) and the same
+print_array dump (--print, reference kernel.cu:115-129).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def _parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="python -m mpi_cuda_process_amd", description=__doc__.split("\n\n")[0])
+    p.add_argument("--stencil", default="7", help="5 | 7 | 27 | life (aliases: mdf, heat7, box27, gol)")
+    p.add_argument("--n", type=int, default=0)
+    p.add_argument("--nx", type=int, default=0)
+    p.add_argument("--ny", type=int, default=0)
+    p.add_argument("--nz", type=int, default=0)
+    p.add_argument("--h", type=int, default=0, help="2D rows")
+    p.add_argument("--w", type=int, default=0, help="2D columns")
+    p.add_argument("--steps", "--iters", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=0)
+    p.add_argument("--dtype", default="f32")
+    p.add_argument("--device", default="auto", help="auto | hip | cpu")
+    p.add_argument("--ranks", type=int, default=None, help="P virtual slabs in this process")
+    p.add_argument("--transport", default="auto", help="auto | rccl | torch | staged | loopback | host")
+    p.add_argument("--residual-every", type=int, default=0)
+    p.add_argument("--temporal", type=int, default=1, help="time steps fused per sweep (2: 3D 7-pt)")
+    p.add_argument("--graph", action="store_true")
+    p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--sync-debug", action="store_true")
+    p.add_argument("--timeout", type=float, default=0.0)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--resume", default="")
+    p.add_argument("--dump", default="", help="write the final grid (checkpoint format) to this directory")
+    p.add_argument("--print", action="store_true", help="print_array dump of the final grid (rank 0)")
+    p.add_argument("--json", action="store_true")
+    return p
+
+
+def _problem(a):
+    from .models import from_name
+
+    kind = from_name(a.stencil).kind  # resolve aliases
+    if kind in ("jacobi5", "life"):
+        h = a.h or a.nz or a.n or 256
+        w = a.w or a.nx or a.n or 256
+        kw = dict(h=h, w=w)
+        if kind == "jacobi5":
+            kw["dtype"] = a.dtype
+        else:
+            kw["seed"] = a.seed
+        return from_name(kind, **kw)
+    n = a.n or 256
+    return from_name(kind, nx=a.nx or n, ny=a.ny or n, nz=a.nz or n, dtype=a.dtype).with_init(seed=a.seed)
+
+
+def print_array(g: np.ndarray, out=sys.stdout) -> None:
+    """The reference's print_array (kernel.cu:115-129): '0' for a cell equal to 1, ' ' otherwise,
+    a newline per row, blank lines around. 3D grids print plane by plane after a "z=<k>" label,
+    like the native CLI."""
+    def rows(a):
+        out.write("\n")
+        for row in a:
+            out.write("".join("0" if v == 1 else " " for v in row) + "\n")
+        out.write("\n")
+
+    if g.ndim == 3 and g.shape[1] > 1:
+        for z in range(g.shape[0]):
+            out.write("z=%d" % z)
+            rows(g[z])
+    else:
+        rows(g.reshape(-1, g.shape[-1]))
+
+
+def main(argv=None) -> int:
+    a = _parser().parse_args(argv)
+    import torch
+    import torch.distributed as dist
+
+    from . import Simulation
+    from .parallel.dist import detect_env, init_distributed
+
+    distributed = detect_env().world > 1 and a.ranks is None
+    if distributed:
+        init_distributed()
+    prob = _problem(a)
+    sim = Simulation(prob, device=a.device, ranks=a.ranks, transport=a.transport, distributed=distributed,
+                     overlap=not a.no_overlap, sync_debug=a.sync_debug, residual_every=a.residual_every,
+                     graph=a.graph, timeout_s=a.timeout, temporal=a.temporal)
+    with sim:
+        if a.resume:
+            sim.load_checkpoint(a.resume)
+        else:
+            sim.init()
+        sim.run(a.warmup)
+        sim.synchronize()
+        if distributed:
+            dist.barrier()
+        t0 = time.perf_counter()
+        sim.run(a.steps)
+        sim.synchronize()
+        dt = time.perf_counter() - t0
+        if distributed:  # the slowest rank defines the step time
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        rank0 = not distributed or dist.get_rank() == 0
+        if a.dump:
+            sim.save_checkpoint(a.dump)
+        if a.print:
+            g = sim.gather()
+            if rank0:
+                print_array(g.reshape(prob.nz, prob.ny, prob.nx))
+        gcs = prob.cells * a.steps / dt / 1e9 if dt > 0 else 0.0
+        if rank0 and a.json:
+            ngpu = (int(os.environ.get("WORLD_SIZE", "1")) if distributed else 1) if sim.device == "hip" else 0
+            print(json.dumps({"metric": "GCells/s", "value": round(gcs, 4), "unit": "GCells/s",
+                              "stencil": prob.kind, "dtype": prob.dtype, "grid": [prob.nx, prob.ny, prob.nz],
+                              "steps": a.steps, "seconds": round(dt, 6),
+                              "ms_per_step": round(dt / max(a.steps, 1) * 1e3, 4), "n_gpus": ngpu,
+                              "device": sim.device, "temporal": sim.temporal, "residual": sim.residual}))
+        elif rank0 and not a.print:
+            print("%s %dx%dx%d %s | %d steps in %.4f s | %.2f GCells/s" % (prob.kind, prob.nx, prob.ny, prob.nz,
+                                                                          prob.dtype, a.steps, dt, gcs))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
