@@ -30,3 +30,16 @@ def test_native_unit_tests_asan_ubsan():
     out = _run("mdfx_tests_asan", {"ASAN_OPTIONS": "detect_leaks=0:abort_on_error=1",
                                    "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
     assert "all passed" in out and "runtime error" not in out
+
+
+def test_cmake_configures(tmp_path):
+    """CMakeLists.txt (the embeddable build) configures against /opt/rocm (hip, rccl, OpenMP);
+    the full build is exercised by scripts/cmake_build.sh."""
+    import shutil
+
+    if shutil.which("cmake") is None:
+        pytest.skip("cmake not installed")
+    p = subprocess.run(["cmake", "-S", ROOT, "-B", str(tmp_path / "b"), "-G", "Ninja"], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=300)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    assert (tmp_path / "b" / "build.ninja").exists()
