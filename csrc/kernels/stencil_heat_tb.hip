@@ -318,5 +318,144 @@ void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hip
 template void launch_heat7_tb2<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
 template void launch_heat7_tb2<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
 
+// ---- 2D 5-point, two steps per sweep ----------------------------------------------------------
+//
+// The reference's own program (MDF_kernel.cu:10-22) fused like heat7_tb2: rows are planes
+// (ny == 1) and each wave is an independent task (x segment of 64*N values, zc rows), so there is
+// no block barrier. Per row c the wave computes u1(c) for its segment and, in lanes 0 / 63, u1 at
+// the one column beyond each segment edge (from a 16-B halo vector those lanes load), then
+// u2(c-1) for the segment. u0 is read once (+ 2 halo vectors per 64 lanes, L2 hits), u2 written
+// once; bitwise equal to two sm::jacobi5 steps.
+template <class T, bool RES>
+__global__ __launch_bounds__(256) void jacobi5_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
+                                                   int zc, int XT, int ntasks, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  const int lane = threadIdx.x & 63;
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;  // wave-uniform; no block barriers in this kernel
+  const int xt = task % XT, zt = task / XT;
+  const int64_t x0 = (int64_t)xt * WX;
+  const int64_t x = x0 + (int64_t)lane * N;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t plane = g.plane;
+  // halo column of this lane: lane 0 -> x0-1 (vector [x0-N, x0)), lane 63 -> x0+WX (vector at x0+WX)
+  const int64_t hcol = lane == 0 ? x0 - 1 : x0 + WX;
+  const int64_t hvec = lane == 0 ? x0 - N : x0 + WX;
+  const bool hin = (lane == 0 && x0 > 0) || (lane == 63 && x0 + WX < g.pitch);
+  const int ha = lane == 0 ? N - 1 : 0;  // element of the halo vector at hcol
+  const int hb = lane == 0 ? N - 2 : 1;  // element one further out
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  const bool hbnd = hcol <= 0 || hcol >= g.nx - 1;
+
+  auto ld = [&](int64_t lz) -> V {
+    V v = vsplat_tb<V>(T(0));
+    if (xin && lz >= 0 && lz < g.lz_max) v = *(const V*)(in + lz * plane + x);
+    return v;
+  };
+  auto ldh = [&](int64_t lz) -> V {
+    V v = vsplat_tb<V>(T(0));
+    if (hin && lz >= 0 && lz < g.lz_max) v = *(const V*)(in + lz * plane + hvec);
+    return v;
+  };
+  V L = ld(zs - 2), M = ld(zs - 1), H = ld(zs);
+  V HL = ldh(zs - 2), HM = ldh(zs - 1), HH = ldh(zs);
+  V Ua = vsplat_tb<V>(T(0)), Ub = Ua;
+  T ub = T(0);  // u1 at the halo column, row c-1
+  double acc = 0.0;
+  for (int64_t c = zs - 1; c <= ze; ++c) {
+    const V NX = ld(c + 2), NXH = ldh(c + 2);
+    // ---- u1 at row c: the segment, then the halo column (lanes 0 / 63)
+    const int64_t gz = c + g.gz_off;
+    const bool zb = gz <= 0 || gz >= g.gnz - 1;
+    V Uc = M;
+    T uc = HM[ha];
+    {
+      T l = lane_up1(M[N - 1]);
+      T rr = lane_down1(M[0]);
+      if (lane == 0) l = HM[N - 1];
+      if (lane == 63) rr = HM[0];
+      if (!zb) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const T xm = e == 0 ? l : M[e - 1];
+          const T xp = e == N - 1 ? rr : M[e + 1];
+          const T v = sm::jacobi5<T>(M[e], xm, xp, L[e], H[e], r);
+          Uc[e] = xb[e] ? M[e] : v;
+        }
+        if (!hbnd) {  // lane 0: neighbours x0-2 | x0 ; lane 63: x0+WX-1 | x0+WX+1
+          const T xm = lane == 0 ? HM[hb] : M[N - 1];
+          const T xp = lane == 0 ? M[0] : HM[hb];
+          uc = sm::jacobi5<T>(HM[ha], xm, xp, HL[ha], HH[ha], r);
+        }
+      }
+    }
+    // ---- u2 at row c-1
+    if (c >= zs + 1) {
+      const int64_t lz = c - 1;
+      const int64_t gz2 = lz + g.gz_off;
+      V o = Ub;
+      T l = lane_up1(Ub[N - 1]);
+      T rr = lane_down1(Ub[0]);
+      if (lane == 0) l = ub;
+      if (lane == 63) rr = ub;
+      if (gz2 != 0 && gz2 != g.gnz - 1) {
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const T xm = e == 0 ? l : Ub[e - 1];
+          const T xp = e == N - 1 ? rr : Ub[e + 1];
+          const T v = sm::jacobi5<T>(Ub[e], xm, xp, Ua[e], Uc[e], r);
+          o[e] = xb[e] ? Ub[e] : v;
+        }
+      }
+      if (xin) {
+        store_nt((V*)(out + lz * plane + x), o);
+        if (RES) {
+#pragma unroll
+          for (int e = 0; e < N; ++e)
+            if (x + e < g.nx) {
+              const double d = (double)o[e] - (double)Ub[e];
+              acc += d * d;
+            }
+        }
+      }
+    }
+    L = M;
+    M = H;
+    H = NX;
+    HL = HM;
+    HM = HH;
+    HH = NXH;
+    Ua = Ub;
+    Ub = Uc;
+    ub = uc;
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T>
+void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  const int64_t planes = g.lz_end - g.lz_begin;
+  if (planes <= 0) return;
+  constexpr int WX = 64 * VT<T>::N;
+  const int XT = (int)((g.nx + WX - 1) / WX);
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const int ntasks = XT * ZT;
+  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((jacobi5_tb2<T, true>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+  else
+    hipLaunchKernelGGL((jacobi5_tb2<T, false>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+}
+template void launch_jacobi5_tb2<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
+template void launch_jacobi5_tb2<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
+
 }  // namespace dev
 }  // namespace mdfx

@@ -15,7 +15,9 @@ CASES = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=1
          models.heat3d(nx=64, ny=64, nz=9, r=0.1),
          # rows wider than one block: overlapping x tiles (3 tiles f32, 3 tiles f64, a 2-tile remainder)
          models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, ny=9, nz=9, dtype="f64"),
-         models.heat3d(nx=1030, ny=7, nz=8)]
+         models.heat3d(nx=1030, ny=7, nz=8),
+         # 2D 5-pt MDF (rows are planes): several segments, a ragged last one, fp64
+         models.mdf2d(h=37, w=1000), models.mdf2d(h=21, w=300, dtype="f64"), models.mdf2d(h=9, w=64)]
 
 
 def _two_single_steps(prob, lay, src, device):
@@ -117,3 +119,12 @@ def test_engine_temporal2_wide_rows(hip, dtype):
     ref, _ = _sim(prob, 7, ranks=1)
     got, _ = _sim(prob, 7, ranks=2, temporal=2)
     assert np.array_equal(ref, got)
+
+
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_engine_temporal2_mdf2d(hip, ranks):
+    """The reference's own 2D MDF problem, fused: equal to single steps for any slab count."""
+    prob = mm.mdf2d(h=300, w=777)
+    ref, rr = _sim(prob, 11, ranks=1, residual_every=11)
+    got, rg = _sim(prob, 11, ranks=ranks, temporal=2, residual_every=11)
+    assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
