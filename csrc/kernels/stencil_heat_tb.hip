@@ -22,6 +22,9 @@
 // Region contract: output storage planes [lz_begin, lz_end) need u0 valid on
 // [lz_begin - 2, lz_end + 2): the engine keeps 2 ghost planes (halo = 2) when temporal blocking is on.
 #include <algorithm>
+#include <cstdio>
+#include <map>
+#include <mutex>
 
 #include "kcommon.hpp"
 #include "mdfx/kernels.hpp"
@@ -251,6 +254,40 @@ bool heat7_tb2_supported(const Geo& g) {
 template bool heat7_tb2_supported<float>(const Geo&);
 template bool heat7_tb2_supported<double>(const Geo&);
 
+// Blocks of kernel `kfn` (256 threads) the whole device holds at once, cached per kernel.
+static int64_t resident_blocks(const void* kfn) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, int64_t> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({dev, kfn});
+  if (it != cache.end()) return it->second;
+  int cus = 0, nb = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 256, 0) != hipSuccess || nb <= 0) nb = 2;
+  if (env_int("MDFX_DEBUG_ZC", 0)) fprintf(stderr, "[mdfx] tb2 residency: %d CUs x %d blocks\n", cus, nb);
+  return cache[{dev, kfn}] = (int64_t)cus * nb;
+}
+
+// z-chunk of a fused sweep over `planes` planes and `tiles` xy tiles: balanced chunks of about 43
+// planes (equal up to one plane), shortened while the grid would not fill the device once.
+// Short chunks keep y-neighbour tiles at nearly the same z, so they share their halo rows in the
+// XCD's L2 (zc 128 fetched 2.00x the field, zc 32 1.25x: profiles/r01_tb2_zc_sweep.txt); balanced
+// ~43-plane chunks were the best or within 1% of it at every slab depth of the 1024^2 strong-
+// scaling shapes, e.g. 1024 x 1024 x 128 (the N = 8 slab): 876 GCells/s at zc 64 vs 1043 at zc 43
+// (profiles/r01_tb2_zc_slabs.txt).
+static int tb2_zc(int64_t planes, int64_t tiles, int64_t resident) {
+  if (planes <= 16) return (int)std::max<int64_t>(planes, 1);
+  int64_t zt = (planes + 43) / 44;
+  int64_t zc = (planes + zt - 1) / zt;
+  while (zt * tiles < resident && zc > 16) {
+    ++zt;
+    zc = (planes + zt - 1) / zt;
+  }
+  return (int)zc;
+}
+
 template <class T, int RY, int WXN, int PF>
 static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int WYN = 4 / WXN;
@@ -258,18 +295,10 @@ static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const int XTn = g.pitch <= 4 * WX ? 1 : (int)((g.pitch + 4 * WX - 1) / (4 * WX));
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
+  const void* kfn = XTn > 1 ? (const void*)&heat7_tb2<T, RY, 4, false, PF, false, true>
+                            : (const void*)&heat7_tb2<T, RY, WXN, false, PF>;
   int zc = env_int("MDFX_ZC", 0);
-  if (zc <= 0) {
-    // Short z-chunks keep the tiles resident on an XCD at nearly the same z, so the u0 halo rows
-    // each tile shares with its y neighbours are still in that XCD's L2 when the neighbour reads
-    // them. 1024^3 fp32: zc 128 fetched 2.00x the field (FETCH_SIZE x2) at 1.026 ms/step, zc 32
-    // 1.25x at 0.964 ms/step (profiles/r01_tb2_zc_sweep.txt); zc 64 0.930 vs zc 32 0.978 ms/step
-    // in one process (profiles/r01_tb2_dpp_zc.txt). Thin slabs trade a little of that for enough
-    // blocks to fill the chip.
-    zc = 64;
-    while (zc > 16 && (int64_t)XTn * YT * ((planes + zc - 1) / zc) < 1024) zc /= 2;
-    zc = (int)std::min<int64_t>(zc, std::max<int64_t>(planes, 1));
-  }
+  if (zc <= 0) zc = tb2_zc(planes, (int64_t)XTn * YT, resident_blocks(kfn));
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XTn * YT * ZT)), blk(256);
   if (XTn > 1) {
