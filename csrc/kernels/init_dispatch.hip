@@ -28,6 +28,7 @@ template <class T>
 void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
                   hipStream_t s);
 void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s);
+void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s);
 template <class T>
 void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
@@ -126,6 +127,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   if (steps == 1) return true;
   if (steps != 2 || lay.halo < 2) return false;
   if (spec.kind == StencilKind::Jacobi5) return spec.dtype == DType::F32 || spec.dtype == DType::F64;
+  if (spec.kind == StencilKind::Life) return true;
   if (spec.kind != StencilKind::Heat7) return false;
   const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
   return spec.dtype == DType::F32 ? dev::heat7_tb2_supported<float>(g) : dev::heat7_tb2_supported<double>(g);
@@ -141,7 +143,9 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
     MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),
                format("no fused %d-step kernel for %s %s at nx=%lld (halo %d)", a.steps, stencil_name(spec.kind),
                       dtype_name(spec.dtype), (long long)a.lay.global.nx, a.lay.halo));
-    if (spec.kind == StencilKind::Jacobi5) {
+    if (spec.kind == StencilKind::Life) {
+      dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
+    } else if (spec.kind == StencilKind::Jacobi5) {
       if (spec.dtype == DType::F32)
         dev::launch_jacobi5_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
       else

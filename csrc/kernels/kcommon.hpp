@@ -67,6 +67,8 @@ namespace dev {
 #ifndef MDFX_NO_DPP
 __device__ __forceinline__ int dpp_shr1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
 __device__ __forceinline__ int dpp_shl1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, false); }
+__device__ __forceinline__ int lane_up1(int v) { return dpp_shr1_i(v); }
+__device__ __forceinline__ int lane_down1(int v) { return dpp_shl1_i(v); }
 __device__ __forceinline__ float lane_up1(float v) { return __int_as_float(dpp_shr1_i(__float_as_int(v))); }
 __device__ __forceinline__ float lane_down1(float v) { return __int_as_float(dpp_shl1_i(__float_as_int(v))); }
 __device__ __forceinline__ double lane_up1(double v) {

@@ -3,7 +3,7 @@
 // Each wave is an independent task (1024 cells of a row x zc rows) marching down the rows. Per
 // row the lane loads 16 cells with one dwordx4 and evaluates them bit-parallel (SWAR) in two
 // 64-bit words: column sums S = north + centre + south (bytes <= 3), then T = S(x-1) + S + S(x+1)
-// via byte shifts with the carry byte taken from the neighbouring lane (ds_bpermute) or, at the
+// via byte shifts with the carry byte taken from the neighbouring lane (DPP shift) or, at the
 // wave edge, from scalar loads; alive' = (T == 3) | (alive & (T == 4)) with exact per-byte
 // equality tests. Reference: game_of_life kernel.cu:10-68 (one int per cell, 8 scalar loads per
 // cell, dead edge branches D9) -> 1 B read + 1 B written per cell here.
@@ -73,8 +73,9 @@ __global__ __launch_bounds__(256) void life_wave(const uint8_t* __restrict__ in,
     U2 o = C;
     if (gz != 0 && gz != g.gnz - 1) {
       const U2 S{P.lo + C.lo + Nx.lo, P.hi + C.hi + Nx.hi};
-      uint64_t sl = __shfl_up(S.hi >> 56, 1, 64);
-      uint64_t sr = __shfl_down(S.lo & 0xFF, 1, 64);
+      // carry bytes from the neighbouring lanes (DPP row shifts; lanes 0 / 63 are replaced below)
+      uint64_t sl = (uint32_t)lane_up1((int)(S.hi >> 56));
+      uint64_t sr = (uint32_t)lane_down1((int)(S.lo & 0xFF));
       if (lane == 0) sl = elP + elC + elN;
       if (lane == 63) sr = erP + erC + erN;
       const U2 L{(S.lo << 8) | sl, (S.hi << 8) | (S.lo >> 56)};
@@ -131,7 +132,9 @@ void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, h
   constexpr int WX = 64 * 16;
   const int XT = (int)((g.nx + WX - 1) / WX);
   int zc = env_int("MDFX_ZC", 0);
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 4096);  // 32768^2: zc 64 beats 128 (profiles/r01_ab_life_u8.json)
+  // 32768^2: zc 64 beats 128 (profiles/r01_ab_life_u8.json), zc 32 beats 64 once the carry bytes
+  // moved to DPP (2414 vs 2351 GCells/s, profiles/r01_life_tb2.txt)
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
@@ -139,6 +142,151 @@ void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, h
     hipLaunchKernelGGL(life_wave<true>, grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
   else
     hipLaunchKernelGGL(life_wave<false>, grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
+}
+
+// ---- two generations per sweep ---------------------------------------------------------------
+//
+// Like jacobi5_tb2: per row c a wave computes generation t+1 of row c for its 1024 cells and, in
+// lanes 0 / 63, of the one cell beyond each segment edge (from a 4-byte load of the two cells
+// beyond the edge), then generation t+2 of row c-1. 1 B read + 1 B written per cell per TWO
+// generations; bitwise equal to two life_wave steps.
+__device__ __forceinline__ U2 ld_u2(const uint8_t* p) {
+  const uint4 q = *(const uint4*)p;
+  return U2{(uint64_t)q.x | ((uint64_t)q.y << 32), (uint64_t)q.z | ((uint64_t)q.w << 32)};
+}
+
+template <bool RES>
+__global__ __launch_bounds__(256) void life_tb2(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                Geo g, int zc, int XT, int ntasks, double* __restrict__ resid) {
+  constexpr int N = 16;
+  constexpr int WX = 64 * N;
+  const int lane = threadIdx.x & 63;
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;  // wave-uniform, no barriers
+  const int xt = task % XT, zt = task / XT;
+  const int64_t x0 = (int64_t)xt * WX;
+  const int64_t x = x0 + (int64_t)lane * N;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t plane = g.plane;
+  // lane 0: cells x0-2, x0-1 (bytes 2, 3 of the word at x0-4); lane 63: x0+WX, x0+WX+1 (bytes 0, 1)
+  const bool hin = (lane == 0 && x0 > 0) || (lane == 63 && x0 + WX < g.pitch);
+  const int64_t hoff = lane == 0 ? x0 - 4 : x0 + WX;
+  const int64_t hcol = lane == 0 ? x0 - 1 : x0 + WX;
+  const bool hframe = hcol <= 0 || hcol >= g.nx - 1;
+  const bool frame = x == 0 || x + N > g.nx - 1;  // frame or pad cells in this lane
+  auto ld = [&](int64_t lz) -> U2 {
+    if (xin && lz >= 0 && lz < g.lz_max) return ld_u2(in + lz * plane + x);
+    return U2{0, 0};
+  };
+  auto ldh = [&](int64_t lz) -> uint32_t {
+    if (hin && lz >= 0 && lz < g.lz_max) return *(const uint32_t*)(in + lz * plane + hoff);
+    return 0u;
+  };
+  // the two halo cells as (adjacent, next): lane 0 -> (byte 3, byte 2), lane 63 -> (byte 0, byte 1)
+  auto hadj = [&](uint32_t w) -> uint64_t { return lane == 0 ? (w >> 24) & 0xFF : w & 0xFF; };
+  auto hnext = [&](uint32_t w) -> uint64_t { return lane == 0 ? (w >> 16) & 0xFF : (w >> 8) & 0xFF; };
+  // own cell next to the halo: lane 0 -> cell 0, lane 63 -> cell 15
+  auto own = [&](const U2& v) -> uint64_t { return lane == 0 ? v.lo & 0xFF : v.hi >> 56; };
+  // one SWAR generation of the lane's 16 cells; esum = 3-row sum of the cell beyond the lane's
+  // wave edge (lane 0: left, lane 63: right)
+  auto gen = [&](const U2& P, const U2& C, const U2& Nn, uint64_t esum) -> U2 {
+    const U2 S{P.lo + C.lo + Nn.lo, P.hi + C.hi + Nn.hi};
+    uint64_t sl = (uint32_t)lane_up1((int)(S.hi >> 56));
+    uint64_t sr = (uint32_t)lane_down1((int)(S.lo & 0xFF));
+    if (lane == 0) sl = esum;
+    if (lane == 63) sr = esum;
+    const U2 L{(S.lo << 8) | sl, (S.hi << 8) | (S.lo >> 56)};
+    const U2 R{(S.lo >> 8) | (S.hi << 56), (S.hi >> 8) | (sr << 56)};
+    const U2 T{L.lo + S.lo + R.lo, L.hi + S.hi + R.hi};
+    U2 o{bytes_eq(T.lo, 3) | (C.lo & bytes_eq(T.lo, 4)), bytes_eq(T.hi, 3) | (C.hi & bytes_eq(T.hi, 4))};
+    if (frame) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const int64_t xe = x + e;
+        if (xe == 0 || xe >= g.nx - 1) {
+          const uint64_t m = 0xFFull << (8 * (e & 7));
+          if (e < 8)
+            o.lo = (o.lo & ~m) | (C.lo & m);
+          else
+            o.hi = (o.hi & ~m) | (C.hi & m);
+        }
+      }
+    }
+    return o;
+  };
+
+  U2 P = ld(zs - 2), C = ld(zs - 1), Nx = ld(zs);
+  uint32_t hP = ldh(zs - 2), hC = ldh(zs - 1), hN = ldh(zs);
+  U2 Ua{0, 0}, Ub{0, 0};
+  uint64_t ha = 0, hb = 0;  // generation t+1 of the halo cell, rows c-2 and c-1
+  double acc = 0.0;
+  for (int64_t c = zs - 1; c <= ze; ++c) {
+    const U2 NN = ld(c + 2);
+    const uint32_t hNN = ldh(c + 2);
+    // ---- generation t+1 of row c (segment + halo cell)
+    const int64_t gz = c + g.gz_off;
+    U2 Uc = C;
+    uint64_t hc = hadj(hC);
+    if (gz > 0 && gz < g.gnz - 1) {
+      Uc = gen(P, C, Nx, hadj(hP) + hadj(hC) + hadj(hN));
+      if (!hframe) {
+        const uint64_t t = (hadj(hP) + hadj(hC) + hadj(hN)) + (hnext(hP) + hnext(hC) + hnext(hN)) +
+                           (own(P) + own(C) + own(Nx));
+        hc = (uint64_t)sm::life_rule((unsigned)t, (unsigned char)hadj(hC));
+      }
+    }
+    // ---- generation t+2 of row c-1
+    if (c >= zs + 1) {
+      const int64_t lz = c - 1;
+      const int64_t gz2 = lz + g.gz_off;
+      U2 o = Ub;
+      if (gz2 != 0 && gz2 != g.gnz - 1) o = gen(Ua, Ub, Uc, ha + hb + hc);
+      if (xin) {
+        uint4 q;
+        q.x = (uint32_t)o.lo;
+        q.y = (uint32_t)(o.lo >> 32);
+        q.z = (uint32_t)o.hi;
+        q.w = (uint32_t)(o.hi >> 32);
+        *(uint4*)(out + lz * plane + x) = q;
+        if (RES) {
+          const uint64_t dlo = o.lo ^ Ub.lo, dhi = o.hi ^ Ub.hi;
+          int cnt = 0;
+          for (int e = 0; e < N; ++e)
+            if (x + e < g.nx) cnt += (int)(((e < 8 ? dlo : dhi) >> (8 * (e & 7))) & 1);
+          acc += (double)cnt;
+        }
+      }
+    }
+    P = C;
+    C = Nx;
+    Nx = NN;
+    hP = hC;
+    hC = hN;
+    hN = hNN;
+    Ua = Ub;
+    Ub = Uc;
+    ha = hb;
+    hb = hc;
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s) {
+  const int64_t planes = g.lz_end - g.lz_begin;
+  if (planes <= 0) return;
+  constexpr int WX = 64 * 16;
+  const int XT = (int)((g.nx + WX - 1) / WX);
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const int ntasks = XT * ZT;
+  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL(life_tb2<true>, grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
+  else
+    hipLaunchKernelGGL(life_tb2<false>, grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
 }
 
 }  // namespace dev

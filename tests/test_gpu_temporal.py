@@ -17,7 +17,9 @@ CASES = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=1
          models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, ny=9, nz=9, dtype="f64"),
          models.heat3d(nx=1030, ny=7, nz=8),
          # 2D 5-pt MDF (rows are planes): several segments, a ragged last one, fp64
-         models.mdf2d(h=37, w=1000), models.mdf2d(h=21, w=300, dtype="f64"), models.mdf2d(h=9, w=64)]
+         models.mdf2d(h=37, w=1000), models.mdf2d(h=21, w=300, dtype="f64"), models.mdf2d(h=9, w=64),
+         # Game of Life (u8 SWAR): several 1024-cell segments, ragged edges
+         models.life2d(h=40, w=3000), models.life2d(h=17, w=1024), models.life2d(h=9, w=100)]
 
 
 def _two_single_steps(prob, lay, src, device):
@@ -128,3 +130,11 @@ def test_engine_temporal2_mdf2d(hip, ranks):
     ref, rr = _sim(prob, 11, ranks=1, residual_every=11)
     got, rg = _sim(prob, 11, ranks=ranks, temporal=2, residual_every=11)
     assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
+
+
+@pytest.mark.parametrize("ranks", [1, 4])
+def test_engine_temporal2_life(hip, ranks):
+    prob = mm.life2d(h=333, w=2100)
+    ref, rr = _sim(prob, 13, ranks=1, residual_every=13)
+    got, rg = _sim(prob, 13, ranks=ranks, temporal=2, residual_every=13)
+    assert np.array_equal(ref, got) and rr == rg
