@@ -8,7 +8,7 @@ import csv
 import glob
 import sys
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_heat7"
 field = float(sys.argv[2]) if len(sys.argv) > 2 else 1024 ** 3 * 4
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(list)
