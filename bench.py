@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--graph", action="store_true", help="replay 2-step cycles as hipGraphs")
     p.add_argument("--temporal", type=int, default=0,
                    help="time steps fused per memory sweep (temporal blocking); 0 = 2 where a fused "
-                        "kernel exists (3D 7-pt, 2D 5-pt, Life), else 1")
+                        "kernel exists (all four stencils; 27-pt rows <= one block), else 1")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
@@ -94,7 +94,7 @@ def main():
     temporal = a.temporal
     if temporal <= 0:
         temporal = 1
-        if a.stencil in ("heat7", "jacobi5", "life") and (not hip or native().hip_supports_steps(
+        if a.stencil in ("heat7", "jacobi5", "life", "box27") and (not hip or native().hip_supports_steps(
                 prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz, 2, 2)):
             temporal = 2
     kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap, graph=a.graph,

@@ -25,6 +25,10 @@ void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipSt
 template <class T>
 void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
+void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid, hipStream_t s);
+template <class T>
+bool box27_tb2_supported(const Geo& g);
+template <class T>
 void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
                   hipStream_t s);
 void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s);
@@ -128,6 +132,10 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   if (steps != 2 || lay.halo < 2) return false;
   if (spec.kind == StencilKind::Jacobi5) return spec.dtype == DType::F32 || spec.dtype == DType::F64;
   if (spec.kind == StencilKind::Life) return true;
+  if (spec.kind == StencilKind::Box27) {
+    const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
+    return spec.dtype == DType::F32 ? dev::box27_tb2_supported<float>(g) : dev::box27_tb2_supported<double>(g);
+  }
   if (spec.kind != StencilKind::Heat7) return false;
   const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
   return spec.dtype == DType::F32 ? dev::heat7_tb2_supported<float>(g) : dev::heat7_tb2_supported<double>(g);
@@ -143,7 +151,12 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
     MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),
                format("no fused %d-step kernel for %s %s at nx=%lld (halo %d)", a.steps, stencil_name(spec.kind),
                       dtype_name(spec.dtype), (long long)a.lay.global.nx, a.lay.halo));
-    if (spec.kind == StencilKind::Life) {
+    if (spec.kind == StencilKind::Box27) {
+      if (spec.dtype == DType::F32)
+        dev::launch_box27_tb2<float>(g, (const float*)a.in, (float*)a.out, spec.coef, a.resid, s);
+      else
+        dev::launch_box27_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.coef, a.resid, s);
+    } else if (spec.kind == StencilKind::Life) {
       dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
     } else if (spec.kind == StencilKind::Jacobi5) {
       if (spec.dtype == DType::F32)

@@ -229,5 +229,254 @@ template void launch_box27<float>(const Geo&, const float*, float*, const Stenci
 template void launch_box27<double>(const Geo&, const double*, double*, const StencilCoef&, double*,
                                    hipStream_t);
 
+// ---- two steps per sweep ----------------------------------------------------------------------
+//
+// The 27-point update fused over two time steps, with the partial-sum factorisation carried
+// through both levels. When u0 plane k enters, each lane forms A0(k), B0(k) for the RY+2 rows of
+// the tile's u1 window and finishes u1(k-1) = (A0(k-2) + B0(k-1)) + A0(k) from a running sum; the
+// u1 plane produced the previous iteration then gets its partials A1, B1 for the RY owned rows and
+// finishes u2(k-3) the same way. Only the running sums, the last A and the centres are carried
+// between planes, so the registers stay close to the 7-point fused kernel. One barrier per plane
+// publishes the wave-seam values of the new u0 plane and of the pending u1 plane together. Rows
+// must fit one block (nx <= 4 * 64 * N); the result is bitwise equal to two box27_zw steps.
+template <class T, int RY, int WXN, bool RES, int PF>
+__global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0,
+                                                 T c1, T c2, T c3, int zc, int YT, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  constexpr int WYN = 4 / WXN;
+  constexpr int R0 = RY + 4;  // u0 rows y0-2 .. y0+RY+1
+  constexpr int R1 = RY + 2;  // u1 rows y0-1 .. y0+RY
+  __shared__ T edge[2][4][R0 + R1][2];
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int yt = t % YT;
+  const int zt = t / YT;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wx = w % WXN, wy = w / WXN;
+  const int64_t xw = (int64_t)wx * WX;
+  const uint32_t xo = (uint32_t)lane * N;
+  const int64_t x = xw + xo;
+  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const T* ib = in + (y0 - 2) * pitch + xw;
+  T* ob = out + y0 * pitch + xw;
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+
+  auto ld = [&](int64_t lz, int k) -> V {
+    V v = vsplat27<V>(T(0));
+    const int64_t y = y0 - 2 + k;
+    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) v = *(const V*)(ib + lz * plane + (int64_t)k * pitch + xo);
+    return v;
+  };
+  // x-neighbour sum of one row vector; `slot` = its seam slot in edge[buf][*]
+  auto hsum = [&](const V& v, int buf, int slot) -> V {
+    T l = lane_up1(v[N - 1]);
+    T r = lane_down1(v[0]);
+    if (lane == 0) l = wx > 0 ? edge[buf][w - 1][slot][1] : T(0);
+    if (lane == 63) r = wx < WXN - 1 ? edge[buf][w + 1][slot][0] : T(0);
+    V h;
+#pragma unroll
+    for (int e = 0; e < N; ++e) h[e] = (e == 0 ? l : v[e - 1]) + (e == N - 1 ? r : v[e + 1]);
+    return h;
+  };
+
+  V Rw[R0];                   // u0 plane k
+  V A0p[R1], S0[R1], C0[R1];  // A0(k-1); A0(k-2) + B0(k-1); u0 plane k-1 (u1 window rows)
+  V U1[R1];                   // u1 plane k-2
+  V A1p[RY], S1[RY], C1[RY];  // A1(k-3); A1(k-4) + B1(k-3); u1 plane k-3 (owned rows)
+#pragma unroll
+  for (int j = 0; j < R0; ++j) Rw[j] = ld(zs - 2, j);
+#pragma unroll
+  for (int j = 0; j < R1; ++j) {
+    A0p[j] = vsplat27<V>(T(0));
+    S0[j] = A0p[j];
+    C0[j] = A0p[j];
+    U1[j] = A0p[j];
+  }
+#pragma unroll
+  for (int i = 0; i < RY; ++i) {
+    A1p[i] = vsplat27<V>(T(0));
+    S1[i] = A1p[i];
+    C1[i] = A1p[i];
+  }
+  double acc = 0.0;
+  int buf = 0;
+  for (int64_t k = zs - 2; k <= ze + 2; ++k) {
+    V NX[R0];
+    if (PF) {
+#pragma unroll
+      for (int j = 0; j < R0; ++j) NX[j] = ld(k + 1, j);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < R0; ++j) edge[buf][w][j][0] = Rw[j][0];
+#pragma unroll
+      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][0] = U1[j][0];
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int j = 0; j < R0; ++j) edge[buf][w][j][1] = Rw[j][N - 1];
+#pragma unroll
+      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][1] = U1[j][N - 1];
+    }
+    __syncthreads();
+
+    // ---- level 0: partials of u0 plane k, u1(k-1) -------------------------------------------
+    V U1n[R1];
+    {
+      V H[R0];
+#pragma unroll
+      for (int j = 0; j < R0; ++j) H[j] = hsum(Rw[j], buf, j);
+      const int64_t gz = k - 1 + g.gz_off;
+      const bool zb = gz <= 0 || gz >= g.gnz - 1;
+#pragma unroll
+      for (int jj = 0; jj < R1; ++jj) {
+        const int j = jj + 1;
+        V A, B;
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const T center = Rw[j][e];
+          const T cross = H[j][e] + (Rw[j - 1][e] + Rw[j + 1][e]);
+          const T diag = H[j - 1][e] + H[j + 1][e];
+          A[e] = sm::box27_A<T>(center, cross, diag, c1, c2, c3);
+          B[e] = sm::box27_B<T>(center, cross, diag, c0, c1, c2);
+        }
+        const int64_t y = y0 - 1 + jj;
+        V u = C0[jj];
+        if (!zb && y > 0 && y < g.ny - 1) {
+#pragma unroll
+          for (int e = 0; e < N; ++e) u[e] = xb[e] ? C0[jj][e] : S0[jj][e] + A[e];
+        }
+        U1n[jj] = u;
+#pragma unroll
+        for (int e = 0; e < N; ++e) S0[jj][e] = A0p[jj][e] + B[e];
+        A0p[jj] = A;
+        C0[jj] = Rw[j];
+      }
+    }
+    // ---- level 1: partials of u1 plane k-2, u2(k-3) ------------------------------------------
+    if (k >= zs + 1) {
+      V H[R1];
+#pragma unroll
+      for (int j = 0; j < R1; ++j) H[j] = hsum(U1[j], buf, R0 + j);
+      const int64_t lz = k - 3;
+      const int64_t gz = lz + g.gz_off;
+      const bool zb = gz == 0 || gz == g.gnz - 1;
+#pragma unroll
+      for (int i = 0; i < RY; ++i) {
+        const int j = i + 1;
+        V A, B;
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const T center = U1[j][e];
+          const T cross = H[j][e] + (U1[j - 1][e] + U1[j + 1][e]);
+          const T diag = H[j - 1][e] + H[j + 1][e];
+          A[e] = sm::box27_A<T>(center, cross, diag, c1, c2, c3);
+          B[e] = sm::box27_B<T>(center, cross, diag, c0, c1, c2);
+        }
+        const int64_t y = y0 + i;
+        if (k >= zs + 3 && y < g.ny) {
+          V o = C1[i];
+          if (!zb && y != 0 && y != g.ny - 1) {
+#pragma unroll
+            for (int e = 0; e < N; ++e) o[e] = xb[e] ? C1[i][e] : S1[i][e] + A[e];
+          }
+          if (xin) {
+            store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
+            if (RES) {
+#pragma unroll
+              for (int e = 0; e < N; ++e)
+                if (x + e < g.nx) {
+                  const double d = (double)o[e] - (double)C1[i][e];
+                  acc += d * d;
+                }
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < N; ++e) S1[i][e] = A1p[i][e] + B[e];
+        A1p[i] = A;
+        C1[i] = U1[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R1; ++j) U1[j] = U1n[j];
+#pragma unroll
+    for (int j = 0; j < R0; ++j) Rw[j] = PF ? NX[j] : ld(k + 1, j);
+    buf ^= 1;
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T>
+bool box27_tb2_supported(const Geo& g) {
+  return g.pitch <= 4 * 64 * VT<T>::N && g.ny >= 1;
+}
+template bool box27_tb2_supported<float>(const Geo&);
+template bool box27_tb2_supported<double>(const Geo&);
+
+template <class T, int RY, int WXN>
+static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
+                               hipStream_t s) {
+  constexpr int WYN = 4 / WXN;
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) {  // balanced ~43-plane chunks, as the 7-point fused kernel (5 pipeline planes here)
+    int64_t zt = (planes + 43) / 44;
+    zc = (int)((planes + zt - 1) / zt);
+    while ((int64_t)YT * zt < 1024 && zc > 16) {
+      ++zt;
+      zc = (int)((planes + zt - 1) / zt);
+    }
+    zc = std::max(zc, 1);
+  }
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
+  const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
+  // next-plane prefetch: fp32 799.7 vs 580.9 GCells/s without, fp64 467.1 vs 494.4 (512^3,
+  // profiles/r01_box27_tb2.txt)
+  const bool pf = env_int("MDFX_TB_PF", sizeof(T) == 4 ? 1 : 0) != 0;
+  if (resid)
+    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, true, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+  else if (pf)
+    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+  else
+    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 0>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+}
+
+template <class T, int RY>
+static void launch_box27_tb2_ry(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
+                                hipStream_t s) {
+  constexpr int WX = 64 * VT<T>::N;
+  if (g.pitch > 2 * WX)
+    launch_box27_tb2_w<T, RY, 4>(g, in, out, c, resid, s);
+  else if (g.pitch > WX)
+    launch_box27_tb2_w<T, RY, 2>(g, in, out, c, resid, s);
+  else
+    launch_box27_tb2_w<T, RY, 1>(g, in, out, c, resid, s);
+}
+
+template <class T>
+void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid, hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  int ry = env_int("MDFX_TB_RY", 0);
+  if (ry <= 0) ry = 2;
+  if (g.ny < 8) ry = 1;
+  if (ry == 1)
+    launch_box27_tb2_ry<T, 1>(g, in, out, c, resid, s);
+  else
+    launch_box27_tb2_ry<T, 2>(g, in, out, c, resid, s);
+}
+template void launch_box27_tb2<float>(const Geo&, const float*, float*, const StencilCoef&, double*, hipStream_t);
+template void launch_box27_tb2<double>(const Geo&, const double*, double*, const StencilCoef&, double*, hipStream_t);
+
 }  // namespace dev
 }  // namespace mdfx

@@ -19,7 +19,10 @@ CASES = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=1
          # 2D 5-pt MDF (rows are planes): several segments, a ragged last one, fp64
          models.mdf2d(h=37, w=1000), models.mdf2d(h=21, w=300, dtype="f64"), models.mdf2d(h=9, w=64),
          # Game of Life (u8 SWAR): several 1024-cell segments, ragged edges
-         models.life2d(h=40, w=3000), models.life2d(h=17, w=1024), models.life2d(h=9, w=100)]
+         models.life2d(h=40, w=3000), models.life2d(h=17, w=1024), models.life2d(h=9, w=100),
+         # 27-point (partial sums through both levels): 4 / 2 / 1 waves across the row, fp64
+         models.box27(nx=1024, ny=11, nz=9), models.box27(nx=512, ny=21, nz=15),
+         models.box27(nx=300, ny=9, nz=12, dtype="f64"), models.box27(nx=64, ny=40, nz=10)]
 
 
 def _two_single_steps(prob, lay, src, device):
@@ -138,3 +141,10 @@ def test_engine_temporal2_life(hip, ranks):
     ref, rr = _sim(prob, 13, ranks=1, residual_every=13)
     got, rg = _sim(prob, 13, ranks=ranks, temporal=2, residual_every=13)
     assert np.array_equal(ref, got) and rr == rg
+
+
+def test_engine_temporal2_box27(hip):
+    prob = mm.box27(nx=512, ny=40, nz=50)
+    ref, rr = _sim(prob, 9, ranks=1, residual_every=9)
+    got, rg = _sim(prob, 9, ranks=3, temporal=2, residual_every=9)
+    assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
