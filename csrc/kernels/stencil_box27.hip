@@ -328,59 +328,27 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
     }
     __syncthreads();
 
-    // ---- level 0: partials of u0 plane k, u1(k-1) -------------------------------------------
-    V U1n[R1];
-    {
-      V H[R0];
-#pragma unroll
-      for (int j = 0; j < R0; ++j) H[j] = hsum(Rw[j], buf, j);
-      const int64_t gz = k - 1 + g.gz_off;
-      const bool zb = gz <= 0 || gz >= g.gnz - 1;
-#pragma unroll
-      for (int jj = 0; jj < R1; ++jj) {
-        const int j = jj + 1;
-        V A, B;
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-          const T center = Rw[j][e];
-          const T cross = H[j][e] + (Rw[j - 1][e] + Rw[j + 1][e]);
-          const T diag = H[j - 1][e] + H[j + 1][e];
-          A[e] = sm::box27_A<T>(center, cross, diag, c1, c2, c3);
-          B[e] = sm::box27_B<T>(center, cross, diag, c0, c1, c2);
-        }
-        const int64_t y = y0 - 1 + jj;
-        V u = C0[jj];
-        if (!zb && y > 0 && y < g.ny - 1) {
-#pragma unroll
-          for (int e = 0; e < N; ++e) u[e] = xb[e] ? C0[jj][e] : S0[jj][e] + A[e];
-        }
-        U1n[jj] = u;
-#pragma unroll
-        for (int e = 0; e < N; ++e) S0[jj][e] = A0p[jj][e] + B[e];
-        A0p[jj] = A;
-        C0[jj] = Rw[j];
-      }
-    }
     // ---- level 1: partials of u1 plane k-2, u2(k-3) ------------------------------------------
     if (k >= zs + 1) {
-      V H[R1];
-#pragma unroll
-      for (int j = 0; j < R1; ++j) H[j] = hsum(U1[j], buf, R0 + j);
+      V Hm = hsum(U1[0], buf, R0), Hc = hsum(U1[1], buf, R0 + 1);
       const int64_t lz = k - 3;
       const int64_t gz = lz + g.gz_off;
       const bool zb = gz == 0 || gz == g.gnz - 1;
 #pragma unroll
       for (int i = 0; i < RY; ++i) {
         const int j = i + 1;
+        const V Hp = hsum(U1[j + 1], buf, R0 + j + 1);
         V A, B;
 #pragma unroll
         for (int e = 0; e < N; ++e) {
           const T center = U1[j][e];
-          const T cross = H[j][e] + (U1[j - 1][e] + U1[j + 1][e]);
-          const T diag = H[j - 1][e] + H[j + 1][e];
+          const T cross = Hc[e] + (U1[j - 1][e] + U1[j + 1][e]);
+          const T diag = Hm[e] + Hp[e];
           A[e] = sm::box27_A<T>(center, cross, diag, c1, c2, c3);
           B[e] = sm::box27_B<T>(center, cross, diag, c0, c1, c2);
         }
+        Hm = Hc;
+        Hc = Hp;
         const int64_t y = y0 + i;
         if (k >= zs + 3 && y < g.ny) {
           V o = C1[i];
@@ -406,8 +374,39 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
         C1[i] = U1[j];
       }
     }
+    // ---- level 0: partials of u0 plane k, u1(k-1) (written over U1, consumed above) ----------
+    {
+      const int64_t gz = k - 1 + g.gz_off;
+      const bool zb = gz <= 0 || gz >= g.gnz - 1;
+      V Hm = hsum(Rw[0], buf, 0), Hc = hsum(Rw[1], buf, 1);
 #pragma unroll
-    for (int j = 0; j < R1; ++j) U1[j] = U1n[j];
+      for (int jj = 0; jj < R1; ++jj) {
+        const int j = jj + 1;
+        const V Hp = hsum(Rw[j + 1], buf, j + 1);
+        V A, B;
+#pragma unroll
+        for (int e = 0; e < N; ++e) {
+          const T center = Rw[j][e];
+          const T cross = Hc[e] + (Rw[j - 1][e] + Rw[j + 1][e]);
+          const T diag = Hm[e] + Hp[e];
+          A[e] = sm::box27_A<T>(center, cross, diag, c1, c2, c3);
+          B[e] = sm::box27_B<T>(center, cross, diag, c0, c1, c2);
+        }
+        Hm = Hc;
+        Hc = Hp;
+        const int64_t y = y0 - 1 + jj;
+        V u = C0[jj];
+        if (!zb && y > 0 && y < g.ny - 1) {
+#pragma unroll
+          for (int e = 0; e < N; ++e) u[e] = xb[e] ? C0[jj][e] : S0[jj][e] + A[e];
+        }
+        U1[jj] = u;
+#pragma unroll
+        for (int e = 0; e < N; ++e) S0[jj][e] = A0p[jj][e] + B[e];
+        A0p[jj] = A;
+        C0[jj] = Rw[j];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < R0; ++j) Rw[j] = PF ? NX[j] : ld(k + 1, j);
     buf ^= 1;
@@ -441,9 +440,9 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
-  // next-plane prefetch: fp32 799.7 vs 580.9 GCells/s without, fp64 467.1 vs 494.4 (512^3,
+  // next-plane prefetch: fp32 985.7 vs 773.3 GCells/s without, fp64 491.8 vs 479.8 (512^3,
   // profiles/r01_box27_tb2.txt)
-  const bool pf = env_int("MDFX_TB_PF", sizeof(T) == 4 ? 1 : 0) != 0;
+  const bool pf = env_int("MDFX_TB_PF", 1) != 0;
   if (resid)
     hipLaunchKernelGGL((box27_tb2<T, RY, WXN, true, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
   else if (pf)
