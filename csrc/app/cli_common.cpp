@@ -37,7 +37,7 @@ struct Opts {
   int64_t ckpt_every = 0;
   std::string ckpt_dir = "mdfx_ckpt", resume;
   bool compat = false;
-  int temporal = 1;
+  int temporal = 0;  // 0 = auto: 2 on HIP where a fused kernel exists, else 1
   bool profile = false;
   int dim = 0;
   std::string dump;
@@ -63,7 +63,8 @@ void usage(const char* prog) {
       "  --print                   dump the final grid like the reference's print_array\n"
       "  --json                    one JSON metrics line ; --verbose per-rank detail ; --quiet\n"
       "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n"
-      "  --temporal 1|2            time steps fused per memory sweep (2: 3D 7-pt, rows <= one block)\n"
+      "  --temporal 0|1|2          time steps fused per memory sweep (0 = auto: 2 on GPUs where a fused\n"
+      "                            kernel exists, 1 on the CPU)\n"
       "  --profile                 per-phase timing of rank 0 (boundary / interior / exchange)\n"
       "  --dim 2|3                 default stencil of that dimension (5 / 7) ; --bc V = --edge V ; --coef R = --r R\n"
       "  --dump DIR                write the final grid (per-slab raw + JSON header, checkpoint format)\n"
@@ -266,6 +267,11 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     } else {
       MDFX_FAIL("unknown transport " + tname);
     }
+    if (o.temporal <= 0)
+      o.temporal = (hip && g.nz >= 4 * (int64_t)nranks &&
+                    hip_supports_steps(spec, FieldLayout::make(g, 0, g.nz, 2, spec.dtype), 2))
+                       ? 2
+                       : 1;
     SolverOptions so;
     so.overlap = o.overlap;
     so.sync_debug = o.sync_debug;
@@ -396,11 +402,11 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
       std::printf(
           "{\"metric\": \"GCells/s\", \"value\": %.4f, \"unit\": \"GCells/s\", \"stencil\": \"%s\", \"dtype\": \"%s\", "
           "\"grid\": [%lld, %lld, %lld], \"steps\": %lld, \"seconds\": %.6f, \"ms_per_step\": %.4f, "
-          "\"ranks\": %d, \"n_gpus\": %d, \"transport\": \"%s\", \"overlap\": %s, \"graph\": %s, \"residual\": %.9g, \"gcells_per_gpu\": %.4f%s}\n",
+          "\"ranks\": %d, \"n_gpus\": %d, \"transport\": \"%s\", \"overlap\": %s, \"graph\": %s, \"residual\": %.9g, \"gcells_per_gpu\": %.4f, \"temporal\": %d%s}\n",
           gcs, stencil_name(kind), dtype_name(spec.dtype), (long long)g.nx, (long long)g.ny, (long long)g.nz,
           (long long)o.steps, dt, o.steps ? dt / o.steps * 1e3 : 0.0, nranks, ngpu, solver.transport().name(),
           o.overlap ? "true" : "false", o.graph ? "true" : "false", solver.stats().last_residual,
-          ngpu ? gcs / ngpu : gcs, extra.c_str());
+          ngpu ? gcs / ngpu : gcs, solver.options().temporal, extra.c_str());
     } else if (root && !o.compat && !o.quiet) {
       std::printf("mdfx: %s %lldx%lldx%lld %s | %d slab(s), %s transport, %s | %lld steps in %.4f s | "
                   "%.4f ms/step | %.2f GCells/s total, %.2f per GPU",
