@@ -5,6 +5,7 @@ P virtual slabs on ONE GPU through the loopback transport exercise the same engi
 RCCL (halo stream, events, double buffering); results must be bitwise equal to P = 1.
 """
 
+import os
 import numpy as np
 import pytest
 import torch
@@ -13,6 +14,8 @@ pytestmark = pytest.mark.gpu
 
 import mpi_cuda_process_amd as m  # noqa: E402
 from mpi_cuda_process_amd.ops import reference  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PROBS = [m.heat3d(nx=96, ny=40, nz=37), m.box27(nx=80, ny=24, nz=23), m.mdf2d(h=61, w=130),
          m.life2d(h=70, w=300), m.heat3d(nx=64, ny=30, nz=26, dtype="f64")]
@@ -149,3 +152,39 @@ def test_watchdog_timeout_option(hip):
         sim.init()
         sim.run(3)
         sim.synchronize()
+
+
+_SERIAL_WORKER = r"""
+import sys; sys.path.insert(0, %(root)r)
+import numpy as np, torch
+import mpi_cuda_process_amd as m
+out = {}
+for name, prob, kw in [("heat7", m.heat3d(nx=300, ny=70, nz=64), dict(ranks=4, temporal=2)),
+                       ("box27", m.box27(nx=200, ny=40, nz=33, dtype="f64"), dict(ranks=3)),
+                       ("life", m.life2d(h=500, w=1500), dict(ranks=5, temporal=2))]:
+    with m.Simulation(prob, device="hip", residual_every=5, **kw) as sim:
+        sim.init()
+        sim.run(11)
+        sim.synchronize()
+        out[name] = sim.gather()
+np.savez(%(out)r, **out)
+"""
+
+
+def test_serialized_runtime_equals_overlapped(hip, tmp_path):
+    """the HIP runtime's own serialisation (AMD_SERIALIZE_KERNEL / _COPY = 3: every kernel
+    and copy waits for the previous one) must not change a single bit of the overlapped multi-slab
+    result: a missing event dependency would show up as a difference here."""
+    import subprocess
+    import sys
+
+    res = {}
+    for tag, extra in (("overlap", {}), ("serial", {"AMD_SERIALIZE_KERNEL": "3", "AMD_SERIALIZE_COPY": "3"})):
+        out = str(tmp_path / ("%s.npz" % tag))
+        env = dict(os.environ, **extra)
+        p = subprocess.run([sys.executable, "-c", _SERIAL_WORKER % dict(root=ROOT, out=out)], env=env,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+        assert p.returncode == 0, p.stderr.decode()[-3000:]
+        res[tag] = np.load(out)
+    for k in ("heat7", "box27", "life"):
+        assert np.array_equal(res["overlap"][k], res["serial"][k]), k
