@@ -40,8 +40,8 @@ TESTS      := $(BIN)/mdfx_tests
 
 LINK_ROCM  := -L$(ROCM)/lib -lamdhip64 -lrccl -lgomp -lpthread -ldl
 
-.PHONY: all lib pymod apps tests asan clean
-all: lib pymod apps tests asan
+.PHONY: all lib pymod apps tests asan devcheck clean
+all: lib pymod apps tests asan devcheck
 
 lib: $(LIB)
 pymod: $(PYMOD)
@@ -98,6 +98,25 @@ $(ASAN_DIR)/%.o: csrc/%.cpp $(HEADERS)
 $(BIN)/mdfx_tests_asan: $(ASAN_DIR)/tests/test_main.o $(ASAN_KOBJ) $(ASAN_HOBJ)
 	@mkdir -p $(BIN)
 	$(CXX_HOST) $(ASAN_HOST) -o $@ $^ $(LINK_ROCM) -fopenmp -Wl,-rpath,$(ROCM)/lib
+
+# Device-check build of the native tests: every tuned-kernel load / store checks its range against
+# the allocation and counts violations (csrc/kernels/kcommon.hpp dcheck); run on a GPU.
+DCK_DIR    := build/devcheck
+DCK_KOBJ   := $(patsubst csrc/%.hip,$(DCK_DIR)/%.o,$(KERNEL_SRC))
+DCK_HOBJ   := $(patsubst csrc/%.cpp,$(DCK_DIR)/%.o,$(HOST_SRC))
+devcheck: $(BIN)/mdfx_tests_devcheck
+
+$(DCK_DIR)/%.o: csrc/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMDFX_DEVICE_CHECKS -c $< -o $@
+
+$(DCK_DIR)/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX_HOST) $(HOSTFLAGS) -DMDFX_DEVICE_CHECKS -c $< -o $@
+
+$(BIN)/mdfx_tests_devcheck: $(DCK_DIR)/tests/test_main.o $(DCK_KOBJ) $(DCK_HOBJ)
+	@mkdir -p $(BIN)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LINK_ROCM) -fopenmp -Wl,-rpath,$(ROCM)/lib
 
 clean:
 	rm -rf build $(LIB) $(PYMOD)

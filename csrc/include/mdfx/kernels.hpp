@@ -73,6 +73,9 @@ MDFX_HD inline double hash_unit(uint64_t seed, uint64_t gidx) {
 void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream);
 void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* stream);
 // Variant selection for kernel A/B benchmarking and tests: "auto", "naive", "tuned".
+// Out-of-allocation accesses counted by the device checks of a `make devcheck` build (-1 when
+// the checks are compiled out, as in release builds).
+int64_t hip_device_check_violations();
 void hip_set_kernel_variant(const char* name);
 const char* hip_kernel_variant();
 

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -74,8 +75,32 @@ __global__ __launch_bounds__(256) void init_kernel(T* __restrict__ buf, Geo g, I
   }
 }
 
+#ifdef MDFX_DEVICE_CHECKS
+// one violation counter per device (make devcheck builds only)
+static std::mutex g_oob_mu;
+static std::map<int, unsigned long long*> g_oob;
+static unsigned long long* oob_counter() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_oob_mu);
+  auto it = g_oob.find(dev);
+  if (it != g_oob.end()) return it->second;
+  void* p = nullptr;
+  if (hipMalloc(&p, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+  return g_oob[dev] = (unsigned long long*)p;
+}
+#endif
+
 static Geo make_geo(const FieldLayout& lay, int64_t lz_begin, int64_t lz_end) {
   Geo g;
+  g.alloc = lay.elems() + kSlackBytes / (int64_t)lay.esize();
+#ifdef MDFX_DEVICE_CHECKS
+  g.oob = oob_counter();
+  // self-test of the checking machinery: pretend the allocation is half its size so in-bounds
+  // accesses beyond that count as violations (nothing is accessed out of bounds)
+  if (env_int("MDFX_DEVCHECK_SELFTEST", 0)) g.alloc = lay.elems() / 2;
+#endif
   g.pitch = lay.pitch;
   g.plane = lay.plane;
   g.nx = lay.global.nx;
@@ -92,6 +117,23 @@ static std::mutex g_variant_mu;
 static std::string g_variant = "auto";
 
 }  // namespace dev
+
+int64_t hip_device_check_violations() {
+#ifdef MDFX_DEVICE_CHECKS
+  int64_t total = 0;
+  std::lock_guard<std::mutex> lk(dev::g_oob_mu);
+  for (auto& kv : dev::g_oob) {
+    unsigned long long h = 0;
+    if (hipSetDevice(kv.first) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(&h, kv.second, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+      MDFX_FAIL("reading the device-check counter failed");
+    total += (int64_t)h;
+  }
+  return total;
+#else
+  return -1;
+#endif
+}
 
 void hip_set_kernel_variant(const char* name) {
   std::lock_guard<std::mutex> lk(dev::g_variant_mu);

@@ -33,7 +33,26 @@ struct Geo {
   int64_t lz_end;    // one past the last storage plane to write
   int64_t gz_off;    // global z = lz + gz_off
   int64_t lz_max;    // storage planes allocated (loads outside [0,lz_max) return 0)
+  int64_t alloc = 0;                 // elements allocated (planes + slack), for device checks
+  unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };
+
+// Debug builds (-DMDFX_DEVICE_CHECKS: make devcheck) check the element range of every tuned-kernel
+// load and store against the allocation and COUNT violations in g.oob, which the host reads back
+// (hip_device_check_violations). Counting instead of trapping keeps a bad index from faulting the
+// GPU. Release builds compile the checks out.
+template <class T>
+__device__ __forceinline__ void dcheck(const Geo& g, const T* base, const T* p, int n) {
+#ifdef MDFX_DEVICE_CHECKS
+  const int64_t i = p - base;
+  if (g.oob && (i < 0 || i + n > g.alloc)) atomicAdd(g.oob, 1ull);
+#else
+  (void)g;
+  (void)base;
+  (void)p;
+  (void)n;
+#endif
+}
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5, T1): blocks b and b+8 share an
 // XCD, so consecutive *tiles* are handed to the same XCD and their shared halo rows hit that

@@ -57,21 +57,27 @@ __global__ __launch_bounds__(256) void box27_zw(const T* __restrict__ in, T* __r
   auto ld = [&](int64_t lz, int j) -> V {
     V v = vsplat27<V>(T(0));
     const int64_t y = y0 - 1 + j;
-    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny)
+    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
+      dcheck(g, in, ib + lz * plane + (int64_t)j * pitch, N);
       v = *(const V*)(ib + lz * plane + (int64_t)j * pitch);
+    }
     return v;
   };
   auto ldl = [&](int64_t lz, int j) -> T {
     const int64_t y = y0 - 1 + j;
-    if (wx == 0 && lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny)
+    if (wx == 0 && lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
+      dcheck(g, in, ib + lz * plane + (int64_t)j * pitch - 1, 1);
       return ib[lz * plane + (int64_t)j * pitch - 1];
+    }
     return T(0);
   };
   auto ldr = [&](int64_t lz, int j) -> T {
     const int64_t y = y0 - 1 + j;
     if (wx == WXN - 1 && lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max && y >= 0 &&
-        y < g.ny)
+        y < g.ny) {
+      dcheck(g, in, ib + lz * plane + (int64_t)j * pitch + N, 1);
       return ib[lz * plane + (int64_t)j * pitch + N];
+    }
     return T(0);
   };
 
@@ -156,6 +162,7 @@ __global__ __launch_bounds__(256) void box27_zw(const T* __restrict__ in, T* __r
         }
       }
       if (xin) {
+        dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch, N);
         store_nt((V*)(ob + lz * plane + (int64_t)i * pitch), o);
         if (RES) {
 #pragma unroll
@@ -272,7 +279,10 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
   auto ld = [&](int64_t lz, int k) -> V {
     V v = vsplat27<V>(T(0));
     const int64_t y = y0 - 2 + k;
-    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) v = *(const V*)(ib + lz * plane + (int64_t)k * pitch + xo);
+    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
+      dcheck(g, in, ib + lz * plane + (int64_t)k * pitch + xo, N);
+      v = *(const V*)(ib + lz * plane + (int64_t)k * pitch + xo);
+    }
     return v;
   };
   // x-neighbour sum of one row vector; `slot` = its seam slot in edge[buf][*]
@@ -357,6 +367,7 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
             for (int e = 0; e < N; ++e) o[e] = xb[e] ? C1[i][e] : S1[i][e] + A[e];
           }
           if (xin) {
+            dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
             store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
             if (RES) {
 #pragma unroll

@@ -71,22 +71,29 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
     const int64_t y = y0 + i;
     if (lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
       const T* p = ib + lz * plane + (int64_t)i * pitch;
-      if (xin) v = *(const V*)(p + xo);
+      if (xin) {
+        dcheck(g, in, p + xo, N);
+        v = *(const V*)(p + xo);
+      }
     }
     return v;
   };
   auto ldl = [&](int64_t lz, int i) -> T {
     if (!EDGE) return T(0);
     const int64_t y = y0 + i;
-    if (wx == 0 && lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max && y < g.ny)
+    if (wx == 0 && lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max && y < g.ny) {
+      dcheck(g, in, ib + lz * plane + (int64_t)i * pitch - 1, 1);
       return ib[lz * plane + (int64_t)i * pitch - 1];
+    }
     return T(0);
   };
   auto ldr = [&](int64_t lz, int i) -> T {
     if (!EDGE) return T(0);
     const int64_t y = y0 + i;
-    if (wx == WXN - 1 && lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max && y < g.ny)
+    if (wx == WXN - 1 && lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max && y < g.ny) {
+      dcheck(g, in, ib + lz * plane + (int64_t)i * pitch + WX, 1);
       return ib[lz * plane + (int64_t)i * pitch + WX];
+    }
     return T(0);
   };
 
@@ -161,6 +168,7 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
         }
       }
       if (xin) {
+        dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
         store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
         if (RES) {
 #pragma unroll
@@ -217,15 +225,24 @@ __global__ __launch_bounds__(256) void jacobi5_wave(const T* __restrict__ in, T*
   const int64_t plane = g.plane;
   auto ld = [&](int64_t lz) -> V {
     V v = vsplat<V>(T(0));
-    if (xin && lz >= 0 && lz < g.lz_max) v = *(const V*)(in + lz * plane + x);
+    if (xin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x, N);
+      v = *(const V*)(in + lz * plane + x);
+    }
     return v;
   };
   auto ldl = [&](int64_t lz) -> T {
-    if (lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max) return in[lz * plane + x - 1];
+    if (lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x - 1, 1);
+      return in[lz * plane + x - 1];
+    }
     return T(0);
   };
   auto ldr = [&](int64_t lz) -> T {
-    if (lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max) return in[lz * plane + x + N];
+    if (lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x + N, 1);
+      return in[lz * plane + x + N];
+    }
     return T(0);
   };
   V P = ld(lzs - 1), C = ld(lzs), Nx = ld(lzs + 1);
@@ -252,6 +269,7 @@ __global__ __launch_bounds__(256) void jacobi5_wave(const T* __restrict__ in, T*
       }
     }
     if (xin) {
+      dcheck(g, (const T*)out, out + lz * plane + x, N);
       store_nt((V*)(out + lz * plane + x), o);
       if (RES) {
 #pragma unroll

@@ -81,7 +81,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
     const int64_t y = y0 - 2 + rr;
     if (lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
       const T* p = ib + lz * plane + (int64_t)rr * pitch;
-      if (xin) v = *(const V*)(p + xo);
+      if (xin) {
+        dcheck(g, in, p + xo, N);
+        v = *(const V*)(p + xo);
+      }
     }
     return v;
   };
@@ -95,8 +98,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
   auto ldhv = [&](int64_t lz) -> V {
     V v = vsplat_tb<V>(T(0));
     const int64_t y = y0 - 2 + lane;
-    if (lane < R0 && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny)
-      v = *(const V*)(ib + lz * plane + (int64_t)lane * pitch + (side == 0 ? -N : WX));
+    if (lane < R0 && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
+      const T* hp = ib + lz * plane + (int64_t)lane * pitch + (side == 0 ? -N : WX);
+      dcheck(g, in, hp, N);
+      v = *(const V*)hp;
+    }
     return v;
   };
   auto puthv = [&](int64_t lz, V v) {
@@ -217,6 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
           }
         }
         if (xin) {
+          dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
           store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
           if (RES) {
 #pragma unroll
@@ -384,12 +391,18 @@ __global__ __launch_bounds__(256) void jacobi5_tb2(const T* __restrict__ in, T* 
 
   auto ld = [&](int64_t lz) -> V {
     V v = vsplat_tb<V>(T(0));
-    if (xin && lz >= 0 && lz < g.lz_max) v = *(const V*)(in + lz * plane + x);
+    if (xin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x, N);
+      v = *(const V*)(in + lz * plane + x);
+    }
     return v;
   };
   auto ldh = [&](int64_t lz) -> V {
     V v = vsplat_tb<V>(T(0));
-    if (hin && lz >= 0 && lz < g.lz_max) v = *(const V*)(in + lz * plane + hvec);
+    if (hin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + hvec, N);
+      v = *(const V*)(in + lz * plane + hvec);
+    }
     return v;
   };
   V L = ld(zs - 2), M = ld(zs - 1), H = ld(zs);
@@ -443,6 +456,7 @@ __global__ __launch_bounds__(256) void jacobi5_tb2(const T* __restrict__ in, T* 
         }
       }
       if (xin) {
+        dcheck(g, (const T*)out, out + lz * plane + x, N);
         store_nt((V*)(out + lz * plane + x), o);
         if (RES) {
 #pragma unroll

@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void life_wave(const uint8_t* __restrict__ in,
   auto ld = [&](int64_t lz) -> U2 {
     U2 v{0, 0};
     if (xin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x, N);
       const uint4 q = *(const uint4*)(in + lz * plane + x);
       v.lo = (uint64_t)q.x | ((uint64_t)q.y << 32);
       v.hi = (uint64_t)q.z | ((uint64_t)q.w << 32);
@@ -55,11 +56,17 @@ __global__ __launch_bounds__(256) void life_wave(const uint8_t* __restrict__ in,
     return v;
   };
   auto ldl = [&](int64_t lz) -> uint64_t {
-    if (lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max) return in[lz * plane + x - 1];
+    if (lane == 0 && x > 0 && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x - 1, 1);
+      return in[lz * plane + x - 1];
+    }
     return 0;
   };
   auto ldr = [&](int64_t lz) -> uint64_t {
-    if (lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max) return in[lz * plane + x + N];
+    if (lane == 63 && x + N < g.pitch && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x + N, 1);
+      return in[lz * plane + x + N];
+    }
     return 0;
   };
   U2 P = ld(lzs - 1), C = ld(lzs), Nx = ld(lzs + 1);
@@ -103,6 +110,7 @@ __global__ __launch_bounds__(256) void life_wave(const uint8_t* __restrict__ in,
       q.y = (uint32_t)(o.lo >> 32);
       q.z = (uint32_t)o.hi;
       q.w = (uint32_t)(o.hi >> 32);
+      dcheck(g, (const uint8_t*)out, out + lz * plane + x, N);
       *(uint4*)(out + lz * plane + x) = q;
       if (RES) {
         uint64_t dlo = o.lo ^ C.lo, dhi = o.hi ^ C.hi;
@@ -177,11 +185,17 @@ __global__ __launch_bounds__(256) void life_tb2(const uint8_t* __restrict__ in, 
   const bool hframe = hcol <= 0 || hcol >= g.nx - 1;
   const bool frame = x == 0 || x + N > g.nx - 1;  // frame or pad cells in this lane
   auto ld = [&](int64_t lz) -> U2 {
-    if (xin && lz >= 0 && lz < g.lz_max) return ld_u2(in + lz * plane + x);
+    if (xin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x, N);
+      return ld_u2(in + lz * plane + x);
+    }
     return U2{0, 0};
   };
   auto ldh = [&](int64_t lz) -> uint32_t {
-    if (hin && lz >= 0 && lz < g.lz_max) return *(const uint32_t*)(in + lz * plane + hoff);
+    if (hin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + hoff, 4);
+      return *(const uint32_t*)(in + lz * plane + hoff);
+    }
     return 0u;
   };
   // the two halo cells as (adjacent, next): lane 0 -> (byte 3, byte 2), lane 63 -> (byte 0, byte 1)
@@ -249,6 +263,7 @@ __global__ __launch_bounds__(256) void life_tb2(const uint8_t* __restrict__ in, 
         q.y = (uint32_t)(o.lo >> 32);
         q.z = (uint32_t)o.hi;
         q.w = (uint32_t)(o.hi >> 32);
+        dcheck(g, (const uint8_t*)out, out + lz * plane + x, N);
         *(uint4*)(out + lz * plane + x) = q;
         if (RES) {
           const uint64_t dlo = o.lo ^ Ub.lo, dhi = o.hi ^ Ub.hi;

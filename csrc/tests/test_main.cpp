@@ -2,6 +2,7 @@
 // decomposition invariance through the engine on the CPU backend, GPU engine when a device exists.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -123,13 +124,71 @@ static void test_graph() {
   }
 }
 
+// fused two-step sweeps (halo 2) == single steps, every stencil, several slab counts, ragged and
+// x-tiled (wider than one block) rows
+static void test_temporal(bool gpu) {
+  struct C {
+    StencilKind k;
+    DType d;
+    Extent3 g;
+  } cs[] = {{StencilKind::Heat7, DType::F32, {1100, 9, 23}},
+            {StencilKind::Heat7, DType::F64, {77, 13, 19}},
+            {StencilKind::Box27, DType::F32, {300, 11, 17}},
+            {StencilKind::Jacobi5, DType::F64, {700, 1, 29}},
+            {StencilKind::Life, DType::U8, {2100, 1, 31}}};
+  for (auto& c : cs)
+    for (int p : {1, 3}) {
+      std::vector<std::vector<char>> outs;
+      for (int t : {1, 2}) {
+        StencilSpec s;
+        s.kind = c.k;
+        s.dtype = c.d;
+        std::vector<int> ranks;
+        std::vector<std::unique_ptr<Backend>> bes;
+        for (int r = 0; r < p; ++r) {
+          ranks.push_back(r);
+          bes.push_back(gpu ? make_hip_backend(0) : make_cpu_backend());
+        }
+        SolverOptions o;
+        o.temporal = t;
+        o.residual_every = 4;
+        Solver sol(s, c.g, p, ranks, std::move(bes), gpu ? make_loopback_transport() : make_host_transport(), o);
+        InitSpec is;
+        is.kind = c.k == StencilKind::Life ? InitKind::LifeRandom : InitKind::Random;
+        sol.init(is);
+        sol.run(9);
+        std::vector<char> out;
+        for (int i = 0; i < p; ++i) {
+          const FieldLayout& l = sol.layout(i);
+          std::vector<char> b((size_t)l.owned_cells() * l.esize());
+          sol.read_owned(i, b.data());
+          out.insert(out.end(), b.begin(), b.end());
+        }
+        outs.push_back(out);
+      }
+      EXPECT(outs[0] == outs[1]);
+    }
+}
+
 int main() {
   test_slab();
   test_layout();
   test_invariance(false);
+  test_temporal(false);
   if (hip_device_count() > 0) {
     test_invariance(true);
+    test_temporal(true);
     test_graph();
+#ifdef MDFX_DEVICE_CHECKS
+    const int64_t v = hip_device_check_violations();
+    std::printf("device checks: %lld out-of-allocation accesses\n", (long long)v);
+    EXPECT(v == 0);
+    // the checks themselves work: with the self-test's halved bound the same kernels count hits
+    setenv("MDFX_DEVCHECK_SELFTEST", "1", 1);
+    (void)run_engine(StencilKind::Heat7, DType::F32, Extent3{64, 16, 20}, 2, 3, true);
+    unsetenv("MDFX_DEVCHECK_SELFTEST");
+    EXPECT(hip_device_check_violations() > v);
+#endif
   }
   if (g_fail) {
     std::fprintf(stderr, "%d failure(s)\n", g_fail);

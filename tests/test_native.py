@@ -43,3 +43,17 @@ def test_cmake_configures(tmp_path):
                        stderr=subprocess.PIPE, timeout=300)
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     assert (tmp_path / "b" / "build.ninja").exists()
+
+
+@pytest.mark.gpu
+def test_native_device_checks_on_gpu(hip):
+    """The device-check build (make devcheck): every tuned-kernel load and store in the native GPU
+    tests (all stencils, single and fused steps, x-tiled rows, P = 1..4, graphs) stays inside its
+    allocation. Violations are counted on the device, not trapped, so this cannot fault the GPU."""
+    exe = os.path.join(BIN, "mdfx_tests_devcheck")
+    if not os.path.exists(exe):
+        pytest.fail("mdfx_tests_devcheck is not built (make -j8 all)")
+    p = subprocess.run([exe], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
+    out = p.stdout.decode() + p.stderr.decode()
+    assert p.returncode == 0, out[-4000:]
+    assert "all passed (cpu + gpu)" in out and "device checks: 0 out-of-allocation accesses" in out
