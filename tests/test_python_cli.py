@@ -41,12 +41,20 @@ def test_python_cli_json_virtual_ranks():
     assert rec["stencil"] == "heat7" and rec["grid"] == [24, 24, 24] and rec["value"] > 0 and rec["residual"] > 0
 
 
-def test_python_cli_under_torchrun_matches_single_process():
+def test_python_cli_under_torchrun_matches_single_process(tmp_path):
     args = ["--device", "cpu", "--stencil", "life", "--h", "26", "--w", "30", "--steps", "7", "--print"]
     single = _run([sys.executable, "-m", "mpi_cuda_process_amd"] + args)
-    multi = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-                  "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "mpi_cuda_process_amd"] + args)
-    # launcher chatter ([Gloo] lines, blank lines) aside, rank 0 prints exactly the same board
-    lines = [l for l in multi.splitlines(keepends=True)
-             if not l.startswith(("[Gloo]", "Expected number of connected peer ranks"))]
-    assert "".join(lines).strip("\n") == single.strip("\n") and "0" in single
+    # each rank's stdout goes to its own file (gloo prints connection chatter from both ranks)
+    logs = str(tmp_path / "logs")
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "--log-dir", logs, "--redirects", "1",
+          "-m", "mpi_cuda_process_amd"] + args)
+    outs = {}
+    for root, _, files in os.walk(logs):
+        if "stdout.log" in files:
+            outs[os.path.basename(root)] = open(os.path.join(root, "stdout.log")).read()
+    assert set(outs) == {"0", "1"}
+    board = "".join(l for l in outs["0"].splitlines(keepends=True)
+                    if not l.startswith("[Gloo]") and "peer ranks" not in l)
+    assert board == single and "0" in single
+    assert "0" not in "".join(l for l in outs["1"].splitlines() if "Gloo" not in l and "peer" not in l)
