@@ -52,8 +52,8 @@ def parse():
                    help="split the grid into P slabs inside ONE process (loopback transport)")
     p.add_argument("--graph", action="store_true", help="replay 2-step cycles as hipGraphs")
     p.add_argument("--temporal", type=int, default=0,
-                   help="time steps fused per memory sweep (temporal blocking); 0 = 2 where a fused "
-                        "kernel exists (all four stencils; 27-pt rows <= one block), else 1")
+                   help="time steps fused per memory sweep (temporal blocking); 0 = auto: 2 for the 3D "
+                        "stencils, 8 (2D MDF) / 4 (Life) for the 2D ones, where a fused kernel exists")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
@@ -93,10 +93,16 @@ def main():
 
     temporal = a.temporal
     if temporal <= 0:
+        # fused depth where a kernel exists: 2 for the 3D stencils, 8 (MDF) / 4 (Life) for the 2D
+        # ones (profiles/r01_deep_temporal_2d.txt), capped so every slab is at least 4 sweeps deep
+        want = {"jacobi5": 8, "life": 4}.get(a.stencil, 2)
+        nslab = max(1, int(os.environ.get("WORLD_SIZE", "1")), a.virtual_ranks)
+        while want > 1 and prob.nz < 4 * want * nslab:
+            want //= 2
         temporal = 1
-        if a.stencil in ("heat7", "jacobi5", "life", "box27") and (not hip or native().hip_supports_steps(
-                prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz, 2, 2)):
-            temporal = 2
+        if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny,
+                                                                prob.nz, want, want)):
+            temporal = want
     kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap, graph=a.graph,
               residual_every=a.residual_every, timeout_s=900.0 if hip else 0.0, temporal=temporal)
     if env:

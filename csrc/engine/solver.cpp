@@ -38,7 +38,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   if (spec_.kind == StencilKind::Life) MDFX_CHECK(spec_.dtype == DType::U8, "life cells are u8");
   if (spec_.kind != StencilKind::Life)
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
-  MDFX_CHECK(opt_.temporal == 1 || opt_.temporal == 2, "temporal blocking depth must be 1 or 2");
+  MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 8, "temporal blocking depth must be 1..8");
   const int halo = opt_.temporal;
   for (size_t i = 0; i < local_ranks.size(); ++i) {
     const int r = local_ranks[i];
@@ -48,6 +48,10 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.be = std::move(backends[i]);
     s.lay = FieldLayout::make(global_, decomp_.z0(r), decomp_.z1(r), halo, spec_.dtype);
     MDFX_CHECK(s.lay.nzl() >= 1, "every slab needs at least one plane");
+    MDFX_CHECK(nranks == 1 || s.lay.nzl() >= halo,
+               format("slab %d has %lld planes, fewer than the %d ghost planes temporal blocking exchanges "
+                      "(use a smaller --temporal or fewer ranks)",
+                      r, (long long)s.lay.nzl(), halo));
     const size_t bytes = s.lay.bytes();
     s.buf[0] = s.be->alloc(bytes);
     s.buf[1] = s.be->alloc(bytes);
@@ -60,8 +64,8 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.resid = (double*)s.be->alloc(2 * sizeof(double));
     if (opt_.temporal > 1 && s.be->kind() == DeviceKind::HIP)
       MDFX_CHECK(hip_supports_steps(spec_, s.lay, opt_.temporal),
-                 format("no fused %d-step kernel for %s %s with nx=%lld (temporal blocking: every stencil; "
-                        "box27 rows up to 1024 fp32 / 512 fp64)",
+                 format("no fused %d-step kernel for %s %s with nx=%lld (fused depths: 2 for every stencil "
+                        "(box27 rows up to 1024 fp32 / 512 fp64); 3, 4, 6, 8 for the 2D stencils)",
                         opt_.temporal, stencil_name(spec_.kind), dtype_name(spec_.dtype), (long long)global_.nx));
     // regions (storage planes); owned = [halo, halo + nzl). The boundary regions are the `halo`
     // planes at each end that the exchange sends: they are computed on the halo stream so the

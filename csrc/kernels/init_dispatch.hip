@@ -26,6 +26,8 @@ void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipSt
 template <class T>
 void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
+void launch_jacobi5_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
+template <class T>
 void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid, hipStream_t s);
 template <class T>
 bool box27_tb2_supported(const Geo& g);
@@ -34,6 +36,7 @@ void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, doubl
                   hipStream_t s);
 void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s);
 void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s);
+void launch_life_tbk(const Geo& g, const uint8_t* in, uint8_t* out, int steps, double* resid, hipStream_t s);
 template <class T>
 void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
@@ -171,9 +174,12 @@ void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* str
 
 bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps) {
   if (steps == 1) return true;
-  if (steps != 2 || lay.halo < 2) return false;
-  if (spec.kind == StencilKind::Jacobi5) return spec.dtype == DType::F32 || spec.dtype == DType::F64;
-  if (spec.kind == StencilKind::Life) return true;
+  if (steps < 2 || lay.halo < steps) return false;
+  const bool k2d = steps == 2 || steps == 3 || steps == 4 || steps == 6 || steps == 8;
+  if (spec.kind == StencilKind::Jacobi5)  // deep temporal blocking of the 2D problems
+    return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d;
+  if (spec.kind == StencilKind::Life) return k2d;
+  if (steps != 2) return false;
   if (spec.kind == StencilKind::Box27) {
     const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
     return spec.dtype == DType::F32 ? dev::box27_tb2_supported<float>(g) : dev::box27_tb2_supported<double>(g);
@@ -199,12 +205,21 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       else
         dev::launch_box27_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.coef, a.resid, s);
     } else if (spec.kind == StencilKind::Life) {
-      dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
-    } else if (spec.kind == StencilKind::Jacobi5) {
-      if (spec.dtype == DType::F32)
-        dev::launch_jacobi5_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
+      if (a.steps > 2 || dev::env_int("MDFX_LIFE_TBK", 0))
+        dev::launch_life_tbk(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.steps, a.resid, s);
       else
+        dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
+    } else if (spec.kind == StencilKind::Jacobi5) {
+      if (a.steps > 2 || dev::env_int("MDFX_J5_TBK", 0)) {
+        if (spec.dtype == DType::F32)
+          dev::launch_jacobi5_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
+        else
+          dev::launch_jacobi5_tbk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
+      } else if (spec.dtype == DType::F32) {
+        dev::launch_jacobi5_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
+      } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
+      }
     } else if (spec.dtype == DType::F32) {
       dev::launch_heat7_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
     } else {

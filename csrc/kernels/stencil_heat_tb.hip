@@ -500,5 +500,135 @@ void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, h
 template void launch_jacobi5_tb2<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
 template void launch_jacobi5_tb2<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
 
+// ---- 2D 5-point, K steps per sweep (K <= N) ---------------------------------------------------
+//
+// Deep temporal blocking for the 2D problem. Wave segments OVERLAP by OV = ceil(K / N) lanes on each
+// side: a wave covers 64 lanes x N columns but owns only lanes OV..63-OV, so the outer lanes carry
+// the neighbour segments' edge columns through the same SIMD instructions. Each level of the
+// pipeline corrupts one more column from the outside in (the outermost neighbour is unknown), so
+// after K <= OV * N levels the owned lanes are still exact and are the only ones stored. Per row the wave
+// keeps a 3-row ring per level; level l produces row q-l when u0 row q arrives. One read and one
+// write of the field per K steps; bitwise equal to K sm::jacobi5 steps.
+template <class T, int K, bool RES>
+__global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
+                                                   int zc, int XT, int ntasks, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  constexpr int N = VT<T>::N;
+  constexpr int OV = (K + N - 1) / N;  // overlap lanes per side
+  constexpr int SEG = (64 - 2 * OV) * N;  // owned columns per wave
+  const int lane = threadIdx.x & 63;
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;  // wave-uniform; no block barriers in this kernel
+  const int xt = task % XT, zt = task / XT;
+  const int64_t x = (int64_t)xt * SEG - OV * N + (int64_t)lane * N;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x >= 0 && x < g.pitch;
+  const bool own = lane >= OV && lane <= 63 - OV && xin;
+  const int64_t plane = g.plane;
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  auto ld = [&](int64_t lz) -> V {
+    V v = vsplat_tb<V>(T(0));
+    if (xin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x, N);
+      v = *(const V*)(in + lz * plane + x);
+    }
+    return v;
+  };
+  // one step of row `C` with rows `P` (z-1) and `Q` (z+1) at global row gz
+  auto step = [&](const V& P, const V& C, const V& Q, int64_t gz, bool inner_only) -> V {
+    V o = C;
+    const T l = lane_up1(C[N - 1]);
+    const T rr = lane_down1(C[0]);
+    const bool bnd = inner_only ? (gz == 0 || gz == g.gnz - 1) : (gz <= 0 || gz >= g.gnz - 1);
+    if (!bnd) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const T xm = e == 0 ? l : C[e - 1];
+        const T xp = e == N - 1 ? rr : C[e + 1];
+        const T v = sm::jacobi5<T>(C[e], xm, xp, P[e], Q[e], r);
+        o[e] = xb[e] ? C[e] : v;
+      }
+    }
+    return o;
+  };
+  // ring[l][0..2] = rows (newest-2 .. newest) of level l; level 0 = u0
+  V ring[K][3];
+#pragma unroll
+  for (int l = 0; l < K; ++l)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) ring[l][j] = vsplat_tb<V>(T(0));
+  ring[0][1] = ld(zs - K - 1);
+  ring[0][2] = ld(zs - K);
+  V nx = ld(zs - K + 1);
+  double acc = 0.0;
+  // newest u0 row q; level l (1..K) produces row q - l
+  for (int64_t q = zs - K + 1; q <= ze - 1 + K; ++q) {
+    ring[0][0] = ring[0][1];
+    ring[0][1] = ring[0][2];
+    ring[0][2] = nx;
+    nx = ld(q + 1);
+#pragma unroll
+    for (int l = 1; l < K; ++l) {
+      const int64_t row = q - l;
+      const V v = step(ring[l - 1][0], ring[l - 1][1], ring[l - 1][2], row + g.gz_off, false);
+      ring[l][0] = ring[l][1];
+      ring[l][1] = ring[l][2];
+      ring[l][2] = v;
+    }
+    const int64_t lz = q - K;
+    if (lz >= zs) {
+      const V& C = ring[K - 1][1];
+      const V o = step(ring[K - 1][0], C, ring[K - 1][2], lz + g.gz_off, true);
+      if (own) {
+        dcheck(g, (const T*)out, out + lz * plane + x, N);
+        store_nt((V*)(out + lz * plane + x), o);
+        if (RES) {
+#pragma unroll
+          for (int e = 0; e < N; ++e)
+            if (x + e < g.nx) {
+              const double d = (double)o[e] - (double)C[e];
+              acc += d * d;
+            }
+        }
+      }
+    }
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T, int K>
+static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  const int64_t planes = g.lz_end - g.lz_begin;
+  if (planes <= 0) return;
+  constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  const int XT = (int)((g.nx + SEG - 1) / SEG);
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const int ntasks = XT * ZT;
+  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((jacobi5_tbk<T, K, true>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+  else
+    hipLaunchKernelGGL((jacobi5_tbk<T, K, false>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+}
+
+template <class T>
+void launch_jacobi5_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
+  switch (steps) {
+    case 2: launch_jacobi5_tbk_k<T, 2>(g, in, out, r, resid, s); break;
+    case 3: launch_jacobi5_tbk_k<T, 3>(g, in, out, r, resid, s); break;
+    case 4: launch_jacobi5_tbk_k<T, 4>(g, in, out, r, resid, s); break;
+    case 6: launch_jacobi5_tbk_k<T, 6>(g, in, out, r, resid, s); break;
+    case 8: launch_jacobi5_tbk_k<T, 8>(g, in, out, r, resid, s); break;
+    default: break;
+  }
+}
+template void launch_jacobi5_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
+template void launch_jacobi5_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
+
 }  // namespace dev
 }  // namespace mdfx

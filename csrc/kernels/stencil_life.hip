@@ -304,5 +304,133 @@ void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resi
     hipLaunchKernelGGL(life_tb2<false>, grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
 }
 
+// ---- K generations per sweep --------------------------------------------------------------------
+//
+// Deep temporal blocking with overlapping wave segments, as jacobi5_tbk: a wave owns lanes 1..62
+// and lanes 0 / 63 carry the neighbours' edge cells; every generation corrupts one more byte of
+// those two lanes from the outside in, so K <= 16 generations leave the owned lanes exact.
+template <int K, bool RES>
+__global__ __launch_bounds__(256) void life_tbk(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                Geo g, int zc, int XT, int ntasks, double* __restrict__ resid) {
+  constexpr int N = 16;
+  constexpr int SEG = 62 * N;
+  static_assert(K >= 1 && K <= N, "generations must not reach past the halo lanes");
+  const int lane = threadIdx.x & 63;
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;  // wave-uniform, no barriers
+  const int xt = task % XT, zt = task / XT;
+  const int64_t x = (int64_t)xt * SEG - N + (int64_t)lane * N;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x >= 0 && x < g.pitch;
+  const bool own = lane >= 1 && lane <= 62 && xin;
+  const bool frame = x == 0 || (x >= 0 && x + N > g.nx - 1);
+  const int64_t plane = g.plane;
+  auto ld = [&](int64_t lz) -> U2 {
+    if (xin && lz >= 0 && lz < g.lz_max) {
+      dcheck(g, in, in + lz * plane + x, N);
+      return ld_u2(in + lz * plane + x);
+    }
+    return U2{0, 0};
+  };
+  auto gen = [&](const U2& P, const U2& C, const U2& Nn, int64_t gz, bool inner_only) -> U2 {
+    const bool bnd = inner_only ? (gz == 0 || gz == g.gnz - 1) : (gz <= 0 || gz >= g.gnz - 1);
+    if (bnd) return C;
+    const U2 S{P.lo + C.lo + Nn.lo, P.hi + C.hi + Nn.hi};
+    const uint64_t sl = (uint32_t)lane_up1((int)(S.hi >> 56));
+    const uint64_t sr = (uint32_t)lane_down1((int)(S.lo & 0xFF));
+    const U2 L{(S.lo << 8) | sl, (S.hi << 8) | (S.lo >> 56)};
+    const U2 R{(S.lo >> 8) | (S.hi << 56), (S.hi >> 8) | (sr << 56)};
+    const U2 T{L.lo + S.lo + R.lo, L.hi + S.hi + R.hi};
+    U2 o{bytes_eq(T.lo, 3) | (C.lo & bytes_eq(T.lo, 4)), bytes_eq(T.hi, 3) | (C.hi & bytes_eq(T.hi, 4))};
+    if (frame) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const int64_t xe = x + e;
+        if (xe == 0 || xe >= g.nx - 1) {
+          const uint64_t m = 0xFFull << (8 * (e & 7));
+          if (e < 8)
+            o.lo = (o.lo & ~m) | (C.lo & m);
+          else
+            o.hi = (o.hi & ~m) | (C.hi & m);
+        }
+      }
+    }
+    return o;
+  };
+  U2 ring[K][3];
+#pragma unroll
+  for (int l = 0; l < K; ++l)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) ring[l][j] = U2{0, 0};
+  ring[0][1] = ld(zs - K - 1);
+  ring[0][2] = ld(zs - K);
+  U2 nx = ld(zs - K + 1);
+  double acc = 0.0;
+  for (int64_t q = zs - K + 1; q <= ze - 1 + K; ++q) {
+    ring[0][0] = ring[0][1];
+    ring[0][1] = ring[0][2];
+    ring[0][2] = nx;
+    nx = ld(q + 1);
+#pragma unroll
+    for (int l = 1; l < K; ++l) {
+      const U2 v = gen(ring[l - 1][0], ring[l - 1][1], ring[l - 1][2], q - l + g.gz_off, false);
+      ring[l][0] = ring[l][1];
+      ring[l][1] = ring[l][2];
+      ring[l][2] = v;
+    }
+    const int64_t lz = q - K;
+    if (lz >= zs) {
+      const U2 C = ring[K - 1][1];
+      const U2 o = gen(ring[K - 1][0], C, ring[K - 1][2], lz + g.gz_off, true);
+      if (own) {
+        uint4 qv;
+        qv.x = (uint32_t)o.lo;
+        qv.y = (uint32_t)(o.lo >> 32);
+        qv.z = (uint32_t)o.hi;
+        qv.w = (uint32_t)(o.hi >> 32);
+        dcheck(g, (const uint8_t*)out, out + lz * plane + x, N);
+        *(uint4*)(out + lz * plane + x) = qv;
+        if (RES) {
+          const uint64_t dlo = o.lo ^ C.lo, dhi = o.hi ^ C.hi;
+          int cnt = 0;
+          for (int e = 0; e < N; ++e)
+            if (x + e < g.nx) cnt += (int)(((e < 8 ? dlo : dhi) >> (8 * (e & 7))) & 1);
+          acc += (double)cnt;
+        }
+      }
+    }
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <int K>
+static void launch_life_tbk_k(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s) {
+  const int64_t planes = g.lz_end - g.lz_begin;
+  if (planes <= 0) return;
+  constexpr int SEG = 62 * 16;
+  const int XT = (int)((g.nx + SEG - 1) / SEG);
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const int ntasks = XT * ZT;
+  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((life_tbk<K, true>), grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
+  else
+    hipLaunchKernelGGL((life_tbk<K, false>), grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
+}
+
+void launch_life_tbk(const Geo& g, const uint8_t* in, uint8_t* out, int steps, double* resid, hipStream_t s) {
+  switch (steps) {
+    case 2: launch_life_tbk_k<2>(g, in, out, resid, s); break;
+    case 3: launch_life_tbk_k<3>(g, in, out, resid, s); break;
+    case 4: launch_life_tbk_k<4>(g, in, out, resid, s); break;
+    case 6: launch_life_tbk_k<6>(g, in, out, resid, s); break;
+    case 8: launch_life_tbk_k<8>(g, in, out, resid, s); break;
+    default: break;
+  }
+}
+
 }  // namespace dev
 }  // namespace mdfx

@@ -295,4 +295,23 @@ def test_temporal2_checkpoint_roundtrip(mdfx, tmp_path):
 
 def test_temporal_depth_validated(mdfx):
     with pytest.raises(RuntimeError):
-        m.Simulation(m.heat3d(n=8), device="cpu", temporal=3)
+        m.Simulation(m.heat3d(n=8), device="cpu", temporal=9)
+    with pytest.raises(RuntimeError, match="ghost planes"):  # slabs thinner than the exchanged halo
+        m.Simulation(m.mdf2d(h=20, w=16), device="cpu", ranks=4, temporal=8)
+
+
+@pytest.mark.parametrize("temporal", [3, 4, 8])
+@pytest.mark.parametrize("prob", [m.mdf2d(h=61, w=37), m.life2d(h=70, w=45)], ids=["mdf", "life"])
+def test_deep_temporal_2d_equals_single_steps_cpu(mdfx, prob, temporal):
+    """Deep temporal blocking (halo = K rows, K fused steps per sweep) of the 2D problems, with
+    residual evaluations that fall inside and between sweeps."""
+    with m.Simulation(prob, device="cpu", residual_every=5) as sim:
+        sim.init()
+        sim.run(23)
+        ref, rr = sim.gather(), sim.residual
+    with m.Simulation(prob, device="cpu", ranks=3, temporal=temporal, residual_every=5) as sim:
+        assert sim.layout(0)["halo"] == temporal
+        sim.init()
+        sim.run(23)
+        assert sim.steps == 23
+        assert np.array_equal(ref, sim.gather()) and abs(sim.residual - rr) <= 1e-9 * max(1.0, rr)

@@ -148,3 +148,47 @@ def test_engine_temporal2_box27(hip):
     ref, rr = _sim(prob, 9, ranks=1, residual_every=9)
     got, rg = _sim(prob, 9, ranks=3, temporal=2, residual_every=9)
     assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
+
+
+DEEP = [models.mdf2d(h=45, w=1000), models.mdf2d(h=33, w=300, dtype="f64"), models.life2d(h=50, w=3000),
+        models.life2d(h=19, w=100)]
+
+
+@pytest.mark.parametrize("prob", DEEP, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("k", [2, 3, 4, 6, 8])
+def test_deep_fused_steps_bitwise(hip, prob, k, monkeypatch):
+    """K fused steps per sweep (overlapping wave segments) == K naive single steps, bitwise; K = 2
+    also through the overlapped-segment kernels (MDFX_J5_TBK / MDFX_LIFE_TBK)."""
+    for force in ((0, 1) if k == 2 else (0,)):
+        monkeypatch.setenv("MDFX_J5_TBK", str(force))
+        monkeypatch.setenv("MDFX_LIFE_TBK", str(force))
+        lay = FieldLayout.make(prob, halo=k)
+        src = alloc_field(lay, "cuda")
+        init_field(prob, lay, src)
+        fused = alloc_field(lay, "cuda")
+        res = torch.zeros((), dtype=torch.float64, device="cuda")
+        apply_stencil(prob, lay, src, fused, steps=k, resid=res)
+        set_kernel_variant("naive")
+        try:
+            cur = alloc_field(lay, "cuda")
+            cur.copy_(src)
+            ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+            for i in range(k):
+                nxt = alloc_field(lay, "cuda")
+                nxt.copy_(cur)
+                apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+                cur = nxt
+        finally:
+            set_kernel_variant("auto")
+        torch.cuda.synchronize()
+        o = lay.owned
+        assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, force)
+        assert abs(res.item() - ref_res.item()) <= 1e-9 * max(1.0, ref_res.item())
+
+
+@pytest.mark.parametrize("prob,k", [(mm.mdf2d(h=400, w=1500), 8), (mm.mdf2d(h=200, w=700, dtype="f64"), 4),
+                                    (mm.life2d(h=300, w=5000), 4), (mm.life2d(h=300, w=2000), 6)])
+def test_engine_deep_temporal_2d(hip, prob, k):
+    ref, rr = _sim(prob, 37, ranks=1, residual_every=9)
+    got, rg = _sim(prob, 37, ranks=4, temporal=k, residual_every=9)
+    assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * max(1.0, rr)
