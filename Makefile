@@ -56,6 +56,10 @@ $(OBJ)/%.o: csrc/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX_HOST) $(HOSTFLAGS) -c $< -o $@
 
+# the AVX2 + FMA copy of the CPU stencils (selected at run time by cpu_kernels.cpp)
+$(OBJ)/cpu/cpu_kernels_avx2.o $(ASAN_DIR)/cpu/cpu_kernels_avx2.o $(DCK_DIR)/cpu/cpu_kernels_avx2.o: HOSTFLAGS += -mavx2 -mfma
+$(OBJ)/cpu/cpu_kernels.o $(OBJ)/cpu/cpu_kernels_avx2.o: csrc/cpu/cpu_stencils.inc
+
 $(LIB): $(KERNEL_OBJ) $(HOST_OBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ $(LINK_ROCM) -Wl,-soname,libmdfx.so -Wl,-rpath,$(ROCM)/lib

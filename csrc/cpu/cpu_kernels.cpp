@@ -12,133 +12,17 @@
 #include "mdfx/kernels.hpp"
 #include "mdfx/stencil_math.hpp"
 
+#define MDFX_CPU_NS cpu_base
+#include "cpu_stencils.inc"
+
 namespace mdfx {
+namespace cpu_avx2 {
+void region(const StencilSpec& spec, const RegionArgs& a);
+}
 
 namespace {
-
-struct Pl {
-  int64_t pitch, plane, nx, ny, gnz, gz_off;
-};
-
-Pl pl_of(const FieldLayout& l) {
-  return Pl{l.pitch, l.plane, l.global.nx, l.global.ny, l.global.nz, l.z0 - l.halo};
-}
-
-template <class T>
-void heat7_cpu(const T* in, T* out, const Pl& g, int64_t lb, int64_t le, T r, double* resid) {
-  double acc = 0.0;
-#pragma omp parallel for schedule(static) reduction(+ : acc) if ((le - lb) * g.ny * g.nx > 65536)
-  for (int64_t lz = lb; lz < le; ++lz) {
-    const int64_t gz = lz + g.gz_off;
-    for (int64_t y = 0; y < g.ny; ++y) {
-      const int64_t row = lz * g.plane + y * g.pitch;
-      const bool inner = gz > 0 && gz < g.gnz - 1 && y > 0 && y < g.ny - 1;
-      for (int64_t x = 0; x < g.nx; ++x) {
-        const int64_t i = row + x;
-        const T c = in[i];
-        T o = c;
-        if (inner && x > 0 && x < g.nx - 1)
-          o = sm::heat7<T>(c, in[i - 1], in[i + 1], in[i - g.pitch], in[i + g.pitch], in[i - g.plane],
-                           in[i + g.plane], r);
-        out[i] = o;
-        const double d = (double)o - (double)c;
-        acc += d * d;
-      }
-    }
-  }
-  if (resid) *resid += acc;
-}
-
-template <class T>
-void jacobi5_cpu(const T* in, T* out, const Pl& g, int64_t lb, int64_t le, T r, double* resid) {
-  double acc = 0.0;
-#pragma omp parallel for schedule(static) reduction(+ : acc) if ((le - lb) * g.nx > 65536)
-  for (int64_t lz = lb; lz < le; ++lz) {
-    const int64_t gz = lz + g.gz_off;
-    const int64_t row = lz * g.plane;
-    const bool inner = gz > 0 && gz < g.gnz - 1;
-    for (int64_t x = 0; x < g.nx; ++x) {
-      const int64_t i = row + x;
-      const T c = in[i];
-      T o = c;
-      if (inner && x > 0 && x < g.nx - 1)
-        o = sm::jacobi5<T>(c, in[i - 1], in[i + 1], in[i - g.plane], in[i + g.plane], r);
-      out[i] = o;
-      const double d = (double)o - (double)c;
-      acc += d * d;
-    }
-  }
-  if (resid) *resid += acc;
-}
-
-template <class T>
-inline void box27_partials(const T* p, int64_t pitch, T& center, T& cross, T& diag) {
-  const T hm = p[-pitch - 1] + p[-pitch + 1];
-  const T h0 = p[-1] + p[1];
-  const T hp = p[pitch - 1] + p[pitch + 1];
-  center = p[0];
-  cross = h0 + (p[-pitch] + p[pitch]);
-  diag = hm + hp;
-}
-
-template <class T>
-void box27_cpu(const T* in, T* out, const Pl& g, int64_t lb, int64_t le, const StencilCoef& cf,
-               double* resid) {
-  const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
-  double acc = 0.0;
-#pragma omp parallel for schedule(static) reduction(+ : acc) if ((le - lb) * g.ny * g.nx > 65536)
-  for (int64_t lz = lb; lz < le; ++lz) {
-    const int64_t gz = lz + g.gz_off;
-    for (int64_t y = 0; y < g.ny; ++y) {
-      const int64_t row = lz * g.plane + y * g.pitch;
-      const bool inner = gz > 0 && gz < g.gnz - 1 && y > 0 && y < g.ny - 1;
-      for (int64_t x = 0; x < g.nx; ++x) {
-        const int64_t i = row + x;
-        const T c = in[i];
-        T o = c;
-        if (inner && x > 0 && x < g.nx - 1) {
-          T ce, cr, dg;
-          box27_partials(in + i - g.plane, g.pitch, ce, cr, dg);
-          const T am = sm::box27_A(ce, cr, dg, c1, c2, c3);
-          box27_partials(in + i, g.pitch, ce, cr, dg);
-          const T bc = sm::box27_B(ce, cr, dg, c0, c1, c2);
-          box27_partials(in + i + g.plane, g.pitch, ce, cr, dg);
-          const T ap = sm::box27_A(ce, cr, dg, c1, c2, c3);
-          o = sm::box27_combine(am, bc, ap);
-        }
-        out[i] = o;
-        const double d = (double)o - (double)c;
-        acc += d * d;
-      }
-    }
-  }
-  if (resid) *resid += acc;
-}
-
-void life_cpu(const uint8_t* in, uint8_t* out, const Pl& g, int64_t lb, int64_t le, double* resid) {
-  double acc = 0.0;
-#pragma omp parallel for schedule(static) reduction(+ : acc) if ((le - lb) * g.nx > 65536)
-  for (int64_t lz = lb; lz < le; ++lz) {
-    const int64_t gz = lz + g.gz_off;
-    const int64_t row = lz * g.plane;
-    const bool inner = gz > 0 && gz < g.gnz - 1;
-    for (int64_t x = 0; x < g.nx; ++x) {
-      const int64_t i = row + x;
-      const uint8_t c = in[i];
-      uint8_t o = c;
-      if (inner && x > 0 && x < g.nx - 1) {
-        unsigned t = 0;
-        for (int dz = -1; dz <= 1; ++dz)
-          for (int dx = -1; dx <= 1; ++dx) t += in[i + dz * g.plane + dx];
-        o = sm::life_rule(t, c);
-      }
-      out[i] = o;
-      acc += (o != c) ? 1.0 : 0.0;
-    }
-  }
-  if (resid) *resid += acc;
-}
-
+using cpu_base::Pl;
+using cpu_base::pl_of;
 }  // namespace
 
 static void cpu_region(const StencilSpec& spec, const RegionArgs& a);
@@ -171,31 +55,15 @@ void cpu_stencil(const StencilSpec& spec, const RegionArgs& a) {
   }
 }
 
+// AVX2 + FMA build when the host supports it (hardware fma instead of libm's software fmaf on
+// baseline x86-64); both are exact, so the choice never changes a result
 static void cpu_region(const StencilSpec& spec, const RegionArgs& a) {
-  const Pl g = pl_of(a.lay);
-  switch (spec.kind) {
-    case StencilKind::Heat7:
-      if (spec.dtype == DType::F32)
-        heat7_cpu<float>((const float*)a.in, (float*)a.out, g, a.lz_begin, a.lz_end, (float)spec.rate(), a.resid);
-      else
-        heat7_cpu<double>((const double*)a.in, (double*)a.out, g, a.lz_begin, a.lz_end, spec.rate(), a.resid);
-      break;
-    case StencilKind::Jacobi5:
-      if (spec.dtype == DType::F32)
-        jacobi5_cpu<float>((const float*)a.in, (float*)a.out, g, a.lz_begin, a.lz_end, (float)spec.rate(), a.resid);
-      else
-        jacobi5_cpu<double>((const double*)a.in, (double*)a.out, g, a.lz_begin, a.lz_end, spec.rate(), a.resid);
-      break;
-    case StencilKind::Box27:
-      if (spec.dtype == DType::F32)
-        box27_cpu<float>((const float*)a.in, (float*)a.out, g, a.lz_begin, a.lz_end, spec.coef, a.resid);
-      else
-        box27_cpu<double>((const double*)a.in, (double*)a.out, g, a.lz_begin, a.lz_end, spec.coef, a.resid);
-      break;
-    case StencilKind::Life:
-      life_cpu((const uint8_t*)a.in, (uint8_t*)a.out, g, a.lz_begin, a.lz_end, a.resid);
-      break;
-  }
+  static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma") &&
+                           !std::getenv("MDFX_CPU_BASELINE");
+  if (avx2)
+    cpu_avx2::region(spec, a);
+  else
+    cpu_base::region(spec, a);
 }
 
 template <class T>

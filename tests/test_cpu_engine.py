@@ -315,3 +315,30 @@ def test_deep_temporal_2d_equals_single_steps_cpu(mdfx, prob, temporal):
         sim.run(23)
         assert sim.steps == 23
         assert np.array_equal(ref, sim.gather()) and abs(sim.residual - rr) <= 1e-9 * max(1.0, rr)
+
+
+def test_cpu_avx2_and_baseline_builds_bitwise_equal(tmp_path):
+    """The CPU stencils exist twice (baseline x86-64 with libm's software fma, and AVX2 + FMA chosen
+    at run time); both are exact, so every stencil must agree bit for bit."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np, mpi_cuda_process_amd as m\n"
+            "out = {}\n"
+            "for name, prob in [('h', m.heat3d(nx=37, ny=21, nz=19)), ('b', m.box27(nx=29, ny=17, nz=13, dtype='f64')),\n"
+            "                   ('j', m.mdf2d(h=77, w=91)), ('l', m.life2d(h=60, w=70))]:\n"
+            "    with m.Simulation(prob, device='cpu', ranks=2, residual_every=3) as sim:\n"
+            "        sim.init(); sim.run(7); out[name] = sim.gather(); out[name + 'r'] = np.array(sim.residual)\n"
+            "np.savez(sys.argv[1], **out)\n") % root
+    res = {}
+    for tag, env in (("avx2", {}), ("base", {"MDFX_CPU_BASELINE": "1"})):
+        f = str(tmp_path / (tag + ".npz"))
+        p = subprocess.run([sys.executable, "-c", code, f], env=dict(os.environ, OMP_NUM_THREADS="2", **env),
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+        assert p.returncode == 0, p.stderr.decode()[-2000:]
+        res[tag] = np.load(f)
+    for k in res["avx2"].files:
+        assert np.array_equal(res["avx2"][k], res["base"][k]), k
