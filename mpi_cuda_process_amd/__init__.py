@@ -3,9 +3,13 @@
 Capabilities of Rodrigovicente/MPI-CUDA-Process (2D 5-point MDF heat/Jacobi and Game of Life,
 slab-decomposed across ranks with ghost-row exchange and interior/boundary stream overlap),
 re-designed for AMD Instinct MI355X (gfx950): hand-written CDNA4 HIP kernels (2.5D z-marching,
-wave64, LDS edge exchange, XCD-aware tiling), a native C++ engine with two HIP streams per slab
-and double buffering, and RCCL point-to-point halo exchange over xGMI — plus 3D 7-point and
-27-point stencils, fp64, residuals, checkpoint/resume and hipGraph replay.
+wave64, DPP lane shifts + LDS seams, XCD-aware tiling, fused multi-step temporal blocking), a
+native C++ engine with two HIP streams per slab and double buffering, and RCCL point-to-point
+halo exchange over xGMI — plus 3D 7-point and 27-point stencils, fp64, residuals,
+checkpoint/resume and hipGraph replay.
+
+Entry points: :class:`Simulation` (decomposed, multi-slab / multi-GPU runs), :func:`advance`
+(functional: k steps of a dense grid tensor), ``python -m mpi_cuda_process_amd`` (CLI).
 
 Layout::
 
@@ -20,8 +24,9 @@ Layout::
 from ._native import hip_available, native, require_hip  # noqa: F401  (imports torch first)
 from .engine import Simulation  # noqa: F401
 from .models import InitCondition, Problem, box27, from_name, heat3d, life2d, mdf2d  # noqa: F401
+from .ops import advance  # noqa: F401
 
 __version__ = "0.1.0"
 
 __all__ = ["Simulation", "Problem", "InitCondition", "mdf2d", "life2d", "heat3d", "box27", "from_name",
-           "native", "hip_available", "require_hip"]
+           "advance", "native", "hip_available", "require_hip"]

@@ -135,3 +135,39 @@ def kernel_variant() -> str:
 
 __all__ = ["FieldLayout", "alloc_field", "init_field", "apply_stencil", "dense_to_field", "field_to_dense",
            "set_kernel_variant", "kernel_variant", "reference", "TORCH_DTYPE"]
+
+
+def advance(problem: Problem, grid: torch.Tensor, steps: int, temporal: int = 0) -> torch.Tensor:
+    """Functional API: ``steps`` time steps of ``problem``'s stencil applied to a dense global grid
+    ``(nz, ny, nx)`` (2D problems: ``(h, 1, w)`` or ``(h, w)``), on the grid's device (HIP kernels
+    on a GPU tensor, the CPU oracle otherwise). Returns a new dense tensor; the input is untouched.
+
+    ``temporal`` fuses that many steps per sweep (0 = the deepest fused kernel that exists for the
+    problem on this device, as the CLI's auto mode). The result is bitwise identical for every depth.
+    """
+    squeeze = grid.dim() == 2
+    g = grid.unsqueeze(1) if squeeze else grid
+    if tuple(g.shape) != (problem.nz, problem.ny, problem.nx):
+        raise ValueError("grid shape %s does not match the problem (%d, %d, %d)" %
+                         (tuple(grid.shape), problem.nz, problem.ny, problem.nx))
+    dev = g.device
+    if temporal <= 0:
+        want = {"jacobi5": 8, "life": 4}.get(problem.kind, 2)
+        while want > 1 and problem.nz < want:
+            want //= 2
+        temporal = 1
+        if dev.type == "cuda" and want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx,
+                                                                         problem.ny, problem.nz, want, want):
+            temporal = want
+    lay = FieldLayout.make(problem, halo=max(1, temporal))
+    a = alloc_field(lay, dev)
+    b = alloc_field(lay, dev)
+    dense_to_field(problem, g.to(TORCH_DTYPE[lay.dtype]), lay, a)
+    left = steps
+    while left > 0:
+        k = temporal if left >= temporal else 1
+        apply_stencil(problem, lay, a, b, steps=k)
+        a, b = b, a
+        left -= k
+    out = field_to_dense(lay, a)
+    return out.squeeze(1) if squeeze else out

@@ -342,3 +342,18 @@ def test_cpu_avx2_and_baseline_builds_bitwise_equal(tmp_path):
         res[tag] = np.load(f)
     for k in res["avx2"].files:
         assert np.array_equal(res["avx2"][k], res["base"][k]), k
+
+
+@pytest.mark.parametrize("prob,steps,temporal", [(m.heat3d(nx=20, ny=9, nz=11), 7, 0), (m.heat3d(nx=20, ny=9, nz=11), 7, 2),
+                                                 (m.mdf2d(h=30, w=17), 9, 4), (m.life2d(h=40, w=33), 6, 3),
+                                                 (m.box27(nx=13, ny=12, nz=10, dtype="f64"), 5, 2)])
+def test_advance_functional_api(mdfx, prob, steps, temporal):
+    with m.Simulation(prob, device="cpu") as sim:
+        sim.init()
+        g0 = torch.from_numpy(sim.gather().copy())
+        sim.run(steps)
+        ref = sim.gather()
+    out = m.advance(prob, g0, steps, temporal=temporal)
+    assert np.array_equal(out.numpy(), ref)
+    if prob.ny == 1:  # 2D grids may be passed as (h, w)
+        assert np.array_equal(m.advance(prob, g0.squeeze(1), steps, temporal=temporal).numpy(), ref.squeeze(1))

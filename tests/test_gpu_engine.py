@@ -188,3 +188,15 @@ def test_serialized_runtime_equals_overlapped(hip, tmp_path):
         res[tag] = np.load(out)
     for k in ("heat7", "box27", "life"):
         assert np.array_equal(res["overlap"][k], res["serial"][k]), k
+
+
+@pytest.mark.parametrize("prob,steps", [(m.heat3d(nx=300, ny=20, nz=24), 9), (m.mdf2d(h=200, w=1100), 19),
+                                        (m.life2d(h=150, w=2500), 13), (m.box27(nx=100, ny=30, nz=20), 6)])
+def test_advance_on_gpu_equals_cpu(hip, prob, steps):
+    """The functional API on a GPU tensor (auto fused depth) == the CPU oracle, bitwise."""
+    with m.Simulation(prob, device="cpu") as sim:
+        sim.init()
+        g0 = torch.from_numpy(sim.gather().copy())
+    gpu = m.advance(prob, g0.cuda(), steps)
+    cpu = m.advance(prob, g0, steps, temporal=1)
+    assert gpu.is_cuda and torch.equal(gpu.cpu(), cpu)
