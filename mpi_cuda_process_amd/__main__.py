@@ -13,11 +13,10 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 import time
 
-import numpy as np
+from .utils import metrics_record, print_array
 
 
 def _parser() -> argparse.ArgumentParser:
@@ -66,24 +65,6 @@ def _problem(a):
     return from_name(kind, nx=a.nx or n, ny=a.ny or n, nz=a.nz or n, dtype=a.dtype).with_init(seed=a.seed)
 
 
-def print_array(g: np.ndarray, out=sys.stdout) -> None:
-    """The reference's print_array (kernel.cu:115-129): '0' for a cell equal to 1, ' ' otherwise,
-    a newline per row, blank lines around. 3D grids print plane by plane after a "z=<k>" label,
-    like the native CLI."""
-    def rows(a):
-        out.write("\n")
-        for row in a:
-            out.write("".join("0" if v == 1 else " " for v in row) + "\n")
-        out.write("\n")
-
-    if g.ndim == 3 and g.shape[1] > 1:
-        for z in range(g.shape[0]):
-            out.write("z=%d" % z)
-            rows(g[z])
-    else:
-        rows(g.reshape(-1, g.shape[-1]))
-
-
 def main(argv=None) -> int:
     a = _parser().parse_args(argv)
     import torch
@@ -123,17 +104,14 @@ def main(argv=None) -> int:
             g = sim.gather()
             if rank0:
                 print_array(g.reshape(prob.nz, prob.ny, prob.nx))
-        gcs = prob.cells * a.steps / dt / 1e9 if dt > 0 else 0.0
+        ngpu = (dist.get_world_size() if distributed else 1) if sim.device == "hip" else 0
+        rec = metrics_record(prob, a.steps, dt, ngpu, {"device": sim.device, "temporal": sim.temporal,
+                                                       "residual": sim.residual})
         if rank0 and a.json:
-            ngpu = (int(os.environ.get("WORLD_SIZE", "1")) if distributed else 1) if sim.device == "hip" else 0
-            print(json.dumps({"metric": "GCells/s", "value": round(gcs, 4), "unit": "GCells/s",
-                              "stencil": prob.kind, "dtype": prob.dtype, "grid": [prob.nx, prob.ny, prob.nz],
-                              "steps": a.steps, "seconds": round(dt, 6),
-                              "ms_per_step": round(dt / max(a.steps, 1) * 1e3, 4), "n_gpus": ngpu,
-                              "device": sim.device, "temporal": sim.temporal, "residual": sim.residual}))
+            print(json.dumps(rec))
         elif rank0 and not a.print:
             print("%s %dx%dx%d %s | %d steps in %.4f s | %.2f GCells/s" % (prob.kind, prob.nx, prob.ny, prob.nz,
-                                                                          prob.dtype, a.steps, dt, gcs))
+                                                                          prob.dtype, a.steps, dt, rec["value"]))
     return 0
 
 

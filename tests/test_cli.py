@@ -125,15 +125,9 @@ def test_mpirun_heat7_json():
 
 
 def _read_dump(d):
-    """Reassemble a --dump / checkpoint directory (per-slab raw + JSON header) into one array."""
-    metas = [json.load(open(os.path.join(d, f))) for f in sorted(os.listdir(d)) if f.endswith(".json")]
-    m0 = metas[0]
-    dt = {"f32": np.float32, "f64": np.float64, "u8": np.uint8}[m0["dtype"]]
-    out = np.zeros((m0["nz"], m0["ny"], m0["nx"]), dtype=dt)
-    for m in metas:
-        raw = np.fromfile(os.path.join(d, "slab_%d.bin" % m["rank"]), dtype=dt)
-        out[m["z0"]:m["z1"]] = raw.reshape(m["z1"] - m["z0"], m["ny"], m["nx"])
-    return out, metas
+    from mpi_cuda_process_amd.utils import read_checkpoint
+
+    return read_checkpoint(d)
 
 
 def test_dump_dim_profile_json_matches_python_engine(tmp_path):
@@ -168,3 +162,23 @@ def test_dim_bc_coef_aliases():
     p = subprocess.run([os.path.join(BIN, "mdfx"), "--backend", "cpu", "--dim", "2", "--stencil", "7"],
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE)
     assert p.returncode != 0 and b"--dim" in p.stderr
+
+
+def test_utils_format_array_and_checkpoint_reader(tmp_path):
+    """utils.format_array reproduces the native print_array bytes; read_checkpoint reassembles any
+    decomposition and rejects incomplete directories."""
+    import mpi_cuda_process_amd as mm
+    from mpi_cuda_process_amd.utils import format_array, read_checkpoint
+
+    ck = str(tmp_path / "ck")
+    out = run([os.path.join(BIN, "life"), "--backend", "cpu", "--init", "life", "--h", "30", "--w", "40", "--steps",
+               "5", "--print", "--quiet", "--ranks", "3", "--dump", ck])
+    grid, metas = read_checkpoint(ck)
+    assert len(metas) == 3 and grid.shape == (30, 1, 40) and format_array(grid) == out
+    with mm.Simulation(mm.life2d(h=30, w=40), device="cpu") as sim:
+        sim.init()
+        sim.run(5)
+        assert np.array_equal(sim.gather(), grid)
+    os.remove(os.path.join(ck, "slab_1.json"))
+    with pytest.raises(ValueError):
+        read_checkpoint(ck)
