@@ -33,7 +33,33 @@ from .parallel.decomp import slab_bounds
 from .parallel.dist import TorchP2PTransport, broadcast_bytes, is_distributed
 
 
+def auto_temporal(problem: Problem, nranks: int, device: str) -> int:
+    """Fused steps per sweep chosen like the CLIs' auto mode: the deepest fused kernel that exists on
+    this device (2 for the 3D stencils, 8 for the 2D MDF, 4 for Life), halved until every slab is
+    at least 4 sweeps deep; 1 on the CPU, where fused sweeps bring nothing."""
+    if device != "hip":
+        return 1
+    want = {"jacobi5": 8, "life": 4}.get(problem.kind, 2)
+    while want > 1 and problem.nz < 4 * want * nranks:
+        want //= 2
+    if want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
+                                                want, want):
+        return want
+    return 1
+
+
 class Simulation:
+    """One decomposed stencil simulation driven by the native engine.
+
+    Parameters: ``device`` hip | cpu | auto; ``ranks`` P virtual slabs in this process (default:
+    one per distributed rank, or 1); ``devices`` GPU ids for the local slabs; ``transport`` auto |
+    rccl | torch | staged | loopback | host; ``overlap`` interior sweep concurrent with boundary
+    planes + exchange; ``sync_debug`` serialise every phase (race screen); ``residual_every`` k:
+    global L2 norm of the update every k steps (NaN/Inf guard); ``graph`` replay two-sweep cycles
+    as hipGraphs; ``timeout_s`` watchdog; ``temporal`` fused steps per sweep (1 = none, 0 = auto,
+    see :func:`auto_temporal`; halo planes = temporal).
+    """
+
     def __init__(self, problem: Problem, *, device: str = "auto", ranks: Optional[int] = None,
                  devices: Optional[Sequence[int]] = None, transport: str = "auto",
                  distributed: Optional[bool] = None, overlap: bool = True, sync_debug: bool = False,
@@ -101,6 +127,8 @@ class Simulation:
                 args["unique_id"] = native().rccl_unique_id()
 
         self.nranks = nranks
+        if temporal <= 0:
+            temporal = auto_temporal(problem, nranks, device)
         self._s = native().Solver(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                   nranks, local_ranks, dev_list, overlap=overlap,
                                   sync_debug=sync_debug, residual_every=residual_every, graph=graph,

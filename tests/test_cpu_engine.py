@@ -357,3 +357,11 @@ def test_advance_functional_api(mdfx, prob, steps, temporal):
     assert np.array_equal(out.numpy(), ref)
     if prob.ny == 1:  # 2D grids may be passed as (h, w)
         assert np.array_equal(m.advance(prob, g0.squeeze(1), steps, temporal=temporal).numpy(), ref.squeeze(1))
+
+
+def test_auto_temporal_rule(mdfx):
+    from mpi_cuda_process_amd.engine import auto_temporal
+
+    assert auto_temporal(m.heat3d(n=64), 1, "cpu") == 1
+    with m.Simulation(m.mdf2d(h=64, w=32), device="cpu", temporal=0) as sim:
+        assert sim.temporal == 1  # the CPU never fuses by default

@@ -200,3 +200,23 @@ def test_advance_on_gpu_equals_cpu(hip, prob, steps):
     gpu = m.advance(prob, g0.cuda(), steps)
     cpu = m.advance(prob, g0, steps, temporal=1)
     assert gpu.is_cuda and torch.equal(gpu.cpu(), cpu)
+
+
+def test_auto_temporal_on_gpu(hip):
+    from mpi_cuda_process_amd.engine import auto_temporal
+
+    assert auto_temporal(m.heat3d(n=64), 1, "hip") == 2
+    assert auto_temporal(m.mdf2d(h=4096, w=64), 4, "hip") == 8
+    assert auto_temporal(m.mdf2d(h=40, w=64), 4, "hip") == 2  # 40 rows over 4 slabs: shallower sweeps
+    assert auto_temporal(m.life2d(h=4096, w=64), 2, "hip") == 4
+    prob = m.life2d(h=400, w=1000)
+    ref, _ = _sim_gather(prob, 21, temporal=1)
+    got, t = _sim_gather(prob, 21, temporal=0, ranks=3)
+    assert t == 4 and np.array_equal(ref, got)
+
+
+def _sim_gather(prob, steps, **kw):
+    with m.Simulation(prob, device="hip", **kw) as sim:
+        sim.init()
+        sim.run(steps)
+        return sim.gather(), sim.temporal
