@@ -24,7 +24,7 @@ from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, i
                                       set_kernel_variant)
 
 KEYS = {"RY": "MDFX_RY", "PF": "MDFX_PF", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
-        "TBPF": "MDFX_TB_PF", "TBBP": "MDFX_TB_BP", "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK"}
+        "TBPF": "MDFX_TB_PF", "TBBP": "MDFX_TB_BP", "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBGL": "MDFX_TB_GL"}
 
 
 def parse_variant(s):

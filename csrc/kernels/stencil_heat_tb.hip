@@ -295,6 +295,193 @@ static int tb2_zc(int64_t planes, int64_t tiles, int64_t resident) {
   return (int)zc;
 }
 
+// ---- LDS-DMA prefetch variant (rows within one block) -------------------------------------------
+//
+// Same arithmetic and schedule as heat7_tb2, but the next u0 plane is not prefetched into VGPRs:
+// each wave streams it with global_load_lds (16 B per lane, no VGPR destination) into its own LDS
+// slot right after the iteration's stores, and copies it into registers one iteration later, just
+// before the next stores, where the oldest plane's registers have already died. That removes the
+// prefetch's six row vectors from the register budget. The loop uses a raw s_barrier with an
+// explicit lgkmcnt(0) (a __syncthreads would make hipcc drain the DMA at every barrier) and an
+// explicit vmcnt(0) before reading the slot (hipcc does not track LDS-DMA writes).
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <class T, int RY, int WXN, bool RES>
+__global__ __launch_bounds__(256) void heat7_tb2_gl(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
+                                                    int zc, int YT, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  constexpr int WYN = 4 / WXN;
+  constexpr int R0 = RY + 4;
+  constexpr int R1 = RY + 2;
+  __shared__ T edge[2][4][R1 + RY][2];
+  __shared__ V pre[4][R0][64];
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int yt = t % YT;
+  const int zt = t / YT;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wx = w % WXN, wy = w / WXN;
+  const int64_t xw = (int64_t)wx * WX;
+  const uint32_t xo = (uint32_t)lane * N;
+  const int64_t x = xw + xo;
+  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const T* ib = in + (y0 - 2) * pitch + xw;
+  T* ob = out + y0 * pitch + xw;
+  auto rowok = [&](int k) { const int64_t y = y0 - 2 + k; return y >= 0 && y < g.ny; };
+  auto ld = [&](int64_t lz, int k) -> V {
+    V v = vsplat_tb<V>(T(0));
+    if (lz >= 0 && lz < g.lz_max && rowok(k) && xin) {
+      dcheck(g, in, ib + lz * plane + (int64_t)k * pitch + xo, N);
+      v = *(const V*)(ib + lz * plane + (int64_t)k * pitch + xo);
+    }
+    return v;
+  };
+  auto issue = [&](int64_t lz) {  // stream u0 plane lz into this wave's slot
+    if (lz < 0 || lz >= g.lz_max) return;
+#pragma unroll
+    for (int k = 0; k < R0; ++k)
+      if (rowok(k) && xin) {
+        dcheck(g, in, ib + lz * plane + (int64_t)k * pitch + xo, N);
+        glds16(ib + lz * plane + (int64_t)k * pitch + xo, &pre[w][k][0]);
+      }
+  };
+  auto take = [&](int64_t lz, V (&dst)[R0]) {  // slot -> registers (after vmcnt(0))
+    const bool zok = lz >= 0 && lz < g.lz_max;
+#pragma unroll
+    for (int k = 0; k < R0; ++k) dst[k] = (zok && rowok(k) && xin) ? pre[w][k][lane] : vsplat_tb<V>(T(0));
+  };
+
+  double acc = 0.0;
+  V L0[R0], M0[R0], H0[R0];  // u0 planes c-1, c, c+1
+  V U1a[R1], U1b[R1];        // u1 planes c-2, c-1
+#pragma unroll
+  for (int k = 0; k < R0; ++k) {
+    L0[k] = ld(zs - 2, k);
+    M0[k] = ld(zs - 1, k);
+    H0[k] = ld(zs, k);
+  }
+#pragma unroll
+  for (int k = 0; k < R1; ++k) {
+    U1a[k] = vsplat_tb<V>(T(0));
+    U1b[k] = vsplat_tb<V>(T(0));
+  }
+  issue(zs + 1);
+  int buf = 0;
+  // c = u1 plane computed this iteration; u2 plane c-1 from c >= zs + 1. L0 (dead once u1(c) is
+  // done) receives the streamed plane c+2, and the three planes rotate at the end.
+  for (int64_t c = zs - 1; c <= ze; ++c) {
+    V U1c[R1];
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < R1; ++j) edge[buf][w][j][0] = M0[j + 1][0];
+#pragma unroll
+      for (int i = 0; i < RY; ++i) edge[buf][w][R1 + i][0] = U1b[i + 1][0];
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int j = 0; j < R1; ++j) edge[buf][w][j][1] = M0[j + 1][N - 1];
+#pragma unroll
+      for (int i = 0; i < RY; ++i) edge[buf][w][R1 + i][1] = U1b[i + 1][N - 1];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): seam writes visible
+    __builtin_amdgcn_s_barrier();
+    {
+      const int64_t gz = c + g.gz_off;
+      const bool zb = (gz <= 0 || gz >= g.gnz - 1);
+#pragma unroll
+      for (int j = 0; j < R1; ++j) {
+        const int64_t y = y0 - 1 + j;
+        const V cc = M0[j + 1];
+        V o = cc;
+        T l = lane_up1(cc[N - 1]);
+        T rr = lane_down1(cc[0]);
+        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][j][1] : T(0);
+        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][j][0] : T(0);
+        if (!zb && y > 0 && y < g.ny - 1) {
+          const V ym = M0[j], yp = M0[j + 2], zm = L0[j + 1], zp = H0[j + 1];
+#pragma unroll
+          for (int e = 0; e < N; ++e) {
+            const T xm = e == 0 ? l : cc[e - 1];
+            const T xp = e == N - 1 ? rr : cc[e + 1];
+            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
+            const int64_t xe = x + e;
+            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
+          }
+        }
+        U1c[j] = o;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA into the slot has landed
+    take(c + 2, L0);
+    if (c >= zs + 1) {
+      const int64_t lz = c - 1;
+      const int64_t gz = lz + g.gz_off;
+      const bool zb = (gz == 0 || gz == g.gnz - 1);
+#pragma unroll
+      for (int i = 0; i < RY; ++i) {
+        const int64_t y = y0 + i;
+        if (y >= g.ny) break;
+        const V cc = U1b[i + 1];
+        V o = cc;
+        T l = lane_up1(cc[N - 1]);
+        T rr = lane_down1(cc[0]);
+        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][R1 + i][1] : T(0);
+        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][R1 + i][0] : T(0);
+        if (!zb && y != 0 && y != g.ny - 1) {
+          const V ym = U1b[i], yp = U1b[i + 2], zm = U1a[i + 1], zp = U1c[i + 1];
+#pragma unroll
+          for (int e = 0; e < N; ++e) {
+            const T xm = e == 0 ? l : cc[e - 1];
+            const T xp = e == N - 1 ? rr : cc[e + 1];
+            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
+            const int64_t xe = x + e;
+            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
+          }
+        }
+        if (xin) {
+          dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
+          store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
+          if (RES) {
+#pragma unroll
+            for (int e = 0; e < N; ++e)
+              if (x + e < g.nx) {
+                const double d = (double)o[e] - (double)cc[e];
+                acc += d * d;
+              }
+          }
+        }
+      }
+    }
+    // the slot has been read (lgkmcnt) before the next DMA overwrites it
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    issue(c + 3);
+    buf ^= 1;
+#pragma unroll
+    for (int k = 0; k < R1; ++k) {
+      U1a[k] = U1b[k];
+      U1b[k] = U1c[k];
+    }
+#pragma unroll
+    for (int k = 0; k < R0; ++k) {
+      const V t0 = L0[k];
+      L0[k] = M0[k];
+      M0[k] = H0[k];
+      H0[k] = t0;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA may outlive the wave
+  if (RES) wave_atomic_add(resid, acc);
+}
+
 template <class T, int RY, int WXN, int PF>
 static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int WYN = 4 / WXN;
@@ -308,6 +495,15 @@ static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   if (zc <= 0) zc = tb2_zc(planes, (int64_t)XTn * YT, resident_blocks(kfn));
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XTn * YT * ZT)), blk(256);
+  // rows within one block: the LDS-DMA prefetch variant, +0.7..4.5% over the register prefetch at
+  // every measured shape, bitwise equal (profiles/r01_tb2_glds.txt); MDFX_TB_GL=0 for the A/B
+  if (XTn == 1 && env_int("MDFX_TB_GL", 1)) {
+    if (resid)
+      hipLaunchKernelGGL((heat7_tb2_gl<T, RY, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    else
+      hipLaunchKernelGGL((heat7_tb2_gl<T, RY, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    return;
+  }
   if (XTn > 1) {
     if (resid)
       hipLaunchKernelGGL((heat7_tb2<T, RY, 4, true, PF, false, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
