@@ -31,13 +31,19 @@ def test_no_kernel_spills_to_scratch(recs):
     assert not bad, bad
 
 
-def test_lds_fits_with_many_blocks_per_cu(recs):
-    # 160 KiB LDS per CU: every kernel leaves room for >= 8 resident blocks
-    assert max(r.get("group_segment_fixed_size", 0) for r in recs.values()) <= 20 * 1024
+def test_lds_never_limits_occupancy(recs):
+    # 160 KiB LDS per CU. Every block is 256 threads (4 waves, one per SIMD), so a kernel with W
+    # waves per SIMD keeps W blocks resident per CU: their LDS must fit next to each other, so LDS
+    # never becomes the occupancy limiter (the VGPR budget is). The LDS-DMA fused kernel
+    # (heat7_tb2_gl, 25 KiB at 3 waves per SIMD) is the largest user.
+    bad = {n: (r.get("group_segment_fixed_size", 0), r["waves_per_simd"]) for n, r in recs.items()
+           if r.get("group_segment_fixed_size", 0) * max(1, r["waves_per_simd"]) > 160 * 1024}
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("name,min_waves", [
     ("mdfx::dev::heat7_tb2<float, 2, 4, false, 1, false, false>", 3),   # headline fused sweep
+    ("mdfx::dev::heat7_tb2_gl<float, 2, 4, false>", 3),                 # headline, LDS-DMA prefetch
     ("mdfx::dev::heat7_tb2<float, 2, 4, false, 1, false, true>", 3),    # x-tiled rows
     ("mdfx::dev::heat7_tb2<double, 2, 4, false, 1, false, true>", 3),
     ("mdfx::dev::heat7_zw<float, 2, 4, false, false, 1>", 6),           # single-step default
