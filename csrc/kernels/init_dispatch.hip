@@ -41,6 +41,10 @@ template <class T>
 void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
 bool heat7_tb2_supported(const Geo& g);
+template <class T>
+void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
+template <class T>
+bool heat7_tbk_supported(const Geo& g, int steps);
 
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -179,6 +183,11 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   if (spec.kind == StencilKind::Jacobi5)  // deep temporal blocking of the 2D problems
     return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d;
   if (spec.kind == StencilKind::Life) return k2d;
+  if (spec.kind == StencilKind::Heat7 && steps > 2) {  // deep temporal blocking (rows within one block)
+    const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
+    return spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, steps)
+                                    : dev::heat7_tbk_supported<double>(g, steps);
+  }
   if (steps != 2) return false;
   if (spec.kind == StencilKind::Box27) {
     const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
@@ -220,6 +229,13 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
       }
+    } else if (a.steps > 2 || (dev::env_int("MDFX_TBK2", 1) &&
+                               (spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, 2)
+                                                         : dev::heat7_tbk_supported<double>(g, 2)))) {
+      if (spec.dtype == DType::F32)
+        dev::launch_heat7_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
+      else
+        dev::launch_heat7_tbk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
     } else if (spec.dtype == DType::F32) {
       dev::launch_heat7_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
     } else {

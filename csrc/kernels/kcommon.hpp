@@ -80,6 +80,27 @@ __device__ __forceinline__ void wave_atomic_add(double* dst, double v) {
 namespace mdfx {
 namespace dev {
 
+// LDS DMA: each active lane loads 16 bytes from its own global address into LDS at
+// `l` + 16 * lane (global_load_lds_dwordx4, gfx950), without a VGPR destination. `l` must be
+// wave-uniform. hipcc does not track these LDS writes: wait with vmcnt(0) before reading them.
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// Raw waits: s_waitcnt encodings for gfx9 (vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]).
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+// Workgroup barrier that does NOT drain outstanding vector-memory operations (a __syncthreads
+// makes hipcc wait for vmcnt(0), which would also wait for an in-flight LDS DMA). LDS writes are
+// completed first; the empty asm statements keep the compiler from moving memory accesses across.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  wait_lgkm0();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Whole-wave lane shifts by one (lane i <- lane i-1 / lane i+1) with DPP wave_shr:1 / wave_shl:1:
 // a VALU move with a DPP modifier instead of a ds_bpermute through the LDS crossbar. The lane that
 // has no source (0 or 63) receives 0; callers overwrite it with the seam value.
@@ -100,11 +121,42 @@ __device__ __forceinline__ double lane_down1(double v) {
   const int lo = dpp_shl1_i((int)(b & 0xffffffffll)), hi = dpp_shl1_i((int)(b >> 32));
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+// lane i <- lane i-1 (up) / lane i+1 (down); the lane without a source (0 / 63) keeps `edge`.
+// DPP with bound_ctrl off leaves that lane's destination at the `old` operand, so the seam value
+// costs no extra instruction.
+__device__ __forceinline__ float lane_up1_or(float edge, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_down1_or(float edge, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double lane_up1_or(double edge, double v) {
+  const long long b = __double_as_longlong(v), o = __double_as_longlong(edge);
+  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(b & 0xffffffffll), 0x138, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x138, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_down1_or(double edge, double v) {
+  const long long b = __double_as_longlong(v), o = __double_as_longlong(edge);
+  const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(b & 0xffffffffll), 0x130, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x130, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 #else
 template <class T>
 __device__ __forceinline__ T lane_up1(T v) { return __shfl_up(v, 1, 64); }
 template <class T>
 __device__ __forceinline__ T lane_down1(T v) { return __shfl_down(v, 1, 64); }
+template <class T>
+__device__ __forceinline__ T lane_up1_or(T edge, T v) {
+  const T s = __shfl_up(v, 1, 64);
+  return (threadIdx.x & 63) == 0 ? edge : s;
+}
+template <class T>
+__device__ __forceinline__ T lane_down1_or(T edge, T v) {
+  const T s = __shfl_down(v, 1, 64);
+  return (threadIdx.x & 63) == 63 ? edge : s;
+}
 #endif
 // A/B twin of lane_up1 / lane_down1 through ds_bpermute (the __shfl path)
 template <class T>

@@ -262,7 +262,7 @@ template bool heat7_tb2_supported<float>(const Geo&);
 template bool heat7_tb2_supported<double>(const Geo&);
 
 // Blocks of kernel `kfn` (256 threads) the whole device holds at once, cached per kernel.
-static int64_t resident_blocks(const void* kfn) {
+int64_t resident_blocks(const void* kfn) {
   static std::mutex mu;
   static std::map<std::pair<int, const void*>, int64_t> cache;
   int dev = 0;
@@ -284,7 +284,7 @@ static int64_t resident_blocks(const void* kfn) {
 // ~43-plane chunks were the best or within 1% of it at every slab depth of the 1024^2 strong-
 // scaling shapes, e.g. 1024 x 1024 x 128 (the N = 8 slab): 876 GCells/s at zc 64 vs 1043 at zc 43
 // (profiles/r01_tb2_zc_slabs.txt).
-static int tb2_zc(int64_t planes, int64_t tiles, int64_t resident) {
+int tb2_zc(int64_t planes, int64_t tiles, int64_t resident) {
   if (planes <= 16) return (int)std::max<int64_t>(planes, 1);
   int64_t zt = (planes + 43) / 44;
   int64_t zc = (planes + zt - 1) / zt;
@@ -304,10 +304,6 @@ static int tb2_zc(int64_t planes, int64_t tiles, int64_t resident) {
 // prefetch's six row vectors from the register budget. The loop uses a raw s_barrier with an
 // explicit lgkmcnt(0) (a __syncthreads would make hipcc drain the DMA at every barrier) and an
 // explicit vmcnt(0) before reading the slot (hipcc does not track LDS-DMA writes).
-__device__ __forceinline__ void glds16(const void* g, void* l) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
-}
 
 template <class T, int RY, int WXN, bool RES>
 __global__ __launch_bounds__(256) void heat7_tb2_gl(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,

@@ -1,0 +1,418 @@
+// Deep temporal blocking for the 3D 7-point heat/Jacobi stencil: K time steps per sweep over
+// memory (K = 2, 3, 4), for rows that fit one block (up to 1024 fp32 / 512 fp64 cells).
+//
+// heat7_tb2 keeps whole planes of every level in registers and rotates them each z-iteration;
+// at K = 2 that is already ~100 VGPRs and most of its VALU work is register moves. Here every
+// level k = 1..K is a *streaming* z-march whose only state between planes is two row vectors per
+// row it owns:
+//   C_k = u_{k-1}(p)       (the centre of plane p, and the z- neighbour of plane p+1)
+//   S_k = partial sum of plane p: (((xm + xp) + ym) + yp) + zm, all from u_{k-1}
+// When u_{k-1}(p+1) arrives, level k finishes u_k(p) = fma(r, fma(-6, C_k, S_k + zp), C_k) --
+// exactly sm::heat7's operation order, so the result is bitwise identical to K single steps --
+// then replaces S_k / C_k with plane p+1's partial and centre. The levels are staggered by one
+// plane: in the z-iteration that brings u0(c), level k turns u_{k-1}(c-k+1) into u_k(c-k), and
+// level K writes u_K(c-K) to memory. Each u0 byte is read from HBM once per chunk and each output
+// byte written once, so a sweep moves the bytes of ONE step for K steps of work.
+//
+// Geometry: a 256-thread block is 4 waves along x (a 1024-cell fp32 row; narrower rows stack wave
+// groups along y). A group owns RY output rows; level k computes the RY + 2(K-k) rows that the
+// levels above it need (the redundant y halo is recomputed instead of exchanged). Per lane one
+// 16-B vector per row.
+//   u0 arrives by LDS DMA: each wave streams its own RY + 2K rows of the next plane, plus one
+//   16-B vector per row beyond each wave edge (the x seams), into its private LDS slot
+//   (global_load_lds, no VGPR destination), one plane ahead. No other wave reads the slot, so
+//   level 1 needs no barrier.
+//   x neighbours: DPP wave shifts whose edge lane takes the seam value as DPP's `old` operand.
+//   Seams of levels 1..K-1 go through a small double-buffered LDS table: K-1 barriers per plane.
+//   Boundaries: held cells (x, y or z on the global boundary) get a zero coefficient,
+//   u' = fma(0, t, u) = u, instead of a select or a branch per row: x through a per-lane
+//   coefficient vector, z once per level and plane, y only in the tiles that touch y = 0 / ny-1
+//   (a second, specialised copy of the level code). Exact for finite data; the one difference
+//   from a copy is that a held -0.0 becomes +0.0.
+//
+// Region contract: output storage planes [lz_begin, lz_end) need u0 valid on
+// [lz_begin - K, lz_end + K) (the engine keeps K ghost planes per side: halo = K).
+#include <algorithm>
+#include <cstdio>
+#include <type_traits>
+
+#include "kcommon.hpp"
+#include "mdfx/kernels.hpp"
+#include "mdfx/stencil_math.hpp"
+
+namespace mdfx {
+namespace dev {
+
+int env_int(const char* name, int dflt);
+int64_t resident_blocks(const void* kfn);
+int tb2_zc(int64_t planes, int64_t tiles, int64_t resident);
+
+// first row of level k (1..K) in the flat per-level state arrays
+template <int RY, int K>
+__host__ __device__ constexpr int tbk_off(int k) {
+  return (k - 1) * RY + 2 * ((k - 1) * K - (k - 1) * k / 2);
+}
+
+// One lane's slice of a row, in the register layout the arithmetic wants.
+//  fp32: the 4 cells as two aligned pairs a = (e1, e2), b = (e0, e3). Then
+//        x sums (xm + xp) = { (l, rr) + a , b + swap(a) }  -> 2 v_pk_add_f32,
+//        and every y / z / update operation is one packed op per pair, with no lane shuffles
+//        or register moves to form misaligned pairs (natural (e0,e1),(e2,e3) pairs need them).
+//  fp64: the 2 cells as they are (no packed fp64 arithmetic on CDNA).
+// `E` is the edge pair (e0, e_{N-1}) the neighbouring waves need.
+template <class T>
+struct RowOps;
+
+template <>
+struct RowOps<float> {
+  typedef float T2 __attribute__((ext_vector_type(2)));
+  typedef float V __attribute__((ext_vector_type(4)));
+  struct Row {
+    T2 a, b;
+  };
+  // natural 16-B vector at p (one ds_read_b128), regrouped into the pair layout
+  static __device__ __forceinline__ Row lds(const float* p) {
+    const V v = *(const V*)p;
+    Row r;
+    r.a = T2{v.y, v.z};
+    r.b = T2{v.x, v.w};
+    return r;
+  }
+  static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}, T2{0.f, 0.f}}; }
+  static __device__ __forceinline__ float first(const Row& c) { return c.b.x; }
+  static __device__ __forceinline__ float last(const Row& c) { return c.b.y; }
+  static __device__ __forceinline__ T2 edges(const Row& c) { return c.b; }
+  // (((xm + xp) + ym) + yp) + zm
+  static __device__ __forceinline__ Row partial(const Row& c, float l, float rr, const Row& ym, const Row& yp,
+                                                const Row& zm) {
+    const T2 lr = T2{l, rr};
+    const T2 sa = T2{c.a.y, c.a.x};
+    Row s;
+    s.b = lr + c.a;  // (l + e1, rr + e2)
+    s.a = c.b + sa;  // (e0 + e2, e3 + e1)
+    s.a = ((s.a + ym.a) + yp.a) + zm.a;
+    s.b = ((s.b + ym.b) + yp.b) + zm.b;
+    return s;
+  }
+  // fma(r, fma(-6, c, S + zp), c) with a per-cell coefficient in the Row layout (0 = held)
+  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m6 = T2{-6.f, -6.f};
+    Row o;
+    o.a = __builtin_elementwise_fma(rc.a, __builtin_elementwise_fma(m6, c.a, S.a + zp.a), c.a);
+    o.b = __builtin_elementwise_fma(rc.b, __builtin_elementwise_fma(m6, c.b, S.b + zp.b), c.b);
+    return o;
+  }
+  static __device__ __forceinline__ Row coef(float r, const bool* held) {
+    return Row{T2{held[1] ? 0.f : r, held[2] ? 0.f : r}, T2{held[0] ? 0.f : r, held[3] ? 0.f : r}};
+  }
+  static __device__ __forceinline__ float get(const Row& c, int e) {
+    return e == 0 ? c.b.x : e == 1 ? c.a.x : e == 2 ? c.a.y : c.b.y;
+  }
+  static __device__ __forceinline__ void set(Row& c, int e, float v) {
+    if (e == 0) c.b.x = v;
+    else if (e == 1) c.a.x = v;
+    else if (e == 2) c.a.y = v;
+    else c.b.y = v;
+  }
+  static __device__ __forceinline__ V vec(const Row& c) { return V{c.b.x, c.a.x, c.a.y, c.b.y}; }
+};
+
+template <>
+struct RowOps<double> {
+  typedef double T2 __attribute__((ext_vector_type(2)));
+  typedef T2 V;
+  struct Row {
+    T2 v;
+  };
+  static __device__ __forceinline__ Row lds(const double* p) { return Row{*(const T2*)p}; }
+  static __device__ __forceinline__ Row zero() { return Row{T2{0.0, 0.0}}; }
+  static __device__ __forceinline__ double first(const Row& c) { return c.v.x; }
+  static __device__ __forceinline__ double last(const Row& c) { return c.v.y; }
+  static __device__ __forceinline__ T2 edges(const Row& c) { return c.v; }
+  static __device__ __forceinline__ Row partial(const Row& c, double l, double rr, const Row& ym, const Row& yp,
+                                                const Row& zm) {
+    Row s;
+    s.v = T2{l + c.v.y, c.v.x + rr};
+    s.v = ((s.v + ym.v) + yp.v) + zm.v;
+    return s;
+  }
+  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m6 = T2{-6.0, -6.0};
+    return Row{__builtin_elementwise_fma(rc.v, __builtin_elementwise_fma(m6, c.v, S.v + zp.v), c.v)};
+  }
+  static __device__ __forceinline__ Row coef(double r, const bool* held) {
+    return Row{T2{held[0] ? 0.0 : r, held[1] ? 0.0 : r}};
+  }
+  static __device__ __forceinline__ double get(const Row& c, int e) { return e == 0 ? c.v.x : c.v.y; }
+  static __device__ __forceinline__ void set(Row& c, int e, double v) {
+    if (e == 0) c.v.x = v;
+    else c.v.y = v;
+  }
+  static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
+};
+
+template <class T, int RY, int K, int WXN, bool RES>
+__global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
+                                                 int zc, int YT, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  using RO = RowOps<T>;
+  using Row = typename RO::Row;
+  using T2 = typename RO::T2;
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  constexpr int WYN = 4 / WXN;
+  constexpr int R0 = RY + 2 * K;              // u0 window rows y0-K .. y0+RY+K-1
+  constexpr int TOT = tbk_off<RY, K>(K + 1);  // state rows over all levels
+  constexpr int NLV = K > 1 ? K - 1 : 1;
+  static_assert(R0 <= 32, "seam DMA uses lanes 0..R0-1 and 32..32+R0-1");
+  __shared__ V slot[4][R0 + 1][64];  // per-wave u0 plane; row R0 holds the seam vectors
+  // level seam table [level][parity][wave][row][side] of edge pairs (e0, e_{N-1}) written by lanes
+  // 0 (side 0) and 63 (side 1), with one pair of padding at each end for the junk half of the reads
+  constexpr int TB_ROW = 4, TB_W = R0 * TB_ROW, TB_PAR = 4 * TB_W, TB_LV = 2 * TB_PAR;
+  __shared__ __attribute__((aligned(16))) T tb[NLV * TB_LV + 4];
+
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int yt = t % YT;
+  const int zt = t / YT;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wx = w % WXN, wy = w / WXN;
+  const int64_t xw = (int64_t)wx * WX;
+  const uint32_t xo = (uint32_t)lane * N;
+  const int64_t x = xw + xo;
+  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const T* ib = in + (y0 - K) * pitch + xw;  // u0 window row k = y0 - K + k
+  T* ob = out + y0 * pitch + xw;
+
+  // held cells get coefficient 0: per lane for x = 0 / x >= nx-1, whole levels for z, whole rows
+  // for y (only in tiles whose computed rows reach y = 0 or y = ny-1)
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  const Row rx = RO::coef(r, xb);
+  const Row r0 = RO::zero();
+  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= g.ny - 2;
+
+  // ---- u0 streaming: rows + seam vectors of plane lz into this wave's slot ----------------------
+  // All lanes of every DMA are active: rows outside [0, ny) and lanes beyond the row read a
+  // clamped in-bounds address (those window cells never feed a valid output, and stay finite).
+  const bool has_l = wx > 0, has_r = xw + WX < pitch;
+  const int srow = lane & 31;
+  const bool son = lane < 32 ? (has_l && srow < R0) : (WXN > 1 && has_r && srow < R0);
+  const int64_t xc = xin ? (int64_t)xo : (int64_t)(pitch - xw - N);
+  const int64_t soff = son ? (lane < 32 ? -(int64_t)N : (int64_t)WX) : xc;
+  auto rowc = [&](int k) -> int64_t {  // window row k, clamped into [0, ny)
+    const int64_t y = y0 - K + k;
+    return (y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y) - (y0 - K);
+  };
+  const int64_t srowc = rowc(srow < R0 ? srow : 0);
+  auto issue = [&](int64_t lz) {
+    const T* pb = ib + lz * plane;
+#pragma unroll
+    for (int k = 0; k < R0; ++k) {
+      const T* a = pb + rowc(k) * pitch + xc;
+      dcheck(g, in, a, N);
+      glds16(a, &slot[w][k][0]);
+    }
+    if (WXN > 1) {
+      const T* a = pb + srowc * pitch + soff;
+      dcheck(g, in, a, N);
+      glds16(a, &slot[w][R0][0]);
+    }
+  };
+  // Seam reads: ONE ds_read2 per row gives lane 0 the left neighbour's last cell in `lo` and lane
+  // 63 the right neighbour's first cell in `hi` (per-lane base, the other half is junk).
+  //   level 0 (DMA'd seam vectors): lo = base0[j*N], hi = base0[j*N + 32*N]
+  //   levels 1.. (edge pair table):  lo = base1[j*4], hi = base1[j*4 + 1]
+  const T* base0 = (const T*)&slot[w][R0][0] + (lane < 32 ? N - 1 : 0);
+  const int wl = wx > 0 ? w - 1 : w, wr = wx < WXN - 1 ? w + 1 : w;
+  const T* base1 = lane < 32 ? &tb[2 + wl * TB_W + 2 + 1] : &tb[2 + wr * TB_W + 0 - 1];
+  T* wrp = &tb[2 + w * TB_W + (lane == 0 ? 0 : 2)];  // this lane's edge-pair slot (lanes 0 / 63)
+
+  Row S[TOT], C[TOT];
+#pragma unroll
+  for (int i = 0; i < TOT; ++i) {
+    S[i] = RO::zero();
+    C[i] = RO::zero();
+  }
+  double acc = 0.0;
+  const int64_t cend = ze + K;
+  issue(zs - K);
+  for (int64_t c = zs - K; c < cend; ++c) {
+    const int par = (int)(c & 1);
+    wait_vm0();  // this wave's DMA of plane c has landed
+    Row X[R0];
+    T LO[R0], HI[R0];
+#pragma unroll
+    for (int k = 0; k < R0; ++k) X[k] = RO::lds((const T*)&slot[w][k][lane]);
+#pragma unroll
+    for (int j = 1; j < R0 - 1; ++j) {
+      LO[j] = base0[j * N];
+      HI[j] = base0[j * N + 32 * N];
+    }
+    wait_lgkm0();  // slot consumed: refill it with the next plane while the levels compute
+    asm volatile("" ::: "memory");
+    if (c + 1 < cend) issue(c + 1);
+
+#pragma unroll
+    for (int k = 1; k <= K; ++k) {
+      const int ROUT = RY + 2 * (K - k);
+      const int off = tbk_off<RY, K>(k);
+      // block-uniform: level k starts once its inputs are valid planes (the first 2K iterations
+      // fill the pipeline)
+      if (c >= zs - K + 2 * k - 2) {
+        if (k >= 2 && WXN > 1) {
+          const T* b1 = base1 + (k - 2) * TB_LV + par * TB_PAR;
+#pragma unroll
+          for (int j = 1; j <= ROUT; ++j) {
+            LO[j] = b1[j * TB_ROW];
+            HI[j] = b1[j * TB_ROW + 1];
+          }
+        }
+        const int64_t gz = c - k + g.gz_off;  // plane finished by this level: c - k
+        const Row rl = (gz <= 0 || gz >= g.gnz - 1) ? r0 : rx;
+        Row Y[R0];
+        auto rows = [&](auto edge) __attribute__((always_inline)) {
+          constexpr bool EDGE = decltype(edge)::value;
+#pragma unroll
+          for (int i = 0; i < ROUT; ++i) {
+            Row ri = rl;
+            if (EDGE) {
+              const int64_t y = y0 - (K - k) + i;
+              if (y == 0 || y == g.ny - 1) ri = r0;
+            }
+            const Row cen = X[i + 1];
+            const Row cold = C[off + i];
+            const Row o = RO::fin(S[off + i], cen, cold, ri);
+            const T l = lane_up1_or(LO[i + 1], RO::last(cen));
+            const T rr = lane_down1_or(HI[i + 1], RO::first(cen));
+            S[off + i] = RO::partial(cen, l, rr, X[i], X[i + 2], cold);
+            C[off + i] = cen;
+            Y[i] = o;
+            if (RES && k == K && c >= zs + K && y0 + i < g.ny && xin) {
+#pragma unroll
+              for (int e = 0; e < N; ++e)
+                if (x + e < g.nx) {
+                  const double d = (double)RO::get(o, e) - (double)RO::get(cold, e);
+                  acc += d * d;
+                }
+            }
+          }
+        };
+        if (yint)
+          rows(std::integral_constant<bool, false>{});
+        else
+          rows(std::integral_constant<bool, true>{});
+        if (k < K) {
+          if (WXN > 1) {  // publish the edge pairs of the rows the next level uses as centres
+            if (lane == 0 || lane == 63) {
+              T* wp = wrp + (k - 1) * TB_LV + par * TB_PAR;
+#pragma unroll
+              for (int j = 1; j < ROUT - 1; ++j) *(T2*)(wp + j * TB_ROW) = RO::edges(Y[j]);
+            }
+            lds_barrier();
+          }
+#pragma unroll
+          for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
+        } else if (c >= zs + K) {  // u_K(c - K) is an owned output plane
+          const int64_t lz = c - K;
+#pragma unroll
+          for (int i = 0; i < RY; ++i) {
+            if (y0 + i < g.ny && xin) {
+              dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
+              store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), RO::vec(Y[i]));
+            }
+          }
+        }
+      }
+    }
+  }
+  wait_vm0();  // no DMA may outlive the wave
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+}  // namespace dev
+}  // namespace mdfx
+
+namespace mdfx {
+namespace dev {
+
+template <class T>
+bool heat7_tbk_supported(const Geo& g, int steps) {
+  constexpr int WX = 64 * VT<T>::N;
+  return steps >= 2 && steps <= 4 && g.pitch <= 4 * WX && g.nx >= 1 && g.ny >= 1;
+}
+template bool heat7_tbk_supported<float>(const Geo&, int);
+template bool heat7_tbk_supported<double>(const Geo&, int);
+
+template <class T, int RY, int K, int WXN>
+static void launch_tbk_w(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int WYN = 4 / WXN;
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
+  const void* kfn = (const void*)&heat7_tbk<T, RY, K, WXN, false>;
+  int zc = env_int("MDFX_ZC", 0);
+  if (zc <= 0) zc = tb2_zc(planes, YT, resident_blocks(kfn));
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+  else
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+}
+
+template <class T, int RY, int K>
+static void launch_tbk_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int WX = 64 * VT<T>::N;
+  if (g.pitch > 2 * WX)
+    launch_tbk_w<T, RY, K, 4>(g, in, out, r, resid, s);
+  else if (g.pitch > WX)
+    launch_tbk_w<T, RY, K, 2>(g, in, out, r, resid, s);
+  else
+    launch_tbk_w<T, RY, K, 1>(g, in, out, r, resid, s);
+}
+
+// K fused steps. Rows per tile from MDFX_TBK_RY, clamped to the tiles instantiated for that depth
+// (K = 2: 1..4, K = 3: 1..3, K = 4: 1..2; deeper levels with more rows would not fit the register
+// file); default 4 / 2 / 2, and 1 on very short columns.
+template <class T>
+void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  // region contract: u0 is read on [lz_begin - K, lz_end + K)
+  MDFX_CHECK(steps >= 2 && steps <= 4 && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+             format("heat7_tbk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
+                    (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
+  const int rymax = steps == 2 ? 4 : steps == 3 ? 3 : 2;
+  int ry = env_int("MDFX_TBK_RY", 0);
+  if (ry <= 0) ry = steps == 2 ? 4 : 2;
+  ry = std::min(ry, rymax);
+  if (g.ny < 8) ry = 1;
+  if (steps == 2) {
+    switch (ry) {
+      case 1: launch_tbk_t<T, 1, 2>(g, in, out, r, resid, s); break;
+      case 2: launch_tbk_t<T, 2, 2>(g, in, out, r, resid, s); break;
+      case 3: launch_tbk_t<T, 3, 2>(g, in, out, r, resid, s); break;
+      default: launch_tbk_t<T, 4, 2>(g, in, out, r, resid, s); break;
+    }
+  } else if (steps == 3) {
+    switch (ry) {
+      case 1: launch_tbk_t<T, 1, 3>(g, in, out, r, resid, s); break;
+      case 2: launch_tbk_t<T, 2, 3>(g, in, out, r, resid, s); break;
+      default: launch_tbk_t<T, 3, 3>(g, in, out, r, resid, s); break;
+    }
+  } else {
+    if (ry == 1)
+      launch_tbk_t<T, 1, 4>(g, in, out, r, resid, s);
+    else
+      launch_tbk_t<T, 2, 4>(g, in, out, r, resid, s);
+  }
+}
+template void launch_heat7_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
+template void launch_heat7_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
+
+}  // namespace dev
+}  // namespace mdfx

@@ -13,7 +13,7 @@ if [[ $MODE == all || $MODE == native ]]; then
   step 300 ./build/bin/mdfx --stencil 7 --n 512 --steps 20 --warmup 5 --residual-every 10 || exit 1
 fi
 if [[ $MODE == all || $MODE == test ]]; then
-  step 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -50 gpurun_out/pytest_gpu.log; exit 1; }
+  step 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -50 gpurun_out/pytest_gpu.log; exit 1; }
   tail -5 gpurun_out/pytest_gpu.log
 fi
 if [[ $MODE == all || $MODE == smoke ]]; then

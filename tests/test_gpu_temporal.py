@@ -44,6 +44,7 @@ def _two_single_steps(prob, lay, src, device):
 @pytest.mark.parametrize("tbry", ["1", "2"])
 def test_fused_two_steps_bitwise(hip, prob, tbry, monkeypatch):
     monkeypatch.setenv("MDFX_TB_RY", tbry)
+    monkeypatch.setenv("MDFX_TBK2", "0")  # heat7_tb2 (the streaming kernel has its own tests below)
     lay = FieldLayout.make(prob, halo=2)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -192,3 +193,70 @@ def test_engine_deep_temporal_2d(hip, prob, k):
     ref, rr = _sim(prob, 37, ranks=1, residual_every=9)
     got, rg = _sim(prob, 37, ranks=4, temporal=k, residual_every=9)
     assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * max(1.0, rr)
+
+
+# 3D 7-point deep temporal blocking (heat7_tbk, streaming per-level partial sums): rows that fit
+# one block (1024 fp32 / 512 fp64) with 4 / 2 / 1 waves across the row, ragged widths, y / z edges
+DEEP3D = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=15),
+          models.heat3d(nx=256, ny=9, nz=12), models.heat3d(nx=500, ny=21, nz=11, dtype="f64"),
+          models.heat3d(nx=64, ny=64, nz=9, r=0.1), models.heat3d(nx=1000, ny=5, nz=14),
+          models.heat3d(nx=300, ny=40, nz=10, dtype="f64")]
+
+
+@pytest.mark.parametrize("prob", DEEP3D, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("k", [2, 3, 4])
+@pytest.mark.parametrize("ry", ["1", "2", "4"])
+def test_heat7_deep_fused_bitwise(hip, prob, k, ry, monkeypatch):
+    """K fused 3D steps per sweep == K naive single steps, bitwise, with the residual of step K."""
+    monkeypatch.setenv("MDFX_TBK2", "1")
+    monkeypatch.setenv("MDFX_TBK_RY", ry)
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res)
+    set_kernel_variant("naive")
+    try:
+        cur = alloc_field(lay, "cuda")
+        cur.copy_(src)
+        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+        for i in range(k):
+            nxt = alloc_field(lay, "cuda")
+            nxt.copy_(cur)
+            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, ry)
+    assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
+def test_heat7_deep_fused_regions_on_a_slab(hip):
+    """A middle slab with 4 ghost planes: boundary + interior region launches == the whole grid."""
+    prob = models.heat3d(nx=1024, ny=20, nz=40)
+    full = FieldLayout.make(prob, halo=4)
+    g = alloc_field(full, "cuda")
+    init_field(prob, full, g)
+    ref = alloc_field(full, "cuda")
+    apply_stencil(prob, full, g, ref, steps=4)
+    lay = FieldLayout.make(prob, 12, 30, halo=4)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    out = alloc_field(lay, "cuda")
+    h = lay.halo
+    apply_stencil(prob, lay, src, out, h, h + 4, steps=4)
+    apply_stencil(prob, lay, src, out, h + 14, h + 18, steps=4)
+    apply_stencil(prob, lay, src, out, h + 4, h + 14, steps=4)
+    torch.cuda.synchronize()
+    assert torch.equal(out[h:h + 18, :, :1024], ref[12 + 4:30 + 4, :, :1024])
+
+
+@pytest.mark.parametrize("k,ranks", [(3, 1), (3, 3), (4, 1), (4, 4)])
+def test_engine_deep_temporal_3d(hip, k, ranks):
+    prob = mm.heat3d(nx=1024, ny=24, nz=60)
+    ref, rr = _sim(prob, 23, ranks=1, residual_every=10)
+    got, rg = _sim(prob, 23, ranks=ranks, temporal=k, residual_every=10)
+    assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
