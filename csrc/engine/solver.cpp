@@ -62,6 +62,10 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.ev_bnd = s.be->create_event();
     s.ev_int = s.be->create_event();
     s.resid = (double*)s.be->alloc(2 * sizeof(double));
+    for (int kk = 2; kk <= opt_.temporal; ++kk) {
+      const bool ok = s.be->kind() != DeviceKind::HIP || hip_supports_steps(spec_, s.lay, kk);
+      depth_ok_[kk] = (i == 0 ? true : depth_ok_[kk]) && ok;
+    }
     if (opt_.temporal > 1 && s.be->kind() == DeviceKind::HIP)
       MDFX_CHECK(hip_supports_steps(spec_, s.lay, opt_.temporal),
                  format("no fused %d-step kernel for %s %s with nx=%lld (fused depths: 2 for every stencil "
@@ -368,8 +372,14 @@ void Solver::run(int64_t steps) {
     int64_t to_res = steps - done + 1;
     if (opt_.residual_every > 0)
       to_res = ((stats_.steps / opt_.residual_every) + 1) * opt_.residual_every - stats_.steps;
-    // a fused sweep may not jump over a residual step: shorter stretches use single steps
-    const int k = (T > 1 && steps - done >= T && to_res >= T) ? T : 1;
+    // a fused sweep may not jump over a residual step; shorter stretches (a step count that is not
+    // a multiple of T, a residual point inside a sweep) use the deepest fused depth that fits
+    int k = 1;
+    for (int kk = std::min<int64_t>({(int64_t)T, steps - done, to_res}); kk > 1; --kk)
+      if (depth_ok_[kk]) {
+        k = kk;
+        break;
+      }
     const bool res = (to_res == k);
     // graph replay for plain (non-residual, non-debug) stretches of >= 2 sweeps. Restricted to one
     // slab per process (the production layout: one rank per GPU): the ROCm 7.0 HIP runtime that

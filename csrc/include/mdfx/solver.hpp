@@ -128,6 +128,8 @@ class Solver {
   void* graph_exec_ = nullptr;  // hipGraphExec_t for the 2-step cycle starting at buffer 0
   int graph_parity_ = -1;
   int graph_k_ = 0;
+  // depth_ok_[k]: every slab can run a k-step fused sweep (k <= temporal); 1 always can
+  bool depth_ok_[9] = {false, true, false, false, false, false, false, false, false};
 };
 
 }  // namespace mdfx

@@ -33,6 +33,7 @@
 // Region contract: output storage planes [lz_begin, lz_end) need u0 valid on
 // [lz_begin - K, lz_end + K) (the engine keeps K ghost planes per side: halo = K).
 #include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <type_traits>
 
@@ -45,7 +46,6 @@ namespace dev {
 
 int env_int(const char* name, int dflt);
 int64_t resident_blocks(const void* kfn);
-int tb2_zc(int64_t planes, int64_t tiles, int64_t resident);
 
 // first row of level k (1..K) in the flat per-level state arrays
 template <int RY, int K>
@@ -341,6 +341,22 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
 namespace mdfx {
 namespace dev {
 
+// z-chunk of a streaming sweep. Each chunk pays 2K planes of pipeline fill, and the z-march
+// needs no short chunks for L2 sharing (y-neighbour tiles are co-resident and march in lockstep),
+// so chunks are long: R whole rounds of resident blocks, R = planes-per-slot / 128 clamped to
+// [1, 4]. One single round has the best minimum but the worst mean sweep time (slow blocks are
+// never rebalanced); about 4 rounds are as fast on average with a small spread. Per-dispatch
+// means on 1024^3 fp32, K = 2 (profiles/r01_tbk/zc_dispatch_stats.txt): zc 512 / 256 / 171 /
+// 128 / 86 -> 1.768 / 1.770 / 1.646 / 1.671 / 1.646 ms per sweep; the N = 8 slab (128 planes,
+// best of 3 x 20): zc 128 / 64 / 43 -> 1025 / 1358 / 1082 GCells/s.
+static int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
+  (void)K;
+  const double per_slot = (double)planes * (double)tiles / (double)resident;
+  const int64_t rounds = std::max<int64_t>(1, std::min<int64_t>(4, (int64_t)(per_slot / 128.0 + 0.5)));
+  const int64_t zt = std::max<int64_t>(1, std::min<int64_t>(planes, (rounds * resident + tiles / 2) / tiles));
+  return (int)((planes + zt - 1) / zt);
+}
+
 template <class T>
 bool heat7_tbk_supported(const Geo& g, int steps) {
   constexpr int WX = 64 * VT<T>::N;
@@ -356,7 +372,8 @@ static void launch_tbk_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   const void* kfn = (const void*)&heat7_tbk<T, RY, K, WXN, false>;
   int zc = env_int("MDFX_ZC", 0);
-  if (zc <= 0) zc = tb2_zc(planes, YT, resident_blocks(kfn));
+  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks(kfn), K);
+  if (env_int("MDFX_DEBUG_ZC", 0)) fprintf(stderr, "[mdfx] tbk K=%d RY=%d: %lld planes x %d tiles -> zc %d\n", K, RY, (long long)planes, YT, zc);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
