@@ -185,7 +185,6 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
   const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
   const bool xin = x < g.pitch;
   const int64_t pitch = g.pitch, plane = g.plane;
-  const T* ib = in + (y0 - K) * pitch + xw;  // u0 window row k = y0 - K + k
   T* ob = out + y0 * pitch + xw;
 
   // held cells get coefficient 0: per lane for x = 0 / x >= nx-1, whole levels for z, whole rows
@@ -203,23 +202,28 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
   const bool has_l = wx > 0, has_r = xw + WX < pitch;
   const int srow = lane & 31;
   const bool son = lane < 32 ? (has_l && srow < R0) : (WXN > 1 && has_r && srow < R0);
-  const int64_t xc = xin ? (int64_t)xo : (int64_t)(pitch - xw - N);
-  const int64_t soff = son ? (lane < 32 ? -(int64_t)N : (int64_t)WX) : xc;
+  // per-lane parts of the DMA addresses as 32-bit byte offsets from the wave-uniform start of the
+  // row (x = 0), so the loads use the SGPR-base + VGPR-offset form (one VGPR per address instead
+  // of a 64-bit pair per row). Every offset is a clamped column in [0, pitch - N], never negative:
+  // lanes beyond the row (possibly a whole wave) read the row's last vector.
+  const uint32_t xcb = (uint32_t)((xin ? x : pitch - N) * (int64_t)sizeof(T));
+  const uint32_t socb = son ? (uint32_t)((lane < 32 ? xw - N : xw + WX) * (int64_t)sizeof(T)) : xcb;
+  const T* ib0 = in + (y0 - K) * pitch;  // u0 window row k, column 0
   auto rowc = [&](int k) -> int64_t {  // window row k, clamped into [0, ny)
     const int64_t y = y0 - K + k;
     return (y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y) - (y0 - K);
   };
   const int64_t srowc = rowc(srow < R0 ? srow : 0);
   auto issue = [&](int64_t lz) {
-    const T* pb = ib + lz * plane;
+    const T* pb = ib0 + lz * plane;
 #pragma unroll
     for (int k = 0; k < R0; ++k) {
-      const T* a = pb + rowc(k) * pitch + xc;
+      const T* a = (const T*)((const char*)(pb + rowc(k) * pitch) + xcb);
       dcheck(g, in, a, N);
       glds16(a, &slot[w][k][0]);
     }
-    if (WXN > 1) {
-      const T* a = pb + srowc * pitch + soff;
+    if (WXN > 1) {  // srowc is per lane: the row term stays in the 64-bit address
+      const T* a = (const T*)((const char*)(pb + srowc * pitch) + socb);
       dcheck(g, in, a, N);
       glds16(a, &slot[w][R0][0]);
     }
@@ -247,13 +251,15 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
     wait_vm0();  // this wave's DMA of plane c has landed
     Row X[R0];
     T LO[R0], HI[R0];
+    auto ld0 = [&](int k) __attribute__((always_inline)) {
+      X[k] = RO::lds((const T*)&slot[w][k][lane]);
+      if (k >= 1 && k < R0 - 1) {
+        LO[k] = base0[k * N];
+        HI[k] = base0[k * N + 32 * N];
+      }
+    };
 #pragma unroll
-    for (int k = 0; k < R0; ++k) X[k] = RO::lds((const T*)&slot[w][k][lane]);
-#pragma unroll
-    for (int j = 1; j < R0 - 1; ++j) {
-      LO[j] = base0[j * N];
-      HI[j] = base0[j * N + 32 * N];
-    }
+    for (int k = 0; k < R0; ++k) ld0(k);
     wait_lgkm0();  // slot consumed: refill it with the next plane while the levels compute
     asm volatile("" ::: "memory");
     if (c + 1 < cend) issue(c + 1);
@@ -323,8 +329,9 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
 #pragma unroll
           for (int i = 0; i < RY; ++i) {
             if (y0 + i < g.ny && xin) {
-              dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
-              store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), RO::vec(Y[i]));
+              T* a = (T*)((char*)(ob + lz * plane + (int64_t)i * pitch) + xo * (uint32_t)sizeof(T));
+              dcheck(g, (const T*)out, a, N);
+              store_nt((V*)a, RO::vec(Y[i]));
             }
           }
         }
