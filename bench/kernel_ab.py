@@ -59,6 +59,11 @@ def main():
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--variants", default="FAM=naive;RY=4,PF=2")
     p.add_argument("--json", default="")
+    p.add_argument("--thief", type=int, default=0,
+                   help="launch this many single-block spin kernels (torch.cuda._sleep, ~--thief-us) on "
+                        "side streams next to every timed launch: emulates the CUs RCCL's send/recv "
+                        "kernels hold during an overlapped halo exchange")
+    p.add_argument("--thief-us", type=float, default=100.0)
     a = p.parse_args()
     nx, ny, nz = a.nx or a.n, a.ny or a.n, a.nz or a.n
     if a.kind == "heat7":
@@ -100,6 +105,8 @@ def main():
         apply_stencil(prob, lay, A, B, steps=steps)
         torch.cuda.synchronize()
         ok[v] = bool(torch.equal(B[lay.owned, :, :nx], refs[steps][lay.owned, :, :nx]))
+    thieves = [torch.cuda.Stream() for _ in range(a.thief)]
+    thief_cycles = int(a.thief_us * 2.4e3)  # gfx950 shader clock ~2.4 GHz
     # copy roof with the same bytes (one read + one write of the field)
     times = {v: [] for v in variants}
     copy_t = []
@@ -119,6 +126,13 @@ def main():
             apply_stencil(prob, lay, A, B, steps=steps)
             e0.record()
             for i in range(a.iters):
+                if thieves:
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    for st in thieves:
+                        st.wait_event(ev)
+                        with torch.cuda.stream(st):
+                            torch.cuda._sleep(thief_cycles)
                 apply_stencil(prob, lay, A if i % 2 == 0 else B, B if i % 2 == 0 else A, steps=steps)
             e1.record()
             torch.cuda.synchronize()

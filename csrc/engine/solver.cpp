@@ -39,6 +39,8 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   if (spec_.kind != StencilKind::Life)
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 8, "temporal blocking depth must be 1..8");
+  // several slabs: leave room in each interior sweep for the halo exchange's kernels
+  if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) hip_set_min_rounds(nranks > 1 ? 2 : 1);
   const int halo = opt_.temporal;
   for (size_t i = 0; i < local_ranks.size(); ++i) {
     const int r = local_ranks[i];

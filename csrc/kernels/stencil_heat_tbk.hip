@@ -33,6 +33,7 @@
 // Region contract: output storage planes [lz_begin, lz_end) need u0 valid on
 // [lz_begin - K, lz_end + K) (the engine keeps K ghost planes per side: halo = K).
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <type_traits>
@@ -356,10 +357,13 @@ namespace dev {
 // means on 1024^3 fp32, K = 2 (profiles/r01_tbk/zc_dispatch_stats.txt): zc 512 / 256 / 171 /
 // 128 / 86 -> 1.768 / 1.770 / 1.646 / 1.671 / 1.646 ms per sweep; the N = 8 slab (128 planes,
 // best of 3 x 20): zc 128 / 64 / 43 -> 1025 / 1358 / 1082 GCells/s.
+static std::atomic<int> g_min_rounds{1};
+
 static int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
   (void)K;
   const double per_slot = (double)planes * (double)tiles / (double)resident;
-  const int64_t rounds = std::max<int64_t>(1, std::min<int64_t>(4, (int64_t)(per_slot / 128.0 + 0.5)));
+  const int64_t rounds = std::max<int64_t>(g_min_rounds.load(std::memory_order_relaxed),
+                                           std::min<int64_t>(4, (int64_t)(per_slot / 128.0 + 0.5)));
   const int64_t zt = std::max<int64_t>(1, std::min<int64_t>(planes, (rounds * resident + tiles / 2) / tiles));
   return (int)((planes + zt - 1) / zt);
 }
@@ -436,6 +440,11 @@ void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double*
   }
 }
 template void launch_heat7_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
+}  // namespace dev
+
+void hip_set_min_rounds(int rounds) { dev::g_min_rounds.store(std::max(1, std::min(4, rounds))); }
+
+namespace dev {
 template void launch_heat7_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
 
 }  // namespace dev
