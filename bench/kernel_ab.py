@@ -25,7 +25,8 @@ from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, i
 
 KEYS = {"RY": "MDFX_RY", "PF": "MDFX_PF", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
         "TBPF": "MDFX_TB_PF", "TBBP": "MDFX_TB_BP", "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBGL": "MDFX_TB_GL",
-        "TBK2": "MDFX_TBK2", "TBKRY": "MDFX_TBK_RY", "TBKDS": "MDFX_TBK_DS", "TBKNS": "MDFX_TBK_NS", "TBKLZ": "MDFX_TBK_LZ"}
+        "TBK2": "MDFX_TBK2", "TBKRY": "MDFX_TBK_RY", "TBKDS": "MDFX_TBK_DS", "TBKNS": "MDFX_TBK_NS", "TBKLZ": "MDFX_TBK_LZ",
+        "XT": "MDFX_TBK_XT", "XRY": "MDFX_TBK_XRY"}
 
 
 def parse_variant(s):

@@ -34,30 +34,32 @@ def check(nx, ny, nz, dtype, K, RY, lz_begin=None, lz_end=None, resident=512):
     pitch, plane, lz_max, alloc = layout(nx, ny, nz, esize, K)
     lzb = K if lz_begin is None else lz_begin
     lze = K + nz if lz_end is None else lz_end
-    assert pitch <= 4 * WX, "rows must fit one block"
+    XT = pitch > 4 * WX  # x tiles of 4 waves (two fused steps only)
+    assert not XT or K == 2, "rows wider than one block need two fused steps"
     WXN = 4 if pitch > 2 * WX else 2 if pitch > WX else 1
     WYN = 4 // WXN
+    XTn = (pitch + 4 * WX - 1) // (4 * WX) if XT else 1
     if ny < 8:
         RY = 1
     R0 = RY + 2 * K
     planes = lze - lzb
     YT = (ny + WYN * RY - 1) // (WYN * RY)
-    zc = tbk_zc(planes, YT, resident)
+    zc = tbk_zc(planes, XTn * YT, resident)
     ZT = (planes + zc - 1) // zc
     lane = np.arange(64)
     bad = 0
-    for yt in range(YT):
+    for xt, yt in ((a, b) for a in range(XTn) for b in range(YT)):
         for zt in range(ZT):
             zs = lzb + zt * zc
             ze = min(lze, zs + zc)
             for w in range(4):
                 wx, wy = w % WXN, w // WXN
-                xw = wx * WX
+                xw = xt * WXN * WX + wx * WX
                 x = xw + lane * N
                 xin = x < pitch
                 y0 = (yt * WYN + wy) * RY
                 xcol = np.where(xin, x, pitch - N)                      # xcb / esize
-                has_l, has_r = wx > 0, xw + WX < pitch
+                has_l, has_r = 0 < xw < pitch, xw + WX < pitch
                 srow = lane & 31
                 son = np.where(lane < 32, has_l & (srow < R0), (WXN > 1) & has_r & (srow < R0))
                 scol = np.where(son, np.where(lane < 32, xw - N, xw + WX), xcol)
@@ -84,24 +86,29 @@ def check(nx, ny, nz, dtype, K, RY, lz_begin=None, lz_end=None, resident=512):
                         if y0 + i < ny:
                             a = lz * plane + (y0 + i) * pitch + x[xin]
                             bad += int(((a < 0) | (a + N > alloc)).sum())
-    return bad, dict(pitch=pitch, WXN=WXN, YT=YT, zc=zc, ZT=ZT)
+    return bad, dict(pitch=pitch, WXN=WXN, XTn=XTn, YT=YT, zc=zc, ZT=ZT)
 
 
 SHAPES = [(1024, 37, 23, "f32"), (700, 19, 15, "f32"), (256, 9, 12, "f32"), (500, 21, 11, "f64"),
           (64, 64, 9, "f32"), (1000, 5, 14, "f32"), (300, 40, 10, "f64"), (1024, 20, 40, "f32"),
           (512, 32, 33, "f64")]
+# rows wider than one block (x tiles, K = 2): the GPU test shapes
+WIDE = [(2048, 13, 11, "f32"), (1100, 9, 9, "f64"), (1030, 7, 8, "f32"), (2048, 21, 12, "f64"),
+        (1300, 17, 10, "f32")]
 
 
 def main():
     fails = 0
-    for (nx, ny, nz, dt) in SHAPES:
-        for K, rys in ((2, (1, 2, 3, 4)), (3, (1, 2, 3)), (4, (1, 2))):
-            for RY in rys:
-                bad, info = check(nx, ny, nz, dt, K, RY)
-                fails += bad > 0
-                if bad:
-                    print("OUT OF BOUNDS", nx, ny, nz, dt, "K", K, "RY", RY, bad, info)
-    print("checked %d shapes x depths: %s" % (len(SHAPES), "FAIL" if fails else "all accesses in bounds"))
+    cases = [(s, K, RY) for s in SHAPES for K, rys in ((2, (1, 2, 3, 4)), (3, (1, 2, 3)), (4, (1, 2)))
+             for RY in rys]
+    cases += [(s, 2, RY) for s in WIDE for RY in (1, 2, 3, 4)]
+    for (nx, ny, nz, dt), K, RY in cases:
+        bad, info = check(nx, ny, nz, dt, K, RY)
+        fails += bad > 0
+        if bad:
+            print("OUT OF BOUNDS", nx, ny, nz, dt, "K", K, "RY", RY, bad, info)
+    print("checked %d shapes x depths: %s" % (len(SHAPES) + len(WIDE),
+                                              "FAIL" if fails else "all accesses in bounds"))
     return 1 if fails else 0
 
 

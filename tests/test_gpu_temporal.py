@@ -234,6 +234,36 @@ def test_heat7_deep_fused_bitwise(hip, prob, k, ry, monkeypatch):
     assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
+WIDE3D = [models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, ny=9, nz=9, dtype="f64"),
+          models.heat3d(nx=1030, ny=7, nz=8), models.heat3d(nx=2048, ny=21, nz=12, dtype="f64"),
+          models.heat3d(nx=1300, ny=17, nz=10, r=0.1)]
+
+
+@pytest.mark.parametrize("prob", WIDE3D, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("xry", ["1", "2", "3", "4"])
+def test_heat7_xtiled_streaming_bitwise(hip, prob, xry, monkeypatch):
+    """Rows wider than one block: the x-tiled streaming sweep (tile-edge waves recompute the
+    level-1 column beyond the tile) == two naive single steps, bitwise."""
+    monkeypatch.setenv("MDFX_TBK2", "1")
+    monkeypatch.setenv("MDFX_TBK_XT", "1")
+    monkeypatch.setenv("MDFX_TBK_XRY", xry)
+    lay = FieldLayout.make(prob, halo=2)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=2, resid=res)
+    set_kernel_variant("naive")
+    try:
+        ref, ref_res = _two_single_steps(prob, lay, src, "cuda")
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], ref[o, :, :lay.nx]), xry
+    assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
 def test_heat7_deep_fused_regions_on_a_slab(hip):
     """A middle slab with 4 ghost planes: boundary + interior region launches == the whole grid."""
     prob = models.heat3d(nx=1024, ny=20, nz=40)
