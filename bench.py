@@ -1,10 +1,22 @@
 #!/usr/bin/env python3
 """Headline benchmark: GCells/s of the 3D 7-point Jacobi stencil on a 1024^3 fp32 grid,
-slab-decomposed over N MI355X GPUs (one process per GPU, RCCL halo exchange over xGMI).
+slab-decomposed over N MI355X GPUs (one process per GPU, device-resident halo exchange over xGMI).
 
-    python bench.py                         # N = 1
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+    python bench.py                              # N = 1
+    python bench.py --gpus 8                     # launches 8 worker processes itself
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
+
+Launch. Under a launcher (RANK / WORLD_SIZE set) this process is one rank and WORLD_SIZE must equal
+--gpus. Without one, --gpus N > 1 spawns N child processes of this script with the launcher
+variables set (before this process touches the GPU) and exits with the worst child status; N
+larger than the visible GPU count is an error, never a silent 1-GPU run.
+
+Correctness gate (N > 1). Before timing, every rank runs a small decomposed problem of the same
+stencil (256 x 256 x 64N, 6 fused sweeps, residual included) through the SAME transport, and
+compares its owned planes bitwise against a full-grid single-slab run on its own GPU. Any mismatch
+on any rank aborts the run non-zero. With --transport auto the transports are tried in order
+(rccl, then ipc on GPUs) and the first that passes the gate is timed; the JSON names it.
 
 The grid is fixed as N grows (strong scaling, the BASELINE.json config "3D 7-pt Jacobi 1024^3 fp32
 slab-decomposed across 8xMI355X"). Data is synthetic: a uniform random initial grid generated on
@@ -12,10 +24,12 @@ the device from a counter-based hash of the global cell index (seed 1). Every ti
 Jacobi update of every cell (boundary planes + halo exchange + interior), nothing is skipped or
 cached. By default two consecutive Jacobi steps are fused into one pass over memory (temporal
 blocking, --temporal 2; bitwise identical to two single steps, tests/test_gpu_temporal.py): every
-step is still computed in full, the fused kernel just keeps u^{t+1} on chip. --temporal 1 measures
-one sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
+step is still computed in full, the fused kernel keeps u^{t+1} on chip. --temporal 1 measures one
+sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
 torch.cuda.synchronize() on both sides; the slowest rank's time is reported. GCells/s =
-nx*ny*nz*K / t / 1e9 for the whole job. Rank 0 prints one JSON line.
+nx*ny*nz*K / t / 1e9 for the whole job. Rank 0 prints one JSON line. The DRAM fields report the
+traffic actually required per time step (one read + one write of every cell per fused sweep, i.e.
+divided by the temporal depth) against the measured 6.29 TB/s copy roof.
 """
 
 from __future__ import annotations
@@ -23,21 +37,23 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 
 METRIC = "GCells/s (whole node), 3D 7-pt Jacobi 1024^3 fp32 at 1/2/4/8 MI355X"
 HBM_MEASURED_TBPS = 6.29  # float4 copy, MI355X_MICROARCH.md (8.0 spec)
+LAUNCH_VARS = ("RANK", "WORLD_SIZE", "OMPI_COMM_WORLD_RANK", "PMI_RANK")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1, help="ranks (one process and one GPU each)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--n", type=int, default=1024, help="cube edge (default 1024)")
@@ -47,7 +63,7 @@ def parse():
     p.add_argument("--stencil", default="heat7", choices=["heat7", "box27", "jacobi5", "life"])
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "u8"])
     p.add_argument("--transport", default="auto",
-                   help="auto|rccl|torch|staged (distributed), loopback (1 process)")
+                   help="auto|rccl|ipc|torch|staged (distributed), loopback (1 process)")
     p.add_argument("--virtual-ranks", type=int, default=0,
                    help="split the grid into P slabs inside ONE process (loopback transport)")
     p.add_argument("--graph", action="store_true", help="replay 2-step cycles as hipGraphs")
@@ -59,59 +75,228 @@ def parse():
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
     p.add_argument("--device", default="auto", choices=["auto", "hip", "cpu"])
     p.add_argument("--repeats", type=int, default=1, help="timed repetitions; the best is reported")
-    return p.parse_args()
+    p.add_argument("--timeout", type=float, default=120.0,
+                   help="watchdog (s): a rank whose streams make no progress for this long aborts the "
+                        "transport and exits non-zero")
+    p.add_argument("--gate-n", type=int, default=0, help="edge of the correctness-gate grid (0 = auto)")
+    p.add_argument("--no-gate", action="store_true", help="skip the N > 1 correctness gate")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="allow more ranks than GPUs (processes share devices; tests of the ipc/staged paths)")
+    return p.parse_args(argv)
 
 
-def main():
-    a = parse()
-    from mpi_cuda_process_amd import Simulation, heat3d, box27, mdf2d, life2d, native
+def launched() -> bool:
+    return any(v in os.environ for v in LAUNCH_VARS)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a, argv) -> int:
+    """Spawn --gpus worker processes of this script (one per GPU) and wait for them."""
+    n = a.gpus
+    ndev = torch.cuda.device_count() if a.device != "cpu" else 0  # counts without initialising HIP
+    if a.device == "hip" and ndev == 0:
+        print("bench: --device hip but no GPU is visible", file=sys.stderr)
+        return 2
+    if ndev > 0 and n > ndev and not a.share_gpu:
+        print("bench: --gpus %d but only %d GPU(s) are visible; refusing to run fewer GPUs than asked "
+              "(--share-gpu lets ranks share devices)" % (n, ndev), file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    worst, first_fail = 0, None
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0:
+                worst = worst or rc
+                if first_fail is None:
+                    first_fail = time.time()
+        if first_fail is not None and live and time.time() - first_fail > 30:
+            for r in live:  # peers of a failed rank block in collectives: end them
+                procs[r].kill()
+            for r in live:
+                procs[r].wait()
+            worst = worst or 1
+            break
+        time.sleep(0.05)
+    if worst:
+        print("bench: a rank exited with status %d" % worst, file=sys.stderr)
+        return 1
+    return 0
+
+
+def make_problem(a, nx, ny, nz):
+    from mpi_cuda_process_amd import box27, heat3d, life2d, mdf2d
+
+    if a.stencil == "heat7":
+        return heat3d(nx=nx, ny=ny, nz=nz, dtype=a.dtype)
+    if a.stencil == "box27":
+        return box27(nx=nx, ny=ny, nz=nz, dtype=a.dtype)
+    if a.stencil == "jacobi5":
+        return mdf2d(h=nz, w=nx, dtype=a.dtype)
+    return life2d(h=nz, w=nx)
+
+
+def pick_temporal(a, prob, nslab, hip):
+    from mpi_cuda_process_amd import native
+
+    if a.temporal > 0:
+        return a.temporal
+    # fused depth where a kernel exists: 2 for the 3D stencils, 8 (MDF) / 4 (Life) for the 2D ones
+    # (profiles/r01_deep_temporal_2d.txt), capped so every slab is at least 4 sweeps deep
+    want = {"jacobi5": 8, "life": 4}.get(a.stencil, 2)
+    while want > 1 and prob.nz < 4 * want * nslab:
+        want //= 2
+    if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz,
+                                                            want, want)):
+        return want
+    return 1
+
+
+def run_gate(a, hip, transport, temporal, world, rank):
+    """Bitwise check of the decomposed engine (same transport, same fused depth) against a
+    full-grid single-slab run on this rank's own device. Returns (passed, record)."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from mpi_cuda_process_amd import Simulation
+
+    n = a.gate_n or (256 if hip else 32)
+    per = max(64 if hip else 8, 4 * temporal)
+    if a.stencil in ("jacobi5", "life"):
+        prob = make_problem(a, n, 1, per * world)
+    else:
+        prob = make_problem(a, n, n, per * world)
+    steps = 6 * temporal
+    kw = dict(device="hip" if hip else "cpu", temporal=temporal, residual_every=steps,
+              timeout_s=a.timeout if hip else 0.0)
+    err = ""
+    ok = False
+    try:
+        with Simulation(prob, distributed=True, transport=transport, **kw) as sim:
+            sim.init()
+            sim.run(steps)
+            sim.synchronize()
+            mine = sim.read_local(0)
+            res = sim.residual
+            lay = sim.layout(0)
+        with Simulation(prob, ranks=1, distributed=False, **kw) as ref:
+            ref.init()
+            ref.run(steps)
+            ref.synchronize()
+            full = ref.read_local(0)
+            rres = ref.residual
+        ok = bool(np.array_equal(mine, full[lay["z0"]:lay["z1"]])) and abs(res - rres) <= 1e-9 * max(1.0, abs(rres))
+        if not ok:
+            err = "rank %d: owned planes or residual differ from the full-grid run (residual %r vs %r)" % (
+                rank, res, rres)
+    except Exception as e:  # noqa: BLE001 - reported and agreed on below
+        err = "rank %d: %s: %s" % (rank, type(e).__name__, e)
+    t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    bad = int(t.item())
+    if err:
+        print("bench gate [%s]: %s" % (transport, err), file=sys.stderr, flush=True)
+    rec = {"grid": [prob.nx, prob.ny, prob.nz], "steps": steps, "transport": transport,
+           "ranks_failed": bad, "passed": bad == 0}
+    return bad == 0, rec
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus > 1 and not launched() and not os.environ.get("MDFX_FORCE_DIST"):
+        return self_launch(a, argv)
+
+    import torch.distributed as dist
+
+    from mpi_cuda_process_amd import Simulation, native
     from mpi_cuda_process_amd.parallel.dist import init_distributed
 
     force = os.environ.get("MDFX_FORCE_DIST", "") == "1"  # distributed path even at WORLD_SIZE 1 (tests)
     env = init_distributed("gloo", force=force) if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or force) else None
     world = dist.get_world_size() if env else 1
     rank = dist.get_rank() if env else 0
-    if env and a.gpus != world:
-        print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
-    hip = torch.cuda.is_available() and a.device != "cpu"
+    if env and world > 1 and a.gpus != world:
+        print("bench: --gpus %d but the launcher started WORLD_SIZE %d ranks" % (a.gpus, world), file=sys.stderr)
+        return 2
+    want_hip = a.device != "cpu"
+    ndev = torch.cuda.device_count() if want_hip else 0
+    if env and want_hip and ndev > 0 and world > ndev and not a.share_gpu:
+        if rank == 0:
+            print("bench: %d ranks but only %d GPU(s) visible" % (world, ndev), file=sys.stderr)
+        return 2
+    hip = want_hip and torch.cuda.is_available()
+    if a.device == "hip" and not hip:
+        print("bench: --device hip but no HIP device is usable", file=sys.stderr)
+        return 2
+    device_id = -1
     if hip:
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        device_id = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
+        torch.cuda.set_device(device_id)
     native().set_kernel_variant(a.variant)
 
     nx, ny, nz = a.nx or a.n, a.ny or a.n, a.nz or a.n
     if a.stencil in ("jacobi5", "life"):
         ny = 1  # 2D grids: nx = width, nz = height
-    if a.stencil == "heat7":
-        prob = heat3d(nx=nx, ny=ny, nz=nz, dtype=a.dtype)
-    elif a.stencil == "box27":
-        prob = box27(nx=nx, ny=ny, nz=nz, dtype=a.dtype)
-    elif a.stencil == "jacobi5":
-        prob = mdf2d(h=nz, w=nx, dtype=a.dtype)
-    else:
-        prob = life2d(h=nz, w=nx)
+    prob = make_problem(a, nx, ny, nz)
+    temporal = pick_temporal(a, prob, max(1, world, a.virtual_ranks), hip)
+    timeout = a.timeout if hip else 0.0
 
-    temporal = a.temporal
-    if temporal <= 0:
-        # fused depth where a kernel exists: 2 for the 3D stencils, 8 (MDF) / 4 (Life) for the 2D
-        # ones (profiles/r01_deep_temporal_2d.txt), capped so every slab is at least 4 sweeps deep
-        want = {"jacobi5": 8, "life": 4}.get(a.stencil, 2)
-        nslab = max(1, int(os.environ.get("WORLD_SIZE", "1")), a.virtual_ranks)
-        while want > 1 and prob.nz < 4 * want * nslab:
-            want //= 2
-        temporal = 1
-        if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny,
-                                                                prob.nz, want, want)):
-            temporal = want
-    kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap, graph=a.graph,
-              residual_every=a.residual_every, timeout_s=900.0 if hip else 0.0, temporal=temporal)
+    # ---- transport (+ correctness gate for N > 1) ----------------------------------------
+    gate = None
+    transport = a.transport
     if env:
-        sim = Simulation(prob, distributed=True, transport=a.transport, **kw)
+        if transport == "auto":
+            candidates = ["rccl", "ipc"] if hip else ["torch"]
+        else:
+            candidates = [transport]
+        if world > 1 and not a.no_gate:
+            gates = []
+            chosen = None
+            for t in candidates:
+                passed, rec = run_gate(a, hip, t, temporal, world, rank)
+                gates.append(rec)
+                if passed:
+                    chosen = t
+                    break
+            gate = gates[-1] if chosen else {"passed": False, "tried": gates}
+            if chosen is None:
+                if rank == 0:
+                    print("bench: correctness gate FAILED for every transport tried (%s); not timing"
+                          % ", ".join(candidates), file=sys.stderr)
+                dist.barrier()
+                dist.destroy_process_group()
+                return 3
+            if len(gates) > 1:
+                gate["fell_back_from"] = [g["transport"] for g in gates[:-1]]
+            transport = chosen
+        else:
+            transport = candidates[0]
+
+    kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap, graph=a.graph,
+              residual_every=a.residual_every, timeout_s=timeout, temporal=temporal)
+    if env:
+        sim = Simulation(prob, distributed=True, transport=transport, **kw)
     else:
         vr = a.virtual_ranks or 1
         sim = Simulation(prob, ranks=vr, distributed=False,
-                         transport="auto" if a.transport in ("auto", "rccl", "torch", "staged") else a.transport,
-                         **kw)
+                         transport=transport if transport in ("loopback", "host") else "auto", **kw)
     sim.init()
 
     def barrier():
@@ -141,15 +326,23 @@ def main():
             dt = float(t.item())
         best = dt if best is None else min(best, dt)
 
+    devices = [device_id]
+    if env:
+        allp = [None] * world
+        dist.all_gather_object(allp, device_id)
+        devices = allp
     cells = prob.cells
     gcells = cells * a.steps / best / 1e9
     ms = best / a.steps * 1e3
     nproc = world if env else 1
-    bpc = prob.bytes_per_cell_per_step
-    roof = HBM_MEASURED_TBPS * 1e12 / bpc / 1e9 * (nproc if hip else 0)
+    per_gpu = gcells / max(nproc, 1)
+    # DRAM actually required per time step: one read + one write of every cell per sweep, and a
+    # sweep advances `temporal` steps
+    dram_tbps = per_gpu * prob.bytes_per_cell_per_step / temporal / 1e3
     if rank == 0:
-        par = ("slab-z%d (1 process/GPU, %s halo over xGMI, interior||boundary streams)" % (world, sim.transport)
-               if env else ("slab-z%d virtual in 1 process (%s)" % (a.virtual_ranks, sim.transport)
+        sim_transport = sim.transport
+        par = ("slab-z%d (1 process/GPU, %s halo, interior||boundary streams)" % (world, sim_transport)
+               if env else ("slab-z%d virtual in 1 process (%s)" % (a.virtual_ranks, sim_transport)
                             if a.virtual_ranks > 1 else "single GPU" if hip else "cpu"))
         model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF",
                  "life": "2D Game of Life"}[a.stencil]
@@ -158,7 +351,7 @@ def main():
             else "GCells/s (whole node), %s %dx%dx%d %s" % (model, nx, ny, nz, a.dtype),
             "value": round(gcells, 3),
             "unit": "GCells/s",
-            "n_gpus": nproc if hip else 0,
+            "n_gpus": nproc,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms, 4),
@@ -173,21 +366,29 @@ def main():
                 "seq_len": nz,
                 "grid": [nx, ny, nz],
                 "parallelism": par,
+                "ranks": nproc,
+                "devices": devices,
+                "distinct_devices": len(set(devices)) if hip else 0,
+                "transport": sim_transport,
+                "comm_size": nproc if sim_transport == "rccl" else 0,
                 "kernel_variant": native().kernel_variant(),
                 "graph": a.graph,
                 "overlap": not a.no_overlap,
                 "temporal_block": temporal,
+                "gate": gate,
             },
-            "per_gpu_gcells": round(gcells / max(nproc, 1), 3),
-            "effective_hbm_TBps_per_gpu": round(gcells * bpc / 1e3 / max(nproc, 1), 3),
-            "pct_of_measured_hbm_roof": round(100.0 * gcells / roof, 1) if roof else None,
+            "per_gpu_gcells": round(per_gpu, 3),
+            "dram_bytes_per_step_per_gpu": int(cells / max(nproc, 1) * prob.bytes_per_cell_per_step / temporal),
+            "achieved_dram_TBps_per_gpu": round(dram_tbps, 3) if hip else None,
+            "pct_of_hbm_copy_roof": round(100.0 * dram_tbps / HBM_MEASURED_TBPS, 1) if hip else None,
         }
         print(json.dumps(rec), flush=True)
     sim.close()
     if env:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

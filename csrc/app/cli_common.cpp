@@ -54,7 +54,7 @@ void usage(const char* prog) {
       "  --backend auto|hip|cpu    device backend\n"
       "  --gpus N                  slabs on GPUs 0..N-1 driven by this one process\n"
       "  --ranks P                 P slabs in this process (several per GPU allowed: loopback)\n"
-      "  --transport auto|rccl|loopback|host|tcp\n"
+      "  --transport auto|rccl|ipc|loopback|host|tcp\n"
       "                            multi-process runs (mpirun / torchrun): rccl on GPUs, tcp on CPUs\n"
       "  --init random|dirichlet|constant|life|compat  --seed --lo --hi --value --edge --interior --density\n"
       "  --r R | --c0 --c1 --c2 --c3   update coefficients\n"
@@ -264,6 +264,15 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     } else if (tname == "tcp") {
       MDFX_CHECK(rv != nullptr, "tcp transport needs a multi-process launch (mpirun / torchrun)");
       tr = make_tcp_transport(*rv);
+    } else if (tname == "ipc") {
+      MDFX_CHECK(rv != nullptr && hip, "ipc transport needs a multi-process launch on HIP devices");
+      Rendezvous* r = rv.get();
+      CallbackFns f;
+      f.allgather = [r](const std::string& mine) { return r->allgather(mine); };
+      f.allreduce_sum = [r](double v) { return r->allreduce_sum(v); };
+      f.allreduce_max = [r](double v) { return r->allreduce_max(v); };
+      f.barrier = [r]() { r->barrier(); };
+      tr = make_ipc_transport(std::move(f));
     } else {
       MDFX_FAIL("unknown transport " + tname);
     }

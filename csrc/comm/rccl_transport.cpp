@@ -14,7 +14,9 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "mdfx/runtime.hpp"
 
@@ -46,6 +48,7 @@ class RcclTransport final : public Transport {
     std::memcpy(id_.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
   }
   ~RcclTransport() override {
+    if (aborted_) return;  // streams may hold RCCL work that never ran: leak rather than block
     for (size_t i = 0; i < comms_.size(); ++i) {
       if (scratch_[i]) {
         (void)hipSetDevice(locals_[i].be->device());
@@ -57,6 +60,14 @@ class RcclTransport final : public Transport {
   }
   const char* name() const override { return "rccl"; }
   bool in_process_only() const override { return false; }
+  bool graph_capturable() const override { return true; }
+  void set_timeout(double s) override { timeout_s_ = s; }
+  void abort() override {
+    if (aborted_) return;
+    aborted_ = true;
+    for (auto c : comms_)
+      if (c) (void)ncclCommAbort(c);
+  }
 
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
     locals_ = locals;
@@ -110,11 +121,24 @@ class RcclTransport final : public Transport {
       NCCLC(ncclAllReduce(scratch_[i], (char*)scratch_[i] + sizeof(double), 1, ncclFloat64, op,
                           comms_[i], aux_[i]));
     NCCLC(ncclGroupEnd());
+    const auto t0 = std::chrono::steady_clock::now();
     for (size_t i = 0; i < locals_.size(); ++i) {
       locals_[i].be->activate();
       HIPC(hipMemcpyAsync(&out[i], (char*)scratch_[i] + sizeof(double), sizeof(double),
                           hipMemcpyDeviceToHost, aux_[i]));
-      HIPC(hipStreamSynchronize(aux_[i]));
+      // poll instead of blocking: a dead peer surfaces as an RCCL async error or the watchdog
+      for (;;) {
+        const hipError_t q = hipStreamQuery(aux_[i]);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIPC(q);
+        check();
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (timeout_s_ > 0 && el > timeout_s_) {
+          abort();
+          MDFX_FAIL(format("watchdog: RCCL all-reduce not done after %.1f s (peer dead or hung)", el));
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
     }
     return out[0];
   }
@@ -123,12 +147,12 @@ class RcclTransport final : public Transport {
   void barrier() override { (void)allreduce(0.0, ncclSum); }
 
   void check() override {
+    if (aborted_) MDFX_FAIL("RCCL communicator was aborted");
     for (auto c : comms_) {
       ncclResult_t ae = ncclSuccess;
       NCCLC(ncclCommGetAsyncError(c, &ae));
       if (ae != ncclSuccess && ae != ncclInProgress) {
-        for (auto cc : comms_) (void)ncclCommAbort(cc);
-        comms_.assign(comms_.size(), nullptr);
+        abort();
         MDFX_FAIL(std::string("RCCL async error: ") + ncclGetErrorString(ae));
       }
     }
@@ -141,6 +165,8 @@ class RcclTransport final : public Transport {
   std::vector<ncclComm_t> comms_;
   std::vector<void*> scratch_;
   std::vector<hipStream_t> aux_;
+  double timeout_s_ = 0.0;
+  bool aborted_ = false;
 };
 
 }  // namespace

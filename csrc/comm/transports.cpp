@@ -51,6 +51,11 @@ class InProcessBase : public Transport {
 class HostTransport final : public InProcessBase {
  public:
   const char* name() const override { return "host"; }
+  void setup(const std::vector<LocalSlab>& locals, int nranks) override {
+    InProcessBase::setup(locals, nranks);
+    // a host memcpy on device pointers would race the streams (or fault): CPU slabs only
+    for (auto& s : locals_) MDFX_CHECK(s.be->kind() == DeviceKind::CPU, "host transport needs CPU backends");
+  }
   void exchange(int b) override {
     for (auto& q : locals_)
       for (int side = 0; side < 2; ++side) {
@@ -68,6 +73,7 @@ class LoopbackTransport final : public InProcessBase {
     for (size_t i = 0; i < ev_.size(); ++i) locals_[i].be->destroy_event(ev_[i]);
   }
   const char* name() const override { return "loopback"; }
+  bool graph_capturable() const override { return true; }
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
     InProcessBase::setup(locals, nranks);
     for (auto& s : locals_) {

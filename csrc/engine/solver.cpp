@@ -1,7 +1,9 @@
 // mdfx engine implementation (see solver.hpp for the schedule).
 #include "mdfx/solver.hpp"
 
+#include <dirent.h>
 #include <hip/hip_runtime_api.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cmath>
@@ -14,6 +16,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include "mdfx/devsync.hpp"
 
 namespace mdfx {
 
@@ -40,7 +44,12 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 8, "temporal blocking depth must be 1..8");
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
-  if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) hip_set_min_rounds(nranks > 1 ? 2 : 1);
+  if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
+    hip_set_min_rounds(nranks > 1 ? 2 : 1);
+    // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
+    hip_set_abort(0);
+    hip_clear_wait_error();
+  }
   const int halo = opt_.temporal;
   for (size_t i = 0; i < local_ranks.size(); ++i) {
     const int r = local_ranks[i];
@@ -103,13 +112,28 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     l.buf[1] = s.buf[1];
     ls.push_back(l);
   }
+  transport_->set_timeout(opt_.timeout_s);
   transport_->setup(ls, nranks_);
 }
 
 Solver::~Solver() {
-  try {
-    sync_all();
-  } catch (...) {
+  if (poisoned_) {
+    // the watchdog fired: the transport was aborted and the device waits released, so the streams
+    // should drain; if they do not within a bound, leak everything rather than hang the exit
+    bool drained = false;
+    try {
+      drained = drain(10.0);
+    } catch (...) {
+    }
+    if (!drained) {
+      (void)transport_.release();
+      return;
+    }
+  } else {
+    try {
+      sync_all();
+    } catch (...) {
+    }
   }
   destroy_graph();
   transport_.reset();  // communicators before the memory they reference
@@ -128,7 +152,9 @@ Solver::~Solver() {
 
 void Solver::set_options(const SolverOptions& o) {
   if (o.graph != opt_.graph || o.overlap != opt_.overlap) destroy_graph();
+  MDFX_CHECK(o.temporal == opt_.temporal, "the temporal blocking depth is fixed at construction");
   opt_ = o;
+  transport_->set_timeout(opt_.timeout_s);
 }
 
 void Solver::init(const InitSpec& is) {
@@ -151,14 +177,46 @@ void Solver::sync_all() {
   }
 }
 
+bool Solver::drain(double limit_s) {
+  if (slabs_[0].be->kind() != DeviceKind::HIP) return true;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (auto& s : slabs_) {
+    s.be->activate();
+    for (void* st : {s.hs, s.cs}) {
+      for (;;) {
+        const hipError_t q = hipStreamQuery((hipStream_t)st);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return false;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s) return false;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
+    }
+  }
+  return true;
+}
+
+void Solver::poison(const std::string& why) {
+  poisoned_ = true;
+  std::fprintf(stderr, "[mdfx] %s: aborting the transport and releasing device waits\n", why.c_str());
+  std::fflush(stderr);
+  try {
+    transport_->abort();
+  } catch (...) {
+  }
+  if (slabs_[0].be->kind() == DeviceKind::HIP) hip_set_abort(1);
+  MDFX_FAIL(why);
+}
+
 void Solver::synchronize() {
+  MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
   if (opt_.timeout_s <= 0 || slabs_[0].be->kind() != DeviceKind::HIP) {
     sync_all();
     transport_->check();
     return;
   }
-  // watchdog: poll the streams and RCCL's async error state instead of blocking forever (the
-  // reference hangs in MPI_Send).
+  // watchdog: poll the streams and the transport's error state instead of blocking forever (the
+  // reference hangs in MPI_Send). On timeout the transport is aborted (ncclCommAbort /
+  // the device abort word), so the process can report and exit instead of hanging in teardown.
   const auto t0 = std::chrono::steady_clock::now();
   for (auto& s : slabs_) {
     s.be->activate();
@@ -167,16 +225,21 @@ void Solver::synchronize() {
         const hipError_t q = hipStreamQuery((hipStream_t)st);
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) HIPC(q);
-        transport_->check();
+        try {
+          transport_->check();
+        } catch (const Error& e) {
+          poison(e.what());
+        }
         const double el =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (el > opt_.timeout_s)
-          MDFX_FAIL(format("watchdog: step stream of rank %d not done after %.1f s", s.rank, el));
+          poison(format("watchdog: step stream of rank %d not done after %.1f s", s.rank, el));
         // 20 us polls: the timed bench loop ends within 20 us of the GPU (6.5 ms for 50 steps at N = 8)
         std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
     }
   }
+  transport_->check();
 }
 
 void Solver::exchange_ghosts() {
@@ -187,7 +250,7 @@ void Solver::exchange_ghosts() {
     s.be->record(s.ev_bnd, s.hs);
   }
   transport_->exchange(cur_);
-  sync_all();
+  synchronize();
   ghosts_dirty_ = false;
 }
 
@@ -283,7 +346,7 @@ void Solver::step(bool want_resid, int k) {
 }
 
 void Solver::finish_residual() {
-  sync_all();
+  synchronize();  // polled under the watchdog: a hung peer must not block the residual forever
   double local = 0.0;
   for (auto& s : slabs_) {
     double h[2] = {0, 0};
@@ -291,7 +354,12 @@ void Solver::finish_residual() {
     s.be->sync_stream(s.hs);
     local += h[0] + h[1];
   }
-  const double g = transport_->allreduce_sum(local);
+  double g = 0.0;
+  try {
+    g = transport_->allreduce_sum(local);
+  } catch (const Error& e) {
+    poison(e.what());
+  }
   stats_.last_residual = std::sqrt(g);
   stats_.residual_step = stats_.steps;
   if (!std::isfinite(stats_.last_residual))
@@ -341,6 +409,14 @@ void Solver::maybe_inject_fault() {
     if (f.kind == "exit") std::_Exit(42);
     if (f.kind == "hang")
       for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+    if (f.kind == "spin") {  // a device kernel that stops making progress (60 s bound)
+      if (slabs_[i].be->kind() == DeviceKind::HIP) {
+        slabs_[i].be->activate();
+        hip_spin(60.0, slabs_[i].cs);
+      } else {
+        for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+      }
+    }
     if (f.kind == "nan") {
       Slab& s = slabs_[i];
       sync_all();
@@ -364,6 +440,7 @@ void Solver::maybe_inject_fault() {
 
 void Solver::run(int64_t steps) {
   MDFX_CHECK(steps >= 0, "negative step count");
+  MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
   if (ghosts_dirty_) exchange_ghosts();
   transport_->check();
   const bool hip = slabs_[0].be->kind() == DeviceKind::HIP;
@@ -383,12 +460,10 @@ void Solver::run(int64_t steps) {
         break;
       }
     const bool res = (to_res == k);
-    // graph replay for plain (non-residual, non-debug) stretches of >= 2 sweeps. Restricted to one
-    // slab per process (the production layout: one rank per GPU): the ROCm 7.0 HIP runtime that
-    // PyTorch bundles crashes in hipStreamEndCapture on the multi-slab loopback capture (the same
-    // capture replays correctly under ROCm 7.2: csrc/tests/test_main.cpp test_graph), so several
-    // slabs in one process always run eagerly.
-    if (opt_.graph && hip && !res && !opt_.sync_debug && !opt_.profile && slabs_.size() == 1) {
+    // graph replay for plain (non-residual, non-debug) stretches of >= 2 sweeps, when the
+    // transport's exchange is pure stream work (rccl, loopback, ipc; the callback / host / tcp
+    // transports move data on the host and always run eagerly).
+    if (opt_.graph && hip && !res && !opt_.sync_debug && !opt_.profile && transport_->graph_capturable()) {
       const int64_t plain = std::min<int64_t>(steps - done, to_res - 1);
       const int64_t pairs = fault().rank >= 0 ? 0 : plain / (2 * k);
       if (pairs > 0) {
@@ -575,6 +650,24 @@ void Solver::save_checkpoint(const std::string& dir) {
       << ", \"rank\": " << slabs_[i].rank << ", \"nranks\": " << nranks_
       << ", \"step\": " << stats_.steps << "}\n";
   }
+  // a directory reused by an earlier save with more ranks keeps its extra slabs: remove them so
+  // no reader can mix them in (readers also take nranks from slab_0 and check every header)
+  bool owns0 = false;
+  for (auto& s : slabs_) owns0 = owns0 || s.rank == 0;
+  if (owns0) {
+    if (DIR* d = ::opendir(dir.c_str())) {
+      std::vector<std::string> stale;
+      while (dirent* e = ::readdir(d)) {
+        int r = -1;
+        char ext[8] = {0};
+        if (std::sscanf(e->d_name, "slab_%d.%7s", &r, ext) == 2 && r >= nranks_ &&
+            (std::strcmp(ext, "bin") == 0 || std::strcmp(ext, "json") == 0))
+          stale.push_back(dir + "/" + e->d_name);
+      }
+      ::closedir(d);
+      for (auto& f : stale) ::unlink(f.c_str());
+    }
+  }
 }
 
 static bool json_int(const std::string& s, const std::string& key, long long& out) {
@@ -587,16 +680,22 @@ static bool json_int(const std::string& s, const std::string& key, long long& ou
 }
 
 void Solver::load_checkpoint(const std::string& dir) {
-  // discover slabs written by any decomposition: slab_<r>.json for r = 0.. until missing
+  // slabs written by any decomposition: slab_0 names the writer's rank count, and every one of
+  // slab_0 .. slab_<nranks-1> must carry that count and the same step
   struct F {
     long long z0, z1, step;
     std::string bin;
   };
   std::vector<F> files;
-  for (int r = 0;; ++r) {
+  long long writer_ranks = -1, writer_step = -1;
+  for (int r = 0; writer_ranks < 0 || r < writer_ranks; ++r) {
     const std::string base = dir + "/slab_" + std::to_string(r);
     std::ifstream j(base + ".json");
-    if (!j.good()) break;
+    if (!j.good()) {
+      MDFX_CHECK(r > 0, "no checkpoint slabs in " + dir);
+      MDFX_FAIL(format("checkpoint %s is incomplete: slab_%d.json missing (written by %lld ranks)", dir.c_str(), r,
+                       writer_ranks));
+    }
     std::stringstream ss;
     ss << j.rdbuf();
     const std::string js = ss.str();
@@ -609,6 +708,15 @@ void Solver::load_checkpoint(const std::string& dir) {
                "checkpoint grid does not match the solver grid");
     MDFX_CHECK(js.find(std::string("\"dtype\": \"") + dtype_name(spec_.dtype) + "\"") != std::string::npos,
                "checkpoint dtype does not match");
+    long long nr = -1;
+    MDFX_CHECK(json_int(js, "nranks", nr) && nr >= 1, "checkpoint header without nranks: " + base + ".json");
+    if (r == 0) {
+      writer_ranks = nr;
+      writer_step = f.step;
+    }
+    MDFX_CHECK(nr == writer_ranks && f.step == writer_step,
+               format("checkpoint slab_%d (nranks %lld, step %lld) does not match slab_0 (nranks %lld, step %lld)", r, nr,
+                      f.step, writer_ranks, writer_step));
     f.bin = base + ".bin";
     files.push_back(f);
   }

@@ -1,0 +1,38 @@
+// mdfx device-side synchronisation: stream-ordered counters for cross-process halo exchange, the
+// process-wide abort word, and the device spin used by fault injection.
+//
+// Reference parity: the reference orders its halo exchange with blocking host MPI calls after a
+// cudaDeviceSynchronize (MDF_kernel.cu:167-175,180-183) and hangs forever when a peer misbehaves
+// (SURVEY D4). Here a process publishes "faces ready" / "faces pulled" as 64-bit counters in
+// uncached device memory that its neighbours map through HIP IPC; waits are tiny kernels on the
+// halo stream, so the host never blocks inside the step loop. Every device wait is bounded: it
+// returns when the counter arrives, when the host raises the abort word (watchdog), or after its
+// timeout, in which case it raises the host-visible error word that Transport::check() reports.
+#pragma once
+
+#include <cstdint>
+
+namespace mdfx {
+
+// Process-wide host-mapped words (allocated on first use; valid for the process lifetime).
+void hip_set_abort(int v);          // non-zero: every spinning device wait returns at once
+int hip_abort_raised();
+int hip_wait_error();               // non-zero after a device wait timed out
+void hip_clear_wait_error();
+
+// Counters live in memory from hip_alloc_uncached (coherent across XCDs, processes and devices).
+void* hip_alloc_uncached(size_t bytes);
+void hip_free_uncached(void* p);
+
+// Stream-ordered: *ctr += 1 (system-scope release: everything earlier on `stream` is visible to
+// any agent that then observes the new value). Single writer per counter.
+void hip_counter_signal(uint64_t* ctr, void* stream);
+// Stream-ordered: ++*expect (a private device counter), then wait until *remote >= *expect with a
+// system-scope acquire. Bounded by timeout_s and the abort word.
+void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream);
+
+// Fault injection (MDFX_FAULT=spin@rank:step): a one-wave kernel that busy-waits on `stream` for
+// `seconds` of device wall clock or until the abort word is raised.
+void hip_spin(double seconds, void* stream);
+
+}  // namespace mdfx

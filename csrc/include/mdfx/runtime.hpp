@@ -80,8 +80,16 @@ class Transport {
   virtual double allreduce_max(double v) = 0;
   virtual void barrier() = 0;
   virtual bool in_process_only() const { return true; }  // every rank lives in this process
-  // Optional async-error poll (RCCL); throws if a peer failed.
+  // Optional async-error poll (RCCL, IPC counters); throws if a peer failed.
   virtual void check() {}
+  // Whether exchange() only enqueues stream work (no host-side data movement or blocking), so a
+  // hipGraph capture of the step loop replays it faithfully: rccl, loopback, ipc.
+  virtual bool graph_capturable() const { return false; }
+  // Watchdog bound for blocking transport calls and device-side waits (seconds; 0 = default).
+  virtual void set_timeout(double) {}
+  // Watchdog escalation: make every outstanding transport operation return (ncclCommAbort, the
+  // device abort word) so the streams drain and the process can exit instead of hanging.
+  virtual void abort() {}
 };
 
 // CPU, all subdomains in this process: memcpy.
@@ -98,7 +106,13 @@ struct CallbackFns {
   std::function<double(double)> allreduce_sum;
   std::function<double(double)> allreduce_max;
   std::function<void()> barrier;
+  // Gather one byte string from every process, indexed by rank (the ipc transport's handle swap).
+  std::function<std::vector<std::string>(const std::string&)> allgather;
 };
 std::unique_ptr<Transport> make_callback_transport(CallbackFns fns);
+// HIP IPC, one slab per process (any number of processes per GPU): faces pulled from the
+// neighbours' mapped buffers by the copy engines, ordered by device-side counters
+// (csrc/comm/ipc_transport.cpp). Needs fns.allgather; residual / barrier go through fns too.
+std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns);
 
 }  // namespace mdfx

@@ -28,7 +28,8 @@ struct SolverOptions {
   bool sync_debug = false;    // device-synchronise after every phase (race differential tests)
   int residual_every = 0;     // compute the global L2 update norm every k steps (0 = never)
   bool graph = false;         // replay a captured 2-step cycle as a hipGraph (HIP only)
-  double timeout_s = 0.0;     // watchdog for synchronize(): abort instead of hanging (0 = off)
+  double timeout_s = 0.0;     // watchdog for synchronize() / residual / blocking transport calls:
+                              // abort the transport and throw instead of hanging (0 = off)
   // Temporal blocking: time steps fused per sweep over memory (1 or 2). With 2 the slabs keep two
   // ghost planes per side, exchanged once per fused step, and every sweep reads u^t once and writes
   // u^{t+2} once (bitwise identical to two single steps). Fixed at construction.
@@ -109,6 +110,8 @@ class Solver {
   void step(bool want_resid, int k);
   void maybe_inject_fault();
   void sync_all();
+  bool drain(double limit_s);                  // bounded stream drain (teardown after an abort)
+  [[noreturn]] void poison(const std::string& why);  // watchdog escalation, then throw
   void finish_residual();
   void run_graph(int64_t pairs, int k);
   void destroy_graph();
@@ -125,6 +128,7 @@ class Solver {
   PhaseStats phases_;
   void* pev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // timing events (slab 0)
   bool ghosts_dirty_ = false;
+  bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
   void* graph_exec_ = nullptr;  // hipGraphExec_t for the 2-step cycle starting at buffer 0
   int graph_parity_ = -1;
   int graph_k_ = 0;

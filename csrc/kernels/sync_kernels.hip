@@ -1,0 +1,137 @@
+// Device-side synchronisation kernels (see mdfx/devsync.hpp): cross-process counters, the abort
+// word and the fault-injection spin. Each kernel is one wave; only lane 0 touches memory, with
+// vector (global) loads / stores and system-scope atomics.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+
+#include "mdfx/common.hpp"
+#include "mdfx/devsync.hpp"
+
+namespace mdfx {
+
+#define HIPC(x)                                                                          \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) ::mdfx::throw_error(__FILE__, __LINE__, std::string("HIP: ") + #x + " -> " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+// [0] abort word, [16] wait-error word (separate 64-B lines); host-mapped, coherent.
+int* g_words = nullptr;
+std::once_flag g_words_once;
+
+int* words() {
+  std::call_once(g_words_once, [] {
+    void* p = nullptr;
+    HIPC(hipHostMalloc(&p, 4096, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    std::fill((int*)p, (int*)p + 1024, 0);
+    g_words = (int*)p;
+  });
+  return g_words;
+}
+
+// device addresses of the words (coherent mapped host memory: the same on every device)
+int* dev_words() {
+  static int* d = [] {
+    void* p = nullptr;
+    HIPC(hipHostGetDevicePointer(&p, words(), 0));
+    return (int*)p;
+  }();
+  return d;
+}
+
+uint64_t ticks_for(double seconds) {
+  static int khz_cache[64] = {0};  // per device; queried once (this runs on every exchange)
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  int khz = dev < 64 ? __atomic_load_n(&khz_cache[dev], __ATOMIC_RELAXED) : 0;
+  if (khz == 0) {
+    HIPC(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    if (khz <= 0) khz = 100000;  // gfx9 constant 100 MHz wall clock
+    if (dev < 64) __atomic_store_n(&khz_cache[dev], khz, __ATOMIC_RELAXED);
+  }
+  const double t = std::max(0.0, seconds) * 1e3 * (double)khz;
+  return t > 1.8e19 ? ~0ull : (uint64_t)t;
+}
+
+__global__ __launch_bounds__(64) void counter_signal_kernel(uint64_t* ctr) {
+  if (threadIdx.x != 0) return;
+  const uint64_t v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(ctr, v + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void counter_wait_kernel(const uint64_t* remote, uint64_t* expect, uint64_t ticks,
+                                                          const int* abort_w, int* err_w) {
+  if (threadIdx.x != 0) return;
+  const uint64_t want = __hip_atomic_load(expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __hip_atomic_store(expect, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // once one wait has timed out the exchange is broken: later waits return at once, so the queued
+  // steps drain in microseconds and the host reports the error (Transport::check)
+  if (__hip_atomic_load(err_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+  const uint64_t t0 = (uint64_t)wall_clock64();
+  for (;;) {
+    if (__hip_atomic_load(remote, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) return;
+    if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+    if ((uint64_t)wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err_w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks, const int* abort_w) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = (uint64_t)wall_clock64();
+  while ((uint64_t)wall_clock64() - t0 < ticks &&
+         __hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
+    __builtin_amdgcn_s_sleep(64);
+}
+
+void check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) MDFX_FAIL(std::string(what) + " launch failed: " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+void hip_set_abort(int v) { __atomic_store_n(&words()[0], v, __ATOMIC_SEQ_CST); }
+int hip_abort_raised() { return __atomic_load_n(&words()[0], __ATOMIC_SEQ_CST); }
+int hip_wait_error() { return __atomic_load_n(&words()[16], __ATOMIC_SEQ_CST); }
+void hip_clear_wait_error() { __atomic_store_n(&words()[16], 0, __ATOMIC_SEQ_CST); }
+
+void* hip_alloc_uncached(size_t bytes) {
+  void* p = nullptr;
+  HIPC(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
+  HIPC(hipMemset(p, 0, bytes));
+  HIPC(hipDeviceSynchronize());
+  return p;
+}
+
+void hip_free_uncached(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+void hip_counter_signal(uint64_t* ctr, void* stream) {
+  hipLaunchKernelGGL(counter_signal_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ctr);
+  check_launch("counter_signal");
+}
+
+void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream) {
+  int* w = dev_words();
+  hipLaunchKernelGGL(counter_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, remote, expect,
+                     ticks_for(timeout_s), (const int*)w, w + 16);
+  check_launch("counter_wait");
+}
+
+void hip_spin(double seconds, void* stream) {
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ticks_for(seconds),
+                     (const int*)dev_words());
+  check_launch("spin");
+}
+
+}  // namespace mdfx

@@ -10,6 +10,7 @@
 
 #include <cstring>
 
+#include "mdfx/devsync.hpp"
 #include "mdfx/solver.hpp"
 
 namespace py = pybind11;
@@ -139,6 +140,59 @@ py::dtype np_dtype(DType t) {
   return py::dtype::of<float>();
 }
 
+// Host callables from a dict {"exchange", "allreduce_sum", "allreduce_max", "barrier",
+// "allgather"}; each re-acquires the GIL (the engine runs with it released).
+CallbackFns callback_fns(py::object callbacks) {
+  if (callbacks.is_none()) throw Error("this transport needs callbacks");
+  py::dict cb = callbacks.cast<py::dict>();
+  CallbackFns f;
+  // callables may be released from a thread that does not hold the GIL (close() releases it)
+  auto keep = [](py::object o) {
+    return std::shared_ptr<py::object>(new py::object(std::move(o)), [](py::object* q) {
+      py::gil_scoped_acquire g;
+      delete q;
+    });
+  };
+  if (cb.contains("exchange")) {
+    auto ex = keep(cb["exchange"]);
+    f.exchange = [ex](int b) {
+      py::gil_scoped_acquire g;
+      (*ex)(b);
+    };
+  }
+  if (cb.contains("allreduce_sum")) {
+    auto ar = keep(cb["allreduce_sum"]);
+    f.allreduce_sum = [ar](double v) {
+      py::gil_scoped_acquire g;
+      return (*ar)(v).cast<double>();
+    };
+  }
+  if (cb.contains("allreduce_max")) {
+    auto am = keep(cb["allreduce_max"]);
+    f.allreduce_max = [am](double v) {
+      py::gil_scoped_acquire g;
+      return (*am)(v).cast<double>();
+    };
+  }
+  if (cb.contains("barrier")) {
+    auto ba = keep(cb["barrier"]);
+    f.barrier = [ba]() {
+      py::gil_scoped_acquire g;
+      (*ba)();
+    };
+  }
+  if (cb.contains("allgather")) {
+    auto ag = keep(cb["allgather"]);
+    f.allgather = [ag](const std::string& mine) {
+      py::gil_scoped_acquire g;
+      std::vector<std::string> out;
+      for (auto item : (*ag)(py::bytes(mine))) out.push_back(item.cast<std::string>());
+      return out;
+    };
+  }
+  return f;
+}
+
 class PySolver {
  public:
   PySolver(const std::string& kind, const std::string& dtype, int64_t nx, int64_t ny, int64_t nz,
@@ -160,47 +214,15 @@ class PySolver {
     } else if (transport == "rccl") {
       tr = make_rccl_transport(std::string(unique_id));
     } else if (transport == "callback") {
-      if (callbacks.is_none()) throw Error("callback transport needs callbacks");
-      py::dict cb = callbacks.cast<py::dict>();
-      CallbackFns f;
-      // callables may be released from a thread that does not hold the GIL (close() releases it)
-      auto keep = [](py::object o) {
-        return std::shared_ptr<py::object>(new py::object(std::move(o)), [](py::object* q) {
-          py::gil_scoped_acquire g;
-          delete q;
-        });
-      };
-      // keep the Python callables alive inside the std::functions; re-acquire the GIL, run()
-      // releases it.
-      auto ex = keep(cb["exchange"]);
-      f.exchange = [ex](int b) {
-        py::gil_scoped_acquire g;
-        (*ex)(b);
-      };
-      if (cb.contains("allreduce_sum")) {
-        auto ar = keep(cb["allreduce_sum"]);
-        f.allreduce_sum = [ar](double v) {
-          py::gil_scoped_acquire g;
-          return (*ar)(v).cast<double>();
-        };
-      }
-      if (cb.contains("allreduce_max")) {
-        auto am = keep(cb["allreduce_max"]);
-        f.allreduce_max = [am](double v) {
-          py::gil_scoped_acquire g;
-          return (*am)(v).cast<double>();
-        };
-      }
-      if (cb.contains("barrier")) {
-        auto ba = keep(cb["barrier"]);
-        f.barrier = [ba]() {
-          py::gil_scoped_acquire g;
-          (*ba)();
-        };
-      }
+      CallbackFns f = callback_fns(callbacks);
+      if (!f.exchange) throw Error("callback transport needs an exchange callback");
       tr = make_callback_transport(std::move(f));
+    } else if (transport == "ipc") {
+      CallbackFns f = callback_fns(callbacks);
+      if (!f.allgather) throw Error("ipc transport needs an allgather callback");
+      tr = make_ipc_transport(std::move(f));
     } else {
-      throw Error("unknown transport '" + transport + "' (host|loopback|rccl|callback)");
+      throw Error("unknown transport '" + transport + "' (host|loopback|rccl|ipc|callback)");
     }
     SolverOptions o;
     o.overlap = overlap;
@@ -234,6 +256,7 @@ PYBIND11_MODULE(_mdfx, m) {
   py::register_exception<Error>(m, "MdfxError", PyExc_RuntimeError);
 
   m.def("hip_device_count", &hip_device_count);
+  m.def("hip_wait_error", &hip_wait_error, "1 after a device-side halo wait timed out");
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("set_kernel_variant", [](const std::string& v) { hip_set_kernel_variant(v.c_str()); });
   m.def("kernel_variant", []() { return std::string(hip_kernel_variant()); });

@@ -10,8 +10,10 @@ virtual            P slabs in this process: ``host`` (CPU memcpy) or ``loopback`
                    copies, possibly over several GPUs) — how multi-rank runs are tested on one GPU
 distributed        one slab per torch.distributed rank (torchrun / mpirun): ``rccl`` (native
                    ncclSend/ncclRecv on the engine's halo stream, unique id broadcast over the
-                   control group) or ``torch`` (torch.distributed p2p through a callback: gloo on
-                   CPU, nccl = RCCL on GPU)
+                   control group), ``ipc`` (native: faces pulled from the neighbours' buffers
+                   mapped through HIP IPC, ordered by device counters; any number of processes
+                   per GPU), or ``torch`` / ``staged`` (torch.distributed p2p through a callback:
+                   gloo on CPU, nccl = RCCL on GPU, or host-staged gloo)
 =================  ==============================================================================
 
 Reference parity: the reference's ``main`` (MDF_kernel.cu:101-236 / kernel.cu:148-283) is this
@@ -30,7 +32,7 @@ from ._native import hip_available, native
 from .models import InitCondition, Problem
 from .ops import TORCH_DTYPE
 from .parallel.decomp import slab_bounds
-from .parallel.dist import TorchP2PTransport, broadcast_bytes, is_distributed
+from .parallel.dist import ControlPlane, TorchP2PTransport, broadcast_bytes, is_distributed
 
 
 def auto_temporal(problem: Problem, nranks: int, device: str) -> int:
@@ -53,7 +55,7 @@ class Simulation:
 
     Parameters: ``device`` hip | cpu | auto; ``ranks`` P virtual slabs in this process (default:
     one per distributed rank, or 1); ``devices`` GPU ids for the local slabs; ``transport`` auto |
-    rccl | torch | staged | loopback | host; ``overlap`` interior sweep concurrent with boundary
+    rccl | ipc | torch | staged | loopback | host; ``overlap`` interior sweep concurrent with boundary
     planes + exchange; ``sync_debug`` serialise every phase (race screen); ``residual_every`` k:
     global L2 norm of the update every k steps (NaN/Inf guard); ``graph`` replay two-sweep cycles
     as hipGraphs; ``timeout_s`` watchdog; ``temporal`` fused steps per sweep (1 = none, 0 = auto,
@@ -96,6 +98,11 @@ class Simulation:
                 uid = native().rccl_unique_id() if rank == 0 else None
                 uid = broadcast_bytes(uid, src=0, group=group)
                 args = dict(transport="rccl", unique_id=uid)
+            elif transport == "ipc":
+                if device != "hip":
+                    raise ValueError("ipc transport needs HIP devices")
+                torch.cuda.set_device(dev_list[0])
+                args = dict(transport="ipc", callbacks=ControlPlane(group).callbacks())
             elif transport in ("torch", "staged"):
                 p2p_group = group
                 staged = transport == "staged" and device == "hip"
@@ -106,7 +113,7 @@ class Simulation:
                 self._torch_transport = TorchP2PTransport(p2p_group, staged=staged)
                 args = dict(transport="callback", callbacks=self._torch_transport.callbacks())
             else:
-                raise ValueError("distributed transport must be rccl|torch|staged|auto")
+                raise ValueError("distributed transport must be rccl|ipc|torch|staged|auto")
         else:
             nranks = ranks or 1
             local_ranks = list(range(nranks))

@@ -67,6 +67,37 @@ def broadcast_bytes(data: Optional[bytes], src: int = 0, group=None) -> bytes:
     return obj[0]
 
 
+class ControlPlane:
+    """Host-side collectives for the native transports that move data on the device themselves
+    (``ipc``): the handle swap (allgather of byte strings), the residual all-reduce and barriers,
+    over a CPU (gloo) process group."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def callbacks(self) -> dict:
+        return {"allgather": self.allgather, "allreduce_sum": self.allreduce_sum,
+                "allreduce_max": self.allreduce_max, "barrier": self.barrier}
+
+    def allgather(self, mine: bytes) -> list:
+        out = [None] * dist.get_world_size(self.group)
+        dist.all_gather_object(out, bytes(mine), group=self.group)
+        return out
+
+    def allreduce_sum(self, v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return float(t.item())
+
+    def allreduce_max(self, v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def barrier(self) -> None:
+        dist.barrier(group=self.group)
+
+
 class TorchP2PTransport:
     """Halo exchange through torch.distributed point-to-point ops (callback transport).
 

@@ -17,16 +17,24 @@ def read_checkpoint(path: str) -> Tuple[np.ndarray, List[dict]]:
     """The dense global grid ``(nz, ny, nx)`` and the per-slab headers of a checkpoint directory.
 
     Only raw bytes and JSON are read (nothing is unpickled)."""
-    metas = []
-    for f in sorted(os.listdir(path)):
-        if f.startswith("slab_") and f.endswith(".json"):
-            with open(os.path.join(path, f)) as fh:
-                metas.append(json.load(fh))
-    if not metas:
-        raise FileNotFoundError("no slab_<r>.json headers in %s" % path)
-    m0 = metas[0]
+    def header(r):
+        f = os.path.join(path, "slab_%d.json" % r)
+        if not os.path.exists(f):
+            raise ValueError("checkpoint %s is incomplete: slab_%d.json is missing" % (path, r))
+        with open(f) as fh:
+            return json.load(fh)
+
+    if not os.path.exists(os.path.join(path, "slab_0.json")):
+        raise FileNotFoundError("no slab_0.json header in %s" % path)
+    m0 = header(0)
+    # slab_0 names the writer's rank count; files of an older save with more ranks are ignored
+    metas = [m0] + [header(r) for r in range(1, int(m0["nranks"]))]
     if any(m.get("format") != "mdfx-slab-v1" for m in metas):
         raise ValueError("not an mdfx-slab-v1 checkpoint")
+    for m in metas:
+        if m["nranks"] != m0["nranks"] or m["step"] != m0["step"]:
+            raise ValueError("slab %d (nranks %d, step %d) does not match slab_0 (nranks %d, step %d)"
+                             % (m["rank"], m["nranks"], m["step"], m0["nranks"], m0["step"]))
     dt = _DT[m0["dtype"]]
     grid = np.zeros((m0["nz"], m0["ny"], m0["nx"]), dtype=dt)
     covered = np.zeros(m0["nz"], dtype=bool)

@@ -365,3 +365,62 @@ def test_auto_temporal_rule(mdfx):
     assert auto_temporal(m.heat3d(n=64), 1, "cpu") == 1
     with m.Simulation(m.mdf2d(h=64, w=32), device="cpu", temporal=0) as sim:
         assert sim.temporal == 1  # the CPU never fuses by default
+
+
+def test_checkpoint_stale_slabs_ignored(mdfx, tmp_path):
+    """Saving with 4 ranks, then with 2 ranks into the same directory: both readers return the
+    2-rank state (the extra slab_2 / slab_3 files are removed, and readers trust slab_0's nranks)."""
+    import mpi_cuda_process_amd as m
+    from mpi_cuda_process_amd.utils.checkpoint import read_checkpoint
+
+    prob = m.heat3d(nx=12, ny=9, nz=16)
+    d = str(tmp_path / "ck")
+    with m.Simulation(prob, device="cpu", ranks=4) as s4:
+        s4.init()
+        s4.run(1)
+        s4.save_checkpoint(d)
+    with m.Simulation(prob, device="cpu", ranks=2) as s2:
+        s2.init()
+        s2.run(5)
+        want = s2.gather()
+        s2.save_checkpoint(d)
+    assert sorted(f for f in os.listdir(d) if f.endswith(".json")) == ["slab_0.json", "slab_1.json"]
+    grid, metas = read_checkpoint(d)
+    assert np.array_equal(grid, want) and {mm["step"] for mm in metas} == {5}
+    with m.Simulation(prob, device="cpu", ranks=3) as s3:
+        s3.load_checkpoint(d)
+        assert np.array_equal(s3.gather(), want) and s3.steps == 5
+
+
+def test_checkpoint_mixed_steps_rejected(mdfx, tmp_path):
+    import json as _json
+
+    import mpi_cuda_process_amd as m
+
+    prob = m.heat3d(nx=10, ny=8, nz=12)
+    d = str(tmp_path / "ck")
+    with m.Simulation(prob, device="cpu", ranks=2) as s:
+        s.init()
+        s.run(2)
+        s.save_checkpoint(d)
+    h = _json.load(open(os.path.join(d, "slab_1.json")))
+    h["step"] = 7
+    _json.dump(h, open(os.path.join(d, "slab_1.json"), "w"))
+    with m.Simulation(prob, device="cpu", ranks=2) as s:
+        with pytest.raises(RuntimeError, match="does not match slab_0"):
+            s.load_checkpoint(d)
+
+
+def test_graph_request_with_host_transport_runs_eagerly(mdfx):
+    """graph=True with a transport whose exchange moves data on the host falls back to eager steps
+    (same result as graph=False)."""
+    import mpi_cuda_process_amd as m
+
+    prob = m.heat3d(nx=14, ny=10, nz=12)
+    outs = []
+    for g in (False, True):
+        with m.Simulation(prob, device="cpu", ranks=3, graph=g) as s:
+            s.init()
+            s.run(6)
+            outs.append(s.gather())
+    assert np.array_equal(outs[0], outs[1])

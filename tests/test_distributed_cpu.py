@@ -108,3 +108,42 @@ def test_bench_multiprocess_cpu_json(mdfx, tmp_path):
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in rec
     assert rec["steps"] == 2 and rec["value"] > 0 and rec["config"]["grid"] == [24, 24, 24]
+
+
+def _bench(args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MDFX_FORCE_DIST")}
+    env.update(OMP_NUM_THREADS="2", **(env_extra or {}))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       timeout=timeout)
+    return p.returncode, p.stdout.decode(), p.stderr.decode()
+
+
+def test_bench_self_launches_ranks_cpu(mdfx):
+    """--gpus N with no launcher environment spawns N ranks itself (never a silent 1-rank run),
+    gates the decomposed engine bitwise against a full-grid run, and reports n_gpus = N."""
+    import json
+
+    rc, out, err = _bench(["--device", "cpu", "--gpus", "3", "--n", "32", "--steps", "2", "--warmup", "1"])
+    assert rc == 0, err
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 3 and rec["config"]["ranks"] == 3
+    gate = rec["config"]["gate"]
+    assert gate["passed"] and gate["transport"] == "torch" and gate["grid"][2] % 3 == 0
+
+
+def test_bench_refuses_more_gpus_than_visible(mdfx):
+    """No GPU here: asking for 2 HIP ranks fails fast instead of running on fewer devices."""
+    rc, out, err = _bench(["--device", "hip", "--gpus", "2", "--n", "32", "--steps", "1"], timeout=120)
+    assert rc != 0 and "GPU" in err and not [l for l in out.splitlines() if l.startswith("{")]
+
+
+def test_bench_gate_catches_a_broken_rank(mdfx):
+    """A NaN injected into rank 1 during the gate run makes the gate fail on every rank and the
+    bench exit non-zero without printing a number."""
+    rc, out, err = _bench(["--device", "cpu", "--gpus", "2", "--n", "32", "--steps", "2", "--warmup", "1"],
+                          env_extra={"MDFX_FAULT": "nan@1:2"})
+    assert rc != 0, out
+    assert "gate FAILED" in err or "gate" in err
+    assert not [l for l in out.splitlines() if l.startswith("{")]

@@ -1,0 +1,168 @@
+"""Device-resident multi-process halo exchange on ONE GPU: 2-3 processes (one slab each) share
+cuda:0 and pull their neighbours' faces through HIP IPC mappings, ordered by device-side counters
+(csrc/comm/ipc_transport.cpp). No host staging: the faces move device-to-device on the copy
+engines, exactly as across GPUs. Plus the watchdog escalation (a spinning device kernel or a dead
+peer ends in a non-zero exit, not a hang) and bench.py's own multi-process launch + gate.
+
+Reference parity: the rank-pair halo exchange of MDF_kernel.cu:166-172,180-183 / kernel.cu:214-216,
+228-230, which in the reference deadlocks."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r"""
+import os, sys, json
+sys.path.insert(0, %(root)r)
+import numpy as np
+import torch, torch.distributed as dist
+import mpi_cuda_process_amd as m
+from mpi_cuda_process_amd.parallel.dist import init_distributed
+env = init_distributed("gloo")
+torch.cuda.set_device(0)
+prob = %(prob)s
+with m.Simulation(prob, device="hip", distributed=True, transport="ipc", residual_every=4,
+                  temporal=%(temporal)d, devices=[0], graph=%(graph)s, timeout_s=60.0) as sim:
+    assert sim.transport == "ipc", sim.transport
+    sim.init()
+    sim.run(%(steps)d)
+    sim.synchronize()
+    g = sim.gather()
+    if env.rank == 0:
+        np.save(%(out)r, g)
+        json.dump({"residual": sim.residual, "nranks": sim.nranks}, open(%(out)r + ".json", "w"))
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(world, argv_of, env_extra=None, timeout=180, expect_ok=True):
+    port = _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env.update(env_extra or {})
+        procs.append(subprocess.Popen(argv_of(r), env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      cwd=ROOT))
+    outs = []
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=timeout)
+            outs.append(o.decode())
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    if expect_ok:
+        for p, o in zip(procs, outs):
+            assert p.returncode == 0, o
+    return procs, outs
+
+
+def _reference(prob, steps, temporal=1):
+    import mpi_cuda_process_amd as m
+
+    with m.Simulation(prob, device="hip", residual_every=4, temporal=temporal) as sim:
+        sim.init()
+        sim.run(steps)
+        return sim.gather(), sim.residual
+
+
+@pytest.mark.parametrize("world,temporal,graph", [(2, 1, False), (3, 1, False), (2, 2, False), (3, 2, False),
+                                                  (3, 2, True)])
+def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
+    import mpi_cuda_process_amd as m
+
+    prob_src = "m.heat3d(nx=256, ny=40, nz=47)"
+    out = str(tmp_path / "g.npy")
+    steps = 13
+    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps)
+    _spawn(world, lambda r: [sys.executable, "-c", code])
+    got = np.load(out)
+    ref, rres = _reference(eval(prob_src), steps)
+    assert np.array_equal(got, ref)
+    meta = json.load(open(out + ".json"))
+    assert meta["nranks"] == world and abs(meta["residual"] - rres) <= 1e-9 * rres
+
+
+@pytest.mark.parametrize("prob_src", ["m.mdf2d(h=203, w=300)", "m.life2d(h=150, w=257)",
+                                      "m.box27(nx=130, ny=33, nz=40, dtype='f64')"])
+def test_ipc_other_stencils(hip, tmp_path, prob_src):
+    import mpi_cuda_process_amd as m
+
+    out = str(tmp_path / "g.npy")
+    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=9)
+    _spawn(3, lambda r: [sys.executable, "-c", code])
+    ref, _ = _reference(eval(prob_src), 9)
+    assert np.array_equal(np.load(out), ref)
+
+
+def test_bench_self_launch_ipc_one_gpu(hip):
+    """bench.py --gpus 2 with no launcher on a 1-GPU box: refused unless --share-gpu; with it, two
+    ranks share cuda:0 over the ipc transport, pass the bitwise gate and report n_gpus = 2."""
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--n", "256", "--steps", "4", "--warmup", "2"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    import torch
+
+    if torch.cuda.device_count() == 1:
+        t0 = time.time()
+        p = subprocess.run(base + ["--gpus", "2"], env=env, capture_output=True, timeout=120, cwd=ROOT)
+        assert p.returncode != 0 and time.time() - t0 < 60 and b"GPU" in p.stderr
+    p = subprocess.run(base + ["--gpus", "2", "--share-gpu", "--transport", "ipc"], env=env, capture_output=True,
+                       timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    lines = [l for l in p.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["transport"] == "ipc" and rec["config"]["gate"]["passed"]
+    assert rec["config"]["distinct_devices"] == 1
+
+
+def test_watchdog_turns_a_spinning_kernel_into_an_exit(hip):
+    """MDFX_FAULT=spin: a device kernel stops making progress (it would spin for 60 s). With a 5 s
+    watchdog the process reports it and exits non-zero well before the kernel's own bound."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import mpi_cuda_process_amd as m\n"
+            "sim = m.Simulation(m.heat3d(n=64), device='hip', timeout_s=5.0)\n"
+            "sim.init(); sim.run(8); sim.synchronize()\n" % ROOT)
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, MDFX_FAULT="spin@0:3"),
+                       capture_output=True, timeout=120)
+    el = time.time() - t0
+    err = p.stderr.decode()
+    assert p.returncode != 0 and "watchdog" in err, err[-2000:]
+    assert el < 40, el
+
+
+def test_ipc_dead_peer_is_an_error_not_a_hang(hip, tmp_path):
+    """Rank 1 dies mid-run: rank 0's device wait times out, raises the error word, and the engine
+    reports a transport failure and exits non-zero instead of hanging."""
+    out = str(tmp_path / "g.npy")
+    code = WORKER.replace("timeout_s=60.0", "timeout_s=5.0") % dict(
+        root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=40)
+    t0 = time.time()
+    procs, outs = _spawn(2, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_FAULT": "exit@1:3"},
+                         timeout=150, expect_ok=False)
+    assert procs[1].returncode == 42
+    assert procs[0].returncode != 0, outs[0]
+    assert time.time() - t0 < 120

@@ -27,6 +27,9 @@ def test_native_unit_tests_cpu():
 
 
 def test_native_unit_tests_asan_ubsan():
+    if not os.path.exists(os.path.join(BIN, "mdfx_tests_asan")):  # not part of the default build
+        subprocess.run(["make", "-C", ROOT, "-j8", "asan"], check=True, timeout=1500,
+                       stdout=subprocess.DEVNULL)
     out = _run("mdfx_tests_asan", {"ASAN_OPTIONS": "detect_leaks=0:abort_on_error=1",
                                    "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
     assert "all passed" in out and "runtime error" not in out
@@ -52,7 +55,7 @@ def test_native_device_checks_on_gpu(hip):
     allocation. Violations are counted on the device, not trapped, so this cannot fault the GPU."""
     exe = os.path.join(BIN, "mdfx_tests_devcheck")
     if not os.path.exists(exe):
-        pytest.fail("mdfx_tests_devcheck is not built (make -j8 all)")
+        pytest.fail("mdfx_tests_devcheck is not built (make -j8 devcheck, on the CPU before the GPU run)")
     p = subprocess.run([exe], stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=900)
     out = p.stdout.decode() + p.stderr.decode()
     assert p.returncode == 0, out[-4000:]
