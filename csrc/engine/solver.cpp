@@ -462,8 +462,13 @@ void Solver::run(int64_t steps) {
     const bool res = (to_res == k);
     // graph replay for plain (non-residual, non-debug) stretches of >= 2 sweeps, when the
     // transport's exchange is pure stream work (rccl, loopback, ipc; the callback / host / tcp
-    // transports move data on the host and always run eagerly).
-    if (opt_.graph && hip && !res && !opt_.sync_debug && !opt_.profile && transport_->graph_capturable()) {
+    // transports move data on the host and always run eagerly). One slab per process (the
+    // production layout): the ROCm 7.0 HIP runtime bundled with PyTorch segfaults in
+    // hipStreamEndCapture on the 3-slab loopback capture (6 streams with cross-slab event waits;
+    // the same capture replays correctly under ROCm 7.2, csrc/tests/test_main.cpp test_graph), so
+    // several slabs in one process run eagerly.
+    if (opt_.graph && hip && !res && !opt_.sync_debug && !opt_.profile && transport_->graph_capturable() &&
+        slabs_.size() == 1) {
       const int64_t plain = std::min<int64_t>(steps - done, to_res - 1);
       const int64_t pairs = fault().rank >= 0 ? 0 : plain / (2 * k);
       if (pairs > 0) {

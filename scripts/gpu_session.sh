@@ -40,6 +40,11 @@ for s in "$@"; do
     prof) (cd /tmp && export TMPDIR=/tmp && run_dir="$R" && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
             --output-format csv -d "$R/gpurun_out/prof" -o bench -- python "$R/bench.py" --steps 20 --warmup 5 \
             > "$R/gpurun_out/prof.log" 2>&1); rc=$?; echo "== prof rc=$rc"; [[ $rc -le 1 ]] || exit $rc ;;
+    pmc_fetch|pmc_write)  # one counter per pass (FETCH_SIZE and WRITE_SIZE cannot share one)
+      ctr=$([[ $s == pmc_fetch ]] && echo FETCH_SIZE || echo WRITE_SIZE)
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
+          -d "$R/gpurun_out/$s" -o run -- python3 "$R/bench.py" --steps 6 --warmup 2 ${BENCH_ARGS:-} \
+          > "$R/gpurun_out/$s.log" 2>&1); rc=$?; echo "== $s rc=$rc"; tail -2 "gpurun_out/$s.log"; [[ $rc -le 1 ]] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
