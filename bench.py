@@ -80,9 +80,20 @@ def parse(argv=None):
                         "transport and exits non-zero")
     p.add_argument("--gate-n", type=int, default=0, help="edge of the correctness-gate grid (0 = auto)")
     p.add_argument("--no-gate", action="store_true", help="skip the N > 1 correctness gate")
+    p.add_argument("--verbose", action="store_true", help="per-rank phase trace on stderr")
     p.add_argument("--share-gpu", action="store_true",
                    help="allow more ranks than GPUs (processes share devices; tests of the ipc/staged paths)")
     return p.parse_args(argv)
+
+
+_T0 = time.time()
+_VERBOSE = False
+
+
+def trace(msg):
+    if _VERBOSE:
+        print("[bench rank %s +%.2fs] %s" % (os.environ.get("RANK", "0"), time.time() - _T0, msg),
+              file=sys.stderr, flush=True)
 
 
 def launched() -> bool:
@@ -189,9 +200,12 @@ def run_gate(a, hip, transport, temporal, world, rank):
     ok = False
     try:
         with Simulation(prob, distributed=True, transport=transport, **kw) as sim:
+            trace("gate: engine up")
             sim.init()
             sim.run(steps)
+            trace("gate: steps enqueued")
             sim.synchronize()
+            trace("gate: steps done")
             mine = sim.read_local(0)
             res = sim.residual
             lay = sim.layout(0)
@@ -220,6 +234,8 @@ def run_gate(a, hip, transport, temporal, world, rank):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
+    global _VERBOSE
+    _VERBOSE = a.verbose
     if a.gpus > 1 and not launched() and not os.environ.get("MDFX_FORCE_DIST"):
         return self_launch(a, argv)
 
@@ -270,7 +286,9 @@ def main(argv=None):
             gates = []
             chosen = None
             for t in candidates:
+                trace("gate %s" % t)
                 passed, rec = run_gate(a, hip, t, temporal, world, rank)
+                trace("gate %s passed=%s" % (t, passed))
                 gates.append(rec)
                 if passed:
                     chosen = t
@@ -297,7 +315,9 @@ def main(argv=None):
         vr = a.virtual_ranks or 1
         sim = Simulation(prob, ranks=vr, distributed=False,
                          transport=transport if transport in ("loopback", "host") else "auto", **kw)
+    trace("engine up (%s)" % sim.transport)
     sim.init()
+    trace("init done")
 
     def barrier():
         if env:
@@ -309,7 +329,9 @@ def main(argv=None):
             torch.cuda.synchronize()
 
     sim.run(a.warmup)
+    trace("warmup enqueued")
     sync()
+    trace("warmup done")
     best = None
     for _ in range(max(1, a.repeats)):
         barrier()
@@ -325,6 +347,7 @@ def main(argv=None):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         best = dt if best is None else min(best, dt)
+        trace("timed %.4f s" % dt)
 
     devices = [device_id]
     if env:

@@ -1,6 +1,6 @@
-// HIP-IPC halo transport: one process per slab, faces pulled straight out of the neighbour's
-// device buffers (mapped with hipIpcOpenMemHandle) by the copy engines, ordered by device-side
-// counters instead of host synchronisation.
+// HIP-IPC halo transport: one process per slab; each process publishes its boundary faces in a
+// small exported "mailbox" allocation, and the neighbours pull them straight into their ghost
+// planes with the copy engines, ordered by device-side counters instead of host synchronisation.
 //
 // Why a second device-resident transport next to RCCL: RCCL's p2p send/recv runs as kernels that
 // occupy CUs the interior sweep wants, and RCCL refuses two ranks on one GPU. A pull through the
@@ -8,20 +8,27 @@
 // one-wave counter kernel, and works for any number of processes sharing a device — which is how
 // the device-resident multi-process path is tested on a one-GPU box (tests/test_gpu_ipc.py).
 //
+// Why mailboxes instead of mapping the neighbours' whole field buffers: only the faces ever cross
+// a process boundary, and the HIP runtime PyTorch bundles (ROCm 7.0) stalls forever in
+// hipIpcOpenMemHandle on an exported hipMalloc of 2 GiB or more (scripts/ipc_probe.py on one
+// MI355X: 1900 MiB maps at once, 2048 MiB and 2 GiB + 16 MiB stall with torch's runtime loaded,
+// and the same 2 GiB + 16 MiB maps at once under /opt/rocm 7.2's) — the field buffer of a 1024^3
+// fp32 slab at N = 2 is 2 GiB + 16 MiB. A mailbox holds 2 parities x 2 sides x
+// `halo` planes (32 MiB at 1024^2 fp32, K = 2); publishing costs one local D2D copy per face.
+//
 // Protocol for exchange e (every process calls exchange() the same number of times; e = 1, 2, ..)
 // on the slab's halo stream, after the boundary kernels that wrote the faces of buffer b:
 //
-//   signal(ready)                                   faces of b published
-//   for each neighbour n:  wait(n.ready >= e)        n's faces of b published
-//                          copy n.face(b) -> my ghost(b)
-//                          signal(pulled[side])      I am done reading n's buffer b
-//   for each neighbour n:  wait(n.pulled[mine] >= e-1)
+//   for each neighbour n:  wait(n.pulled[mine] >= e - 2)   n is done with mailbox slot b (exchange e-2)
+//   copy my faces of b -> mailbox[b][side]               (local)
+//   signal(ready)                                        exchange e published
+//   for each neighbour n:  wait(n.ready >= e)
+//                          copy n.mailbox[b][other side] -> my ghost(b)
+//                          signal(pulled[side])
 //
-// The last wait keeps the next boundary kernel (which rewrites the faces of buffer 1-b, sent in
-// exchange e-1) from overwriting faces a neighbour has not pulled yet; `pulled` starts at 1 so the
-// first exchange needs no special case. All counters live in device memory (private `expect`
-// counters advance inside the wait kernel), so the enqueued work is identical for every exchange
-// and a captured hipGraph replays correctly.
+// `pulled` starts at 2 so the first two exchanges need no special case. All counters live in
+// device memory (private `expect` counters advance inside the wait kernel), so the enqueued work is
+// identical for every exchange and a captured hipGraph replays correctly.
 //
 // Reference parity: the per-element host-staged MPI_Send/MPI_Recv loops of
 // MDF_kernel.cu:167-169,180-183 (D5, D12) with their rank-1 self-addressing (D3).
@@ -53,8 +60,8 @@ constexpr size_t kCounterBytes = 128 * 8;
 struct IpcRecord {
   char magic[8];
   int32_t rank = -1, device = -1, pid = 0, pad = 0;
-  uint64_t bytes = 0;  // per field buffer
-  hipIpcMemHandle_t buf[2];
+  uint64_t face_bytes = 0;  // one face (halo planes); the mailbox holds 4
+  hipIpcMemHandle_t mbox;
   hipIpcMemHandle_t ctr;
 };
 
@@ -67,10 +74,10 @@ class IpcTransport final : public Transport {
     if (!dev_ok_) return;
     (void)hipSetDevice(self_.be->device());
     for (auto& p : peers_) {
-      for (void* q : p.buf)
-        if (q) (void)hipIpcCloseMemHandle(q);
+      if (p.mbox) (void)hipIpcCloseMemHandle(p.mbox);
       if (p.ctr) (void)hipIpcCloseMemHandle(p.ctr);
     }
+    if (mbox_) (void)hipFree(mbox_);
     hip_free_uncached(ctr_);
   }
   const char* name() const override { return "ipc"; }
@@ -85,20 +92,23 @@ class IpcTransport final : public Transport {
     MDFX_CHECK(self_.be->kind() == DeviceKind::HIP, "ipc transport needs a HIP backend");
     self_.be->activate();
     ctr_ = (uint64_t*)hip_alloc_uncached(kCounterBytes);
-    const uint64_t one = 1;
-    HIPC(hipMemcpy(ctr_ + kPulled + 0, &one, 8, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(ctr_ + kPulled + 1, &one, 8, hipMemcpyHostToDevice));
-    HIPC(hipDeviceSynchronize());
+    const uint64_t two = 2;  // exchanges 1 and 2 find their mailbox slot free
+    HIPC(hipMemcpy(ctr_ + kPulled + 0, &two, 8, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(ctr_ + kPulled + 1, &two, 8, hipMemcpyHostToDevice));
     dev_ok_ = true;
+    // every face has the same size (halo planes of one field layout)
+    face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
+    HIPC(hipMalloc(&mbox_, 4 * face_));
+    HIPC(hipMemset(mbox_, 0, 4 * face_));
+    HIPC(hipDeviceSynchronize());
 
     IpcRecord mine;
-    std::memcpy(mine.magic, "MDFXIPC1", 8);
+    std::memcpy(mine.magic, "MDFXIPC2", 8);
     mine.rank = self_.rank;
     mine.device = self_.be->device();
     mine.pid = (int32_t)::getpid();
-    mine.bytes = self_.lay.bytes();
-    HIPC(hipIpcGetMemHandle(&mine.buf[0], self_.buf[0]));
-    HIPC(hipIpcGetMemHandle(&mine.buf[1], self_.buf[1]));
+    mine.face_bytes = face_;
+    HIPC(hipIpcGetMemHandle(&mine.mbox, mbox_));
     HIPC(hipIpcGetMemHandle(&mine.ctr, ctr_));
     const std::vector<std::string> all =
         f_.allgather(std::string((const char*)&mine, sizeof(mine)));  // also the setup barrier
@@ -112,41 +122,40 @@ class IpcTransport final : public Transport {
       IpcRecord r;
       MDFX_CHECK(all[p.rank].size() == sizeof(IpcRecord), "ipc: malformed handle record");
       std::memcpy(&r, all[p.rank].data(), sizeof(r));
-      MDFX_CHECK(std::memcmp(r.magic, "MDFXIPC1", 8) == 0 && r.rank == p.rank, "ipc: handle record mismatch");
+      MDFX_CHECK(std::memcmp(r.magic, "MDFXIPC2", 8) == 0 && r.rank == p.rank, "ipc: handle record mismatch");
       MDFX_CHECK(r.pid != mine.pid, "ipc transport: neighbouring slabs must live in different processes");
-      for (int b = 0; b < 2; ++b)
-        HIPC(hipIpcOpenMemHandle(&p.buf[b], r.buf[b], hipIpcMemLazyEnablePeerAccess));
+      MDFX_CHECK(r.face_bytes == face_, "ipc: neighbour face size does not match this slab's");
+      HIPC(hipIpcOpenMemHandle(&p.mbox, r.mbox, hipIpcMemLazyEnablePeerAccess));
       HIPC(hipIpcOpenMemHandle(&p.ctr, r.ctr, hipIpcMemLazyEnablePeerAccess));
       p.device = r.device;
-      // the neighbour's slab, addressed through the mapped buffers
-      p.slab.rank = p.rank;
-      p.slab.lay = FieldLayout::make(self_.lay.global, dec.z0(p.rank), dec.z1(p.rank), self_.lay.halo, self_.lay.dtype);
-      MDFX_CHECK(p.slab.lay.bytes() == r.bytes, "ipc: neighbour buffer size does not match its layout");
-      p.slab.buf[0] = p.buf[0];
-      p.slab.buf[1] = p.buf[1];
     }
     f_.barrier ? f_.barrier() : (void)f_.allgather("");
   }
 
+  // mailbox slot of buffer parity b, side s (0 = lo, 1 = hi), in a process's mailbox
+  char* slot(void* mbox, int b, int s) const { return (char*)mbox + (size_t)(2 * b + s) * face_; }
+
   void exchange(int b) override {
     self_.be->activate();
-    void* hs = self_.halo_stream;
-    hip_counter_signal(ctr_ + kReady, hs);
+    hipStream_t hs = (hipStream_t)self_.halo_stream;
+    // publish: the neighbour on `side` must be done with slot b (exchange e-2) before it is reused
     for (int side = 0; side < 2; ++side) {
       const Peer& p = peers_[side];
       if (p.rank < 0) continue;
       const HaloSpan mine = halo_span(self_, b, side, nranks_);
-      const HaloSpan theirs = halo_span(p.slab, b, 1 - side, nranks_);
-      MDFX_CHECK(mine.bytes == theirs.bytes && mine.peer == p.rank, "ipc: face geometry mismatch");
-      hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs);
-      HIPC(hipMemcpyAsync(mine.recv, theirs.send, mine.bytes, hipMemcpyDeviceToDevice, (hipStream_t)hs));
-      hip_counter_signal(ctr_ + kPulled + side, hs);
+      MDFX_CHECK(mine.bytes == face_ && mine.peer == p.rank, "ipc: face geometry mismatch");
+      hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs);
+      HIPC(hipMemcpyAsync(slot(mbox_, b, side), mine.send, face_, hipMemcpyDeviceToDevice, hs));
     }
+    hip_counter_signal(ctr_ + kReady, hs);
+    // pull: the neighbour on `side` published its (1 - side) face of exchange e
     for (int side = 0; side < 2; ++side) {
       const Peer& p = peers_[side];
       if (p.rank < 0) continue;
-      // the neighbour on `side` pulls from me as its (1 - side) neighbour
-      hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs);
+      const HaloSpan mine = halo_span(self_, b, side, nranks_);
+      hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs);
+      HIPC(hipMemcpyAsync(mine.recv, slot(p.mbox, b, 1 - side), face_, hipMemcpyDeviceToDevice, hs));
+      hip_counter_signal(ctr_ + kPulled + side, hs);
     }
   }
 
@@ -166,14 +175,15 @@ class IpcTransport final : public Transport {
   struct Peer {
     int rank = -1;
     int device = -1;
-    void* buf[2] = {nullptr, nullptr};
+    void* mbox = nullptr;
     void* ctr = nullptr;
-    LocalSlab slab;
   };
   CallbackFns f_;
   LocalSlab self_;
   int nranks_ = 1;
   uint64_t* ctr_ = nullptr;
+  void* mbox_ = nullptr;
+  size_t face_ = 0;
   bool dev_ok_ = false;
   Peer peers_[2];
   double timeout_s_ = 300.0;

@@ -80,6 +80,8 @@ class Simulation:
         self.group = group
 
         if self.distributed:
+            if transport in ("rccl", "ipc") and device != "hip":
+                raise ValueError("%s transport needs HIP devices" % transport)
             world = dist.get_world_size(group)
             rank = dist.get_rank(group)
             nranks, local_ranks = world, [rank]

@@ -5,7 +5,8 @@
 # (gpurun rules: no further GPU work after a fault, no retries).
 #
 #   scripts/gpu_session.sh <step> [<step> ...]     steps: native ipc gputests smoke bench bench_t1
-#                                                  bench_v8 prof pmc_fetch pmc_write
+#                                                  bench_v8 prof pmc_fetch pmc_write, or name=command
+#                                                  (limit $LIMIT s, default 300)
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -37,6 +38,10 @@ for s in "$@"; do
     bench) run 300 bench python bench.py ;;
     bench_t1) run 300 bench_t1 python bench.py --temporal 1 ;;
     bench_v8) run 300 bench_v8 python bench.py --virtual-ranks 8 ;;
+    bench_ipc2) run 300 bench_ipc2 python bench.py --gpus 2 --share-gpu --transport ipc ;;
+    bench_ipc4) run 300 bench_ipc4 python bench.py --gpus 4 --share-gpu --transport ipc ;;
+    bench_refuse) run 120 bench_refuse bash -c 'python bench.py --gpus 2 --n 256; test $? -eq 2' ;;  # must refuse
+    rccl2) run 150 rccl2 python bench.py --gpus 2 --share-gpu --transport rccl --n 256 --steps 4 --warmup 2 ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run_dir="$R" && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
             --output-format csv -d "$R/gpurun_out/prof" -o bench -- python "$R/bench.py" --steps 20 --warmup 5 \
             > "$R/gpurun_out/prof.log" 2>&1); rc=$?; echo "== prof rc=$rc"; [[ $rc -le 1 ]] || exit $rc ;;
@@ -45,6 +50,7 @@ for s in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
           -d "$R/gpurun_out/$s" -o run -- python3 "$R/bench.py" --steps 6 --warmup 2 ${BENCH_ARGS:-} \
           > "$R/gpurun_out/$s.log" 2>&1); rc=$?; echo "== $s rc=$rc"; tail -2 "gpurun_out/$s.log"; [[ $rc -le 1 ]] || exit $rc ;;
+    *=*) run "${LIMIT:-300}" "${s%%=*}" bash -c "${s#*=}" ;;  # ad-hoc step: name=command
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -147,3 +147,53 @@ def test_bench_gate_catches_a_broken_rank(mdfx):
     assert rc != 0, out
     assert "gate FAILED" in err or "gate" in err
     assert not [l for l in out.splitlines() if l.startswith("{")]
+
+
+CONTROL = r"""
+import os, sys, json, struct
+sys.path.insert(0, %(root)r)
+import torch.distributed as dist
+from mpi_cuda_process_amd.parallel.dist import init_distributed, ControlPlane
+env = init_distributed("gloo")
+cp = ControlPlane()
+cb = cp.callbacks()
+# an IpcRecord-shaped byte string: magic, ints, embedded NULs, two 64-byte handles
+rec = b"MDFXIPC2" + struct.pack("<iiiiQ", env.rank, 0, 1000 + env.rank, 0, 8 << 20) + bytes(64) + bytes([env.rank]) * 64
+allr = cb["allgather"](rec)
+ok = [len(x) == len(rec) and struct.unpack("<i", x[8:12])[0] == r and x[-1] == r for r, x in enumerate(allr)]
+s = cb["allreduce_sum"](float(env.rank + 1))
+mx = cb["allreduce_max"](float(env.rank))
+cb["barrier"]()
+json.dump({"ok": all(ok) and len(allr) == env.world, "sum": s, "max": mx}, open(%(out)r + str(env.rank), "w"))
+dist.destroy_process_group()
+"""
+
+
+def test_ipc_control_plane_marshalling_cpu(mdfx, tmp_path):
+    """The ipc transport's host control plane (gloo): binary handle records with embedded NULs
+    come back from allgather intact and in rank order; the residual all-reduces and the barrier
+    work across 3 processes."""
+    import json
+
+    out = str(tmp_path / "cp")
+    port = _free_port()
+    procs = []
+    for r in range(3):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", CONTROL % dict(root=ROOT, out=out)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    for p in procs:
+        o, _ = p.communicate(timeout=120)
+        assert p.returncode == 0, o.decode()
+    for r in range(3):
+        rec = json.load(open(out + str(r)))
+        assert rec == {"ok": True, "sum": 6.0, "max": 2.0}
+
+
+def test_ipc_transport_needs_hip(mdfx):
+    import mpi_cuda_process_amd as m
+
+    with pytest.raises(ValueError, match="ipc"):
+        # distributed=True without a process group is refused before any native call
+        m.Simulation(m.heat3d(n=8), device="cpu", distributed=True, transport="ipc")

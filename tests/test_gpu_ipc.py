@@ -166,3 +166,16 @@ def test_ipc_dead_peer_is_an_error_not_a_hang(hip, tmp_path):
     assert procs[1].returncode == 42
     assert procs[0].returncode != 0, outs[0]
     assert time.time() - t0 < 120
+
+
+def test_ipc_slabs_larger_than_2gib(hip):
+    """1024^3 fp32 over 2 processes: each slab's field buffers are 2 GiB + 16 MiB. Mapping such a
+    buffer through HIP IPC stalls forever under the HIP runtime PyTorch bundles (scripts/
+    ipc_probe.py), so the transport exports only small face mailboxes: this run must finish."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--transport",
+                        "ipc", "--n", "1024", "--steps", "4", "--warmup", "2", "--timeout", "30"],
+                       env=env, capture_output=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    rec = json.loads([l for l in p.stdout.decode().splitlines() if l.startswith("{")][0])
+    assert rec["n_gpus"] == 2 and rec["config"]["gate"]["passed"] and rec["config"]["transport"] == "ipc"

@@ -100,7 +100,7 @@ def test_bench_distributed_rccl_world1(hip):
 
 def test_bench_staged_two_processes(hip):
     outs = _spawn(2, lambda r: [sys.executable, os.path.join(ROOT, "bench.py"), "--n", "256", "--steps", "4",
-                                "--warmup", "2", "--gpus", "2", "--transport", "staged"],
+                                "--warmup", "2", "--gpus", "2", "--transport", "staged", "--share-gpu"],
                   env_extra={"HIP_VISIBLE_DEVICES": "0"})
     lines = [l for l in outs[0].splitlines() if l.startswith("{")]
     assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
