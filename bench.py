@@ -66,7 +66,10 @@ def parse(argv=None):
                    help="auto|rccl|ipc|torch|staged (distributed), loopback (1 process)")
     p.add_argument("--virtual-ranks", type=int, default=0,
                    help="split the grid into P slabs inside ONE process (loopback transport)")
-    p.add_argument("--graph", action="store_true", help="replay 2-step cycles as hipGraphs")
+    p.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                   help="replay 2-sweep cycles as hipGraphs; auto = gate and time both, keep the faster")
+    p.add_argument("--trial-steps", type=int, default=16,
+                   help="steps of each short timed trial that picks transport / graph mode (auto)")
     p.add_argument("--temporal", type=int, default=0,
                    help="time steps fused per memory sweep (temporal blocking); 0 = auto: 2 for the 3D "
                         "stencils, 8 (2D MDF) / 4 (Life) for the 2D ones, where a fused kernel exists")
@@ -179,9 +182,9 @@ def pick_temporal(a, prob, nslab, hip):
     return 1
 
 
-def run_gate(a, hip, transport, temporal, world, rank):
-    """Bitwise check of the decomposed engine (same transport, same fused depth) against a
-    full-grid single-slab run on this rank's own device. Returns (passed, record)."""
+def run_gate(a, hip, transport, temporal, world, rank, graph=False):
+    """Bitwise check of the decomposed engine (same transport, same fused depth, same graph mode)
+    against a full-grid single-slab run on this rank's own device. Returns (passed, record)."""
     import numpy as np
     import torch.distributed as dist
 
@@ -197,9 +200,10 @@ def run_gate(a, hip, transport, temporal, world, rank):
     kw = dict(device="hip" if hip else "cpu", temporal=temporal, residual_every=steps,
               timeout_s=a.timeout if hip else 0.0)
     err = ""
+    tag = transport + ("+graph" if graph else "")
     ok = False
     try:
-        with Simulation(prob, distributed=True, transport=transport, **kw) as sim:
+        with Simulation(prob, distributed=True, transport=transport, graph=graph, **kw) as sim:
             trace("gate: engine up")
             sim.init()
             sim.run(steps)
@@ -225,8 +229,8 @@ def run_gate(a, hip, transport, temporal, world, rank):
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     bad = int(t.item())
     if err:
-        print("bench gate [%s]: %s" % (transport, err), file=sys.stderr, flush=True)
-    rec = {"grid": [prob.nx, prob.ny, prob.nz], "steps": steps, "transport": transport,
+        print("bench gate [%s]: %s" % (tag, err), file=sys.stderr, flush=True)
+    rec = {"grid": [prob.nx, prob.ny, prob.nz], "steps": steps, "transport": transport, "graph": graph,
            "ranks_failed": bad, "passed": bad == 0}
     return bad == 0, rec
 
@@ -274,70 +278,59 @@ def main(argv=None):
     temporal = pick_temporal(a, prob, max(1, world, a.virtual_ranks), hip)
     timeout = a.timeout if hip else 0.0
 
-    # ---- transport (+ correctness gate for N > 1) ----------------------------------------
+    # ---- transport / graph mode: correctness gate (N > 1), then short timed trials ---------
+    # Every (transport, graph) candidate that passes the bitwise gate gets a short timed trial on
+    # the full problem; the fastest is timed for real. With one candidate there is no trial.
+    transports = [a.transport]
+    if env and a.transport == "auto":
+        transports = ["rccl", "ipc"] if hip else ["torch"]
+    elif not env:
+        transports = [a.transport if a.transport in ("loopback", "host") else "auto"]
+    graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True] if hip else [False])
+    cands = [(t, g) for t in transports for g in graphs]
     gate = None
-    transport = a.transport
-    if env:
-        if transport == "auto":
-            candidates = ["rccl", "ipc"] if hip else ["torch"]
-        else:
-            candidates = [transport]
-        if world > 1 and not a.no_gate:
-            gates = []
-            chosen = None
-            for t in candidates:
-                trace("gate %s" % t)
-                passed, rec = run_gate(a, hip, t, temporal, world, rank)
-                trace("gate %s passed=%s" % (t, passed))
-                gates.append(rec)
-                if passed:
-                    chosen = t
-                    break
-            gate = gates[-1] if chosen else {"passed": False, "tried": gates}
-            if chosen is None:
-                if rank == 0:
-                    print("bench: correctness gate FAILED for every transport tried (%s); not timing"
-                          % ", ".join(candidates), file=sys.stderr)
-                dist.barrier()
-                dist.destroy_process_group()
-                return 3
-            if len(gates) > 1:
-                gate["fell_back_from"] = [g["transport"] for g in gates[:-1]]
-            transport = chosen
-        else:
-            transport = candidates[0]
+    if env and world > 1 and not a.no_gate:
+        recs, ok = [], []
+        for t, g in cands:
+            if g and (t, False) in cands and (t, False) not in ok:
+                continue  # a transport whose eager run failed is not tried with graphs
+            trace("gate %s graph=%s" % (t, g))
+            passed, rec = run_gate(a, hip, t, temporal, world, rank, graph=g)
+            trace("gate %s graph=%s passed=%s" % (t, g, passed))
+            recs.append(rec)
+            if passed:
+                ok.append((t, g))
+        gate = {"passed": bool(ok), "runs": recs}
+        if not ok:
+            if rank == 0:
+                print("bench: correctness gate FAILED for every transport tried (%s); not timing"
+                      % ", ".join(sorted(set(t for t, _ in cands))), file=sys.stderr)
+            dist.barrier()
+            dist.destroy_process_group()
+            return 3
+        cands = ok
 
-    kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap, graph=a.graph,
+    kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap,
               residual_every=a.residual_every, timeout_s=timeout, temporal=temporal)
-    if env:
-        sim = Simulation(prob, distributed=True, transport=transport, **kw)
-    else:
-        vr = a.virtual_ranks or 1
-        sim = Simulation(prob, ranks=vr, distributed=False,
-                         transport=transport if transport in ("loopback", "host") else "auto", **kw)
-    trace("engine up (%s)" % sim.transport)
-    sim.init()
-    trace("init done")
+
+    def make_sim(transport, graph):
+        if env:
+            return Simulation(prob, distributed=True, transport=transport, graph=graph, **kw)
+        return Simulation(prob, ranks=a.virtual_ranks or 1, distributed=False, transport=transport, graph=graph, **kw)
 
     def barrier():
         if env:
             dist.barrier()
 
-    def sync():
-        sim.synchronize()
-        if hip:
-            torch.cuda.synchronize()
-
-    sim.run(a.warmup)
-    trace("warmup enqueued")
-    sync()
-    trace("warmup done")
-    best = None
-    for _ in range(max(1, a.repeats)):
+    def timed(sim, steps):
+        def sync():
+            sim.synchronize()
+            if hip:
+                torch.cuda.synchronize()
         barrier()
         sync()
         t0 = time.perf_counter()
-        sim.run(a.steps)
+        sim.run(steps)
         sync()
         t1 = time.perf_counter()
         barrier()
@@ -346,6 +339,43 @@ def main(argv=None):
             t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
+        return dt
+
+    trials = []
+    sim, sim_t = None, None
+    if len(cands) > 1:
+        n_trial = max(2, min(a.trial_steps, a.steps))
+        for t, g in cands:
+            if sim is not None and sim_t != t:
+                sim.close()
+                sim = None
+            if sim is None:
+                sim, sim_t = make_sim(t, g), t
+                sim.init()
+            sim.set_options(graph=g)
+            sim.run(max(2, min(a.warmup, 4)))
+            dt = timed(sim, n_trial)
+            trace("trial %s graph=%s: %.3f ms/step" % (t, g, dt / n_trial * 1e3))
+            trials.append({"transport": sim.transport, "graph": g, "ms_per_step": round(dt / n_trial * 1e3, 4)})
+        chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
+        if sim_t != chosen[0]:
+            sim.close()
+            sim = None
+    else:
+        chosen = cands[0]
+    if sim is None:
+        sim = make_sim(*chosen)
+    sim.set_options(graph=chosen[1])
+    trace("engine up (%s, graph=%s)" % (sim.transport, chosen[1]))
+    sim.init()  # every timed run starts from the same initial grid
+    trace("init done")
+    sim.run(a.warmup)
+    trace("warmup enqueued")
+    timed(sim, 0)
+    trace("warmup done")
+    best = None
+    for _ in range(max(1, a.repeats)):
+        dt = timed(sim, a.steps)
         best = dt if best is None else min(best, dt)
         trace("timed %.4f s" % dt)
 
@@ -395,7 +425,8 @@ def main(argv=None):
                 "transport": sim_transport,
                 "comm_size": nproc if sim_transport == "rccl" else 0,
                 "kernel_variant": native().kernel_variant(),
-                "graph": a.graph,
+                "graph": chosen[1],
+                "trials": trials,
                 "overlap": not a.no_overlap,
                 "temporal_block": temporal,
                 "gate": gate,

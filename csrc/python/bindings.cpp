@@ -376,19 +376,34 @@ PYBIND11_MODULE(_mdfx, m) {
              p.chk().exchange_ghosts();
            })
       .def("set_options",
-           [](PySolver& p, bool overlap, bool sync_debug, int residual_every, bool graph,
-              double timeout_s, bool profile) {
+           [](PySolver& p, py::kwargs kw) {
+             // only the options named change; the rest keep their current values
              SolverOptions o = p.chk().options();
-             o.profile = profile;
-             o.overlap = overlap;
-             o.sync_debug = sync_debug;
-             o.residual_every = residual_every;
-             o.graph = graph;
-             o.timeout_s = timeout_s;
+             for (auto item : kw) {
+               const std::string k = py::str(item.first);
+               if (k == "overlap") o.overlap = item.second.cast<bool>();
+               else if (k == "sync_debug") o.sync_debug = item.second.cast<bool>();
+               else if (k == "residual_every") o.residual_every = item.second.cast<int>();
+               else if (k == "graph") o.graph = item.second.cast<bool>();
+               else if (k == "timeout_s") o.timeout_s = item.second.cast<double>();
+               else if (k == "profile") o.profile = item.second.cast<bool>();
+               else throw py::key_error("unknown solver option " + k);
+             }
              p.chk().set_options(o);
-           },
-           py::arg("overlap") = true, py::arg("sync_debug") = false, py::arg("residual_every") = 0,
-           py::arg("graph") = false, py::arg("timeout_s") = 0.0, py::arg("profile") = false)
+           })
+      .def("options",
+           [](PySolver& p) {
+             const SolverOptions& o = p.chk().options();
+             py::dict d;
+             d["overlap"] = o.overlap;
+             d["sync_debug"] = o.sync_debug;
+             d["residual_every"] = o.residual_every;
+             d["graph"] = o.graph;
+             d["timeout_s"] = o.timeout_s;
+             d["profile"] = o.profile;
+             d["temporal"] = o.temporal;
+             return d;
+           })
       .def_property_readonly("num_local", [](PySolver& p) { return p.chk().num_local(); })
       .def_property_readonly("temporal", [](PySolver& p) { return p.chk().options().temporal; })
       .def_property_readonly("nranks", [](PySolver& p) { return p.chk().nranks(); })

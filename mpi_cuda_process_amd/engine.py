@@ -187,7 +187,13 @@ class Simulation:
         self._s.synchronize()
 
     def set_options(self, **kw):
+        """Change run options (overlap, sync_debug, residual_every, graph, timeout_s, profile);
+        options not named keep their values."""
         self._s.set_options(**kw)
+
+    @property
+    def options(self) -> dict:
+        return dict(self._s.options())
 
     @property
     def temporal(self) -> int:

@@ -130,7 +130,8 @@ def test_bench_self_launches_ranks_cpu(mdfx):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 3 and rec["config"]["ranks"] == 3
     gate = rec["config"]["gate"]
-    assert gate["passed"] and gate["transport"] == "torch" and gate["grid"][2] % 3 == 0
+    run = gate["runs"][0]
+    assert gate["passed"] and run["transport"] == "torch" and run["grid"][2] % 3 == 0
 
 
 def test_bench_refuses_more_gpus_than_visible(mdfx):
