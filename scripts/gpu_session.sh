@@ -47,9 +47,10 @@ for s in "$@"; do
             > "$R/gpurun_out/prof.log" 2>&1); rc=$?; echo "== prof rc=$rc"; [[ $rc -le 1 ]] || exit $rc ;;
     pmc_fetch|pmc_write)  # one counter per pass (FETCH_SIZE and WRITE_SIZE cannot share one)
       ctr=$([[ $s == pmc_fetch ]] && echo FETCH_SIZE || echo WRITE_SIZE)
-      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
-          -d "$R/gpurun_out/$s" -o run -- python3 "$R/bench.py" --steps 6 --warmup 2 ${BENCH_ARGS:-} \
-          > "$R/gpurun_out/$s.log" 2>&1); rc=$?; echo "== $s rc=$rc"; tail -2 "gpurun_out/$s.log"; [[ $rc -le 1 ]] || exit $rc ;;
+      out="$s${PMC_TAG:+_$PMC_TAG}"
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
+          -d "$R/gpurun_out/$out" -o run -- python3 "$R/bench.py" --steps 6 --warmup 2 ${BENCH_ARGS:-} \
+          > "$R/gpurun_out/$out.log" 2>&1); rc=$?; echo "== $out rc=$rc"; tail -2 "gpurun_out/$out.log"; [[ $rc -le 1 ]] || exit $rc ;;
     *=*) run "${LIMIT:-300}" "${s%%=*}" bash -c "${s#*=}" ;;  # ad-hoc step: name=command
     *) echo "unknown step $s"; exit 2 ;;
   esac
