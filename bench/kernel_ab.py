@@ -2,11 +2,12 @@
 """A/B harness for the stencil kernels on one MI355X (cdna_hip_programming.md §5.4 rule 24:
 variants interleaved in ONE process, several rounds, best and median reported).
 
-Variants are environment settings read by the native dispatcher at launch time
-(MDFX_RY, MDFX_PF, MDFX_ZC, MDFX_BLOCKS) plus the kernel family (tuned / naive). Every variant's
-single-step output is first checked bitwise against the naive kernel.
+Variants are the native dispatcher's tuning knobs (MDFX_RY, MDFX_ZC, MDFX_BLOCKS, MDFX_TB_RY,
+MDFX_TBK_RY, MDFX_J5_TBK, MDFX_LIFE_TBK; cached by the native layer and re-read per variant) plus
+the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
+bitwise against the naive kernel.
 
-    python bench/kernel_ab.py --kind heat7 --n 1024 --variants "RY=4,PF=2;RY=4,PF=1;RY=2,PF=2"
+    python bench/kernel_ab.py --kind heat7 --n 1024 --variants "RY=4;RY=2;STEPS=2;STEPS=2,TBKRY=2"
 """
 
 import argparse
@@ -23,10 +24,8 @@ import mpi_cuda_process_amd as m  # noqa: E402
 from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, init_field,  # noqa: E402
                                       set_kernel_variant)
 
-KEYS = {"RY": "MDFX_RY", "PF": "MDFX_PF", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
-        "TBPF": "MDFX_TB_PF", "TBBP": "MDFX_TB_BP", "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBGL": "MDFX_TB_GL",
-        "TBK2": "MDFX_TBK2", "TBKRY": "MDFX_TBK_RY", "TBKDS": "MDFX_TBK_DS", "TBKNS": "MDFX_TBK_NS", "TBKLZ": "MDFX_TBK_LZ",
-        "XT": "MDFX_TBK_XT", "XRY": "MDFX_TBK_XRY"}
+KEYS = {"RY": "MDFX_RY", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
+        "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBKRY": "MDFX_TBK_RY"}
 
 
 def parse_variant(s):
@@ -46,6 +45,7 @@ def apply_env(env):
     for k in KEYS.values():
         os.environ.pop(k, None)
     os.environ.update(env)
+    m.native().reload_knobs()
 
 
 def main():

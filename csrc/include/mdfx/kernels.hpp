@@ -77,6 +77,8 @@ void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* str
 // the checks are compiled out, as in release builds).
 int64_t hip_device_check_violations();
 void hip_set_kernel_variant(const char* name);
+// Re-read the MDFX_* kernel tuning knobs from the environment (they are cached at first use).
+void hip_reload_knobs();
 // Minimum whole rounds of resident blocks per streaming fused sweep (default 1, at most 4). The
 // engine asks for 2 when slabs exchange halos: the exchange's RCCL / copy kernels then find CUs
 // freed after half the interior sweep, and blocks they displace delay it by half a round at most

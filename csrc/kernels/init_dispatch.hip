@@ -5,6 +5,7 @@
 // in place on the device from the *global* cell index, so every decomposition yields the same grid
 // and no host copy is needed.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -46,10 +47,37 @@ void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double*
 template <class T>
 bool heat7_tbk_supported(const Geo& g, int steps);
 
-int env_int(const char* name, int dflt) {
+static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   if (!v || !*v) return dflt;
   return std::atoi(v);
+}
+
+static Knobs read_knobs() {
+  Knobs k;
+  k.zc = env_int("MDFX_ZC", 0);
+  k.blocks = env_int("MDFX_BLOCKS", 4096);
+  k.ry = env_int("MDFX_RY", 0);
+  k.tb_ry = env_int("MDFX_TB_RY", 0);
+  k.tbk_ry = env_int("MDFX_TBK_RY", 0);
+  k.j5_tbk = env_int("MDFX_J5_TBK", 0);
+  k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
+  k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
+  k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
+  return k;
+}
+
+// Published snapshots are never freed (a launch on another thread may still read the previous
+// one); a reload allocates a few dozen bytes.
+static std::atomic<const Knobs*> g_knobs{nullptr};
+
+const Knobs& knobs() {
+  const Knobs* k = g_knobs.load(std::memory_order_acquire);
+  if (!k) {
+    hip_reload_knobs();
+    k = g_knobs.load(std::memory_order_acquire);
+  }
+  return *k;
 }
 
 struct InitArgs {
@@ -106,7 +134,7 @@ static Geo make_geo(const FieldLayout& lay, int64_t lz_begin, int64_t lz_end) {
   g.oob = oob_counter();
   // self-test of the checking machinery: pretend the allocation is half its size so in-bounds
   // accesses beyond that count as violations (nothing is accessed out of bounds)
-  if (env_int("MDFX_DEVCHECK_SELFTEST", 0)) g.alloc = lay.elems() / 2;
+  if (knobs().devcheck_selftest) g.alloc = lay.elems() / 2;
 #endif
   g.pitch = lay.pitch;
   g.plane = lay.plane;
@@ -140,6 +168,10 @@ int64_t hip_device_check_violations() {
 #else
   return -1;
 #endif
+}
+
+void hip_reload_knobs() {
+  dev::g_knobs.store(new dev::Knobs(dev::read_knobs()), std::memory_order_release);
 }
 
 void hip_set_kernel_variant(const char* name) {
@@ -214,12 +246,12 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       else
         dev::launch_box27_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.coef, a.resid, s);
     } else if (spec.kind == StencilKind::Life) {
-      if (a.steps > 2 || dev::env_int("MDFX_LIFE_TBK", 0))
+      if (a.steps > 2 || dev::knobs().life_tbk)
         dev::launch_life_tbk(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.steps, a.resid, s);
       else
         dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
     } else if (spec.kind == StencilKind::Jacobi5) {
-      if (a.steps > 2 || dev::env_int("MDFX_J5_TBK", 0)) {
+      if (a.steps > 2 || dev::knobs().j5_tbk) {
         if (spec.dtype == DType::F32)
           dev::launch_jacobi5_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
         else
@@ -229,9 +261,9 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
       }
-    } else if (a.steps > 2 || (dev::env_int("MDFX_TBK2", 1) &&
-                               (spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, 2)
-                                                         : dev::heat7_tbk_supported<double>(g, 2)))) {
+    } else if (a.steps > 2 || (spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, 2)
+                                                        : dev::heat7_tbk_supported<double>(g, 2))) {
+      // rows within one block: the streaming K-step kernel; wider rows (K = 2): heat7_tb2 x tiles
       if (spec.dtype == DType::F32)
         dev::launch_heat7_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
       else

@@ -158,11 +158,22 @@ __device__ __forceinline__ T lane_down1_or(T edge, T v) {
   return (threadIdx.x & 63) == 63 ? edge : s;
 }
 #endif
-// A/B twin of lane_up1 / lane_down1 through ds_bpermute (the __shfl path)
-template <class T>
-__device__ __forceinline__ T lane_up1_bp(T v) { return __shfl_up(v, 1, 64); }
-template <class T>
-__device__ __forceinline__ T lane_down1_bp(T v) { return __shfl_down(v, 1, 64); }
+
+// Host-side kernel tuning knobs (MDFX_* environment variables), read once per process and cached:
+// the dispatchers run on every launch and never call getenv there. hip_reload_knobs() re-reads
+// them (tests that change a knob in-process; Python: native().reload_knobs()).
+struct Knobs {
+  int zc = 0;          // MDFX_ZC: planes per z chunk of every streaming kernel (0: automatic)
+  int blocks = 4096;   // MDFX_BLOCKS: block target of the single-sweep 3D 7-point kernel
+  int ry = 0;          // MDFX_RY: rows per tile of the single-sweep 3D kernels (0: per-dtype default)
+  int tb_ry = 0;       // MDFX_TB_RY: rows per tile of heat7_tb2 (x-tiled rows) / box27_tb2 (0: 2)
+  int tbk_ry = 0;      // MDFX_TBK_RY: rows per tile of heat7_tbk (0: 4 at K = 2, 2 deeper)
+  int j5_tbk = 0;      // MDFX_J5_TBK: 2D MDF two-step sweeps through the K-step kernel
+  int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
+  int debug_zc = 0;    // MDFX_DEBUG_ZC: print the z chunking of the streaming kernels
+  int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
+};
+const Knobs& knobs();
 
 }  // namespace dev
 }  // namespace mdfx

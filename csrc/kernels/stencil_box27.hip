@@ -18,7 +18,6 @@ namespace mdfx {
 namespace dev {
 
 int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target);
-int env_int(const char* name, int dflt);
 
 template <class V, class T>
 __device__ __forceinline__ V vsplat27(T v) {
@@ -193,7 +192,7 @@ static void launch_box27_t(const Geo& g, const T* in, T* out, const StencilCoef&
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + WXN * WX - 1) / (WXN * WX));
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XT * YT * ZT)), blk(256);
@@ -222,14 +221,11 @@ template <class T>
 void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
                   hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  int ry = env_int("MDFX_RY", 0);
-  if (ry <= 0) ry = 2;
-  if (g.ny < 8) ry = 1;
-  switch (ry) {
-    case 1: launch_box27_ry<T, 1>(g, in, out, c, resid, s); break;
-    case 4: launch_box27_ry<T, 4>(g, in, out, c, resid, s); break;
-    default: launch_box27_ry<T, 2>(g, in, out, c, resid, s); break;
-  }
+  // 2 rows per tile (MDFX_RY=1 for one), 1 on short columns
+  if (knobs().ry == 1 || g.ny < 8)
+    launch_box27_ry<T, 1>(g, in, out, c, resid, s);
+  else
+    launch_box27_ry<T, 2>(g, in, out, c, resid, s);
 }
 template void launch_box27<float>(const Geo&, const float*, float*, const StencilCoef&, double*,
                                   hipStream_t);
@@ -438,7 +434,7 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   constexpr int WYN = 4 / WXN;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   if (zc <= 0) {  // balanced ~43-plane chunks, as the 7-point fused kernel (5 pipeline planes here)
     int64_t zt = (planes + 43) / 44;
     zc = (int)((planes + zt - 1) / zt);
@@ -451,15 +447,12 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
-  // next-plane prefetch: fp32 985.7 vs 773.3 GCells/s without, fp64 491.8 vs 479.8 (512^3,
+  // next-plane prefetch always: fp32 985.7 vs 773.3 GCells/s without, fp64 491.8 vs 479.8 (512^3,
   // profiles/r01_box27_tb2.txt)
-  const bool pf = env_int("MDFX_TB_PF", 1) != 0;
   if (resid)
     hipLaunchKernelGGL((box27_tb2<T, RY, WXN, true, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-  else if (pf)
-    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
   else
-    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 0>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
 }
 
 template <class T, int RY>
@@ -477,10 +470,7 @@ static void launch_box27_tb2_ry(const Geo& g, const T* in, T* out, const Stencil
 template <class T>
 void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  int ry = env_int("MDFX_TB_RY", 0);
-  if (ry <= 0) ry = 2;
-  if (g.ny < 8) ry = 1;
-  if (ry == 1)
+  if (knobs().tb_ry == 1 || g.ny < 8)
     launch_box27_tb2_ry<T, 1>(g, in, out, c, resid, s);
   else
     launch_box27_tb2_ry<T, 2>(g, in, out, c, resid, s);

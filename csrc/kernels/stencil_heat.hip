@@ -303,8 +303,6 @@ int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target) {
   return (int)std::max<int64_t>(zc, 1);
 }
 
-int env_int(const char* name, int dflt);
-
 template <class T, int RY, int WXN, bool EDGE, int PF>
 static void launch_heat7_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N;
@@ -313,9 +311,9 @@ static void launch_heat7_t(const Geo& g, const T* in, T* out, T r, double* resid
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + WXN * WX - 1) / (WXN * WX));
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   // ~16 blocks per CU: 512^3 fp32 ran 0.2018 ms at 4096 blocks vs 0.2296 ms at 2048
-  if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, env_int("MDFX_BLOCKS", 4096));
+  if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, knobs().blocks);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XT * YT * ZT)), blk(256);
   if (resid)
@@ -325,34 +323,28 @@ static void launch_heat7_t(const Geo& g, const T* in, T* out, T r, double* resid
 }
 
 template <class T, int RY, int WXN>
-static void launch_heat7_e(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s, int pf) {
+static void launch_heat7_e(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int WX = 64 * VT<T>::N;
+  // planes of prefetch: 1 for fp32, 2 for fp64 (bench/kernel_ab.py, see launch_heat7)
+  constexpr int PF = sizeof(T) == 4 ? 1 : 2;
   // one block spans the whole row: the x neighbours at the block edge are the Dirichlet
   // boundary, so the block-edge loads vanish from the kernel.
-  const bool edge = g.nx > (int64_t)WXN * WX;
-  if (edge) {
-    if (pf == 1)
-      launch_heat7_t<T, RY, WXN, true, 1>(g, in, out, r, resid, s);
-    else
-      launch_heat7_t<T, RY, WXN, true, 2>(g, in, out, r, resid, s);
-  } else {
-    if (pf == 1)
-      launch_heat7_t<T, RY, WXN, false, 1>(g, in, out, r, resid, s);
-    else
-      launch_heat7_t<T, RY, WXN, false, 2>(g, in, out, r, resid, s);
-  }
+  if (g.nx > (int64_t)WXN * WX)
+    launch_heat7_t<T, RY, WXN, true, PF>(g, in, out, r, resid, s);
+  else
+    launch_heat7_t<T, RY, WXN, false, PF>(g, in, out, r, resid, s);
 }
 
 template <class T, int RY>
-static void launch_heat7_ry(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s, int pf) {
+static void launch_heat7_ry(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int WX = 64 * VT<T>::N;
   // waves along x only as far as the row is wide; the rest stack along y.
   if (g.nx > 2 * WX)
-    launch_heat7_e<T, RY, 4>(g, in, out, r, resid, s, pf);
+    launch_heat7_e<T, RY, 4>(g, in, out, r, resid, s);
   else if (g.nx > WX)
-    launch_heat7_e<T, RY, 2>(g, in, out, r, resid, s, pf);
+    launch_heat7_e<T, RY, 2>(g, in, out, r, resid, s);
   else
-    launch_heat7_e<T, RY, 1>(g, in, out, r, resid, s, pf);
+    launch_heat7_e<T, RY, 1>(g, in, out, r, resid, s);
 }
 
 template <class T>
@@ -361,17 +353,14 @@ void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStre
   // defaults from bench/kernel_ab.py on MI355X, 1024^3 fp32 (profiles/r01_ab_heat7_f32.json):
   // RY=2 PF=1 1.546 ms (694.5 GCells/s) > RY=4 PF=1 1.584 > RY=4 PF=2 1.603 > RY=2 PF=2 1.662
   // fp64 1024^3: RY=4 PF=2 3.395 ms (316 GCells/s) > RY=4 PF=1 3.415 > RY=2 PF=1 3.479
-  // (profiles/r01_ab_heat7_f64.json)
-  int ry = env_int("MDFX_RY", 0);
+  // (profiles/r01_ab_heat7_f64.json). MDFX_RY picks 1, 2 or 4 rows per tile.
+  int ry = knobs().ry;
   if (ry <= 0) ry = sizeof(T) == 4 ? 2 : 4;
-  int pf = env_int("MDFX_PF", 0);
-  if (pf <= 0) pf = sizeof(T) == 4 ? 1 : 2;
   if (g.ny < 8) ry = 1;
   switch (ry) {
-    case 1: launch_heat7_ry<T, 1>(g, in, out, r, resid, s, pf); break;
-    case 2: launch_heat7_ry<T, 2>(g, in, out, r, resid, s, pf); break;
-    case 8: launch_heat7_ry<T, 8>(g, in, out, r, resid, s, pf); break;
-    default: launch_heat7_ry<T, 4>(g, in, out, r, resid, s, pf); break;
+    case 1: launch_heat7_ry<T, 1>(g, in, out, r, resid, s); break;
+    case 2: launch_heat7_ry<T, 2>(g, in, out, r, resid, s); break;
+    default: launch_heat7_ry<T, 4>(g, in, out, r, resid, s); break;
   }
 }
 template void launch_heat7<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
@@ -383,7 +372,7 @@ void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipSt
   if (planes <= 0) return;
   constexpr int WX = 64 * VT<T>::N;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;

@@ -34,7 +34,6 @@ namespace mdfx {
 namespace dev {
 
 int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target);
-int env_int(const char* name, int dflt);
 
 template <class V, class T>
 __device__ __forceinline__ V vsplat_tb(T v) {
@@ -44,7 +43,7 @@ __device__ __forceinline__ V vsplat_tb(T v) {
   return r;
 }
 
-template <class T, int RY, int WXN, bool RES, int PF, bool BP = false, bool XT = false>
+template <class T, int RY, int WXN, bool RES, int PF, bool XT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <= 2 ? 3 : 1))) void heat7_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g,
                                                  T r, int zc, int YT, int XTn, double* __restrict__ resid) {
   using V = typename VT<T>::type;
@@ -178,8 +177,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
         const int64_t y = y0 - 1 + j;
         const V cc = M0[j + 1];
         V o = cc;
-        T l = BP ? lane_up1_bp(cc[N - 1]) : lane_up1(cc[N - 1]);
-        T rr = BP ? lane_down1_bp(cc[0]) : lane_down1(cc[0]);
+        T l = lane_up1(cc[N - 1]);
+        T rr = lane_down1(cc[0]);
         if (lane == 0) l = wx > 0 ? edge[buf][w - 1][j][1] : (hl ? hx[c & 3][0][j + 1][0] : T(0));
         if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][j][0] : (hr ? hx[c & 3][1][j + 1][0] : T(0));
         if (!zb && y > 0 && y < g.ny - 1) {
@@ -207,8 +206,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
         if (y >= g.ny) break;
         const V cc = U1b[i + 1];
         V o = cc;
-        T l = BP ? lane_up1_bp(cc[N - 1]) : lane_up1(cc[N - 1]);
-        T rr = BP ? lane_down1_bp(cc[0]) : lane_down1(cc[0]);
+        T l = lane_up1(cc[N - 1]);
+        T rr = lane_down1(cc[0]);
         if (lane == 0) l = wx > 0 ? edge[buf][w - 1][R1 + i][1] : (hl ? u1h(lz, 0, i, L0[i + 2][0]) : T(0));
         if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][R1 + i][0] : (hr ? u1h(lz, 1, i, L0[i + 2][N - 1]) : T(0));
         if (!zb && y != 0 && y != g.ny - 1) {
@@ -273,7 +272,7 @@ int64_t resident_blocks(const void* kfn) {
   int cus = 0, nb = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 256, 0) != hipSuccess || nb <= 0) nb = 2;
-  if (env_int("MDFX_DEBUG_ZC", 0)) fprintf(stderr, "[mdfx] tb2 residency: %d CUs x %d blocks\n", cus, nb);
+  if (knobs().debug_zc) fprintf(stderr, "[mdfx] tb2 residency: %d CUs x %d blocks\n", cus, nb);
   return cache[{dev, kfn}] = (int64_t)cus * nb;
 }
 
@@ -295,253 +294,35 @@ int tb2_zc(int64_t planes, int64_t tiles, int64_t resident) {
   return (int)zc;
 }
 
-// ---- LDS-DMA prefetch variant (rows within one block) -------------------------------------------
-//
-// Same arithmetic and schedule as heat7_tb2, but the next u0 plane is not prefetched into VGPRs:
-// each wave streams it with global_load_lds (16 B per lane, no VGPR destination) into its own LDS
-// slot right after the iteration's stores, and copies it into registers one iteration later, just
-// before the next stores, where the oldest plane's registers have already died. That removes the
-// prefetch's six row vectors from the register budget. The loop uses a raw s_barrier with an
-// explicit lgkmcnt(0) (a __syncthreads would make hipcc drain the DMA at every barrier) and an
-// explicit vmcnt(0) before reading the slot (hipcc does not track LDS-DMA writes).
-
-template <class T, int RY, int WXN, bool RES>
-__global__ __launch_bounds__(256) void heat7_tb2_gl(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                    int zc, int YT, double* __restrict__ resid) {
-  using V = typename VT<T>::type;
-  constexpr int N = VT<T>::N;
-  constexpr int WX = 64 * N;
-  constexpr int WYN = 4 / WXN;
-  constexpr int R0 = RY + 4;
-  constexpr int R1 = RY + 2;
-  __shared__ T edge[2][4][R1 + RY][2];
-  __shared__ V pre[4][R0][64];
-  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
-  const int yt = t % YT;
-  const int zt = t / YT;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wx = w % WXN, wy = w / WXN;
-  const int64_t xw = (int64_t)wx * WX;
-  const uint32_t xo = (uint32_t)lane * N;
-  const int64_t x = xw + xo;
-  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
-  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
-  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
-  const bool xin = x < g.pitch;
-  const int64_t pitch = g.pitch, plane = g.plane;
-  const T* ib = in + (y0 - 2) * pitch + xw;
-  T* ob = out + y0 * pitch + xw;
-  auto rowok = [&](int k) { const int64_t y = y0 - 2 + k; return y >= 0 && y < g.ny; };
-  auto ld = [&](int64_t lz, int k) -> V {
-    V v = vsplat_tb<V>(T(0));
-    if (lz >= 0 && lz < g.lz_max && rowok(k) && xin) {
-      dcheck(g, in, ib + lz * plane + (int64_t)k * pitch + xo, N);
-      v = *(const V*)(ib + lz * plane + (int64_t)k * pitch + xo);
-    }
-    return v;
-  };
-  auto issue = [&](int64_t lz) {  // stream u0 plane lz into this wave's slot
-    if (lz < 0 || lz >= g.lz_max) return;
-#pragma unroll
-    for (int k = 0; k < R0; ++k)
-      if (rowok(k) && xin) {
-        dcheck(g, in, ib + lz * plane + (int64_t)k * pitch + xo, N);
-        glds16(ib + lz * plane + (int64_t)k * pitch + xo, &pre[w][k][0]);
-      }
-  };
-  auto take = [&](int64_t lz, V (&dst)[R0]) {  // slot -> registers (after vmcnt(0))
-    const bool zok = lz >= 0 && lz < g.lz_max;
-#pragma unroll
-    for (int k = 0; k < R0; ++k) dst[k] = (zok && rowok(k) && xin) ? pre[w][k][lane] : vsplat_tb<V>(T(0));
-  };
-
-  double acc = 0.0;
-  V L0[R0], M0[R0], H0[R0];  // u0 planes c-1, c, c+1
-  V U1a[R1], U1b[R1];        // u1 planes c-2, c-1
-#pragma unroll
-  for (int k = 0; k < R0; ++k) {
-    L0[k] = ld(zs - 2, k);
-    M0[k] = ld(zs - 1, k);
-    H0[k] = ld(zs, k);
-  }
-#pragma unroll
-  for (int k = 0; k < R1; ++k) {
-    U1a[k] = vsplat_tb<V>(T(0));
-    U1b[k] = vsplat_tb<V>(T(0));
-  }
-  issue(zs + 1);
-  int buf = 0;
-  // c = u1 plane computed this iteration; u2 plane c-1 from c >= zs + 1. L0 (dead once u1(c) is
-  // done) receives the streamed plane c+2, and the three planes rotate at the end.
-  for (int64_t c = zs - 1; c <= ze; ++c) {
-    V U1c[R1];
-    if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < R1; ++j) edge[buf][w][j][0] = M0[j + 1][0];
-#pragma unroll
-      for (int i = 0; i < RY; ++i) edge[buf][w][R1 + i][0] = U1b[i + 1][0];
-    }
-    if (lane == 63) {
-#pragma unroll
-      for (int j = 0; j < R1; ++j) edge[buf][w][j][1] = M0[j + 1][N - 1];
-#pragma unroll
-      for (int i = 0; i < RY; ++i) edge[buf][w][R1 + i][1] = U1b[i + 1][N - 1];
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): seam writes visible
-    __builtin_amdgcn_s_barrier();
-    {
-      const int64_t gz = c + g.gz_off;
-      const bool zb = (gz <= 0 || gz >= g.gnz - 1);
-#pragma unroll
-      for (int j = 0; j < R1; ++j) {
-        const int64_t y = y0 - 1 + j;
-        const V cc = M0[j + 1];
-        V o = cc;
-        T l = lane_up1(cc[N - 1]);
-        T rr = lane_down1(cc[0]);
-        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][j][1] : T(0);
-        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][j][0] : T(0);
-        if (!zb && y > 0 && y < g.ny - 1) {
-          const V ym = M0[j], yp = M0[j + 2], zm = L0[j + 1], zp = H0[j + 1];
-#pragma unroll
-          for (int e = 0; e < N; ++e) {
-            const T xm = e == 0 ? l : cc[e - 1];
-            const T xp = e == N - 1 ? rr : cc[e + 1];
-            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
-            const int64_t xe = x + e;
-            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
-          }
-        }
-        U1c[j] = o;
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA into the slot has landed
-    take(c + 2, L0);
-    if (c >= zs + 1) {
-      const int64_t lz = c - 1;
-      const int64_t gz = lz + g.gz_off;
-      const bool zb = (gz == 0 || gz == g.gnz - 1);
-#pragma unroll
-      for (int i = 0; i < RY; ++i) {
-        const int64_t y = y0 + i;
-        if (y >= g.ny) break;
-        const V cc = U1b[i + 1];
-        V o = cc;
-        T l = lane_up1(cc[N - 1]);
-        T rr = lane_down1(cc[0]);
-        if (lane == 0) l = wx > 0 ? edge[buf][w - 1][R1 + i][1] : T(0);
-        if (lane == 63) rr = wx < WXN - 1 ? edge[buf][w + 1][R1 + i][0] : T(0);
-        if (!zb && y != 0 && y != g.ny - 1) {
-          const V ym = U1b[i], yp = U1b[i + 2], zm = U1a[i + 1], zp = U1c[i + 1];
-#pragma unroll
-          for (int e = 0; e < N; ++e) {
-            const T xm = e == 0 ? l : cc[e - 1];
-            const T xp = e == N - 1 ? rr : cc[e + 1];
-            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
-            const int64_t xe = x + e;
-            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
-          }
-        }
-        if (xin) {
-          dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
-          store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
-          if (RES) {
-#pragma unroll
-            for (int e = 0; e < N; ++e)
-              if (x + e < g.nx) {
-                const double d = (double)o[e] - (double)cc[e];
-                acc += d * d;
-              }
-          }
-        }
-      }
-    }
-    // the slot has been read (lgkmcnt) before the next DMA overwrites it
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    issue(c + 3);
-    buf ^= 1;
-#pragma unroll
-    for (int k = 0; k < R1; ++k) {
-      U1a[k] = U1b[k];
-      U1b[k] = U1c[k];
-    }
-#pragma unroll
-    for (int k = 0; k < R0; ++k) {
-      const V t0 = L0[k];
-      L0[k] = M0[k];
-      M0[k] = H0[k];
-      H0[k] = t0;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA may outlive the wave
-  if (RES) wave_atomic_add(resid, acc);
-}
-
-template <class T, int RY, int WXN, int PF>
-static void launch_tb2_w(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  constexpr int WYN = 4 / WXN;
+// Rows wider than one block (the streaming heat7_tbk covers rows within one block): aligned x
+// tiles of 4 * 64 * N cells, RY rows each, the next u0 plane prefetched into registers.
+template <class T, int RY>
+static void launch_tb2_xt(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N, WX = 64 * N;
-  const int XTn = g.pitch <= 4 * WX ? 1 : (int)((g.pitch + 4 * WX - 1) / (4 * WX));
+  const int XTn = (int)((g.pitch + 4 * WX - 1) / (4 * WX));
   const int64_t planes = g.lz_end - g.lz_begin;
-  const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  const void* kfn = XTn > 1 ? (const void*)&heat7_tb2<T, RY, 4, false, PF, false, true>
-                            : (const void*)&heat7_tb2<T, RY, WXN, false, PF>;
-  int zc = env_int("MDFX_ZC", 0);
+  const int YT = (int)((g.ny + RY - 1) / RY);
+  const void* kfn = (const void*)&heat7_tb2<T, RY, 4, false, 1, true>;
+  int zc = knobs().zc;
   if (zc <= 0) zc = tb2_zc(planes, (int64_t)XTn * YT, resident_blocks(kfn));
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XTn * YT * ZT)), blk(256);
-  // rows within one block: the LDS-DMA prefetch variant, +0.7..4.5% over the register prefetch at
-  // every measured shape, bitwise equal (profiles/r01_tb2_glds.txt); MDFX_TB_GL=0 for the A/B
-  if (XTn == 1 && env_int("MDFX_TB_GL", 1)) {
-    if (resid)
-      hipLaunchKernelGGL((heat7_tb2_gl<T, RY, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
-    else
-      hipLaunchKernelGGL((heat7_tb2_gl<T, RY, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
-    return;
-  }
-  if (XTn > 1) {
-    if (resid)
-      hipLaunchKernelGGL((heat7_tb2<T, RY, 4, true, PF, false, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
-    else
-      hipLaunchKernelGGL((heat7_tb2<T, RY, 4, false, PF, false, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
-  } else if (resid)
-    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, true, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
-  else if (RY == 2 && env_int("MDFX_TB_BP", 0))  // A/B: neighbour lanes through ds_bpermute
-    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
+  if (resid)
+    hipLaunchKernelGGL((heat7_tb2<T, RY, 4, true, 1, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
   else
-    hipLaunchKernelGGL((heat7_tb2<T, RY, WXN, false, PF>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
-}
-
-template <class T, int RY, int PF>
-static void launch_tb2_t(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  constexpr int WX = 64 * VT<T>::N;
-  // as many waves along x as the row needs (the block must span the row), the rest along y:
-  // 512^3 fp32 otherwise leaves half of every block idle
-  if (g.pitch > 2 * WX)
-    launch_tb2_w<T, RY, 4, PF>(g, in, out, r, resid, s);
-  else if (g.pitch > WX)
-    launch_tb2_w<T, RY, 2, PF>(g, in, out, r, resid, s);
-  else
-    launch_tb2_w<T, RY, 1, PF>(g, in, out, r, resid, s);
+    hipLaunchKernelGGL((heat7_tb2<T, RY, 4, false, 1, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
 }
 
 template <class T>
 void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  int ry = env_int("MDFX_TB_RY", 0);
-  if (ry <= 0) ry = 2;
-  // RY=2 with the next u0 plane prefetched: 1.008 ms/step vs 1.037 without (profiles/r01_ab_tb2_f32.json)
-  const int pf = env_int("MDFX_TB_PF", 1);
-  if (g.ny < 8) ry = 1;
-  switch (ry * 2 + (pf ? 1 : 0)) {
-    case 2: launch_tb2_t<T, 1, 0>(g, in, out, r, resid, s); break;
-    case 3: launch_tb2_t<T, 1, 1>(g, in, out, r, resid, s); break;
-    case 5: launch_tb2_t<T, 2, 1>(g, in, out, r, resid, s); break;
-    case 8: launch_tb2_t<T, 4, 0>(g, in, out, r, resid, s); break;
-    case 9: launch_tb2_t<T, 4, 1>(g, in, out, r, resid, s); break;
-    default: launch_tb2_t<T, 2, 0>(g, in, out, r, resid, s); break;
-  }
+  MDFX_CHECK(g.pitch > 4 * 64 * VT<T>::N, "heat7_tb2 serves rows wider than one block (heat7_tbk covers the rest)");
+  // RY = 2 (MDFX_TB_RY=1 for one row per tile): f64 2048^3 533 GCells/s vs 505 at RY = 4 and 429 at
+  // RY = 1, and the x-tiled heat7_tbk at 483 (profiles/r02_ab_f64_2048.txt)
+  if (knobs().tb_ry == 1 || g.ny < 8)
+    launch_tb2_xt<T, 1>(g, in, out, r, resid, s);
+  else
+    launch_tb2_xt<T, 2>(g, in, out, r, resid, s);
 }
 template void launch_heat7_tb2<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
 template void launch_heat7_tb2<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
@@ -679,7 +460,7 @@ void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, h
   if (planes <= 0) return;
   constexpr int WX = 64 * VT<T>::N;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
@@ -797,7 +578,7 @@ static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double*
   if (planes <= 0) return;
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;

@@ -45,7 +45,6 @@
 namespace mdfx {
 namespace dev {
 
-int env_int(const char* name, int dflt);
 int64_t resident_blocks(const void* kfn);
 
 // first row of level k (1..K) in the flat per-level state arrays
@@ -152,9 +151,9 @@ struct RowOps<double> {
   static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
 };
 
-template <class T, int RY, int K, int WXN, bool RES, bool XT>
+template <class T, int RY, int K, int WXN, bool RES>
 __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                 int zc, int YT, int XTn, double* __restrict__ resid) {
+                                                 int zc, int YT, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
   using Row = typename RO::Row;
@@ -166,26 +165,19 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
   constexpr int TOT = tbk_off<RY, K>(K + 1);  // state rows over all levels
   constexpr int NLV = K > 1 ? K - 1 : 1;
   static_assert(R0 <= 32, "seam DMA uses lanes 0..R0-1 and 32..32+R0-1");
-  static_assert(!XT || (WXN == 4 && K == 2), "x tiles: four waves across the tile, two fused steps");
-  constexpr int TW = WXN * WX;          // tile width (the whole row unless XT)
-  constexpr int R1 = RY + 2 * (K - 1);  // level-1 rows
   __shared__ V slot[4][R0 + 1][64];  // per-wave u0 plane; row R0 holds the seam vectors
   // level seam table [level][parity][wave][row][side] of edge pairs (e0, e_{N-1}) written by lanes
   // 0 (side 0) and 63 (side 1), with one pair of padding at each end for the junk half of the reads
-  // (XT: slots 4 / 5 hold the level-1 values of the columns just left / right of the tile)
-  constexpr int TB_ROW = 4, TB_W = R0 * TB_ROW, TB_PAR = (XT ? 6 : 4) * TB_W, TB_LV = 2 * TB_PAR;
+  constexpr int TB_ROW = 4, TB_W = R0 * TB_ROW, TB_PAR = 4 * TB_W, TB_LV = 2 * TB_PAR;
   __shared__ __attribute__((aligned(16))) T tb[NLV * TB_LV + 4];
 
-  const unsigned t0 = xcd_remap(blockIdx.x, gridDim.x);
-  const int xt = XT ? (int)(t0 % (unsigned)XTn) : 0;  // x tiles fastest: neighbours share seam lines in L2
-  const unsigned t = XT ? t0 / (unsigned)XTn : t0;
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
   const int yt = t % YT;
   const int zt = t / YT;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wx = w % WXN, wy = w / WXN;
-  const int64_t X0 = (int64_t)xt * TW;
-  const int64_t xw = X0 + (int64_t)wx * WX;
+  const int64_t xw = (int64_t)wx * WX;
   const uint32_t xo = (uint32_t)lane * N;
   const int64_t x = xw + xo;
   const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
@@ -243,23 +235,7 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
   //   levels 1.. (edge pair table):  lo = base1[j*4], hi = base1[j*4 + 1]
   const T* base0 = (const T*)&slot[w][R0][0] + (lane < 32 ? N - 1 : 0);
   const int wl = wx > 0 ? w - 1 : w, wr = wx < WXN - 1 ? w + 1 : w;
-  // XT: the tile-edge waves also carry the level-1 values of the column just beyond the tile
-  // (X0 - 1 / X0 + TW), computed from the DMA'd seam vectors with the same streaming recurrence
-  // (one scalar S / C per row); level 2 reads them as its seam from table slots 4 / 5.
-  const bool hxl = XT && wx == 0 && X0 > 0;
-  const bool hxr = XT && wx == WXN - 1 && xw + WX < pitch;
-  const T* base1 = lane < 32 ? (hxl ? &tb[2 + 4 * TB_W + 2 + 1] : &tb[2 + wl * TB_W + 2 + 1])
-                             : (hxr ? &tb[2 + 5 * TB_W + 0 - 1] : &tb[2 + wr * TB_W + 0 - 1]);
-  T* hwp = &tb[2 + (lane < 32 ? 4 * TB_W + 3 : 5 * TB_W)];  // halo slot this lane writes (lane 0 / 63)
-  const T* hb0 = (const T*)&slot[w][R0][lane < 32 ? 0 : 32] + (lane < 32 ? N - 1 : 0);  // next column out
-  const T* hb2 = (const T*)&slot[w][R0][lane < 32 ? 0 : 32] + (lane < 32 ? N - 2 : 1);  // the one after
-  const T rxh = (hxr && xw + WX >= g.nx - 1) ? T(0) : r;  // the right halo column may be held (nx-1)
-  T Sh[R1], Ch[R1];
-#pragma unroll
-  for (int i = 0; i < R1; ++i) {
-    Sh[i] = T(0);
-    Ch[i] = T(0);
-  }
+  const T* base1 = lane < 32 ? &tb[2 + wl * TB_W + 2 + 1] : &tb[2 + wr * TB_W + 0 - 1];
   T* wrp = &tb[2 + w * TB_W + (lane == 0 ? 0 : 2)];  // this lane's edge-pair slot (lanes 0 / 63)
 
   Row S[TOT], C[TOT];
@@ -275,16 +251,12 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
     const int par = (int)(c & 1);
     wait_vm0();  // this wave's DMA of plane c has landed
     Row X[R0];
-    T LO[R0], HI[R0], H[R0], H2[R0];
+    T LO[R0], HI[R0];
     auto ld0 = [&](int k) __attribute__((always_inline)) {
       X[k] = RO::lds((const T*)&slot[w][k][lane]);
       if (k >= 1 && k < R0 - 1) {
         LO[k] = base0[k * N];
         HI[k] = base0[k * N + 32 * N];
-      }
-      if (XT && (hxl || hxr)) {
-        H[k] = hb0[k * N];
-        H2[k] = hb2[k * N];
       }
     };
 #pragma unroll
@@ -342,24 +314,6 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
           rows(std::integral_constant<bool, false>{});
         else
           rows(std::integral_constant<bool, true>{});
-        if (XT && k == 1 && (hxl || hxr)) {  // level 1 at the halo column, rows 1..R1-2
-          const bool zh1 = gz <= 0 || gz >= g.gnz - 1;
-          T U[R1];
-#pragma unroll
-          for (int i = 1; i < R1 - 1; ++i) {
-            const int64_t y = y0 - (K - 1) + i;
-            const T rh = (zh1 || y == 0 || y == g.ny - 1) ? T(0) : rxh;
-            const T own = lane < 32 ? RO::first(X[i + 1]) : RO::last(X[i + 1]);
-            U[i] = sm::fmaT(rh, sm::fmaT(T(-6), Ch[i], Sh[i] + H[i + 1]), Ch[i]);
-            Sh[i] = (((H2[i + 1] + own) + H[i]) + H[i + 2]) + Ch[i];
-            Ch[i] = H[i + 1];
-          }
-          if ((hxl && lane == 0) || (hxr && lane == 63)) {
-            T* hp = hwp + par * TB_PAR;
-#pragma unroll
-            for (int j = 1; j < R1 - 1; ++j) hp[j * TB_ROW] = U[j];
-          }
-        }
         if (k < K) {
           if (WXN > 1) {  // publish the edge pairs of the rows the next level uses as centres
             if (lane == 0 || lane == 63) {
@@ -417,9 +371,9 @@ static int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
 template <class T>
 bool heat7_tbk_supported(const Geo& g, int steps) {
   constexpr int WX = 64 * VT<T>::N;
-  // any width at K = 2 (x tiles); deeper sweeps need the row in one block
-  const bool xt = steps == 2 && env_int("MDFX_TBK_XT", 0) != 0;
-  return steps >= 2 && steps <= 4 && (xt || g.pitch <= 4 * WX) && g.nx >= 1 && g.ny >= 1;
+  // the row in one block (wider rows at K = 2: heat7_tb2 x tiles, 533 vs 483 GCells/s for these
+  // kernels' x tiles at 2048^3 fp64, profiles/r02_ab_f64_2048.txt)
+  return steps >= 2 && steps <= 4 && g.pitch <= 4 * WX && g.nx >= 1 && g.ny >= 1;
 }
 template bool heat7_tbk_supported<float>(const Geo&, int);
 template bool heat7_tbk_supported<double>(const Geo&, int);
@@ -429,35 +383,16 @@ static void launch_tbk_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   constexpr int WYN = 4 / WXN;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  const void* kfn = (const void*)&heat7_tbk<T, RY, K, WXN, false, false>;
-  int zc = env_int("MDFX_ZC", 0);
+  const void* kfn = (const void*)&heat7_tbk<T, RY, K, WXN, false>;
+  int zc = knobs().zc;
   if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks(kfn), K);
-  if (env_int("MDFX_DEBUG_ZC", 0)) fprintf(stderr, "[mdfx] tbk K=%d RY=%d: %lld planes x %d tiles -> zc %d\n", K, RY, (long long)planes, YT, zc);
+  if (knobs().debug_zc) fprintf(stderr, "[mdfx] tbk K=%d RY=%d: %lld planes x %d tiles -> zc %d\n", K, RY, (long long)planes, YT, zc);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
-    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, true, false>), grd, blk, 0, s, in, out, g, r, zc, YT, 1, resid);
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
   else
-    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, false, false>), grd, blk, 0, s, in, out, g, r, zc, YT, 1, resid);
-}
-
-// Rows wider than one block (K = 2): aligned x tiles of 4 * 64 * N cells, the tile-edge waves
-// recomputing the level-1 column beyond each tile edge (heat7_tbk XT).
-template <class T, int RY>
-static void launch_tbk_xt(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  constexpr int TW = 4 * 64 * VT<T>::N;
-  const int XTn = (int)((g.pitch + TW - 1) / TW);
-  const int64_t planes = g.lz_end - g.lz_begin;
-  const int YT = (int)((g.ny + RY - 1) / RY);
-  const void* kfn = (const void*)&heat7_tbk<T, RY, 2, 4, false, true>;
-  int zc = env_int("MDFX_ZC", 0);
-  if (zc <= 0) zc = tbk_zc(planes, (int64_t)XTn * YT, resident_blocks(kfn), 2);
-  const int ZT = (int)((planes + zc - 1) / zc);
-  const dim3 grd((unsigned)((int64_t)XTn * YT * ZT)), blk(256);
-  if (resid)
-    hipLaunchKernelGGL((heat7_tbk<T, RY, 2, 4, true, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
-  else
-    hipLaunchKernelGGL((heat7_tbk<T, RY, 2, 4, false, true>), grd, blk, 0, s, in, out, g, r, zc, YT, XTn, resid);
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
 }
 
 template <class T, int RY, int K>
@@ -471,9 +406,9 @@ static void launch_tbk_t(const Geo& g, const T* in, T* out, T r, double* resid, 
     launch_tbk_w<T, RY, K, 1>(g, in, out, r, resid, s);
 }
 
-// K fused steps. Rows per tile from MDFX_TBK_RY, clamped to the tiles instantiated for that depth
-// (K = 2: 1..4, K = 3: 1..3, K = 4: 1..2; deeper levels with more rows would not fit the register
-// file); default 4 / 2 / 2, and 1 on very short columns.
+// K fused steps. Rows per tile: 4 at K = 2 and 2 deeper (1 on very short columns); MDFX_TBK_RY
+// picks 1, 2 or 4 (K = 2) / 1 or 2 (K = 3, 4). K = 2: RY 4 1351 GCells/s vs 3 1199, 2 1189;
+// K = 3: RY 2 1146 vs 3 844 (register spills) (profiles/r01_tbk/ab_1024_f32.log).
 template <class T>
 void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
@@ -481,36 +416,21 @@ void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double*
   MDFX_CHECK(steps >= 2 && steps <= 4 && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_tbk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
-  const int rymax = steps == 2 ? 4 : steps == 3 ? 3 : 2;
-  int ry = env_int("MDFX_TBK_RY", 0);
+  MDFX_CHECK(g.pitch <= 4 * 64 * VT<T>::N, "heat7_tbk: the row must fit one block");
+  int ry = knobs().tbk_ry;
   if (ry <= 0) ry = steps == 2 ? 4 : 2;
-  ry = std::min(ry, rymax);
   if (g.ny < 8) ry = 1;
-  if (g.pitch > 4 * 64 * VT<T>::N) {
-    MDFX_CHECK(steps == 2, "heat7_tbk: rows wider than one block need two fused steps");
-    // 3-row tiles by default: with the halo-column state, 4-row x tiles need 266 VGPRs (1 wave/SIMD)
-    const int xry = env_int("MDFX_TBK_XRY", 0) > 0 ? std::min(env_int("MDFX_TBK_XRY", 0), 4) : std::min(ry, 3);
-    switch (xry) {
-      case 1: launch_tbk_xt<T, 1>(g, in, out, r, resid, s); break;
-      case 2: launch_tbk_xt<T, 2>(g, in, out, r, resid, s); break;
-      case 3: launch_tbk_xt<T, 3>(g, in, out, r, resid, s); break;
-      default: launch_tbk_xt<T, 4>(g, in, out, r, resid, s); break;
-    }
-    return;
-  }
   if (steps == 2) {
     switch (ry) {
       case 1: launch_tbk_t<T, 1, 2>(g, in, out, r, resid, s); break;
       case 2: launch_tbk_t<T, 2, 2>(g, in, out, r, resid, s); break;
-      case 3: launch_tbk_t<T, 3, 2>(g, in, out, r, resid, s); break;
       default: launch_tbk_t<T, 4, 2>(g, in, out, r, resid, s); break;
     }
   } else if (steps == 3) {
-    switch (ry) {
-      case 1: launch_tbk_t<T, 1, 3>(g, in, out, r, resid, s); break;
-      case 2: launch_tbk_t<T, 2, 3>(g, in, out, r, resid, s); break;
-      default: launch_tbk_t<T, 3, 3>(g, in, out, r, resid, s); break;
-    }
+    if (ry == 1)
+      launch_tbk_t<T, 1, 3>(g, in, out, r, resid, s);
+    else
+      launch_tbk_t<T, 2, 3>(g, in, out, r, resid, s);
   } else {
     if (ry == 1)
       launch_tbk_t<T, 1, 4>(g, in, out, r, resid, s);

@@ -17,7 +17,6 @@ namespace mdfx {
 namespace dev {
 
 int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target);
-int env_int(const char* name, int dflt);
 
 struct U2 {
   uint64_t lo, hi;
@@ -139,7 +138,7 @@ void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, h
   if (planes <= 0) return;
   constexpr int WX = 64 * 16;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   // 32768^2: zc 64 beats 128 (profiles/r01_ab_life_u8.json), zc 32 beats 64 once the carry bytes
   // moved to DPP (2414 vs 2351 GCells/s, profiles/r01_life_tb2.txt)
   if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
@@ -293,7 +292,7 @@ void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resi
   if (planes <= 0) return;
   constexpr int WX = 64 * 16;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
@@ -410,7 +409,7 @@ static void launch_life_tbk_k(const Geo& g, const uint8_t* in, uint8_t* out, dou
   if (planes <= 0) return;
   constexpr int SEG = 62 * 16;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
-  int zc = env_int("MDFX_ZC", 0);
+  int zc = knobs().zc;
   if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;

@@ -185,8 +185,10 @@ int main() {
     EXPECT(v == 0);
     // the checks themselves work: with the self-test's halved bound the same kernels count hits
     setenv("MDFX_DEVCHECK_SELFTEST", "1", 1);
+    hip_reload_knobs();  // the knobs are cached
     (void)run_engine(StencilKind::Heat7, DType::F32, Extent3{64, 16, 20}, 2, 3, true);
     unsetenv("MDFX_DEVCHECK_SELFTEST");
+    hip_reload_knobs();
     EXPECT(hip_device_check_violations() > v);
 #endif
   }

@@ -42,9 +42,11 @@ def _two_single_steps(prob, lay, src, device):
 
 @pytest.mark.parametrize("prob", CASES, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("tbry", ["1", "2"])
-def test_fused_two_steps_bitwise(hip, prob, tbry, monkeypatch):
-    monkeypatch.setenv("MDFX_TB_RY", tbry)
-    monkeypatch.setenv("MDFX_TBK2", "0")  # heat7_tb2 (the streaming kernel has its own tests below)
+def test_fused_two_steps_bitwise(hip, prob, tbry, knob):
+    """The default two-step dispatch (heat7_tbk for rows within one block, heat7_tb2 x tiles for
+    wider rows, jacobi5_tb2, life_tb2, box27_tb2) == two naive single steps and the CPU oracle;
+    MDFX_TB_RY 1 / 2 rows per tile for the x-tiled and 27-point kernels."""
+    knob("MDFX_TB_RY", tbry)
     lay = FieldLayout.make(prob, halo=2)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -157,12 +159,12 @@ DEEP = [models.mdf2d(h=45, w=1000), models.mdf2d(h=33, w=300, dtype="f64"), mode
 
 @pytest.mark.parametrize("prob", DEEP, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k", [2, 3, 4, 6, 8])
-def test_deep_fused_steps_bitwise(hip, prob, k, monkeypatch):
+def test_deep_fused_steps_bitwise(hip, prob, k, knob):
     """K fused steps per sweep (overlapping wave segments) == K naive single steps, bitwise; K = 2
     also through the overlapped-segment kernels (MDFX_J5_TBK / MDFX_LIFE_TBK)."""
     for force in ((0, 1) if k == 2 else (0,)):
-        monkeypatch.setenv("MDFX_J5_TBK", str(force))
-        monkeypatch.setenv("MDFX_LIFE_TBK", str(force))
+        knob("MDFX_J5_TBK", force)
+        knob("MDFX_LIFE_TBK", force)
         lay = FieldLayout.make(prob, halo=k)
         src = alloc_field(lay, "cuda")
         init_field(prob, lay, src)
@@ -206,10 +208,9 @@ DEEP3D = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=
 @pytest.mark.parametrize("prob", DEEP3D, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k", [2, 3, 4])
 @pytest.mark.parametrize("ry", ["1", "2", "4"])
-def test_heat7_deep_fused_bitwise(hip, prob, k, ry, monkeypatch):
+def test_heat7_deep_fused_bitwise(hip, prob, k, ry, knob):
     """K fused 3D steps per sweep == K naive single steps, bitwise, with the residual of step K."""
-    monkeypatch.setenv("MDFX_TBK2", "1")
-    monkeypatch.setenv("MDFX_TBK_RY", ry)
+    knob("MDFX_TBK_RY", ry)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -240,13 +241,11 @@ WIDE3D = [models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, ny=9, nz=
 
 
 @pytest.mark.parametrize("prob", WIDE3D, ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("xry", ["1", "2", "3", "4"])
-def test_heat7_xtiled_streaming_bitwise(hip, prob, xry, monkeypatch):
-    """Rows wider than one block: the x-tiled streaming sweep (tile-edge waves recompute the
-    level-1 column beyond the tile) == two naive single steps, bitwise."""
-    monkeypatch.setenv("MDFX_TBK2", "1")
-    monkeypatch.setenv("MDFX_TBK_XT", "1")
-    monkeypatch.setenv("MDFX_TBK_XRY", xry)
+@pytest.mark.parametrize("tbry", ["1", "2"])
+def test_heat7_xtiled_fused_bitwise(hip, prob, tbry, knob):
+    """Rows wider than one block: heat7_tb2's x tiles (the edge waves recompute the neighbour
+    tile's u1 column) == two naive single steps, bitwise, with the residual of step 2."""
+    knob("MDFX_TB_RY", tbry)
     lay = FieldLayout.make(prob, halo=2)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -260,7 +259,7 @@ def test_heat7_xtiled_streaming_bitwise(hip, prob, xry, monkeypatch):
         set_kernel_variant("auto")
     torch.cuda.synchronize()
     o = lay.owned
-    assert torch.equal(fused[o, :, :lay.nx], ref[o, :, :lay.nx]), xry
+    assert torch.equal(fused[o, :, :lay.nx], ref[o, :, :lay.nx]), tbry
     assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
