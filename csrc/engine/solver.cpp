@@ -438,6 +438,15 @@ void Solver::maybe_inject_fault() {
   }
 }
 
+// Whether the loaded HIP runtime captures the multi-slab step (see Solver::run).
+static bool multislab_graph_ok() {
+  static const bool ok = [] {
+    int v = 0;
+    return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
+  }();
+  return ok;
+}
+
 void Solver::run(int64_t steps) {
   MDFX_CHECK(steps >= 0, "negative step count");
   MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
@@ -462,13 +471,14 @@ void Solver::run(int64_t steps) {
     const bool res = (to_res == k);
     // graph replay for plain (non-residual, non-debug) stretches of >= 2 sweeps, when the
     // transport's exchange is pure stream work (rccl, loopback, ipc; the callback / host / tcp
-    // transports move data on the host and always run eagerly). One slab per process (the
-    // production layout): the ROCm 7.0 HIP runtime bundled with PyTorch segfaults in
-    // hipStreamEndCapture on the 3-slab loopback capture (6 streams with cross-slab event waits;
-    // the same capture replays correctly under ROCm 7.2, csrc/tests/test_main.cpp test_graph), so
-    // several slabs in one process run eagerly.
+    // transports move data on the host and always run eagerly). Several slabs in one process need
+    // a HIP runtime >= 7.2: the 7.0 runtime PyTorch bundles segfaults in hipStreamEndCapture on the
+    // multi-slab loopback capture (6 streams with cross-slab event waits), while the identical
+    // binary and capture replay bitwise under 7.2 (csrc/tests/test_main.cpp test_graph run against
+    // both runtimes: profiles/r02_graph_runtime.txt). One slab per process (the production layout)
+    // replays under both.
     if (opt_.graph && hip && !res && !opt_.sync_debug && !opt_.profile && transport_->graph_capturable() &&
-        slabs_.size() == 1) {
+        (slabs_.size() == 1 || multislab_graph_ok())) {
       const int64_t plain = std::min<int64_t>(steps - done, to_res - 1);
       const int64_t pairs = fault().rank >= 0 ? 0 : plain / (2 * k);
       if (pairs > 0) {

@@ -6,6 +6,8 @@
 #include <cstring>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "mdfx/solver.hpp"
 
 using namespace mdfx;
@@ -89,6 +91,9 @@ static void test_invariance(bool gpu) {
 
 static void test_graph() {
   // eager vs hipGraph replay, loopback with 3 slabs on device 0
+  int rtv = 0;
+  (void)hipRuntimeGetVersion(&rtv);
+  std::fprintf(stderr, "[graph probe] HIP runtime %d\n", rtv);
   for (int P : {1, 3}) {
     std::vector<std::vector<char>> outs;
     for (bool graph : {false, true}) {
