@@ -15,7 +15,7 @@ import sys
 for root in sys.argv[1:]:
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(root + "/run_counter_collection.csv")):
-        if "heat7" not in r["Kernel_Name"]:
+        if "mdfx::dev" not in r["Kernel_Name"] or "init_kernel" in r["Kernel_Name"]:
             continue
         k = r["Kernel_Name"].split("(")[0].replace("void mdfx::dev::", "")
         agg[k][r["Counter_Name"]].append((float(r["Counter_Value"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
