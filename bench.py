@@ -68,6 +68,9 @@ def parse(argv=None):
                    help="split the grid into P slabs inside ONE process (loopback transport)")
     p.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                    help="replay 2-sweep cycles as hipGraphs; auto = gate and time both, keep the faster")
+    p.add_argument("--rounds", default="auto", choices=["auto", "1", "2"],
+                   help="minimum rounds of resident blocks per fused sweep; auto = 1 on one GPU, timed "
+                        "trial of 1 and 2 with several ranks (2 leaves CUs for exchange kernels mid-sweep)")
     p.add_argument("--trial-steps", type=int, default=16,
                    help="steps of each short timed trial that picks transport / graph mode (auto)")
     p.add_argument("--temporal", type=int, default=0,
@@ -288,6 +291,10 @@ def main(argv=None):
         transports = [a.transport if a.transport in ("loopback", "host") else "auto"]
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True] if hip else [False])
     cands = [(t, g) for t in transports for g in graphs]
+    if a.rounds != "auto":
+        rounds = [int(a.rounds)]
+    else:
+        rounds = [2, 1] if (hip and env and world > 1) else [0]
     gate = None
     if env and world > 1 and not a.no_gate:
         recs, ok = [], []
@@ -310,13 +317,18 @@ def main(argv=None):
             return 3
         cands = ok
 
+    cands = [(t, g, r) for t, g in cands for r in rounds]  # the round count needs no gate of its own
     kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap,
               residual_every=a.residual_every, timeout_s=timeout, temporal=temporal)
 
-    def make_sim(transport, graph):
+    def make_sim(transport, graph, rounds=0):
         if env:
-            return Simulation(prob, distributed=True, transport=transport, graph=graph, **kw)
-        return Simulation(prob, ranks=a.virtual_ranks or 1, distributed=False, transport=transport, graph=graph, **kw)
+            sim = Simulation(prob, distributed=True, transport=transport, graph=graph, **kw)
+        else:
+            sim = Simulation(prob, ranks=a.virtual_ranks or 1, distributed=False, transport=transport, graph=graph,
+                             **kw)
+        sim.set_options(min_rounds=rounds)
+        return sim
 
     def barrier():
         if env:
@@ -345,18 +357,19 @@ def main(argv=None):
     sim, sim_t = None, None
     if len(cands) > 1:
         n_trial = max(2, min(a.trial_steps, a.steps))
-        for t, g in cands:
+        for t, g, rr in cands:
             if sim is not None and sim_t != t:
                 sim.close()
                 sim = None
             if sim is None:
-                sim, sim_t = make_sim(t, g), t
+                sim, sim_t = make_sim(t, g, rr), t
                 sim.init()
-            sim.set_options(graph=g)
+            sim.set_options(graph=g, min_rounds=rr)
             sim.run(max(2, min(a.warmup, 4)))
             dt = timed(sim, n_trial)
-            trace("trial %s graph=%s: %.3f ms/step" % (t, g, dt / n_trial * 1e3))
-            trials.append({"transport": sim.transport, "graph": g, "ms_per_step": round(dt / n_trial * 1e3, 4)})
+            trace("trial %s graph=%s rounds=%s: %.3f ms/step" % (t, g, rr, dt / n_trial * 1e3))
+            trials.append({"transport": sim.transport, "graph": g, "min_rounds": rr,
+                           "ms_per_step": round(dt / n_trial * 1e3, 4)})
         chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
         if sim_t != chosen[0]:
             sim.close()
@@ -365,8 +378,8 @@ def main(argv=None):
         chosen = cands[0]
     if sim is None:
         sim = make_sim(*chosen)
-    sim.set_options(graph=chosen[1])
-    trace("engine up (%s, graph=%s)" % (sim.transport, chosen[1]))
+    sim.set_options(graph=chosen[1], min_rounds=chosen[2])
+    trace("engine up (%s, graph=%s, rounds=%s)" % (sim.transport, chosen[1], chosen[2]))
     sim.init()  # every timed run starts from the same initial grid
     trace("init done")
     sim.run(a.warmup)
@@ -426,6 +439,7 @@ def main(argv=None):
                 "comm_size": nproc if sim_transport == "rccl" else 0,
                 "kernel_variant": native().kernel_variant(),
                 "graph": chosen[1],
+                "min_rounds": chosen[2] or ("2 (auto)" if nproc > 1 or a.virtual_ranks > 1 else "1 (auto)"),
                 "trials": trials,
                 "overlap": not a.no_overlap,
                 "temporal_block": temporal,

@@ -45,7 +45,6 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 8, "temporal blocking depth must be 1..8");
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
-    hip_set_min_rounds(nranks > 1 ? 2 : 1);
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
     hip_set_abort(0);
     hip_clear_wait_error();
@@ -151,7 +150,7 @@ Solver::~Solver() {
 }
 
 void Solver::set_options(const SolverOptions& o) {
-  if (o.graph != opt_.graph || o.overlap != opt_.overlap) destroy_graph();
+  if (o.graph != opt_.graph || o.overlap != opt_.overlap || o.min_rounds != opt_.min_rounds) destroy_graph();
   MDFX_CHECK(o.temporal == opt_.temporal, "the temporal blocking depth is fixed at construction");
   opt_ = o;
   transport_->set_timeout(opt_.timeout_s);
@@ -453,6 +452,7 @@ void Solver::run(int64_t steps) {
   if (ghosts_dirty_) exchange_ghosts();
   transport_->check();
   const bool hip = slabs_[0].be->kind() == DeviceKind::HIP;
+  if (hip) hip_set_min_rounds(opt_.min_rounds > 0 ? opt_.min_rounds : (nranks_ > 1 ? 2 : 1));
   const int T = opt_.temporal;
   int64_t done = 0;
   while (done < steps) {

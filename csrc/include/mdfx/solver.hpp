@@ -37,6 +37,10 @@ struct SolverOptions {
   // Per-phase hipEvent timing of slab 0 (boundary / interior / exchange / whole step); syncs the
   // host once per step, so it is a diagnostic mode, not a benchmark mode.
   bool profile = false;
+  // Minimum whole rounds of resident blocks per streaming fused sweep (hip_set_min_rounds):
+  // 0 = automatic (2 with several slabs, so exchange kernels that need CUs find some mid-sweep; 1
+  // otherwise). Fewer rounds mean longer z chunks, hence less pipeline fill per chunk.
+  int min_rounds = 0;
 };
 
 struct PhaseStats {

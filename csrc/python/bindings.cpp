@@ -387,6 +387,7 @@ PYBIND11_MODULE(_mdfx, m) {
                else if (k == "residual_every") o.residual_every = item.second.cast<int>();
                else if (k == "graph") o.graph = item.second.cast<bool>();
                else if (k == "timeout_s") o.timeout_s = item.second.cast<double>();
+               else if (k == "min_rounds") o.min_rounds = item.second.cast<int>();
                else if (k == "profile") o.profile = item.second.cast<bool>();
                else throw py::key_error("unknown solver option " + k);
              }
@@ -403,6 +404,7 @@ PYBIND11_MODULE(_mdfx, m) {
              d["timeout_s"] = o.timeout_s;
              d["profile"] = o.profile;
              d["temporal"] = o.temporal;
+             d["min_rounds"] = o.min_rounds;
              return d;
            })
       .def_property_readonly("num_local", [](PySolver& p) { return p.chk().num_local(); })
