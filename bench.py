@@ -291,6 +291,12 @@ def main(argv=None):
         transports = [a.transport if a.transport in ("loopback", "host") else "auto"]
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True] if hip else [False])
     cands = [(t, g) for t in transports for g in graphs]
+    if hip and a.graph == "auto" and len(graphs) > 1:
+        # rccl steps are captured only under HIP >= 7.2 (RcclTransport::graph_capturable); under the
+        # runtime PyTorch bundles a graph candidate would just repeat the eager one
+        from mpi_cuda_process_amd import native as _nat
+        if not _nat().hip_runtime_version() >= 70200000:
+            cands = [(t, g) for t, g in cands if not (t == "rccl" and g)]
     if a.rounds != "auto":
         rounds = [int(a.rounds)]
     else:

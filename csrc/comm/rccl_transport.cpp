@@ -60,7 +60,17 @@ class RcclTransport final : public Transport {
   }
   const char* name() const override { return "rccl"; }
   bool in_process_only() const override { return false; }
-  bool graph_capturable() const override { return true; }
+  // RCCL's grouped send/recv joins its own internal streams to the caller's with events; the HIP
+  // 7.0 runtime PyTorch bundles segfaults in hipStreamEndCapture on such multi-stream captures
+  // (profiles/r02_graph_runtime.txt), so RCCL steps are captured only under HIP >= 7.2 and run
+  // eagerly otherwise.
+  bool graph_capturable() const override {
+    static const bool ok = [] {
+      int v = 0;
+      return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
+    }();
+    return ok;
+  }
   void set_timeout(double s) override { timeout_s_ = s; }
   void abort() override {
     if (aborted_) return;

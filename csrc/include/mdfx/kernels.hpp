@@ -77,6 +77,9 @@ void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* str
 // the checks are compiled out, as in release builds).
 int64_t hip_device_check_violations();
 void hip_set_kernel_variant(const char* name);
+// hipRuntimeGetVersion of the HIP runtime in this process (e.g. 70051831 for PyTorch's bundled
+// 7.0, 70226015 for /opt/rocm 7.2); 0 when no runtime answers.
+int hip_runtime_version();
 // Re-read the MDFX_* kernel tuning knobs from the environment (they are cached at first use).
 void hip_reload_knobs();
 // Minimum whole rounds of resident blocks per streaming fused sweep (default 1, at most 4). The

@@ -170,6 +170,11 @@ int64_t hip_device_check_violations() {
 #endif
 }
 
+int hip_runtime_version() {
+  int v = 0;
+  return hipRuntimeGetVersion(&v) == hipSuccess ? v : 0;
+}
+
 void hip_reload_knobs() {
   dev::g_knobs.store(new dev::Knobs(dev::read_knobs()), std::memory_order_release);
 }
