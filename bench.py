@@ -180,7 +180,7 @@ def pick_temporal(a, prob, nslab, hip):
     while want > 1 and prob.nz < 4 * want * nslab:
         want //= 2
     if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz,
-                                                            want, want)):
+                                                            want, want, prob.ref_precision)):
         return want
     return 1
 

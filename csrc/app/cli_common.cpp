@@ -37,6 +37,7 @@ struct Opts {
   int64_t ckpt_every = 0;
   std::string ckpt_dir = "mdfx_ckpt", resume;
   bool compat = false;
+  bool ref_precision = false;
   int temporal = 0;  // 0 = auto: 2 on HIP where a fused kernel exists, else 1
   bool profile = false;
   int dim = 0;
@@ -58,6 +59,8 @@ void usage(const char* prog) {
       "                            multi-process runs (mpirun / torchrun): rccl on GPUs, tcp on CPUs\n"
       "  --init random|dirichlet|constant|life|compat  --seed --lo --hi --value --edge --interior --density\n"
       "  --r R | --c0 --c1 --c2 --c3   update coefficients\n"
+      "  --ref-precision           2D MDF: the reference's fp32-sum / fp64-scale evaluation of the update\n"
+      "                            (default in the reference dialogue; single-step sweeps)\n"
       "  --residual-every K        global L2 norm of the update every K steps\n"
       "  --checkpoint-every K --checkpoint-dir D ; --resume D\n"
       "  --print                   dump the final grid like the reference's print_array\n"
@@ -124,6 +127,7 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--variant") o.variant = need(i);
     else if (a == "--timeout") o.timeout = std::atof(need(i));
     else if (a == "--compat") o.compat = true;
+    else if (a == "--ref-precision") o.ref_precision = true;
     else if (a == "--temporal") o.temporal = std::atoi(need(i));
     else if (a == "--profile") o.profile = true;
     else if (a == "--dim") o.dim = std::atoi(need(i));
@@ -226,6 +230,8 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     spec.coef.c1 = o.c1;
     spec.coef.c2 = o.c2;
     spec.coef.c3 = o.c3;
+    // the reference dialogue reproduces the reference's arithmetic too (MDF_kernel.cu:20, D17)
+    spec.coef.ref_precision = kind == StencilKind::Jacobi5 && (o.ref_precision || o.compat);
     hip_set_kernel_variant(o.variant.c_str());
 
     // ---- backend / slabs / transport ------------------------------------------------------

@@ -59,6 +59,10 @@ inline bool stencil_is_2d(StencilKind k) { return k == StencilKind::Jacobi5 || k
 struct StencilCoef {
   double r = -1.0;  // < 0 -> default 1/(2d) (Jacobi)
   double c0 = 0.25, c1 = 1.0 / 20.0, c2 = 1.0 / 40.0, c3 = 3.0 / 160.0;
+  // 2D MDF only: evaluate the update exactly as the reference does (sm::jacobi5_ref: fp32 sum and
+  // -4u, fp64 scale and add, one more rounding at the store) instead of wholly in the field type.
+  // Single-step sweeps only (no fused kernel implements it).
+  bool ref_precision = false;
 };
 
 struct StencilSpec {

@@ -37,6 +37,17 @@ MDFX_HDI T jacobi5(T c, T xm, T xp, T zm, T zp, T r) {
   return fmaT(r, fmaT(T(-4), c, s), c);
 }
 
+// The reference's own evaluation of the MDF update (MDF_kernel.cu:20), for pinning its
+// semantics bit for bit: the fp32 neighbour sum ((E+W)+N)+S and the -4u term contracted into an
+// fp32 fma by hipcc, then `0.25*(...) + u` with a double literal, i.e. one fp64 fma on the widened
+// values, rounded back to the field type by the store. (E+W == W+E: IEEE addition commutes.)
+template <class T>
+MDFX_HDI T jacobi5_ref(T c, T xm, T xp, T zm, T zp, T r) {
+  const T s = ((xm + xp) + zm) + zp;
+  const T t = fmaT(T(-4), c, s);
+  return (T)fma((double)r, (double)t, (double)c);
+}
+
 // 3D 27-point as a sum of per-plane partials. For one plane and one output column (x, y):
 //   center = v(x,y); cross = (v(x-1,y)+v(x+1,y)) + (v(x,y-1)+v(x,y+1));
 //   diag   = (v(x-1,y-1)+v(x+1,y-1)) + (v(x-1,y+1)+v(x+1,y+1))

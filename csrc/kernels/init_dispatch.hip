@@ -23,7 +23,7 @@ void naive_launch(const StencilSpec& spec, const Geo& g, const void* in, void* o
 template <class T>
 void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
-void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
+void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s, bool ref);
 template <class T>
 void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
@@ -218,7 +218,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   if (steps < 2 || lay.halo < steps) return false;
   const bool k2d = steps == 2 || steps == 3 || steps == 4 || steps == 6 || steps == 8;
   if (spec.kind == StencilKind::Jacobi5)  // deep temporal blocking of the 2D problems
-    return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d;
+    return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d && !spec.coef.ref_precision;
   if (spec.kind == StencilKind::Life) return k2d;
   if (spec.kind == StencilKind::Heat7 && steps > 2) {  // deep temporal blocking (rows within one block)
     const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
@@ -299,9 +299,11 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
         break;
       case StencilKind::Jacobi5:
         if (spec.dtype == DType::F32)
-          dev::launch_jacobi5<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
+          dev::launch_jacobi5<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s,
+                                     spec.coef.ref_precision);
         else
-          dev::launch_jacobi5<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
+          dev::launch_jacobi5<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s,
+                                      spec.coef.ref_precision);
         break;
       case StencilKind::Box27:
         if (spec.dtype == DType::F32)

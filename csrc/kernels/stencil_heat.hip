@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
 
 // 2D 5-point: rows are planes (ny == 1). Each wave is an independent task (x segment of 64*N
 // values, zc rows); block = 4 tasks. Wave-edge x neighbours come from scalar global loads.
-template <class T, bool RES>
+template <class T, bool RES, bool REF>
 __global__ __launch_bounds__(256) void jacobi5_wave(const T* __restrict__ in, T* __restrict__ out,
                                                     Geo g, T r, int zc, int XT, int ntasks,
                                                     double* __restrict__ resid) {
@@ -263,7 +263,8 @@ __global__ __launch_bounds__(256) void jacobi5_wave(const T* __restrict__ in, T*
       for (int e = 0; e < N; ++e) {
         const T xm = e == 0 ? l : c[e - 1];
         const T xp = e == N - 1 ? rr : c[e + 1];
-        const T v = sm::jacobi5<T>(c[e], xm, xp, P[e], Nx[e], r);
+        const T v = REF ? sm::jacobi5_ref<T>(c[e], xm, xp, P[e], Nx[e], r)
+                        : sm::jacobi5<T>(c[e], xm, xp, P[e], Nx[e], r);
         const int64_t xe = x + e;
         o[e] = (xe == 0 || xe >= g.nx - 1) ? c[e] : v;
       }
@@ -367,7 +368,7 @@ template void launch_heat7<float>(const Geo&, const float*, float*, float, doubl
 template void launch_heat7<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
 
 template <class T>
-void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s, bool ref) {
   const int64_t planes = g.lz_end - g.lz_begin;
   if (planes <= 0) return;
   constexpr int WX = 64 * VT<T>::N;
@@ -377,13 +378,19 @@ void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipSt
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
-  if (resid)
-    hipLaunchKernelGGL((jacobi5_wave<T, true>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
-  else
-    hipLaunchKernelGGL((jacobi5_wave<T, false>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+  if (ref) {
+    if (resid)
+      hipLaunchKernelGGL((jacobi5_wave<T, true, true>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+    else
+      hipLaunchKernelGGL((jacobi5_wave<T, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+  } else if (resid) {
+    hipLaunchKernelGGL((jacobi5_wave<T, true, false>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+  } else {
+    hipLaunchKernelGGL((jacobi5_wave<T, false, false>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+  }
 }
-template void launch_jacobi5<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
-template void launch_jacobi5<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
+template void launch_jacobi5<float>(const Geo&, const float*, float*, float, double*, hipStream_t, bool);
+template void launch_jacobi5<double>(const Geo&, const double*, double*, double, double*, hipStream_t, bool);
 
 }  // namespace dev
 }  // namespace mdfx

@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void naive_heat7(const T* __restrict__ in, T* 
 
 template <class T, bool RES>
 __global__ __launch_bounds__(256) void naive_jacobi5(const T* __restrict__ in, T* __restrict__ out,
-                                                     Geo g, T r, double* __restrict__ resid) {
+                                                     Geo g, T r, int ref, double* __restrict__ resid) {
   const int64_t n = g.nx * (g.lz_end - g.lz_begin);
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -49,7 +49,8 @@ __global__ __launch_bounds__(256) void naive_jacobi5(const T* __restrict__ in, T
     const T c = in[idx];
     T o = c;
     if (x > 0 && x < g.nx - 1 && gz > 0 && gz < g.gnz - 1)
-      o = sm::jacobi5<T>(c, in[idx - 1], in[idx + 1], in[idx - g.plane], in[idx + g.plane], r);
+      o = ref ? sm::jacobi5_ref<T>(c, in[idx - 1], in[idx + 1], in[idx - g.plane], in[idx + g.plane], r)
+              : sm::jacobi5<T>(c, in[idx - 1], in[idx + 1], in[idx - g.plane], in[idx + g.plane], r);
     out[idx] = o;
     if (RES) {
       const double d = (double)o - (double)c;
@@ -157,9 +158,9 @@ void naive_launch(const StencilSpec& spec, const Geo& g, const void* in, void* o
       break;
     case StencilKind::Jacobi5:
       if (spec.dtype == DType::F32)
-        MDFX_NAIVE(naive_jacobi5, float, (float)spec.rate());
+        MDFX_NAIVE(naive_jacobi5, float, (float)spec.rate(), (int)spec.coef.ref_precision);
       else
-        MDFX_NAIVE(naive_jacobi5, double, spec.rate());
+        MDFX_NAIVE(naive_jacobi5, double, spec.rate(), (int)spec.coef.ref_precision);
       break;
     case StencilKind::Box27: {
       const auto& c = spec.coef;

@@ -78,8 +78,9 @@ py::capsule make_dlpack(void* data, int device, DType dt, std::vector<int64_t> s
 }
 
 StencilSpec make_spec(const std::string& kind, const std::string& dtype, double r, double c0,
-                      double c1, double c2, double c3) {
+                      double c1, double c2, double c3, bool ref_precision = false) {
   StencilSpec s;
+  s.coef.ref_precision = ref_precision;
   s.kind = stencil_from_name(kind);
   s.dtype = dtype_from_name(dtype);
   s.coef.r = r;
@@ -199,8 +200,8 @@ class PySolver {
            int nranks, std::vector<int> local_ranks, std::vector<int> devices,
            const std::string& transport, py::bytes unique_id, py::object callbacks, bool overlap,
            bool sync_debug, int residual_every, bool graph, double timeout_s, double r, double c0,
-           double c1, double c2, double c3, int temporal) {
-    const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3);
+           double c1, double c2, double c3, int temporal, bool ref_precision) {
+    const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3, ref_precision);
     if (devices.size() == 1 && local_ranks.size() > 1) devices.assign(local_ranks.size(), devices[0]);
     if (devices.size() != local_ranks.size())
       throw Error("devices must have one entry per local rank (or a single entry)");
@@ -281,7 +282,7 @@ PYBIND11_MODULE(_mdfx, m) {
       [](const std::string& kind, const std::string& dtype, uintptr_t in, uintptr_t out, int64_t nx,
          int64_t ny, int64_t nz, int64_t z0, int64_t z1, int halo, int64_t lz_begin, int64_t lz_end,
          int device, uintptr_t stream, uintptr_t resid, double r, double c0, double c1, double c2,
-         double c3, int steps) {
+         double c3, int steps, bool ref_precision) {
         RegionArgs a;
         a.in = (const void*)in;
         a.out = (void*)out;
@@ -290,7 +291,7 @@ PYBIND11_MODULE(_mdfx, m) {
         a.lz_end = lz_end;
         a.resid = (double*)resid;
         a.steps = steps;
-        const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3);
+        const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3, ref_precision);
         if (device < 0)
           cpu_stencil(spec, a);
         else
@@ -300,7 +301,7 @@ PYBIND11_MODULE(_mdfx, m) {
       py::arg("ny"), py::arg("nz"), py::arg("z0"), py::arg("z1"), py::arg("halo"),
       py::arg("lz_begin"), py::arg("lz_end"), py::arg("device"), py::arg("stream") = 0,
       py::arg("resid_ptr") = 0, py::arg("r") = -1.0, py::arg("c0") = 0.25, py::arg("c1") = 0.05,
-      py::arg("c2") = 0.025, py::arg("c3") = 3.0 / 160.0, py::arg("steps") = 1);
+      py::arg("c2") = 0.025, py::arg("c3") = 3.0 / 160.0, py::arg("steps") = 1, py::arg("ref_precision") = false);
   m.def(
       "init_field",
       [](const std::string& kind, const std::string& dtype, uintptr_t buf, int64_t nx, int64_t ny,
@@ -319,10 +320,11 @@ PYBIND11_MODULE(_mdfx, m) {
       py::arg("value") = 0.0, py::arg("edge") = 100.0, py::arg("interior") = 0.0,
       py::arg("density") = 0.15);
   m.def("hip_supports_steps", [](const std::string& kind, const std::string& dtype, int64_t nx, int64_t ny,
-                                 int64_t nz, int halo, int steps) {
-    StencilSpec s = make_spec(kind, dtype, -1, 0, 0, 0, 0);
+                                 int64_t nz, int halo, int steps, bool ref_precision) {
+    StencilSpec s = make_spec(kind, dtype, -1, 0, 0, 0, 0, ref_precision);
     return hip_supports_steps(s, FieldLayout::make(Extent3{nx, ny, nz}, 0, nz, halo, dtype_from_name(dtype)), steps);
-  });
+  }, py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ny"), py::arg("nz"), py::arg("halo"),
+     py::arg("steps"), py::arg("ref_precision") = false);
   m.def("life_compat_init", [](int64_t h, int64_t w, double density, unsigned seed) {
     py::array_t<uint8_t> a({h, w});
     cpu_life_compat_init(a.mutable_data(), h, w, density, seed);
@@ -332,14 +334,14 @@ PYBIND11_MODULE(_mdfx, m) {
   py::class_<PySolver>(m, "Solver")
       .def(py::init<const std::string&, const std::string&, int64_t, int64_t, int64_t, int,
                     std::vector<int>, std::vector<int>, const std::string&, py::bytes, py::object,
-                    bool, bool, int, bool, double, double, double, double, double, double, int>(),
+                    bool, bool, int, bool, double, double, double, double, double, double, int, bool>(),
            py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ny"), py::arg("nz"),
            py::arg("nranks"), py::arg("local_ranks"), py::arg("devices"), py::arg("transport"),
            py::arg("unique_id") = py::bytes(""), py::arg("callbacks") = py::none(),
            py::arg("overlap") = true, py::arg("sync_debug") = false, py::arg("residual_every") = 0,
            py::arg("graph") = false, py::arg("timeout_s") = 0.0, py::arg("r") = -1.0,
            py::arg("c0") = 0.25, py::arg("c1") = 0.05, py::arg("c2") = 0.025,
-           py::arg("c3") = 3.0 / 160.0, py::arg("temporal") = 1)
+           py::arg("c3") = 3.0 / 160.0, py::arg("temporal") = 1, py::arg("ref_precision") = false)
       .def("close", &PySolver::close)
       .def("phase_times",
            [](PySolver& p) {

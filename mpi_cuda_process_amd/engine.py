@@ -45,7 +45,7 @@ def auto_temporal(problem: Problem, nranks: int, device: str) -> int:
     while want > 1 and problem.nz < 4 * want * nranks:
         want //= 2
     if want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
-                                                want, want):
+                                                want, want, problem.ref_precision):
         return want
     return 1
 

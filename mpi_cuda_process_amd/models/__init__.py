@@ -46,6 +46,9 @@ class Problem:
     c1: float = 1.0 / 20.0
     c2: float = 1.0 / 40.0
     c3: float = 3.0 / 160.0
+    # 2D MDF: evaluate the update exactly as the reference does (fp32 sum, fp64 scale and add;
+    # MDF_kernel.cu:20) instead of wholly in the field type; single-step sweeps only
+    ref_precision: bool = False
     init: InitCondition = field(default_factory=InitCondition)
 
     def __post_init__(self):
@@ -84,7 +87,7 @@ class Problem:
         return replace(self, init=replace(self.init, **kw))
 
     def coef_kwargs(self) -> dict:
-        return dict(r=self.r, c0=self.c0, c1=self.c1, c2=self.c2, c3=self.c3)
+        return dict(r=self.r, c0=self.c0, c1=self.c1, c2=self.c2, c3=self.c3, ref_precision=self.ref_precision)
 
     def describe(self) -> str:
         shape = "%dx%d" % (self.nz, self.nx) if self.dims == 2 else "%dx%dx%d" % (self.nx, self.ny, self.nz)
@@ -92,9 +95,10 @@ class Problem:
 
 
 def mdf2d(h: int = 256, w: int = 256, dtype: str = "f32", r: float = 0.25,
-          init: Optional[InitCondition] = None) -> Problem:
-    """2D 5-point MDF (finite-difference) heat / Jacobi problem, Dirichlet edges 100."""
-    return Problem("jacobi5", nx=w, ny=1, nz=h, dtype=dtype, r=r,
+          init: Optional[InitCondition] = None, ref_precision: bool = False) -> Problem:
+    """2D 5-point MDF (finite-difference) heat / Jacobi problem, Dirichlet edges 100.
+    ``ref_precision`` pins the reference's mixed fp32/fp64 evaluation of the update."""
+    return Problem("jacobi5", nx=w, ny=1, nz=h, dtype=dtype, r=r, ref_precision=ref_precision,
                    init=init or InitCondition(kind="dirichlet", edge=100.0, interior=0.0))
 
 

@@ -157,7 +157,8 @@ def advance(problem: Problem, grid: torch.Tensor, steps: int, temporal: int = 0)
             want //= 2
         temporal = 1
         if dev.type == "cuda" and want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx,
-                                                                         problem.ny, problem.nz, want, want):
+                                                                         problem.ny, problem.nz, want, want,
+                                                                         problem.ref_precision):
             temporal = want
     lay = FieldLayout.make(problem, halo=max(1, temporal))
     a = alloc_field(lay, dev)

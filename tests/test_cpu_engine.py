@@ -424,3 +424,51 @@ def test_graph_request_with_host_transport_runs_eagerly(mdfx):
             s.run(6)
             outs.append(s.gather())
     assert np.array_equal(outs[0], outs[1])
+
+
+def _reference_mdf_numpy(g, steps):
+    """The reference's MDF update (MDF_kernel.cu:20) emulated in numpy: fp32 sum ((E+W)+N)+S, the
+    contracted fmaf(-4, C, sum) (exact in fp64, then one rounding to fp32), then 0.25*t + C in fp64
+    (0.25*t is exact) rounded to fp32 at the store; boundary cells held."""
+    u = g.astype(np.float32)
+    for _ in range(steps):
+        c = u[1:-1, 1:-1]
+        s = ((u[1:-1, 2:] + u[1:-1, :-2]) + u[:-2, 1:-1]) + u[2:, 1:-1]  # fp32 adds
+        t = (np.float64(-4.0) * c.astype(np.float64) + s.astype(np.float64)).astype(np.float32)
+        v = (np.float64(0.25) * t.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
+        n = u.copy()
+        n[1:-1, 1:-1] = v
+        u = n
+    return u
+
+
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_mdf_ref_precision_matches_reference_arithmetic(mdfx, ranks):
+    """mdf2d(ref_precision=True) reproduces the reference's mixed fp32/fp64 update bit for bit
+    (random data, so the rounding differences from the all-fp32 update actually occur)."""
+    import mpi_cuda_process_amd as m
+
+    prob = m.mdf2d(h=37, w=53, ref_precision=True).with_init(kind="random", seed=3, lo=-50.0, hi=150.0)
+    with m.Simulation(prob, device="cpu", ranks=ranks) as sim:
+        sim.init()
+        g0 = sim.gather()[:, 0, :]
+        sim.run(7)
+        got = sim.gather()[:, 0, :]
+    want = _reference_mdf_numpy(g0, 7)
+    assert np.array_equal(got, want)
+    plain = m.mdf2d(h=37, w=53).with_init(kind="random", seed=3, lo=-50.0, hi=150.0)
+    with m.Simulation(plain, device="cpu") as sim:
+        sim.init()
+        sim.run(7)
+        other = sim.gather()[:, 0, :]
+    assert np.abs(other - want).max() < 1e-3  # same update up to rounding
+
+
+def test_mdf_ref_precision_has_no_fused_kernel(mdfx):
+    import mpi_cuda_process_amd as m
+
+    assert not m.native().hip_supports_steps("jacobi5", "f32", 64, 1, 64, 2, 2, True)
+    from mpi_cuda_process_amd.engine import auto_temporal
+
+    assert auto_temporal(m.mdf2d(h=4096, w=512, ref_precision=True), 1, "hip") == 1
+    assert auto_temporal(m.mdf2d(h=4096, w=512), 1, "hip") == 8

@@ -220,3 +220,23 @@ def _sim_gather(prob, steps, **kw):
         sim.init()
         sim.run(steps)
         return sim.gather(), sim.temporal
+
+
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_mdf_ref_precision_gpu_equals_cpu(hip, ranks):
+    """The reference-precision MDF update (fp32 sum, fp64 scale and add) is bitwise the same on the
+    gfx950 wave kernel and the CPU oracle, decomposed or not."""
+    import numpy as np
+
+    import mpi_cuda_process_amd as m
+
+    prob = m.mdf2d(h=300, w=777, ref_precision=True).with_init(kind="random", seed=5, lo=-10.0, hi=110.0)
+    out = {}
+    for dev in ("cpu", "hip"):
+        with m.Simulation(prob, device=dev, ranks=ranks if dev == "hip" else 1, residual_every=9) as sim:
+            assert sim.temporal == 1
+            sim.init()
+            sim.run(9)
+            out[dev] = (sim.gather(), sim.residual)
+    assert np.array_equal(out["cpu"][0], out["hip"][0])
+    assert abs(out["cpu"][1] - out["hip"][1]) <= 1e-9 * out["cpu"][1]
