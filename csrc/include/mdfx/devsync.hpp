@@ -31,6 +31,10 @@ void hip_counter_signal(uint64_t* ctr, void* stream);
 // system-scope acquire. Bounded by timeout_s and the abort word.
 void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream);
 
+// Tests: leave a quiet-NaN pattern in every CU's LDS (synchronous, current device), so a kernel
+// that reads LDS it never wrote produces NaN instead of silently using stale finite data.
+void hip_poison_lds();
+
 // Fault injection (MDFX_FAULT=spin@rank:step): a one-wave kernel that busy-waits on `stream` for
 // `seconds` of device wall clock or until the abort word is raised.
 void hip_spin(double seconds, void* stream);

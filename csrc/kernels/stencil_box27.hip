@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void box27_zw(const T* __restrict__ in, T* __r
 #pragma unroll
         for (int j = 0; j < RR; ++j) edge[buf][w][j][1] = R[j][N - 1];
       }
-      __syncthreads();
+      lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
     }
     V H[RR];
 #pragma unroll
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
 #pragma unroll
       for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][1] = U1[j][N - 1];
     }
-    __syncthreads();
+    lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
 
     // ---- level 1: partials of u1 plane k-2, u2(k-3) ------------------------------------------
     if (k >= zs + 1) {

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void heat7_zw(const T* __restrict__ in, T* __r
 #pragma unroll
         for (int i = 0; i < RY; ++i) edge[buf][w][i][1] = C[i][N - 1];
       }
-      __syncthreads();
+      lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
     }
     const int64_t gz = lz + g.gz_off;
     const bool zb = (gz == 0 || gz == g.gnz - 1);

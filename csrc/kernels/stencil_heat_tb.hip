@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
       puthv(c + 1, HV);
       HV = ldhv(c + 2);
     }
-    __syncthreads();
+    lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
 
     // ---- u1 at plane c ------------------------------------------------------------------
     V U1c[R1];

@@ -255,8 +255,11 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
     auto ld0 = [&](int k) __attribute__((always_inline)) {
       X[k] = RO::lds((const T*)&slot[w][k][lane]);
       if (k >= 1 && k < R0 - 1) {
-        LO[k] = base0[k * N];
-        HI[k] = base0[k * N + 32 * N];
+        // a wave edge without a neighbouring wave (the global x boundary, or a narrow row's only
+        // wave) has no DMA'd seam: its slot row holds stale LDS, possibly a NaN pattern, which
+        // the held edge cell's zero coefficient would not cancel (0 * NaN): use 0 instead
+        LO[k] = has_l ? base0[k * N] : T(0);
+        HI[k] = (WXN > 1 && has_r) ? base0[k * N + 32 * N] : T(0);
       }
     };
 #pragma unroll

@@ -92,6 +92,14 @@ __global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks, const int* abo
     __builtin_amdgcn_s_sleep(64);
 }
 
+// Fills its 40 KiB of LDS with a quiet-NaN pattern: four resident blocks cover a CU's 160 KiB,
+// so kernels that run next find NaN wherever they read LDS they did not write (tests).
+__global__ __launch_bounds__(256) void lds_poison_kernel() {
+  __shared__ uint32_t buf[10240];
+  for (int i = threadIdx.x; i < 10240; i += 256) buf[i] = 0x7fc00001u;
+  __syncthreads();
+}
+
 void check_launch(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) MDFX_FAIL(std::string(what) + " launch failed: " + hipGetErrorString(e));
@@ -126,6 +134,15 @@ void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s
   hipLaunchKernelGGL(counter_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, remote, expect,
                      ticks_for(timeout_s), (const int*)w, w + 16);
   check_launch("counter_wait");
+}
+
+void hip_poison_lds() {
+  int dev = 0, cus = 0;
+  HIPC(hipGetDevice(&dev));
+  HIPC(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  hipLaunchKernelGGL(lds_poison_kernel, dim3(8 * std::max(cus, 1)), dim3(256), 0, nullptr);
+  check_launch("lds_poison");
+  HIPC(hipDeviceSynchronize());
 }
 
 void hip_spin(double seconds, void* stream) {

@@ -261,6 +261,7 @@ PYBIND11_MODULE(_mdfx, m) {
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("set_kernel_variant", [](const std::string& v) { hip_set_kernel_variant(v.c_str()); });
   m.def("reload_knobs", &hip_reload_knobs, "re-read the MDFX_* kernel tuning knobs from the environment");
+  m.def("poison_lds", &hip_poison_lds, "fill every CU's LDS with NaN (tests for stale-LDS reads)");
   m.def("hip_runtime_version", &hip_runtime_version,
         "version of the HIP runtime the process loaded (PyTorch's bundled one under torch), 0 if none");
   m.def("kernel_variant", []() { return std::string(hip_kernel_variant()); });

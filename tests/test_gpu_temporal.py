@@ -289,3 +289,40 @@ def test_engine_deep_temporal_3d(hip, k, ranks):
     ref, rr = _sim(prob, 23, ranks=1, residual_every=10)
     got, rg = _sim(prob, 23, ranks=ranks, temporal=k, residual_every=10)
     assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
+
+
+STALE_LDS = [models.heat3d(nx=256, ny=9, nz=12), models.heat3d(nx=500, ny=21, nz=11, dtype="f64"),
+             models.heat3d(nx=700, ny=19, nz=15), models.heat3d(nx=1024, ny=12, nz=9),
+             models.heat3d(nx=2048, ny=13, nz=11), models.box27(nx=300, ny=9, nz=12, dtype="f64"),
+             models.box27(nx=1024, ny=11, nz=9), models.mdf2d(h=37, w=1000), models.life2d(h=40, w=3000)]
+
+
+@pytest.mark.parametrize("prob", STALE_LDS, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("k", [1, 2])
+def test_kernels_never_read_stale_lds(hip, prob, k):
+    """Every CU's LDS is filled with NaN right before the tuned kernel runs: a kernel that read LDS
+    it had not written (e.g. a missing wave-seam at the global x boundary, held with a zero
+    coefficient that cannot cancel NaN) would now differ from the naive single steps."""
+    from mpi_cuda_process_amd import native
+
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    out = alloc_field(lay, "cuda")
+    torch.cuda.synchronize()
+    native().poison_lds()
+    apply_stencil(prob, lay, src, out, steps=k)
+    set_kernel_variant("naive")
+    try:
+        cur = alloc_field(lay, "cuda")
+        cur.copy_(src)
+        for _ in range(k):
+            nxt = alloc_field(lay, "cuda")
+            nxt.copy_(cur)
+            apply_stencil(prob, lay, cur, nxt)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(out[o, :, :lay.nx], cur[o, :, :lay.nx])
