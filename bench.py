@@ -392,6 +392,7 @@ def main(argv=None):
     trace("warmup enqueued")
     timed(sim, 0)
     trace("warmup done")
+    replays0 = sim.graph_replays
     best = None
     for _ in range(max(1, a.repeats)):
         dt = timed(sim, a.steps)
@@ -445,6 +446,7 @@ def main(argv=None):
                 "comm_size": nproc if sim_transport == "rccl" else 0,
                 "kernel_variant": native().kernel_variant(),
                 "graph": chosen[1],
+                "graph_replays_timed": sim.graph_replays - replays0,
                 "min_rounds": chosen[2] or ("2 (auto)" if nproc > 1 or a.virtual_ranks > 1 else "1 (auto)"),
                 "trials": trials,
                 "overlap": not a.no_overlap,

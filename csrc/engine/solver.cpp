@@ -595,6 +595,7 @@ void Solver::run_graph(int64_t pairs, int k) {
     s.be->record(s.ev_int, s.cs);
   }
   stats_.steps += 2 * (int64_t)k * pairs;
+  stats_.graph_replays += pairs;
   GDBG("replayed");
 }
 

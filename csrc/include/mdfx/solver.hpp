@@ -52,6 +52,7 @@ struct StepStats {
   int64_t steps = 0;
   double last_residual = -1.0;  // sqrt(sum over the grid of (u_new - u_old)^2), -1 if never
   int64_t residual_step = -1;
+  int64_t graph_replays = 0;  // 2-sweep cycles replayed from a captured hipGraph
 };
 
 class Solver {

@@ -418,6 +418,7 @@ PYBIND11_MODULE(_mdfx, m) {
       .def_property_readonly("steps", [](PySolver& p) { return p.chk().stats().steps; })
       .def_property_readonly("residual", [](PySolver& p) { return p.chk().stats().last_residual; })
       .def_property_readonly("residual_step", [](PySolver& p) { return p.chk().stats().residual_step; })
+      .def_property_readonly("graph_replays", [](PySolver& p) { return p.chk().stats().graph_replays; })
       .def_property_readonly("current_index", [](PySolver& p) { return p.chk().current_index(); })
       .def_property_readonly("transport_name", [](PySolver& p) { return std::string(p.chk().transport().name()); })
       .def("local_rank", [](PySolver& p, int i) { return p.chk().local_rank(i); })

@@ -192,6 +192,12 @@ class Simulation:
         self._s.set_options(**kw)
 
     @property
+    def graph_replays(self) -> int:
+        """2-sweep cycles replayed from a captured hipGraph so far (0: every step ran eagerly, e.g.
+        graph replay off or not capturable under this HIP runtime)."""
+        return self._s.graph_replays
+
+    @property
     def options(self) -> dict:
         return dict(self._s.options())
 
