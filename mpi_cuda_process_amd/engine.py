@@ -77,6 +77,7 @@ class Simulation:
             distributed = is_distributed() and ranks is None
         self.distributed = bool(distributed)
         self._torch_transport = None
+        self._control = None  # host control plane of the ipc transport (teardown barrier)
         self.group = group
 
         if self.distributed:
@@ -104,7 +105,8 @@ class Simulation:
                 if device != "hip":
                     raise ValueError("ipc transport needs HIP devices")
                 torch.cuda.set_device(dev_list[0])
-                args = dict(transport="ipc", callbacks=ControlPlane(group).callbacks())
+                self._control = ControlPlane(group, timeout_s=max(60.0, 2 * timeout_s))
+                args = dict(transport="ipc", callbacks=self._control.callbacks())
             elif transport in ("torch", "staged"):
                 p2p_group = group
                 staged = transport == "staged" and device == "hip"
@@ -150,6 +152,14 @@ class Simulation:
     # ---- lifecycle -------------------------------------------------------------------------
     def close(self):
         if self._s is not None:
+            if self._control is not None:
+                # ipc: a neighbour may still be pulling this process's last faces out of its
+                # exported mailbox; every rank drains its own streams, then all meet, then free
+                try:
+                    self._s.synchronize()
+                    self._control.barrier()
+                except Exception:  # noqa: BLE001 - a failed peer / poisoned engine: free anyway
+                    pass
             self._s.close()
             self._s = None
 

@@ -72,8 +72,9 @@ class ControlPlane:
     (``ipc``): the handle swap (allgather of byte strings), the residual all-reduce and barriers,
     over a CPU (gloo) process group."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, timeout_s: float = 300.0):
         self.group = group
+        self.timeout_s = timeout_s
 
     def callbacks(self) -> dict:
         return {"allgather": self.allgather, "allreduce_sum": self.allreduce_sum,
@@ -95,7 +96,11 @@ class ControlPlane:
         return float(t.item())
 
     def barrier(self) -> None:
-        dist.barrier(group=self.group)
+        # bounded (gloo): a dead peer raises after timeout_s instead of blocking for the group timeout
+        if dist.get_backend(self.group) == "gloo":
+            dist.monitored_barrier(group=self.group, timeout=datetime.timedelta(seconds=self.timeout_s))
+        else:
+            dist.barrier(group=self.group)
 
 
 class TorchP2PTransport:
