@@ -408,7 +408,9 @@ def main(argv=None):
     gcells = cells * a.steps / best / 1e9
     ms = best / a.steps * 1e3
     nproc = world if env else 1
-    per_gpu = gcells / max(nproc, 1)
+    # per physical GPU: ranks that share a device (--share-gpu) count once
+    ngpu_phys = len(set(devices)) if hip else nproc
+    per_gpu = gcells / max(ngpu_phys, 1)
     # DRAM actually required per time step: one read + one write of every cell per sweep, and a
     # sweep advances `temporal` steps
     dram_tbps = per_gpu * prob.bytes_per_cell_per_step / temporal / 1e3
@@ -454,7 +456,7 @@ def main(argv=None):
                 "gate": gate,
             },
             "per_gpu_gcells": round(per_gpu, 3),
-            "dram_bytes_per_step_per_gpu": int(cells / max(nproc, 1) * prob.bytes_per_cell_per_step / temporal),
+            "dram_bytes_per_step_per_gpu": int(cells / max(ngpu_phys, 1) * prob.bytes_per_cell_per_step / temporal),
             "achieved_dram_TBps_per_gpu": round(dram_tbps, 3) if hip else None,
             "pct_of_hbm_copy_roof": round(100.0 * dram_tbps / HBM_MEASURED_TBPS, 1) if hip else None,
         }
