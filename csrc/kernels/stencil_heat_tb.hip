@@ -473,15 +473,19 @@ void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, h
 template void launch_jacobi5_tb2<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
 template void launch_jacobi5_tb2<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
 
-// ---- 2D 5-point, K steps per sweep (K <= N) ---------------------------------------------------
+// ---- 2D 5-point, K steps per sweep ------------------------------------------------------------
 //
 // Deep temporal blocking for the 2D problem. Wave segments OVERLAP by OV = ceil(K / N) lanes on each
 // side: a wave covers 64 lanes x N columns but owns only lanes OV..63-OV, so the outer lanes carry
 // the neighbour segments' edge columns through the same SIMD instructions. Each level of the
 // pipeline corrupts one more column from the outside in (the outermost neighbour is unknown), so
-// after K <= OV * N levels the owned lanes are still exact and are the only ones stored. Per row the wave
-// keeps a 3-row ring per level; level l produces row q-l when u0 row q arrives. One read and one
-// write of the field per K steps; bitwise equal to K sm::jacobi5 steps.
+// after K <= OV * N levels the owned lanes are still exact and are the only ones stored.
+// Each level is a streaming recurrence over rows, as in heat7_tbk: its only state between rows is
+// the partial sum S = (xm + xp) + zm of row p and the centre C = u_{l-1}(p). When u_{l-1}(p+1)
+// arrives it finishes u_l(p) = fma(r, fma(-4, C, S + zp), C) -- sm::jacobi5's operation order, so
+// bitwise equal to K single steps -- and replaces S / C with row p+1's. No register rotation, and
+// held cells take a zero coefficient (fma(0, t, u) = u for finite t; every lane, inside the grid or
+// not, holds finite data) instead of a select. One read and one write of the field per K steps.
 template <class T, int K, bool RES>
 __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                    int zc, int XT, int ntasks, double* __restrict__ resid) {
@@ -499,9 +503,10 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   const bool xin = x >= 0 && x < g.pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
   const int64_t plane = g.plane;
-  bool xb[N];
+  V rx;  // per-cell coefficient: 0 on the held columns x = 0, x >= nx - 1
 #pragma unroll
-  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  for (int e = 0; e < N; ++e) rx[e] = ((x + e == 0) || (x + e >= g.nx - 1)) ? T(0) : r;
+  const V r0 = vsplat_tb<V>(T(0));
   auto ld = [&](int64_t lz) -> V {
     V v = vsplat_tb<V>(T(0));
     if (xin && lz >= 0 && lz < g.lz_max) {
@@ -510,59 +515,48 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
     }
     return v;
   };
-  // one step of row `C` with rows `P` (z-1) and `Q` (z+1) at global row gz
-  auto step = [&](const V& P, const V& C, const V& Q, int64_t gz, bool inner_only) -> V {
-    V o = C;
-    const T l = lane_up1(C[N - 1]);
-    const T rr = lane_down1(C[0]);
-    const bool bnd = inner_only ? (gz == 0 || gz == g.gnz - 1) : (gz <= 0 || gz >= g.gnz - 1);
-    if (!bnd) {
+  V S[K], C[K];  // level l = 1..K at index l - 1
 #pragma unroll
-      for (int e = 0; e < N; ++e) {
-        const T xm = e == 0 ? l : C[e - 1];
-        const T xp = e == N - 1 ? rr : C[e + 1];
-        const T v = sm::jacobi5<T>(C[e], xm, xp, P[e], Q[e], r);
-        o[e] = xb[e] ? C[e] : v;
-      }
-    }
-    return o;
-  };
-  // ring[l][0..2] = rows (newest-2 .. newest) of level l; level 0 = u0
-  V ring[K][3];
-#pragma unroll
-  for (int l = 0; l < K; ++l)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) ring[l][j] = vsplat_tb<V>(T(0));
-  ring[0][1] = ld(zs - K - 1);
-  ring[0][2] = ld(zs - K);
-  V nx = ld(zs - K + 1);
+  for (int l = 0; l < K; ++l) {
+    S[l] = vsplat_tb<V>(T(0));
+    C[l] = S[l];
+  }
+  V nx = ld(zs - K);
   double acc = 0.0;
-  // newest u0 row q; level l (1..K) produces row q - l
-  for (int64_t q = zs - K + 1; q <= ze - 1 + K; ++q) {
-    ring[0][0] = ring[0][1];
-    ring[0][1] = ring[0][2];
-    ring[0][2] = nx;
+  // newest u0 row q; level l finishes row q - l (each level's first two rows are priming garbage
+  // that no level needs)
+  for (int64_t q = zs - K; q <= ze - 1 + K; ++q) {
+    V X = nx;
     nx = ld(q + 1);
 #pragma unroll
-    for (int l = 1; l < K; ++l) {
+    for (int l = 1; l <= K; ++l) {
       const int64_t row = q - l;
-      const V v = step(ring[l - 1][0], ring[l - 1][1], ring[l - 1][2], row + g.gz_off, false);
-      ring[l][0] = ring[l][1];
-      ring[l][1] = ring[l][2];
-      ring[l][2] = v;
-    }
-    const int64_t lz = q - K;
-    if (lz >= zs) {
-      const V& C = ring[K - 1][1];
-      const V o = step(ring[K - 1][0], C, ring[K - 1][2], lz + g.gz_off, true);
-      if (own) {
-        dcheck(g, (const T*)out, out + lz * plane + x, N);
-        store_nt((V*)(out + lz * plane + x), o);
+      const int64_t gz = row + g.gz_off;
+      const V rc = (gz <= 0 || gz >= g.gnz - 1) ? r0 : rx;
+      const V c = C[l - 1];
+      V o;
+#pragma unroll
+      for (int e = 0; e < N; ++e) o[e] = sm::fmaT(rc[e], sm::fmaT(T(-4), c[e], S[l - 1][e] + X[e]), c[e]);
+      // row + 1's partial from the arriving row X: (xm + xp) + zm
+      const T lft = lane_up1(X[N - 1]);
+      const T rgt = lane_down1(X[0]);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const T xm = e == 0 ? lft : X[e - 1];
+        const T xp = e == N - 1 ? rgt : X[e + 1];
+        S[l - 1][e] = (xm + xp) + c[e];
+      }
+      C[l - 1] = X;
+      if (l < K) {
+        X = o;
+      } else if (row >= zs && own) {
+        dcheck(g, (const T*)out, out + row * plane + x, N);
+        store_nt((V*)(out + row * plane + x), o);
         if (RES) {
 #pragma unroll
           for (int e = 0; e < N; ++e)
             if (x + e < g.nx) {
-              const double d = (double)o[e] - (double)C[e];
+              const double d = (double)o[e] - (double)c[e];
               acc += d * d;
             }
         }
