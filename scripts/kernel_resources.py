@@ -22,7 +22,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 FIELDS = ("vgpr_count", "agpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count",
-          "private_segment_fixed_size", "group_segment_fixed_size")
+          "private_segment_fixed_size", "group_segment_fixed_size", "max_flat_workgroup_size")
 
 
 def _demangle(names):

@@ -31,13 +31,20 @@ def test_no_kernel_spills_to_scratch(recs):
     assert not bad, bad
 
 
+def _blocks_per_cu(r):
+    # a block of B threads spreads B / 256 waves over each of the 4 SIMDs
+    per_simd = max(1, r.get("max_flat_workgroup_size", 256) // 256)
+    return r["waves_per_simd"] // per_simd
+
+
 def test_lds_never_limits_occupancy(recs):
-    # 160 KiB LDS per CU. Every block is 256 threads (4 waves, one per SIMD), so a kernel with W
-    # waves per SIMD keeps W blocks resident per CU: their LDS must fit next to each other, so LDS
-    # never becomes the occupancy limiter (the VGPR budget is). The streaming K-step kernel
-    # (heat7_tbk: LDS-DMA planes + seam tables, up to 49 KiB at one wave per SIMD) is the largest user.
+    # 160 KiB LDS per CU. A kernel with W waves per SIMD and blocks of B threads keeps W * 256 / B
+    # blocks resident per CU (W for the 256-thread blocks most kernels use): their LDS must fit next
+    # to each other, so LDS never becomes the occupancy limiter (the VGPR budget is). The streaming
+    # K-step kernel (heat7_tbk: LDS-DMA planes + seam tables, up to 49 KiB at one wave per SIMD)
+    # is the largest user.
     bad = {n: (r.get("group_segment_fixed_size", 0), r["waves_per_simd"]) for n, r in recs.items()
-           if r.get("group_segment_fixed_size", 0) * max(1, r["waves_per_simd"]) > 160 * 1024}
+           if _blocks_per_cu(r) < 1 or r.get("group_segment_fixed_size", 0) * _blocks_per_cu(r) > 160 * 1024}
     assert not bad, bad
 
 
