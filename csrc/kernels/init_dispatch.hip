@@ -62,6 +62,7 @@ static Knobs read_knobs() {
   k.tbk_ry = env_int("MDFX_TBK_RY", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
+  k.b27_tbk = env_int("MDFX_B27_TBK", 0);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;

@@ -101,6 +101,20 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// LDS store outside the compiler's view. hipcc's wait-count pass treats a compiler-visible LDS
+// store as a possible alias of an in-flight LDS DMA (global_load_lds) and puts s_waitcnt vmcnt(0)
+// in front of it, which drains the next plane's DMA in the middle of the plane's compute. The
+// stores below go to tables no DMA writes; lds_barrier()'s lgkmcnt(0) completes them.
+template <class V>
+__device__ __forceinline__ void lds_store(void* p, const V& v) {
+  const unsigned a = (unsigned)(uintptr_t)((__attribute__((address_space(3))) void*)p);
+  static_assert(sizeof(V) == 8 || sizeof(V) == 16, "8- or 16-byte LDS stores");
+  if constexpr (sizeof(V) == 8)
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+  else
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
 // Whole-wave lane shifts by one (lane i <- lane i-1 / lane i+1) with DPP wave_shr:1 / wave_shl:1:
 // a VALU move with a DPP modifier instead of a ds_bpermute through the LDS crossbar. The lane that
 // has no source (0 or 63) receives 0; callers overwrite it with the seam value.
@@ -170,6 +184,7 @@ struct Knobs {
   int tbk_ry = 0;      // MDFX_TBK_RY: rows per tile of heat7_tbk (0: 4 at K = 2, 2 deeper)
   int j5_tbk = 0;      // MDFX_J5_TBK: 2D MDF two-step sweeps through the K-step kernel
   int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
+  int b27_tbk = 0;     // MDFX_B27_TBK: 27-point fused kernel (0: per dtype, -1: box27_tb2, 1/2/4: box27_tbk rows)
   int debug_zc = 0;    // MDFX_DEBUG_ZC: print the z chunking of the streaming kernels
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
 };

@@ -1,0 +1,167 @@
+// Register layouts and arithmetic of one lane's 16-B row slice for the streaming multi-level
+// kernels (heat7_tbk, box27_tbk), plus the flat per-level state indexing they share.
+#pragma once
+
+#include "kcommon.hpp"
+
+namespace mdfx {
+namespace dev {
+
+// first row of level k (1..K) in the flat per-level state arrays
+template <int RY, int K>
+__host__ __device__ constexpr int tbk_off(int k) {
+  return (k - 1) * RY + 2 * ((k - 1) * K - (k - 1) * k / 2);
+}
+
+// One lane's slice of a row, in the register layout the arithmetic wants.
+//  fp32: the 4 cells as two aligned pairs a = (e1, e2), b = (e0, e3). Then
+//        x sums (xm + xp) = { (l, rr) + a , b + swap(a) }  -> 2 v_pk_add_f32,
+//        and every y / z / update operation is one packed op per pair, with no lane shuffles
+//        or register moves to form misaligned pairs (natural (e0,e1),(e2,e3) pairs need them).
+//  fp64: the 2 cells as they are (no packed fp64 arithmetic on CDNA).
+// `E` is the edge pair (e0, e_{N-1}) the neighbouring waves need.
+template <class T>
+struct RowOps;
+
+template <>
+struct RowOps<float> {
+  typedef float T2 __attribute__((ext_vector_type(2)));
+  typedef float V __attribute__((ext_vector_type(4)));
+  struct Row {
+    T2 a, b;
+  };
+  // natural 16-B vector at p (one ds_read_b128), regrouped into the pair layout
+  static __device__ __forceinline__ Row lds(const float* p) {
+    const V v = *(const V*)p;
+    Row r;
+    r.a = T2{v.y, v.z};
+    r.b = T2{v.x, v.w};
+    return r;
+  }
+  // the same from two ds_read2_b32 that land each pair in an aligned register pair (a 16-B read
+  // would need 4 moves to regroup). The caller waits for lgkmcnt(0) and then passes the row
+  // through fence() before the first use.
+  static __device__ __forceinline__ Row lds_pairs(const float* p) {
+    const unsigned a = (unsigned)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
+    Row r;
+    asm volatile("ds_read2_b32 %0, %2 offset0:1 offset1:2\n\tds_read2_b32 %1, %2 offset1:3"
+                 : "=v"(r.a), "=v"(r.b)
+                 : "v"(a));
+    return r;
+  }
+  static __device__ __forceinline__ void fence(Row& r) { asm volatile("" : "+v"(r.a), "+v"(r.b)); }
+  static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}, T2{0.f, 0.f}}; }
+  static __device__ __forceinline__ float first(const Row& c) { return c.b.x; }
+  static __device__ __forceinline__ float last(const Row& c) { return c.b.y; }
+  static __device__ __forceinline__ T2 edges(const Row& c) { return c.b; }
+  // (((xm + xp) + ym) + yp) + zm
+  static __device__ __forceinline__ Row partial(const Row& c, float l, float rr, const Row& ym, const Row& yp,
+                                                const Row& zm) {
+    const T2 lr = T2{l, rr};
+    const T2 sa = T2{c.a.y, c.a.x};
+    Row s;
+    s.b = lr + c.a;  // (l + e1, rr + e2)
+    s.a = c.b + sa;  // (e0 + e2, e3 + e1)
+    s.a = ((s.a + ym.a) + yp.a) + zm.a;
+    s.b = ((s.b + ym.b) + yp.b) + zm.b;
+    return s;
+  }
+  // fma(r, fma(-6, c, S + zp), c) with a per-cell coefficient in the Row layout (0 = held)
+  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m6 = T2{-6.f, -6.f};
+    Row o;
+    o.a = __builtin_elementwise_fma(rc.a, __builtin_elementwise_fma(m6, c.a, S.a + zp.a), c.a);
+    o.b = __builtin_elementwise_fma(rc.b, __builtin_elementwise_fma(m6, c.b, S.b + zp.b), c.b);
+    return o;
+  }
+  static __device__ __forceinline__ Row coef(float r, const bool* held) {
+    return Row{T2{held[1] ? 0.f : r, held[2] ? 0.f : r}, T2{held[0] ? 0.f : r, held[3] ? 0.f : r}};
+  }
+  static __device__ __forceinline__ float get(const Row& c, int e) {
+    return e == 0 ? c.b.x : e == 1 ? c.a.x : e == 2 ? c.a.y : c.b.y;
+  }
+  static __device__ __forceinline__ void set(Row& c, int e, float v) {
+    if (e == 0) c.b.x = v;
+    else if (e == 1) c.a.x = v;
+    else if (e == 2) c.a.y = v;
+    else c.b.y = v;
+  }
+  static __device__ __forceinline__ V vec(const Row& c) { return V{c.b.x, c.a.x, c.a.y, c.b.y}; }
+  // ---- 27-point helpers (box27_tbk) ----
+  static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.a + y.a, x.b + y.b}; }
+  // xm + xp of every cell; l / rr are the cells beyond the slice's ends
+  static __device__ __forceinline__ Row hsum(const Row& c, float l, float rr) {
+    Row h;
+    h.b = T2{l, rr} + c.a;           // (l + e1, rr + e2)
+    h.a = c.b + T2{c.a.y, c.a.x};    // (e0 + e2, e3 + e1)
+    return h;
+  }
+  // fma(k2, d, fma(k1, x, k0 * c)): sm::box27_A / box27_B
+  static __device__ __forceinline__ Row lin3(const Row& c, const Row& x, const Row& d, float k0, float k1, float k2) {
+    const T2 K0{k0, k0}, K1{k1, k1}, K2{k2, k2};
+    Row o;
+    o.a = __builtin_elementwise_fma(K2, d.a, __builtin_elementwise_fma(K1, x.a, K0 * c.a));
+    o.b = __builtin_elementwise_fma(K2, d.b, __builtin_elementwise_fma(K1, x.b, K0 * c.b));
+    return o;
+  }
+  // per cell: held ? h : o
+  static __device__ __forceinline__ Row sel(const bool* held, const Row& h, const Row& o) {
+    Row r;
+    r.b.x = held[0] ? h.b.x : o.b.x;
+    r.a.x = held[1] ? h.a.x : o.a.x;
+    r.a.y = held[2] ? h.a.y : o.a.y;
+    r.b.y = held[3] ? h.b.y : o.b.y;
+    return r;
+  }
+};
+
+template <>
+struct RowOps<double> {
+  typedef double T2 __attribute__((ext_vector_type(2)));
+  typedef T2 V;
+  struct Row {
+    T2 v;
+  };
+  static __device__ __forceinline__ Row lds(const double* p) { return Row{*(const T2*)p}; }
+  static __device__ __forceinline__ Row lds_pairs(const double* p) { return lds(p); }
+  static __device__ __forceinline__ void fence(Row&) {}
+  static __device__ __forceinline__ Row zero() { return Row{T2{0.0, 0.0}}; }
+  static __device__ __forceinline__ double first(const Row& c) { return c.v.x; }
+  static __device__ __forceinline__ double last(const Row& c) { return c.v.y; }
+  static __device__ __forceinline__ T2 edges(const Row& c) { return c.v; }
+  static __device__ __forceinline__ Row partial(const Row& c, double l, double rr, const Row& ym, const Row& yp,
+                                                const Row& zm) {
+    Row s;
+    s.v = T2{l + c.v.y, c.v.x + rr};
+    s.v = ((s.v + ym.v) + yp.v) + zm.v;
+    return s;
+  }
+  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m6 = T2{-6.0, -6.0};
+    return Row{__builtin_elementwise_fma(rc.v, __builtin_elementwise_fma(m6, c.v, S.v + zp.v), c.v)};
+  }
+  static __device__ __forceinline__ Row coef(double r, const bool* held) {
+    return Row{T2{held[0] ? 0.0 : r, held[1] ? 0.0 : r}};
+  }
+  static __device__ __forceinline__ double get(const Row& c, int e) { return e == 0 ? c.v.x : c.v.y; }
+  static __device__ __forceinline__ void set(Row& c, int e, double v) {
+    if (e == 0) c.v.x = v;
+    else c.v.y = v;
+  }
+  static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
+  static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.v + y.v}; }
+  static __device__ __forceinline__ Row hsum(const Row& c, double l, double rr) {
+    return Row{T2{l + c.v.y, c.v.x + rr}};
+  }
+  static __device__ __forceinline__ Row lin3(const Row& c, const Row& x, const Row& d, double k0, double k1,
+                                             double k2) {
+    const T2 K0{k0, k0}, K1{k1, k1}, K2{k2, k2};
+    return Row{__builtin_elementwise_fma(K2, d.v, __builtin_elementwise_fma(K1, x.v, K0 * c.v))};
+  }
+  static __device__ __forceinline__ Row sel(const bool* held, const Row& h, const Row& o) {
+    return Row{T2{held[0] ? h.v.x : o.v.x, held[1] ? h.v.y : o.v.y}};
+  }
+};
+
+}  // namespace dev
+}  // namespace mdfx

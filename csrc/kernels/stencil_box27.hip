@@ -9,8 +9,10 @@
 // cell from HBM). x-neighbours: lane shuffles + LDS for wave edges + one scalar load at the block
 // edge, as in heat7_zw.
 #include <algorithm>
+#include <type_traits>
 
 #include "kcommon.hpp"
+#include "rowops.hpp"
 #include "mdfx/kernels.hpp"
 #include "mdfx/stencil_math.hpp"
 
@@ -18,6 +20,8 @@ namespace mdfx {
 namespace dev {
 
 int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target);
+int64_t resident_blocks(const void* kfn);
+int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
 
 template <class V, class T>
 __device__ __forceinline__ V vsplat27(T v) {
@@ -421,6 +425,236 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
   if (RES) wave_atomic_add(resid, acc);
 }
 
+// ---- K steps per sweep, streaming levels (box27_tbk) ---------------------------------------------
+//
+// heat7_tbk's organisation applied to the 27-point update: u0 planes arrive by LDS DMA (each wave
+// its own RY + 2K rows plus the x-seam vectors, one plane ahead), and every level k = 1..K is a
+// streaming z-march over RY + 2(K-k) rows whose state per row is the partial-sum pipeline of
+// box27_zw: A = A(p-1), S = A(p-2) + B(p-1) and the centre C = u(p-1). When plane p of u_{k-1}
+// arrives, the level forms its x sums H = xm + xp (DPP shifts, seams from LDS), then per row
+//   cross = H + (ym + yp), diag = Hm + Hp, a = box27_A, b = box27_B
+//   u_k(p-1) = S + a;  S = A + b;  A = a;  C = centre
+// -- box27_combine's order, so the result is bitwise equal to K single box27_zw steps. Rows sit in
+// the pair layout of RowOps (fp32: every operation a packed v_pk op, the x sums without moves).
+// Held cells (x / y / z boundary) keep their centre through a select that only the waves and
+// levels that contain such cells execute. Seams of levels 1..K-1: double-buffered LDS edge table,
+// one barrier per level and plane. Region contract as heat7_tbk: u0 valid on [lz_begin - K, lz_end + K).
+template <class T, int RY, int K, int WXN, bool RES>
+__global__ __launch_bounds__(256) void box27_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
+                                                 T c2, T c3, int zc, int YT, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  using RO = RowOps<T>;
+  using Row = typename RO::Row;
+  constexpr int N = VT<T>::N;
+  constexpr int WX = 64 * N;
+  constexpr int WYN = 4 / WXN;
+  constexpr int R0 = RY + 2 * K;              // u0 window rows y0-K .. y0+RY+K-1
+  constexpr int TOT = tbk_off<RY, K>(K + 1);  // state rows over all levels
+  constexpr int NLV = K > 1 ? K - 1 : 1;
+  static_assert(R0 <= 32, "seam DMA uses lanes 0..R0-1 and 32..32+R0-1");
+  __shared__ V slot[4][R0 + 1][64];  // per-wave u0 plane; row R0 holds the seam vectors
+  constexpr int TB_ROW = 4, TB_W = R0 * TB_ROW, TB_PAR = 4 * TB_W, TB_LV = 2 * TB_PAR;
+  __shared__ __attribute__((aligned(16))) T tb[NLV * TB_LV + 4];
+
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int yt = t % YT;
+  const int zt = t / YT;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wx = w % WXN, wy = w / WXN;
+  const int64_t xw = (int64_t)wx * WX;
+  const uint32_t xo = (uint32_t)lane * N;
+  const int64_t x = xw + xo;
+  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  T* ob = out + y0 * pitch + xw;
+
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  // wave-uniform: does this wave hold any x-boundary cell, are all computed rows y-interior
+  const bool xedge = xw == 0 || xw + WX >= g.nx;
+  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= g.ny - 2;
+
+  // ---- u0 streaming (heat7_tbk's DMA: clamped in-bounds addresses, 32-bit lane offsets) ---------
+  const bool has_l = xw > 0 && xw < pitch, has_r = xw + WX < pitch;
+  const int srow = lane & 31;
+  const bool son = lane < 32 ? (has_l && srow < R0) : (WXN > 1 && has_r && srow < R0);
+  const uint32_t xcb = (uint32_t)((xin ? x : pitch - N) * (int64_t)sizeof(T));
+  const uint32_t socb = son ? (uint32_t)((lane < 32 ? xw - N : xw + WX) * (int64_t)sizeof(T)) : xcb;
+  const T* ib0 = in + (y0 - K) * pitch;
+  auto rowc = [&](int k) -> int64_t {
+    const int64_t y = y0 - K + k;
+    return (y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y) - (y0 - K);
+  };
+  const int64_t srowc = rowc(srow < R0 ? srow : 0);
+  auto issue = [&](int64_t lz) {
+    const T* pb = ib0 + lz * plane;
+#pragma unroll
+    for (int k = 0; k < R0; ++k) {
+      const T* a = (const T*)((const char*)(pb + rowc(k) * pitch) + xcb);
+      dcheck(g, in, a, N);
+      glds16(a, &slot[w][k][0]);
+    }
+    if (WXN > 1) {
+      const T* a = (const T*)((const char*)(pb + srowc * pitch) + socb);
+      dcheck(g, in, a, N);
+      glds16(a, &slot[w][R0][0]);
+    }
+  };
+  const int wl = wx > 0 ? w - 1 : w, wr = wx < WXN - 1 ? w + 1 : w;
+  const T* base1 = lane < 32 ? &tb[2 + wl * TB_W + 2 + 1] : &tb[2 + wr * TB_W + 0 - 1];
+  T* wrp = &tb[2 + w * TB_W + (lane == 0 ? 0 : 2)];
+
+  Row A[TOT], S[TOT], C[TOT];
+#pragma unroll
+  for (int i = 0; i < TOT; ++i) {
+    A[i] = RO::zero();
+    S[i] = RO::zero();
+    C[i] = RO::zero();
+  }
+  double acc = 0.0;
+  const int64_t cend = ze + K;
+  const T* base0 = (const T*)&slot[w][R0][0] + (lane < 32 ? N - 1 : 0);
+  issue(zs - K);
+  for (int64_t c = zs - K; c < cend; ++c) {
+    const int par = (int)(c & 1);
+    wait_vm0();  // this wave's DMA of plane c has landed
+    Row X[R0];
+    T LO[R0], HI[R0];
+#pragma unroll
+    for (int k = 0; k < R0; ++k) {
+      X[k] = RO::lds_pairs((const T*)&slot[w][k][lane]);
+      // a wave edge without a neighbouring wave has no DMA'd seam (stale LDS): 0 instead
+      LO[k] = has_l ? base0[k * N] : T(0);
+      HI[k] = (WXN > 1 && has_r) ? base0[k * N + 32 * N] : T(0);
+    }
+    wait_lgkm0();  // slot consumed: refill it with the next plane while the levels compute
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < R0; ++k) RO::fence(X[k]);
+    if (c + 1 < cend) issue(c + 1);
+
+#pragma unroll
+    for (int k = 1; k <= K; ++k) {
+      const int ROUT = RY + 2 * (K - k);
+      const int off = tbk_off<RY, K>(k);
+      if (c >= zs - K + 2 * k - 2) {  // block-uniform pipeline fill
+        if (k >= 2 && WXN > 1) {
+          const T* b1 = base1 + (k - 2) * TB_LV + par * TB_PAR;
+#pragma unroll
+          for (int j = 0; j < ROUT + 2; ++j) {
+            LO[j] = b1[j * TB_ROW];
+            HI[j] = b1[j * TB_ROW + 1];
+          }
+        }
+        const int64_t gz = c - k + g.gz_off;  // plane finished by this level: c - k
+        const bool zh = gz <= 0 || gz >= g.gnz - 1;
+        Row H[R0], Y[R0];
+#pragma unroll
+        for (int j = 0; j < ROUT + 2; ++j) {
+          const T l = lane_up1_or(LO[j], RO::last(X[j]));
+          const T rr = lane_down1_or(HI[j], RO::first(X[j]));
+          H[j] = RO::hsum(X[j], l, rr);
+        }
+        auto rows = [&](auto hold) __attribute__((always_inline)) {
+          constexpr bool HOLD = decltype(hold)::value;
+#pragma unroll
+          for (int i = 0; i < ROUT; ++i) {
+            const Row cen = X[i + 1];
+            const Row cross = RO::add(H[i + 1], RO::add(X[i], X[i + 2]));
+            const Row diag = RO::add(H[i], H[i + 2]);
+            const Row a = RO::lin3(cen, cross, diag, c1, c2, c3);
+            const Row b = RO::lin3(cen, cross, diag, c0, c1, c2);
+            const Row cold = C[off + i];
+            Row o = RO::add(S[off + i], a);
+            if (HOLD) {
+              const int64_t y = y0 - (K - k) + i;
+              const bool rh = zh || y <= 0 || y >= g.ny - 1;
+              bool h[N];
+#pragma unroll
+              for (int e = 0; e < N; ++e) h[e] = rh || xb[e];
+              o = RO::sel(h, cold, o);
+            }
+            S[off + i] = RO::add(A[off + i], b);
+            A[off + i] = a;
+            C[off + i] = cen;
+            Y[i] = o;
+            if (RES && k == K && c >= zs + K && y0 + i < g.ny && xin) {
+#pragma unroll
+              for (int e = 0; e < N; ++e)
+                if (x + e < g.nx) {
+                  const double d = (double)RO::get(o, e) - (double)RO::get(cold, e);
+                  acc += d * d;
+                }
+            }
+          }
+        };
+        if (zh || xedge || !yint)
+          rows(std::integral_constant<bool, true>{});
+        else
+          rows(std::integral_constant<bool, false>{});
+        if (k < K) {
+          if (WXN > 1) {  // publish the edge pairs of every row: the next level's whole window
+            if (lane == 0 || lane == 63) {
+              T* wp = wrp + (k - 1) * TB_LV + par * TB_PAR;
+#pragma unroll
+              for (int j = 0; j < ROUT; ++j) lds_store(wp + j * TB_ROW, RO::edges(Y[j]));
+            }
+            lds_barrier();
+          }
+#pragma unroll
+          for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
+        } else if (c >= zs + K) {  // u_K(c - K) is an owned output plane
+          const int64_t lz = c - K;
+#pragma unroll
+          for (int i = 0; i < RY; ++i) {
+            if (y0 + i < g.ny && xin) {
+              T* a = (T*)((char*)(ob + lz * plane + (int64_t)i * pitch) + xo * (uint32_t)sizeof(T));
+              dcheck(g, (const T*)out, a, N);
+              store_nt((V*)a, RO::vec(Y[i]));
+            }
+          }
+        }
+      }
+    }
+  }
+  wait_vm0();  // no DMA may outlive the wave
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T, int RY, int K, int WXN>
+static void launch_box27_tbk_w(const Geo& g, const T* in, T* out, const StencilCoef& cf, double* resid,
+                               hipStream_t s) {
+  constexpr int WYN = 4 / WXN;
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
+  int zc = knobs().zc;
+  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks((const void*)&box27_tbk<T, RY, K, WXN, false>), K);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
+  const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
+  if (resid)
+    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+  else
+    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+}
+
+template <class T, int RY, int K>
+static void launch_box27_tbk_ry(const Geo& g, const T* in, T* out, const StencilCoef& cf, double* resid,
+                                hipStream_t s) {
+  constexpr int WX = 64 * VT<T>::N;
+  if (g.pitch > 2 * WX)
+    launch_box27_tbk_w<T, RY, K, 4>(g, in, out, cf, resid, s);
+  else if (g.pitch > WX)
+    launch_box27_tbk_w<T, RY, K, 2>(g, in, out, cf, resid, s);
+  else
+    launch_box27_tbk_w<T, RY, K, 1>(g, in, out, cf, resid, s);
+}
+
 template <class T>
 bool box27_tb2_supported(const Geo& g) {
   return g.pitch <= 4 * 64 * VT<T>::N && g.ny >= 1;
@@ -470,6 +704,19 @@ static void launch_box27_tb2_ry(const Geo& g, const T* in, T* out, const Stencil
 template <class T>
 void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
+  // fp64: box27_tbk with 4 rows per tile, fp32: box27_tb2 (one MI355X, GCells/s, tb2 / tbk RY 2 /
+  // tbk RY 4: 512^3 fp32 896 / 892 / 857, 1024^3 fp32 1006 / 896 / 970, 512^3 fp64 487 / 460 / 530;
+  // profiles/r02_box27_tbk.txt). MDFX_B27_TBK: -1 box27_tb2, 1 / 2 / 4 box27_tbk with that many rows.
+  const int ry = knobs().b27_tbk != 0 ? knobs().b27_tbk : std::is_same<T, double>::value ? 4 : -1;
+  if (ry > 0) {
+    if (ry == 1 || g.ny < 8)
+      launch_box27_tbk_ry<T, 1, 2>(g, in, out, c, resid, s);
+    else if (ry == 4)
+      launch_box27_tbk_ry<T, 4, 2>(g, in, out, c, resid, s);
+    else
+      launch_box27_tbk_ry<T, 2, 2>(g, in, out, c, resid, s);
+    return;
+  }
   if (knobs().tb_ry == 1 || g.ny < 8)
     launch_box27_tb2_ry<T, 1>(g, in, out, c, resid, s);
   else

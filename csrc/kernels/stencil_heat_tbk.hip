@@ -39,6 +39,7 @@
 #include <type_traits>
 
 #include "kcommon.hpp"
+#include "rowops.hpp"
 #include "mdfx/kernels.hpp"
 #include "mdfx/stencil_math.hpp"
 
@@ -47,117 +48,12 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn);
 
-// first row of level k (1..K) in the flat per-level state arrays
-template <int RY, int K>
-__host__ __device__ constexpr int tbk_off(int k) {
-  return (k - 1) * RY + 2 * ((k - 1) * K - (k - 1) * k / 2);
-}
-
-// One lane's slice of a row, in the register layout the arithmetic wants.
-//  fp32: the 4 cells as two aligned pairs a = (e1, e2), b = (e0, e3). Then
-//        x sums (xm + xp) = { (l, rr) + a , b + swap(a) }  -> 2 v_pk_add_f32,
-//        and every y / z / update operation is one packed op per pair, with no lane shuffles
-//        or register moves to form misaligned pairs (natural (e0,e1),(e2,e3) pairs need them).
-//  fp64: the 2 cells as they are (no packed fp64 arithmetic on CDNA).
-// `E` is the edge pair (e0, e_{N-1}) the neighbouring waves need.
-template <class T>
-struct RowOps;
-
-template <>
-struct RowOps<float> {
-  typedef float T2 __attribute__((ext_vector_type(2)));
-  typedef float V __attribute__((ext_vector_type(4)));
-  struct Row {
-    T2 a, b;
-  };
-  // natural 16-B vector at p (one ds_read_b128), regrouped into the pair layout
-  static __device__ __forceinline__ Row lds(const float* p) {
-    const V v = *(const V*)p;
-    Row r;
-    r.a = T2{v.y, v.z};
-    r.b = T2{v.x, v.w};
-    return r;
-  }
-  static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}, T2{0.f, 0.f}}; }
-  static __device__ __forceinline__ float first(const Row& c) { return c.b.x; }
-  static __device__ __forceinline__ float last(const Row& c) { return c.b.y; }
-  static __device__ __forceinline__ T2 edges(const Row& c) { return c.b; }
-  // (((xm + xp) + ym) + yp) + zm
-  static __device__ __forceinline__ Row partial(const Row& c, float l, float rr, const Row& ym, const Row& yp,
-                                                const Row& zm) {
-    const T2 lr = T2{l, rr};
-    const T2 sa = T2{c.a.y, c.a.x};
-    Row s;
-    s.b = lr + c.a;  // (l + e1, rr + e2)
-    s.a = c.b + sa;  // (e0 + e2, e3 + e1)
-    s.a = ((s.a + ym.a) + yp.a) + zm.a;
-    s.b = ((s.b + ym.b) + yp.b) + zm.b;
-    return s;
-  }
-  // fma(r, fma(-6, c, S + zp), c) with a per-cell coefficient in the Row layout (0 = held)
-  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
-    const T2 m6 = T2{-6.f, -6.f};
-    Row o;
-    o.a = __builtin_elementwise_fma(rc.a, __builtin_elementwise_fma(m6, c.a, S.a + zp.a), c.a);
-    o.b = __builtin_elementwise_fma(rc.b, __builtin_elementwise_fma(m6, c.b, S.b + zp.b), c.b);
-    return o;
-  }
-  static __device__ __forceinline__ Row coef(float r, const bool* held) {
-    return Row{T2{held[1] ? 0.f : r, held[2] ? 0.f : r}, T2{held[0] ? 0.f : r, held[3] ? 0.f : r}};
-  }
-  static __device__ __forceinline__ float get(const Row& c, int e) {
-    return e == 0 ? c.b.x : e == 1 ? c.a.x : e == 2 ? c.a.y : c.b.y;
-  }
-  static __device__ __forceinline__ void set(Row& c, int e, float v) {
-    if (e == 0) c.b.x = v;
-    else if (e == 1) c.a.x = v;
-    else if (e == 2) c.a.y = v;
-    else c.b.y = v;
-  }
-  static __device__ __forceinline__ V vec(const Row& c) { return V{c.b.x, c.a.x, c.a.y, c.b.y}; }
-};
-
-template <>
-struct RowOps<double> {
-  typedef double T2 __attribute__((ext_vector_type(2)));
-  typedef T2 V;
-  struct Row {
-    T2 v;
-  };
-  static __device__ __forceinline__ Row lds(const double* p) { return Row{*(const T2*)p}; }
-  static __device__ __forceinline__ Row zero() { return Row{T2{0.0, 0.0}}; }
-  static __device__ __forceinline__ double first(const Row& c) { return c.v.x; }
-  static __device__ __forceinline__ double last(const Row& c) { return c.v.y; }
-  static __device__ __forceinline__ T2 edges(const Row& c) { return c.v; }
-  static __device__ __forceinline__ Row partial(const Row& c, double l, double rr, const Row& ym, const Row& yp,
-                                                const Row& zm) {
-    Row s;
-    s.v = T2{l + c.v.y, c.v.x + rr};
-    s.v = ((s.v + ym.v) + yp.v) + zm.v;
-    return s;
-  }
-  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
-    const T2 m6 = T2{-6.0, -6.0};
-    return Row{__builtin_elementwise_fma(rc.v, __builtin_elementwise_fma(m6, c.v, S.v + zp.v), c.v)};
-  }
-  static __device__ __forceinline__ Row coef(double r, const bool* held) {
-    return Row{T2{held[0] ? 0.0 : r, held[1] ? 0.0 : r}};
-  }
-  static __device__ __forceinline__ double get(const Row& c, int e) { return e == 0 ? c.v.x : c.v.y; }
-  static __device__ __forceinline__ void set(Row& c, int e, double v) {
-    if (e == 0) c.v.x = v;
-    else c.v.y = v;
-  }
-  static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
-};
-
 template <class T, int RY, int K, int WXN, bool RES>
 __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                  int zc, int YT, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
   using Row = typename RO::Row;
-  using T2 = typename RO::T2;
   constexpr int N = VT<T>::N;
   constexpr int WX = 64 * N;
   constexpr int WYN = 4 / WXN;
@@ -322,7 +218,11 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
             if (lane == 0 || lane == 63) {
               T* wp = wrp + (k - 1) * TB_LV + par * TB_PAR;
 #pragma unroll
-              for (int j = 1; j < ROUT - 1; ++j) *(T2*)(wp + j * TB_ROW) = RO::edges(Y[j]);
+              // a compiler-visible store: hipcc drains this wave's in-flight DMA (vmcnt(0)) before
+              // it. Measured faster here than lds_store() without the drain (1024^3 fp32 K=2 1274
+              // vs 1125 GCells/s, K=3 1121 vs 1071); the occupancy-1 kernels (K=4, box27_tbk)
+              // gain from lds_store() instead (profiles/r02_lds_store_drain.txt)
+              for (int j = 1; j < ROUT - 1; ++j) *(typename RO::T2*)(wp + j * TB_ROW) = RO::edges(Y[j]);
             }
             lds_barrier();
           }
@@ -362,7 +262,7 @@ namespace dev {
 // best of 3 x 20): zc 128 / 64 / 43 -> 1025 / 1358 / 1082 GCells/s.
 static std::atomic<int> g_min_rounds{1};
 
-static int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
+int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
   (void)K;
   const double per_slot = (double)planes * (double)tiles / (double)resident;
   const int64_t rounds = std::max<int64_t>(g_min_rounds.load(std::memory_order_relaxed),

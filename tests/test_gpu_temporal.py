@@ -70,6 +70,35 @@ def test_fused_two_steps_bitwise(hip, prob, tbry, knob):
     assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
+BOX27 = [models.box27(nx=1024, ny=11, nz=9), models.box27(nx=512, ny=21, nz=15),
+         models.box27(nx=300, ny=9, nz=12, dtype="f64"), models.box27(nx=64, ny=40, nz=10),
+         models.box27(nx=500, ny=30, nz=13, dtype="f64", c0=0.3, c1=0.05, c2=0.02, c3=0.01),
+         models.box27(nx=200, ny=5, nz=9)]
+
+
+@pytest.mark.parametrize("prob", BOX27, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("kernel", ["-1", "1", "2", "4"])
+def test_box27_fused_kernels_bitwise(hip, prob, kernel, knob):
+    """Both fused 27-point kernels (MDFX_B27_TBK=-1: box27_tb2; 1 / 2 / 4: box27_tbk with that
+    many rows per tile) == two naive single steps, bitwise, with the residual of step 2."""
+    knob("MDFX_B27_TBK", kernel)
+    lay = FieldLayout.make(prob, halo=2)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=2, resid=res)
+    set_kernel_variant("naive")
+    try:
+        ref, ref_res = _two_single_steps(prob, lay, src, "cuda")
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], ref[o, :, :lay.nx])
+    assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
 def test_fused_region_on_a_slab_with_ghosts(hip):
     """A middle slab (z0 > 0, z1 < nz) with 2 ghost planes each side, interior + boundary regions."""
     prob = models.heat3d(nx=512, ny=16, nz=30)
@@ -146,8 +175,9 @@ def test_engine_temporal2_life(hip, ranks):
     assert np.array_equal(ref, got) and rr == rg
 
 
-def test_engine_temporal2_box27(hip):
-    prob = mm.box27(nx=512, ny=40, nz=50)
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_engine_temporal2_box27(hip, dtype):
+    prob = mm.box27(nx=512, ny=40, nz=50, dtype=dtype)
     ref, rr = _sim(prob, 9, ranks=1, residual_every=9)
     got, rg = _sim(prob, 9, ranks=3, temporal=2, residual_every=9)
     assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
