@@ -91,9 +91,10 @@ def test_multiprocess_gpu_matches_single(hip, tmp_path, world, temporal):
 
 
 def test_bench_distributed_rccl_world1(hip):
-    """bench.py through the distributed path (gloo control plane + native RCCL transport)."""
+    """bench.py through the distributed path (gloo control plane + native RCCL transport; with
+    --transport auto the short trials may pick ipc instead, so the transport is named)."""
     outs = _spawn(1, lambda r: [sys.executable, os.path.join(ROOT, "bench.py"), "--n", "256", "--steps", "6",
-                                "--warmup", "2"], env_extra={"MDFX_FORCE_DIST": "1"})
+                                "--warmup", "2", "--transport", "rccl"], env_extra={"MDFX_FORCE_DIST": "1"})
     rec = json.loads([l for l in outs[0].splitlines() if l.startswith("{")][0])
     assert rec["value"] > 0 and "rccl" in rec["config"]["parallelism"]
 
