@@ -4,9 +4,9 @@
 // row the lane loads 16 cells with one dwordx4 and evaluates them bit-parallel (SWAR) in two
 // 64-bit words: column sums S = north + centre + south (bytes <= 3), then T = S(x-1) + S + S(x+1)
 // via byte shifts with the carry byte taken from the neighbouring lane (DPP shift) or, at the
-// wave edge, from scalar loads; alive' = (T == 3) | (alive & (T == 4)) with exact per-byte
-// equality tests. Reference: game_of_life kernel.cu:10-68 (one int per cell, 8 scalar loads per
-// cell, dead edge branches D9) -> 1 B read + 1 B written per cell here.
+// wave edge, from scalar loads; alive' = ((T - alive) | alive) == 3 (the B3/S23 rule in one
+// exact per-byte comparison, life_next). Reference: game_of_life kernel.cu:10-68 (one int per
+// cell, 8 scalar loads per cell, dead edge branches D9) -> 1 B read + 1 B written per cell here.
 #include <algorithm>
 
 #include "kcommon.hpp"
@@ -22,11 +22,13 @@ struct U2 {
   uint64_t lo, hi;
 };
 
-__device__ __forceinline__ uint64_t bytes_eq(uint64_t t, uint64_t k) {
-  // bytes of t are < 0x80: exact zero-byte detection of t ^ k, result 0x01 per equal byte.
-  const uint64_t x = t ^ (k * 0x0101010101010101ull);
-  const uint64_t z = ~((x + 0x7F7F7F7F7F7F7F7Full) | x) & 0x8080808080808080ull;
-  return z >> 7;
+// B3/S23 on 8 cells at once. t = 3x3 sum including the cell (bytes 0..9), c = the cell (0 / 1).
+// With n = t - c the neighbour count, the cell lives next iff n == 3 or (c and n == 2), i.e.
+// iff (n | c) == 3: one byte compare instead of two. u = (n | c) ^ 3 is at most 11 per byte, so
+// u + 0x7F sets bit 7 exactly when u != 0 and never carries into the next byte. 0x01 per live byte.
+__device__ __forceinline__ uint64_t life_next(uint64_t t, uint64_t c) {
+  const uint64_t u = ((t - c) | c) ^ 0x0303030303030303ull;
+  return (~(u + 0x7F7F7F7F7F7F7F7Full) & 0x8080808080808080ull) >> 7;
 }
 
 template <bool RES>
@@ -87,8 +89,8 @@ __global__ __launch_bounds__(256) void life_wave(const uint8_t* __restrict__ in,
       const U2 L{(S.lo << 8) | sl, (S.hi << 8) | (S.lo >> 56)};
       const U2 R{(S.lo >> 8) | (S.hi << 56), (S.hi >> 8) | (sr << 56)};
       const U2 T{L.lo + S.lo + R.lo, L.hi + S.hi + R.hi};
-      o.lo = bytes_eq(T.lo, 3) | (C.lo & bytes_eq(T.lo, 4));
-      o.hi = bytes_eq(T.hi, 3) | (C.hi & bytes_eq(T.hi, 4));
+      o.lo = life_next(T.lo, C.lo);
+      o.hi = life_next(T.hi, C.hi);
       if (x == 0 || x + N > g.nx - 1) {  // frame or pad cells in this lane: copy through
 #pragma unroll
         for (int e = 0; e < N; ++e) {
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(256) void life_tb2(const uint8_t* __restrict__ in, 
     const U2 L{(S.lo << 8) | sl, (S.hi << 8) | (S.lo >> 56)};
     const U2 R{(S.lo >> 8) | (S.hi << 56), (S.hi >> 8) | (sr << 56)};
     const U2 T{L.lo + S.lo + R.lo, L.hi + S.hi + R.hi};
-    U2 o{bytes_eq(T.lo, 3) | (C.lo & bytes_eq(T.lo, 4)), bytes_eq(T.hi, 3) | (C.hi & bytes_eq(T.hi, 4))};
+    U2 o{life_next(T.lo, C.lo), life_next(T.hi, C.hi)};
     if (frame) {
 #pragma unroll
       for (int e = 0; e < N; ++e) {
@@ -332,16 +334,16 @@ __global__ __launch_bounds__(256) void life_tbk(const uint8_t* __restrict__ in, 
     }
     return U2{0, 0};
   };
-  auto gen = [&](const U2& P, const U2& C, const U2& Nn, int64_t gz, bool inner_only) -> U2 {
+  // one generation of a row from S = its column sums (north + centre + south) and its centre C
+  auto gen = [&](const U2& S, const U2& C, int64_t gz, bool inner_only) -> U2 {
     const bool bnd = inner_only ? (gz == 0 || gz == g.gnz - 1) : (gz <= 0 || gz >= g.gnz - 1);
     if (bnd) return C;
-    const U2 S{P.lo + C.lo + Nn.lo, P.hi + C.hi + Nn.hi};
     const uint64_t sl = (uint32_t)lane_up1((int)(S.hi >> 56));
     const uint64_t sr = (uint32_t)lane_down1((int)(S.lo & 0xFF));
     const U2 L{(S.lo << 8) | sl, (S.hi << 8) | (S.lo >> 56)};
     const U2 R{(S.lo >> 8) | (S.hi << 56), (S.hi >> 8) | (sr << 56)};
     const U2 T{L.lo + S.lo + R.lo, L.hi + S.hi + R.hi};
-    U2 o{bytes_eq(T.lo, 3) | (C.lo & bytes_eq(T.lo, 4)), bytes_eq(T.hi, 3) | (C.hi & bytes_eq(T.hi, 4))};
+    U2 o{life_next(T.lo, C.lo), life_next(T.hi, C.hi)};
     if (frame) {
 #pragma unroll
       for (int e = 0; e < N; ++e) {
@@ -357,45 +359,48 @@ __global__ __launch_bounds__(256) void life_tbk(const uint8_t* __restrict__ in, 
     }
     return o;
   };
-  U2 ring[K][3];
+  // streaming levels: level l (1..K) keeps V = the sum of the last two rows of its input u_{l-1}
+  // and C = the last row; when input row r arrives, S = V + r finishes u_l(r-1) = gen(S, C), then
+  // V = C + r and C = r. No row ring to rotate (the sums are byte-exact, so the order is free).
+  U2 V[K], Cl[K];
 #pragma unroll
-  for (int l = 0; l < K; ++l)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) ring[l][j] = U2{0, 0};
-  ring[0][1] = ld(zs - K - 1);
-  ring[0][2] = ld(zs - K);
+  for (int l = 0; l < K; ++l) V[l] = Cl[l] = U2{0, 0};
+  {
+    const U2 a = ld(zs - K - 1), b = ld(zs - K);
+    V[0] = U2{a.lo + b.lo, a.hi + b.hi};
+    Cl[0] = b;
+  }
   U2 nx = ld(zs - K + 1);
   double acc = 0.0;
   for (int64_t q = zs - K + 1; q <= ze - 1 + K; ++q) {
-    ring[0][0] = ring[0][1];
-    ring[0][1] = ring[0][2];
-    ring[0][2] = nx;
+    U2 X = nx;  // u0(q)
     nx = ld(q + 1);
-#pragma unroll
-    for (int l = 1; l < K; ++l) {
-      const U2 v = gen(ring[l - 1][0], ring[l - 1][1], ring[l - 1][2], q - l + g.gz_off, false);
-      ring[l][0] = ring[l][1];
-      ring[l][1] = ring[l][2];
-      ring[l][2] = v;
-    }
     const int64_t lz = q - K;
-    if (lz >= zs) {
-      const U2 C = ring[K - 1][1];
-      const U2 o = gen(ring[K - 1][0], C, ring[K - 1][2], lz + g.gz_off, true);
-      if (own) {
-        uint4 qv;
-        qv.x = (uint32_t)o.lo;
-        qv.y = (uint32_t)(o.lo >> 32);
-        qv.z = (uint32_t)o.hi;
-        qv.w = (uint32_t)(o.hi >> 32);
-        dcheck(g, (const uint8_t*)out, out + lz * plane + x, N);
-        *(uint4*)(out + lz * plane + x) = qv;
-        if (RES) {
-          const uint64_t dlo = o.lo ^ C.lo, dhi = o.hi ^ C.hi;
-          int cnt = 0;
-          for (int e = 0; e < N; ++e)
-            if (x + e < g.nx) cnt += (int)(((e < 8 ? dlo : dhi) >> (8 * (e & 7))) & 1);
-          acc += (double)cnt;
+#pragma unroll
+    for (int l = 1; l <= K; ++l) {
+      const U2 S{V[l - 1].lo + X.lo, V[l - 1].hi + X.hi};
+      const U2 C = Cl[l - 1];
+      V[l - 1] = U2{C.lo + X.lo, C.hi + X.hi};
+      Cl[l - 1] = X;
+      if (l < K) {
+        X = gen(S, C, q - l + g.gz_off, false);  // u_l(q - l)
+      } else if (lz >= zs) {
+        const U2 o = gen(S, C, lz + g.gz_off, true);
+        if (own) {
+          uint4 qv;
+          qv.x = (uint32_t)o.lo;
+          qv.y = (uint32_t)(o.lo >> 32);
+          qv.z = (uint32_t)o.hi;
+          qv.w = (uint32_t)(o.hi >> 32);
+          dcheck(g, (const uint8_t*)out, out + lz * plane + x, N);
+          *(uint4*)(out + lz * plane + x) = qv;
+          if (RES) {
+            const uint64_t dlo = o.lo ^ C.lo, dhi = o.hi ^ C.hi;
+            int cnt = 0;
+            for (int e = 0; e < N; ++e)
+              if (x + e < g.nx) cnt += (int)(((e < 8 ? dlo : dhi) >> (8 * (e & 7))) & 1);
+            acc += (double)cnt;
+          }
         }
       }
     }
