@@ -13,6 +13,8 @@ run c5_heat7_2048_f64_resid --n 2048 --dtype f64 --steps 20 --warmup 2 --residua
 run x_heat7_1024_f64 --n 1024 --dtype f64 --steps 30 --warmup 5 || exit 1
 run x_mdf2d_16k_f32 --stencil jacobi5 --nx 16384 --nz 16384 --steps 100 --warmup 10 || exit 1
 run x_life_32k --stencil life --dtype u8 --nx 32768 --nz 32768 --steps 100 --warmup 10 || exit 1
+run x_box27_1024_f32 --stencil box27 --n 1024 --steps 20 --warmup 4 || exit 1
+run x_mdf2d_16k_f64 --stencil jacobi5 --dtype f64 --nx 16384 --nz 16384 --steps 100 --warmup 10 || exit 1
 run x_heat7_1024_f32_v8 --n 1024 --steps 50 --warmup 10 --virtual-ranks 8 || exit 1
 run x_heat7_1024_f32_ipc2 --n 1024 --steps 50 --warmup 10 --gpus 2 --share-gpu --transport ipc || exit 1
 run x_heat7_1024_f32_ipc8 --n 1024 --steps 50 --warmup 10 --gpus 8 --share-gpu --transport ipc || exit 1
