@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Host-side emulation of heat7_tbk's global address arithmetic (DMA rows, DMA seams, stores) for
-every block, lane, row and plane of a launch, checked against the allocation. Run before taking a
+every block, lane, row and plane of a launch, checked against the allocation. box27_tbk uses the
+same addressing (K = 2, RY 1 / 2 / 4), so its GPU test shapes are checked here too. Run before taking a
 changed kernel to the GPU: an out-of-bounds index here would be an illegal access there.
 
     python scripts/check_tbk_addresses.py      # the GPU test shapes + the bench shapes
@@ -92,6 +93,9 @@ def check(nx, ny, nz, dtype, K, RY, lz_begin=None, lz_end=None, resident=512):
 SHAPES = [(1024, 37, 23, "f32"), (700, 19, 15, "f32"), (256, 9, 12, "f32"), (500, 21, 11, "f64"),
           (64, 64, 9, "f32"), (1000, 5, 14, "f32"), (300, 40, 10, "f64"), (1024, 20, 40, "f32"),
           (512, 32, 33, "f64")]
+# box27_tbk's GPU test shapes (two fused steps only)
+BOX27 = [(1024, 11, 9, "f32"), (512, 21, 15, "f32"), (300, 9, 12, "f64"), (64, 40, 10, "f32"),
+         (500, 30, 13, "f64"), (200, 5, 9, "f32"), (512, 512, 512, "f64")]
 # rows wider than one block (x tiles, K = 2): the GPU test shapes
 WIDE = [(2048, 13, 11, "f32"), (1100, 9, 9, "f64"), (1030, 7, 8, "f32"), (2048, 21, 12, "f64"),
         (1300, 17, 10, "f32")]
@@ -102,12 +106,13 @@ def main():
     cases = [(s, K, RY) for s in SHAPES for K, rys in ((2, (1, 2, 3, 4)), (3, (1, 2, 3)), (4, (1, 2)))
              for RY in rys]
     cases += [(s, 2, RY) for s in WIDE for RY in (1, 2, 3, 4)]
+    cases += [(s, 2, RY) for s in BOX27 for RY in (1, 2, 4)]
     for (nx, ny, nz, dt), K, RY in cases:
         bad, info = check(nx, ny, nz, dt, K, RY)
         fails += bad > 0
         if bad:
             print("OUT OF BOUNDS", nx, ny, nz, dt, "K", K, "RY", RY, bad, info)
-    print("checked %d shapes x depths: %s" % (len(SHAPES) + len(WIDE),
+    print("checked %d shapes x depths: %s" % (len(SHAPES) + len(WIDE) + len(BOX27),
                                               "FAIL" if fails else "all accesses in bounds"))
     return 1 if fails else 0
 
