@@ -74,6 +74,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
   const int64_t pitch = g.pitch, plane = g.plane;
   const T* ib = in + (y0 - 2) * pitch + xw;  // u0 row r of the window = y0 - 2 + r
   T* ob = out + y0 * pitch + xw;
+  // x-held cells (x = 0, x >= nx - 1) get coefficient 0: u' = fma(0, t, u) = u for finite data,
+  // no per-cell select (y / z holds are whole rows / planes and branch uniformly)
+  T rxe[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) rxe[e] = (x + e == 0 || x + e >= g.nx - 1) ? T(0) : r;
 
   auto ld = [&](int64_t lz, int rr) -> V {
     V v = vsplat_tb<V>(T(0));
@@ -187,9 +192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
           for (int e = 0; e < N; ++e) {
             const T xm = e == 0 ? l : cc[e - 1];
             const T xp = e == N - 1 ? rr : cc[e + 1];
-            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
-            const int64_t xe = x + e;
-            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
+            o[e] = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], rxe[e]);
           }
         }
         U1c[j] = o;
@@ -216,9 +219,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(XT && RY <=
           for (int e = 0; e < N; ++e) {
             const T xm = e == 0 ? l : cc[e - 1];
             const T xp = e == N - 1 ? rr : cc[e + 1];
-            const T v = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], r);
-            const int64_t xe = x + e;
-            o[e] = (xe == 0 || xe >= g.nx - 1) ? cc[e] : v;
+            o[e] = sm::heat7<T>(cc[e], xm, xp, ym[e], yp[e], zm[e], zp[e], rxe[e]);
           }
         }
         if (xin) {
