@@ -119,8 +119,9 @@ __device__ __forceinline__ void lds_store(void* p, const V& v) {
 // a VALU move with a DPP modifier instead of a ds_bpermute through the LDS crossbar. The lane that
 // has no source (0 or 63) receives 0; callers overwrite it with the seam value.
 #ifndef MDFX_NO_DPP
-__device__ __forceinline__ int dpp_shr1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }
-__device__ __forceinline__ int dpp_shl1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, false); }
+// bound_ctrl on: the lane without a source reads 0 with no `old` operand to materialise first
+__device__ __forceinline__ int dpp_shr1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int dpp_shl1_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, true); }
 __device__ __forceinline__ int lane_up1(int v) { return dpp_shr1_i(v); }
 __device__ __forceinline__ int lane_down1(int v) { return dpp_shl1_i(v); }
 __device__ __forceinline__ float lane_up1(float v) { return __int_as_float(dpp_shr1_i(__float_as_int(v))); }

@@ -1,5 +1,5 @@
 // Register layouts and arithmetic of one lane's 16-B row slice for the streaming multi-level
-// kernels (heat7_tbk, box27_tbk), plus the flat per-level state indexing they share.
+// kernels (heat7_tbk, box27_tbk, jacobi5_tbk), plus the flat per-level state indexing they share.
 #pragma once
 
 #include "kcommon.hpp"
@@ -74,6 +74,14 @@ struct RowOps<float> {
     o.b = __builtin_elementwise_fma(rc.b, __builtin_elementwise_fma(m6, c.b, S.b + zp.b), c.b);
     return o;
   }
+  // fma(r, fma(-4, c, S + zp), c): sm::jacobi5 with S = (xm + xp) + zm
+  static __device__ __forceinline__ Row fin4(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m4 = T2{-4.f, -4.f};
+    Row o;
+    o.a = __builtin_elementwise_fma(rc.a, __builtin_elementwise_fma(m4, c.a, S.a + zp.a), c.a);
+    o.b = __builtin_elementwise_fma(rc.b, __builtin_elementwise_fma(m4, c.b, S.b + zp.b), c.b);
+    return o;
+  }
   static __device__ __forceinline__ Row coef(float r, const bool* held) {
     return Row{T2{held[1] ? 0.f : r, held[2] ? 0.f : r}, T2{held[0] ? 0.f : r, held[3] ? 0.f : r}};
   }
@@ -139,6 +147,10 @@ struct RowOps<double> {
   static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
     const T2 m6 = T2{-6.0, -6.0};
     return Row{__builtin_elementwise_fma(rc.v, __builtin_elementwise_fma(m6, c.v, S.v + zp.v), c.v)};
+  }
+  static __device__ __forceinline__ Row fin4(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m4 = T2{-4.0, -4.0};
+    return Row{__builtin_elementwise_fma(rc.v, __builtin_elementwise_fma(m4, c.v, S.v + zp.v), c.v)};
   }
   static __device__ __forceinline__ Row coef(double r, const bool* held) {
     return Row{T2{held[0] ? 0.0 : r, held[1] ? 0.0 : r}};

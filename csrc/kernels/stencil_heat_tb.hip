@@ -22,11 +22,13 @@
 // Region contract: output storage planes [lz_begin, lz_end) need u0 valid on
 // [lz_begin - 2, lz_end + 2): the engine keeps 2 ghost planes (halo = 2) when temporal blocking is on.
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <map>
 #include <mutex>
 
 #include "kcommon.hpp"
+#include "rowops.hpp"
 #include "mdfx/kernels.hpp"
 #include "mdfx/stencil_math.hpp"
 
@@ -491,11 +493,14 @@ template <class T, int K, bool RES>
 __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                    int zc, int XT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
+  using RO = RowOps<T>;
+  using Row = typename RO::Row;
   constexpr int N = VT<T>::N;
   constexpr int OV = (K + N - 1) / N;  // overlap lanes per side
   constexpr int SEG = (64 - 2 * OV) * N;  // owned columns per wave
   const int lane = threadIdx.x & 63;
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  // wave-uniform task index in an SGPR, so every row index and row test below is scalar
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (task >= ntasks) return;  // wave-uniform; no block barriers in this kernel
   const int xt = task % XT, zt = task / XT;
   const int64_t x = (int64_t)xt * SEG - OV * N + (int64_t)lane * N;
@@ -504,66 +509,75 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   const bool xin = x >= 0 && x < g.pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
   const int64_t plane = g.plane;
-  V rx;  // per-cell coefficient: 0 on the held columns x = 0, x >= nx - 1
+  // rows live in RowOps' pair layout (fp32: packed ops without register moves between levels);
+  // per-cell coefficient 0 on the held columns x = 0, x >= nx - 1
+  bool held[N];
 #pragma unroll
-  for (int e = 0; e < N; ++e) rx[e] = ((x + e == 0) || (x + e >= g.nx - 1)) ? T(0) : r;
-  const V r0 = vsplat_tb<V>(T(0));
-  auto ld = [&](int64_t lz) -> V {
-    V v = vsplat_tb<V>(T(0));
-    if (xin && lz >= 0 && lz < g.lz_max) {
-      dcheck(g, in, in + lz * plane + x, N);
-      v = *(const V*)(in + lz * plane + x);
-    }
-    return v;
+  for (int e = 0; e < N; ++e) held[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  const Row rx = RO::coef(r, held);
+  const Row r0 = RO::zero();
+  // Loads without lane predication: lanes outside the row read the nearest in-row vector and rows
+  // past the storage read its last row. Those values are finite and only ever meet held or unowned
+  // cells (the left halo lane of the first segment feeds only x = 0, which is held; lanes beyond
+  // the row feed only x >= nx - 1 and themselves).
+  const T* ib = in + (x < 0 ? 0 : x >= g.pitch ? g.pitch - N : x);
+  auto ld = [&](int64_t lz) -> Row {
+    const int64_t lzc = lz < 0 ? 0 : lz >= g.lz_max ? g.lz_max - 1 : lz;
+    dcheck(g, in, ib + lzc * plane, N);
+    return RO::lds(ib + lzc * plane);  // a 16-B vector regrouped into the pair layout
   };
-  V S[K], C[K];  // level l = 1..K at index l - 1
+  Row S[K], C[K];  // level l = 1..K at index l - 1
 #pragma unroll
   for (int l = 0; l < K; ++l) {
-    S[l] = vsplat_tb<V>(T(0));
-    C[l] = S[l];
+    S[l] = RO::zero();
+    C[l] = RO::zero();
   }
-  V nx = ld(zs - K);
+  Row nx = ld(zs - K);
   double acc = 0.0;
   // newest u0 row q; level l finishes row q - l (each level's first two rows are priming garbage
   // that no level needs)
+  // rows of the chunk's pipeline (zs - K - 1 .. ze + K - 1) that are all interior in z need no
+  // z test: one loop copy without it, one with the per-level test for chunks at the z boundary
+  const bool zint = zs - K - 1 + g.gz_off >= 1 && ze + K - 1 + g.gz_off <= g.gnz - 2;
+  auto march = [&](auto ztest) __attribute__((always_inline)) {
+  constexpr bool ZT = decltype(ztest)::value;
   for (int64_t q = zs - K; q <= ze - 1 + K; ++q) {
-    V X = nx;
+    Row X = nx;
     nx = ld(q + 1);
 #pragma unroll
     for (int l = 1; l <= K; ++l) {
       const int64_t row = q - l;
       const int64_t gz = row + g.gz_off;
-      const V rc = (gz <= 0 || gz >= g.gnz - 1) ? r0 : rx;
-      const V c = C[l - 1];
-      V o;
-#pragma unroll
-      for (int e = 0; e < N; ++e) o[e] = sm::fmaT(rc[e], sm::fmaT(T(-4), c[e], S[l - 1][e] + X[e]), c[e]);
+      const Row rc = (ZT && (gz <= 0 || gz >= g.gnz - 1)) ? r0 : rx;
+      const Row c = C[l - 1];
+      const Row o = RO::fin4(S[l - 1], X, c, rc);
       // row + 1's partial from the arriving row X: (xm + xp) + zm
-      const T lft = lane_up1(X[N - 1]);
-      const T rgt = lane_down1(X[0]);
-#pragma unroll
-      for (int e = 0; e < N; ++e) {
-        const T xm = e == 0 ? lft : X[e - 1];
-        const T xp = e == N - 1 ? rgt : X[e + 1];
-        S[l - 1][e] = (xm + xp) + c[e];
-      }
+      const T lft = lane_up1(RO::last(X));
+      const T rgt = lane_down1(RO::first(X));
+      S[l - 1] = RO::add(RO::hsum(X, lft, rgt), c);
       C[l - 1] = X;
       if (l < K) {
         X = o;
       } else if (row >= zs && own) {
         dcheck(g, (const T*)out, out + row * plane + x, N);
-        store_nt((V*)(out + row * plane + x), o);
+        store_nt((V*)(out + row * plane + x), RO::vec(o));
         if (RES) {
 #pragma unroll
           for (int e = 0; e < N; ++e)
             if (x + e < g.nx) {
-              const double d = (double)o[e] - (double)c[e];
+              const double d = (double)RO::get(o, e) - (double)RO::get(c, e);
               acc += d * d;
             }
         }
       }
     }
   }
+  };
+  // (fp64: one loop copy with the test; the second copy costs the VGPRs of occupancy 4 at K = 8)
+  if (zint && sizeof(T) == 4)
+    march(std::integral_constant<bool, false>{});
+  else
+    march(std::integral_constant<bool, true>{});
   if (RES) wave_atomic_add(resid, acc);
 }
 
