@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void box27_zw(const T* __restrict__ in, T* __r
   const int yt = (t / XT) % YT;
   const int zt = t / (XT * YT);
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wx = w % WXN, wy = w / WXN;
   const int64_t x = ((int64_t)xt * WXN + wx) * WX + (int64_t)lane * N;
   const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void jacobi5_wave(const T* __restrict__ in, T*
   constexpr int N = VT<T>::N;
   constexpr int WX = 64 * N;
   const int lane = threadIdx.x & 63;
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (task >= ntasks) return;  // wave-uniform; no block barriers in this kernel
   const int xt = task % XT, zt = task / XT;
   const int64_t x = (int64_t)xt * WX + (int64_t)lane * N;

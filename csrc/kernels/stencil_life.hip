@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void life_wave(const uint8_t* __restrict__ in,
   constexpr int N = 16;
   constexpr int WX = 64 * N;
   const int lane = threadIdx.x & 63;
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (task >= ntasks) return;  // wave-uniform, no barriers
   const int xt = task % XT, zt = task / XT;
   const int64_t x = (int64_t)xt * WX + (int64_t)lane * N;
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void life_tb2(const uint8_t* __restrict__ in, 
   constexpr int N = 16;
   constexpr int WX = 64 * N;
   const int lane = threadIdx.x & 63;
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (task >= ntasks) return;  // wave-uniform, no barriers
   const int xt = task % XT, zt = task / XT;
   const int64_t x0 = (int64_t)xt * WX;
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void life_tbk(const uint8_t* __restrict__ in, 
   constexpr int SEG = 62 * N;
   static_assert(K >= 1 && K <= N, "generations must not reach past the halo lanes");
   const int lane = threadIdx.x & 63;
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (task >= ntasks) return;  // wave-uniform, no barriers
   const int xt = task % XT, zt = task / XT;
   const int64_t x = (int64_t)xt * SEG - N + (int64_t)lane * N;
