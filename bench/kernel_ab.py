@@ -3,7 +3,8 @@
 variants interleaved in ONE process, several rounds, best and median reported).
 
 Variants are the native dispatcher's tuning knobs (MDFX_RY, MDFX_ZC, MDFX_BLOCKS, MDFX_TB_RY,
-MDFX_TBK_RY, MDFX_J5_TBK, MDFX_LIFE_TBK; cached by the native layer and re-read per variant) plus
+MDFX_TBK_RY, MDFX_J5_TBK, MDFX_LIFE_TBK, MDFX_B27_TBK; cached by the native layer and re-read per
+variant) plus
 the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
 bitwise against the naive kernel.
 
@@ -25,7 +26,7 @@ from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, i
                                       set_kernel_variant)
 
 KEYS = {"RY": "MDFX_RY", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
-        "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBKRY": "MDFX_TBK_RY"}
+        "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBKRY": "MDFX_TBK_RY", "B27TBK": "MDFX_B27_TBK"}
 
 
 def parse_variant(s):
