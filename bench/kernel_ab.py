@@ -4,8 +4,7 @@ variants interleaved in ONE process, several rounds, best and median reported).
 
 Variants are the native dispatcher's tuning knobs (MDFX_RY, MDFX_ZC, MDFX_BLOCKS, MDFX_TB_RY,
 MDFX_TBK_RY, MDFX_J5_TBK, MDFX_LIFE_TBK, MDFX_B27_TBK; cached by the native layer and re-read per
-variant) plus
-the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
+variant) plus the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
 bitwise against the naive kernel.
 
     python bench/kernel_ab.py --kind heat7 --n 1024 --variants "RY=4;RY=2;STEPS=2;STEPS=2,TBKRY=2"
