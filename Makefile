@@ -125,8 +125,11 @@ $(BIN)/mdfx_tests_devcheck: $(DCK_DIR)/tests/test_main.o $(DCK_KOBJ) $(DCK_HOBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LINK_ROCM) -fopenmp -Wl,-rpath,$(ROCM)/lib
 
 # kernel-variant micro-benchmark (A/B scratch, not part of the engine): make micro
-micro: $(BIN)/s7v
+micro: $(BIN)/s7v $(BIN)/copy_roof
 $(BIN)/s7v: bench/micro/stencil7_variants.hip
+	@mkdir -p $(BIN)
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
+$(BIN)/copy_roof: bench/micro/copy_roof.hip
 	@mkdir -p $(BIN)
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
