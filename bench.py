@@ -323,17 +323,21 @@ def main(argv=None):
             return 3
         cands = ok
 
-    cands = [(t, g, r) for t, g in cands for r in rounds]  # the round count needs no gate of its own
+    # the round count and the overlap mode need no gate of their own (scheduling only; the
+    # overlapped == serialised equality is a test). Several processes: interior || boundary +
+    # exchange (overlap) against one full sweep after the exchange, whichever the trial finds faster.
+    overlaps = [True, False] if (hip and env and world > 1 and not a.no_overlap) else [not a.no_overlap]
+    cands = [(t, g, r, ov) for t, g in cands for r in rounds for ov in overlaps]
     kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap,
               residual_every=a.residual_every, timeout_s=timeout, temporal=temporal)
 
-    def make_sim(transport, graph, rounds=0):
+    def make_sim(transport, graph, rounds=0, overlap=True):
         if env:
             sim = Simulation(prob, distributed=True, transport=transport, graph=graph, **kw)
         else:
             sim = Simulation(prob, ranks=a.virtual_ranks or 1, distributed=False, transport=transport, graph=graph,
                              **kw)
-        sim.set_options(min_rounds=rounds)
+        sim.set_options(min_rounds=rounds, overlap=overlap)
         return sim
 
     def barrier():
@@ -363,18 +367,18 @@ def main(argv=None):
     sim, sim_t = None, None
     if len(cands) > 1:
         n_trial = max(2, min(a.trial_steps, a.steps))
-        for t, g, rr in cands:
+        for t, g, rr, ov in cands:
             if sim is not None and sim_t != t:
                 sim.close()
                 sim = None
             if sim is None:
-                sim, sim_t = make_sim(t, g, rr), t
+                sim, sim_t = make_sim(t, g, rr, ov), t
                 sim.init()
-            sim.set_options(graph=g, min_rounds=rr)
+            sim.set_options(graph=g, min_rounds=rr, overlap=ov)
             sim.run(max(2, min(a.warmup, 4)))
             dt = timed(sim, n_trial)
-            trace("trial %s graph=%s rounds=%s: %.3f ms/step" % (t, g, rr, dt / n_trial * 1e3))
-            trials.append({"transport": sim.transport, "graph": g, "min_rounds": rr,
+            trace("trial %s graph=%s rounds=%s overlap=%s: %.3f ms/step" % (t, g, rr, ov, dt / n_trial * 1e3))
+            trials.append({"transport": sim.transport, "graph": g, "min_rounds": rr, "overlap": ov,
                            "ms_per_step": round(dt / n_trial * 1e3, 4)})
         chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
         if sim_t != chosen[0]:
@@ -384,8 +388,8 @@ def main(argv=None):
         chosen = cands[0]
     if sim is None:
         sim = make_sim(*chosen)
-    sim.set_options(graph=chosen[1], min_rounds=chosen[2])
-    trace("engine up (%s, graph=%s, rounds=%s)" % (sim.transport, chosen[1], chosen[2]))
+    sim.set_options(graph=chosen[1], min_rounds=chosen[2], overlap=chosen[3])
+    trace("engine up (%s, graph=%s, rounds=%s, overlap=%s)" % (sim.transport, chosen[1], chosen[2], chosen[3]))
     sim.init()  # every timed run starts from the same initial grid
     trace("init done")
     sim.run(a.warmup)
@@ -416,7 +420,8 @@ def main(argv=None):
     dram_tbps = per_gpu * prob.bytes_per_cell_per_step / temporal / 1e3
     if rank == 0:
         sim_transport = sim.transport
-        par = ("slab-z%d (1 process/GPU, %s halo, interior||boundary streams)" % (world, sim_transport)
+        par = ("slab-z%d (1 process/GPU, %s halo, %s)" % (
+            world, sim_transport, "interior||boundary streams" if chosen[3] else "exchange then one sweep")
                if env else ("slab-z%d virtual in 1 process (%s)" % (a.virtual_ranks, sim_transport)
                             if a.virtual_ranks > 1 else "single GPU" if hip else "cpu"))
         model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF",
@@ -451,7 +456,7 @@ def main(argv=None):
                 "graph_replays_timed": sim.graph_replays - replays0,
                 "min_rounds": chosen[2] or ("2 (auto)" if nproc > 1 or a.virtual_ranks > 1 else "1 (auto)"),
                 "trials": trials,
-                "overlap": not a.no_overlap,
+                "overlap": chosen[3],
                 "temporal_block": temporal,
                 "gate": gate,
             },
