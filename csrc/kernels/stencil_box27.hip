@@ -250,6 +250,8 @@ template <class T, int RY, int WXN, bool RES, int PF>
 __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0,
                                                  T c1, T c2, T c3, int zc, int YT, double* __restrict__ resid) {
   using V = typename VT<T>::type;
+  using RO = RowOps<T>;  // rows in the pair layout: packed fp32 ops without lane-element shuffles
+  using Row = typename RO::Row;
   constexpr int N = VT<T>::N;
   constexpr int WX = 64 * N;
   constexpr int WYN = 4 / WXN;
@@ -276,111 +278,88 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
 #pragma unroll
   for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
 
-  auto ld = [&](int64_t lz, int k) -> V {
-    V v = vsplat27<V>(T(0));
+  auto ld = [&](int64_t lz, int k) -> Row {
     const int64_t y = y0 - 2 + k;
     if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
       dcheck(g, in, ib + lz * plane + (int64_t)k * pitch + xo, N);
-      v = *(const V*)(ib + lz * plane + (int64_t)k * pitch + xo);
+      return RO::lds(ib + lz * plane + (int64_t)k * pitch + xo);  // 16-B load, regrouped into pairs
     }
-    return v;
+    return RO::zero();
   };
-  // x-neighbour sum of one row vector; `slot` = its seam slot in edge[buf][*]
-  auto hsum = [&](const V& v, int buf, int slot) -> V {
-    T l = lane_up1(v[N - 1]);
-    T r = lane_down1(v[0]);
-    if (lane == 0) l = wx > 0 ? edge[buf][w - 1][slot][1] : T(0);
-    if (lane == 63) r = wx < WXN - 1 ? edge[buf][w + 1][slot][0] : T(0);
-    V h;
-#pragma unroll
-    for (int e = 0; e < N; ++e) h[e] = (e == 0 ? l : v[e - 1]) + (e == N - 1 ? r : v[e + 1]);
-    return h;
+  // x-neighbour sum of one row; `slot` = its seam slot in edge[buf][*] (the wave-edge lanes take
+  // the neighbouring wave's edge cell as DPP's `old` operand)
+  auto hsum = [&](const Row& v, int buf, int slot) -> Row {
+    const T le = wx > 0 ? edge[buf][w - 1][slot][1] : T(0);
+    const T re = wx < WXN - 1 ? edge[buf][w + 1][slot][0] : T(0);
+    return RO::hsum(v, lane_up1_or(le, RO::last(v)), lane_down1_or(re, RO::first(v)));
   };
 
-  V Rw[R0];                   // u0 plane k
-  V A0p[R1], S0[R1], C0[R1];  // A0(k-1); A0(k-2) + B0(k-1); u0 plane k-1 (u1 window rows)
-  V U1[R1];                   // u1 plane k-2
-  V A1p[RY], S1[RY], C1[RY];  // A1(k-3); A1(k-4) + B1(k-3); u1 plane k-3 (owned rows)
+  Row Rw[R0];                   // u0 plane k
+  Row A0p[R1], S0[R1], C0[R1];  // A0(k-1); A0(k-2) + B0(k-1); u0 plane k-1 (u1 window rows)
+  Row U1[R1];                   // u1 plane k-2
+  Row A1p[RY], S1[RY], C1[RY];  // A1(k-3); A1(k-4) + B1(k-3); u1 plane k-3 (owned rows)
 #pragma unroll
   for (int j = 0; j < R0; ++j) Rw[j] = ld(zs - 2, j);
 #pragma unroll
-  for (int j = 0; j < R1; ++j) {
-    A0p[j] = vsplat27<V>(T(0));
-    S0[j] = A0p[j];
-    C0[j] = A0p[j];
-    U1[j] = A0p[j];
-  }
+  for (int j = 0; j < R1; ++j) A0p[j] = S0[j] = C0[j] = U1[j] = RO::zero();
 #pragma unroll
-  for (int i = 0; i < RY; ++i) {
-    A1p[i] = vsplat27<V>(T(0));
-    S1[i] = A1p[i];
-    C1[i] = A1p[i];
-  }
+  for (int i = 0; i < RY; ++i) A1p[i] = S1[i] = C1[i] = RO::zero();
   double acc = 0.0;
   int buf = 0;
   for (int64_t k = zs - 2; k <= ze + 2; ++k) {
-    V NX[R0];
+    Row NX[R0];
     if (PF) {
 #pragma unroll
       for (int j = 0; j < R0; ++j) NX[j] = ld(k + 1, j);
     }
     if (lane == 0) {
 #pragma unroll
-      for (int j = 0; j < R0; ++j) edge[buf][w][j][0] = Rw[j][0];
+      for (int j = 0; j < R0; ++j) edge[buf][w][j][0] = RO::first(Rw[j]);
 #pragma unroll
-      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][0] = U1[j][0];
+      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][0] = RO::first(U1[j]);
     }
     if (lane == 63) {
 #pragma unroll
-      for (int j = 0; j < R0; ++j) edge[buf][w][j][1] = Rw[j][N - 1];
+      for (int j = 0; j < R0; ++j) edge[buf][w][j][1] = RO::last(Rw[j]);
 #pragma unroll
-      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][1] = U1[j][N - 1];
+      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][1] = RO::last(U1[j]);
     }
     lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
 
     // ---- level 1: partials of u1 plane k-2, u2(k-3) ------------------------------------------
     if (k >= zs + 1) {
-      V Hm = hsum(U1[0], buf, R0), Hc = hsum(U1[1], buf, R0 + 1);
+      Row Hm = hsum(U1[0], buf, R0), Hc = hsum(U1[1], buf, R0 + 1);
       const int64_t lz = k - 3;
       const int64_t gz = lz + g.gz_off;
       const bool zb = gz == 0 || gz == g.gnz - 1;
 #pragma unroll
       for (int i = 0; i < RY; ++i) {
         const int j = i + 1;
-        const V Hp = hsum(U1[j + 1], buf, R0 + j + 1);
-        V A, B;
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-          const T center = U1[j][e];
-          const T cross = Hc[e] + (U1[j - 1][e] + U1[j + 1][e]);
-          const T diag = Hm[e] + Hp[e];
-          A[e] = sm::box27_A<T>(center, cross, diag, c1, c2, c3);
-          B[e] = sm::box27_B<T>(center, cross, diag, c0, c1, c2);
-        }
+        const Row Hp = hsum(U1[j + 1], buf, R0 + j + 1);
+        const Row cross = RO::add(Hc, RO::add(U1[j - 1], U1[j + 1]));
+        const Row diag = RO::add(Hm, Hp);
+        const Row A = RO::lin3(U1[j], cross, diag, c1, c2, c3);  // sm::box27_A
+        const Row B = RO::lin3(U1[j], cross, diag, c0, c1, c2);  // sm::box27_B
         Hm = Hc;
         Hc = Hp;
         const int64_t y = y0 + i;
         if (k >= zs + 3 && y < g.ny) {
-          V o = C1[i];
-          if (!zb && y != 0 && y != g.ny - 1) {
-#pragma unroll
-            for (int e = 0; e < N; ++e) o[e] = xb[e] ? C1[i][e] : S1[i][e] + A[e];
-          }
+          Row o = C1[i];
+          if (!zb && y != 0 && y != g.ny - 1) o = RO::sel(xb, C1[i], RO::add(S1[i], A));
           if (xin) {
             dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
-            store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), o);
+            store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), RO::vec(o));
             if (RES) {
 #pragma unroll
               for (int e = 0; e < N; ++e)
                 if (x + e < g.nx) {
-                  const double d = (double)o[e] - (double)C1[i][e];
+                  const double d = (double)RO::get(o, e) - (double)RO::get(C1[i], e);
                   acc += d * d;
                 }
             }
           }
         }
-#pragma unroll
-        for (int e = 0; e < N; ++e) S1[i][e] = A1p[i][e] + B[e];
+        S1[i] = RO::add(A1p[i], B);
         A1p[i] = A;
         C1[i] = U1[j];
       }
@@ -389,31 +368,22 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
     {
       const int64_t gz = k - 1 + g.gz_off;
       const bool zb = gz <= 0 || gz >= g.gnz - 1;
-      V Hm = hsum(Rw[0], buf, 0), Hc = hsum(Rw[1], buf, 1);
+      Row Hm = hsum(Rw[0], buf, 0), Hc = hsum(Rw[1], buf, 1);
 #pragma unroll
       for (int jj = 0; jj < R1; ++jj) {
         const int j = jj + 1;
-        const V Hp = hsum(Rw[j + 1], buf, j + 1);
-        V A, B;
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-          const T center = Rw[j][e];
-          const T cross = Hc[e] + (Rw[j - 1][e] + Rw[j + 1][e]);
-          const T diag = Hm[e] + Hp[e];
-          A[e] = sm::box27_A<T>(center, cross, diag, c1, c2, c3);
-          B[e] = sm::box27_B<T>(center, cross, diag, c0, c1, c2);
-        }
+        const Row Hp = hsum(Rw[j + 1], buf, j + 1);
+        const Row cross = RO::add(Hc, RO::add(Rw[j - 1], Rw[j + 1]));
+        const Row diag = RO::add(Hm, Hp);
+        const Row A = RO::lin3(Rw[j], cross, diag, c1, c2, c3);
+        const Row B = RO::lin3(Rw[j], cross, diag, c0, c1, c2);
         Hm = Hc;
         Hc = Hp;
         const int64_t y = y0 - 1 + jj;
-        V u = C0[jj];
-        if (!zb && y > 0 && y < g.ny - 1) {
-#pragma unroll
-          for (int e = 0; e < N; ++e) u[e] = xb[e] ? C0[jj][e] : S0[jj][e] + A[e];
-        }
+        Row u = C0[jj];
+        if (!zb && y > 0 && y < g.ny - 1) u = RO::sel(xb, C0[jj], RO::add(S0[jj], A));
         U1[jj] = u;
-#pragma unroll
-        for (int e = 0; e < N; ++e) S0[jj][e] = A0p[jj][e] + B[e];
+        S0[jj] = RO::add(A0p[jj], B);
         A0p[jj] = A;
         C0[jj] = Rw[j];
       }
@@ -704,10 +674,13 @@ static void launch_box27_tb2_ry(const Geo& g, const T* in, T* out, const Stencil
 template <class T>
 void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  // fp64: box27_tbk with 4 rows per tile, fp32: box27_tb2 (one MI355X, GCells/s, tb2 / tbk RY 2 /
-  // tbk RY 4: 512^3 fp32 896 / 892 / 857, 1024^3 fp32 1006 / 896 / 970, 512^3 fp64 487 / 460 / 530;
-  // profiles/r02_box27_tbk.txt). MDFX_B27_TBK: -1 box27_tb2, 1 / 2 / 4 box27_tbk with that many rows.
-  const int ry = knobs().b27_tbk != 0 ? knobs().b27_tbk : std::is_same<T, double>::value ? 4 : -1;
+  // fp64: box27_tbk with 4 rows per tile, fp32: box27_tb2 (interleaved A/B on one MI355X, GCells/s,
+  // tb2 / tbk RY 2 / tbk RY 4: 512^3 fp32 987 / 942 / 884, 1024^3 fp32 995 / 873 / 985, 512^3 fp64
+  // 492 / 468 / 553; profiles/r02_box27_tbk.txt). box27_tb2 exists for fp32 only (its pair-layout
+  // rows cost the fp64 instance occupancy: 489 -> 341). MDFX_B27_TBK: -1 box27_tb2 (fp32; fp64:
+  // box27_tbk with 2 rows), 1 / 2 / 4 box27_tbk with that many rows.
+  int ry = knobs().b27_tbk != 0 ? knobs().b27_tbk : std::is_same<T, double>::value ? 4 : -1;
+  if (ry < 0 && std::is_same<T, double>::value) ry = 2;
   if (ry > 0) {
     if (ry == 1 || g.ny < 8)
       launch_box27_tbk_ry<T, 1, 2>(g, in, out, c, resid, s);
@@ -717,10 +690,12 @@ void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, d
       launch_box27_tbk_ry<T, 2, 2>(g, in, out, c, resid, s);
     return;
   }
-  if (knobs().tb_ry == 1 || g.ny < 8)
-    launch_box27_tb2_ry<T, 1>(g, in, out, c, resid, s);
-  else
-    launch_box27_tb2_ry<T, 2>(g, in, out, c, resid, s);
+  if constexpr (std::is_same<T, float>::value) {
+    if (knobs().tb_ry == 1 || g.ny < 8)
+      launch_box27_tb2_ry<T, 1>(g, in, out, c, resid, s);
+    else
+      launch_box27_tb2_ry<T, 2>(g, in, out, c, resid, s);
+  }
 }
 template void launch_box27_tb2<float>(const Geo&, const float*, float*, const StencilCoef&, double*, hipStream_t);
 template void launch_box27_tb2<double>(const Geo&, const double*, double*, const StencilCoef&, double*, hipStream_t);
