@@ -174,9 +174,9 @@ def pick_temporal(a, prob, nslab, hip):
 
     if a.temporal > 0:
         return a.temporal
-    # fused depth where a kernel exists: 2 for the 3D stencils, 8 (MDF) / 6 (Life) for the 2D ones
+    # fused depth where a kernel exists: 2 for the 3D stencils, 8 (MDF) / 12 (Life) for the 2D ones
     # (profiles/r02_mdf2d/, profiles/r02_life.txt), capped so every slab is at least 4 sweeps deep
-    want = {"jacobi5": 8, "life": 6}.get(a.stencil, 2)
+    want = {"jacobi5": 8, "life": 12}.get(a.stencil, 2)
     while want > 1 and prob.nz < 4 * want * nslab:
         want //= 2
     if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz,

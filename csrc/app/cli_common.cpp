@@ -66,8 +66,8 @@ void usage(const char* prog) {
       "  --print                   dump the final grid like the reference's print_array\n"
       "  --json                    one JSON metrics line ; --verbose per-rank detail ; --quiet\n"
       "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n"
-      "  --temporal 0..8           time steps fused per memory sweep (0 = auto on GPUs: 2 for 3D, 8 for\n"
-      "                            the 2D MDF, 6 for Life; 1 on the CPU)\n"
+      "  --temporal 0..16          time steps fused per memory sweep (0 = auto on GPUs: 2 for 3D, 8 for\n"
+      "                            the 2D MDF, 12 for Life; 1 on the CPU)\n"
       "  --profile                 per-phase timing of rank 0 (boundary / interior / exchange)\n"
       "  --dim 2|3                 default stencil of that dimension (5 / 7) ; --bc V = --edge V ; --coef R = --r R\n"
       "  --dump DIR                write the final grid (per-slab raw + JSON header, checkpoint format)\n"
@@ -283,7 +283,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
       MDFX_FAIL("unknown transport " + tname);
     }
     if (o.temporal <= 0) {  // auto: deepest fused sweep with a kernel, slabs >= 4 sweeps deep
-      int want = kind == StencilKind::Jacobi5 ? 8 : (kind == StencilKind::Life ? 6 : 2);
+      int want = kind == StencilKind::Jacobi5 ? 8 : (kind == StencilKind::Life ? 12 : 2);
       while (want > 1 && g.nz < 4 * (int64_t)want * nranks) want /= 2;
       o.temporal = (hip && want > 1 &&
                     hip_supports_steps(spec, FieldLayout::make(g, 0, g.nz, want, spec.dtype), want))

@@ -42,7 +42,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   if (spec_.kind == StencilKind::Life) MDFX_CHECK(spec_.dtype == DType::U8, "life cells are u8");
   if (spec_.kind != StencilKind::Life)
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
-  MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 8, "temporal blocking depth must be 1..8");
+  MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 16, "temporal blocking depth must be 1..16");
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
@@ -79,7 +79,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     if (opt_.temporal > 1 && s.be->kind() == DeviceKind::HIP)
       MDFX_CHECK(hip_supports_steps(spec_, s.lay, opt_.temporal),
                  format("no fused %d-step kernel for %s %s with nx=%lld (fused depths: 2 for every stencil "
-                        "(box27 rows up to 1024 fp32 / 512 fp64); 3, 4, 6, 8 for the 2D stencils)",
+                        "(box27 rows up to 1024 fp32 / 512 fp64); 3, 4, 6, 8 for the 2D stencils, also 12, 16 for Life)",
                         opt_.temporal, stencil_name(spec_.kind), dtype_name(spec_.dtype), (long long)global_.nx));
     // regions (storage planes); owned = [halo, halo + nzl). The boundary regions are the `halo`
     // planes at each end that the exchange sends: they are computed on the halo stream so the

@@ -138,7 +138,7 @@ class Solver {
   int graph_parity_ = -1;
   int graph_k_ = 0;
   // depth_ok_[k]: every slab can run a k-step fused sweep (k <= temporal); 1 always can
-  bool depth_ok_[9] = {false, true, false, false, false, false, false, false, false};
+  bool depth_ok_[17] = {false, true};
 };
 
 }  // namespace mdfx

@@ -63,6 +63,7 @@ static Knobs read_knobs() {
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
   k.b27_tbk = env_int("MDFX_B27_TBK", 0);
+  k.life_bits = env_int("MDFX_LIFE_BITS", 1);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
@@ -220,7 +221,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   const bool k2d = steps == 2 || steps == 3 || steps == 4 || steps == 6 || steps == 8;
   if (spec.kind == StencilKind::Jacobi5)  // deep temporal blocking of the 2D problems
     return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d && !spec.coef.ref_precision;
-  if (spec.kind == StencilKind::Life) return k2d;
+  if (spec.kind == StencilKind::Life) return k2d || steps == 12 || steps == 16;  // 12 / 16: life_bits
   if (spec.kind == StencilKind::Heat7 && steps > 2) {  // deep temporal blocking (rows within one block)
     const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
     return spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, steps)

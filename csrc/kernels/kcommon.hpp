@@ -185,6 +185,7 @@ struct Knobs {
   int tbk_ry = 0;      // MDFX_TBK_RY: rows per tile of heat7_tbk (0: 4 at K = 2, 2 deeper)
   int j5_tbk = 0;      // MDFX_J5_TBK: 2D MDF two-step sweeps through the K-step kernel
   int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
+  int life_bits = 1;   // MDFX_LIFE_BITS: Life sweeps of K > 2 generations bit-sliced (0: SWAR life_tbk)
   int b27_tbk = 0;     // MDFX_B27_TBK: 27-point fused kernel (0: per dtype, -1: box27_tb2, 1/2/4: box27_tbk rows)
   int debug_zc = 0;    // MDFX_DEBUG_ZC: print the z chunking of the streaming kernels
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)

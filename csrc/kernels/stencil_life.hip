@@ -425,7 +425,172 @@ static void launch_life_tbk_k(const Geo& g, const uint8_t* in, uint8_t* out, dou
     hipLaunchKernelGGL((life_tbk<K, false>), grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
 }
 
+// ---- K generations per sweep, bit-sliced (life_bits) ---------------------------------------------
+//
+// One bit per cell inside the sweep: each lane loads 32 u8 cells of a row (two 16-B vectors), packs
+// them into a 32-bit word (bit j = cell x + j: per 4 cells one multiply-gather, v_mul + v_bfe),
+// runs K generations on the words and unpacks the last one back to bytes for the store. A
+// generation of 32 cells is ~22 bitwise ops instead of ~100 SWAR byte ops for 16:
+//   row sums on arrival (L / R = the row shifted by one cell, the cell beyond the lane through a
+//   DPP lane shift and v_alignbit):  2-sum c = L + R  (c0 = L ^ R, c1 = L & R),
+//                                     3-sum s = L + X + R  (s0 = c0 ^ X, s1 = maj(L, X, R))
+//   neighbours of row r: N = s(r-1) + s(r+1) + c(r) (a 4-bit ripple of full adders, 10 ops)
+//   B3/S23: alive' = (N | alive) == 3  ->  n1 & (n0 | alive) & ~(n2 | n3)
+// Each level keeps the 3-sums of its last two input rows, the 2-sum and the cells of the last row.
+// Waves overlap by one lane per side like life_tbk (a generation corrupts one more cell of the
+// halo lanes from the outside in: K <= 32). Held cells (x = 0, x >= nx - 1, the first / last row)
+// keep their state through a per-lane bit mask. Bitwise equal to K single generations.
+__device__ __forceinline__ uint32_t life_pack4(uint32_t d) {  // bytes 0/1 -> bits 0..3
+  return __builtin_amdgcn_ubfe(d * 0x01020408u, 24, 4);
+}
+__device__ __forceinline__ uint32_t life_unpack4(uint32_t w, int k) {  // bits 4k..4k+3 -> bytes 0/1
+  return (__builtin_amdgcn_ubfe(w, 4 * k, 4) * 0x00204081u) & 0x01010101u;
+}
+
+template <int K, bool RES>
+__global__ __launch_bounds__(256) void life_bits(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                 Geo g, int zc, int XT, int ntasks, double* __restrict__ resid) {
+  constexpr int CW = 32;        // cells per lane
+  constexpr int SEG = 62 * CW;  // owned cells per wave
+  static_assert(K >= 1 && K <= CW, "generations must not reach past the halo lanes");
+  const int lane = threadIdx.x & 63;
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (task >= ntasks) return;  // wave-uniform, no barriers
+  const int xt = task % XT, zt = task / XT;
+  const int64_t x = (int64_t)xt * SEG - CW + (int64_t)lane * CW;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  // pitch is a multiple of 256 cells, x of 32: a lane is wholly inside the row or wholly outside
+  const bool xin = x >= 0 && x < g.pitch;
+  const bool own = lane >= 1 && lane <= 62 && xin;
+  const int64_t plane = g.plane;
+  // held cells (x + j == 0 or x + j >= nx - 1) and cells inside the grid (x + j < nx)
+  const int64_t hf = g.nx - 1 - x, vf = g.nx - x;
+  const uint32_t hm = (x == 0 ? 1u : 0u) | (hf <= 0 ? ~0u : hf >= 32 ? 0u : ~0u << hf);
+  const uint32_t vm = vf >= 32 ? ~0u : vf <= 0 ? 0u : (1u << vf) - 1u;
+  // lanes outside the row read the nearest in-row vectors, rows past the storage its last row:
+  // finite values that only meet halo lanes or held cells
+  const uint8_t* ib = in + (x < 0 ? 0 : x >= g.pitch ? g.pitch - CW : x);
+  auto ld = [&](int64_t lz) -> uint32_t {
+    const int64_t lzc = lz < 0 ? 0 : lz >= g.lz_max ? g.lz_max - 1 : lz;
+    dcheck(g, in, ib + lzc * plane, CW);
+    const uint4* p = (const uint4*)(ib + lzc * plane);
+    const uint4 a = p[0], b = p[1];
+    return life_pack4(a.x) | life_pack4(a.y) << 4 | life_pack4(a.z) << 8 | life_pack4(a.w) << 12 |
+           life_pack4(b.x) << 16 | life_pack4(b.y) << 20 | life_pack4(b.z) << 24 | life_pack4(b.w) << 28;
+  };
+  struct RowSums {
+    uint32_t s0, s1, c0, c1;
+  };
+  auto sums = [&](uint32_t X) -> RowSums {
+    const uint32_t up = (uint32_t)lane_up1((int)X), dn = (uint32_t)lane_down1((int)X);
+    const uint32_t L = __builtin_amdgcn_alignbit(X, up, 31);  // cell x + j - 1
+    const uint32_t R = __builtin_amdgcn_alignbit(dn, X, 1);   // cell x + j + 1
+    RowSums r;
+    r.c0 = L ^ R;
+    r.c1 = L & R;
+    r.s0 = r.c0 ^ X;
+    r.s1 = (r.c0 & X) | (~r.c0 & L);  // maj(L, X, R)
+    return r;
+  };
+  // next state of row r from the 3-sums of rows r - 1 (a) and r + 1 (b) and row r's 2-sum / cells
+  auto gen = [&](const RowSums& a, const RowSums& b, const RowSums& c, uint32_t self) -> uint32_t {
+    const uint32_t x0 = a.s0 ^ b.s0;
+    const uint32_t n0 = x0 ^ c.c0;
+    const uint32_t k0 = (x0 & c.c0) | (~x0 & a.s0);  // maj(a0, b0, c0)
+    const uint32_t y1 = a.s1 ^ b.s1;
+    const uint32_t k1a = (y1 & c.c1) | (~y1 & a.s1);  // maj(a1, b1, c1)
+    const uint32_t z1 = y1 ^ c.c1;
+    const uint32_t n1 = z1 ^ k0;
+    const uint32_t k1b = z1 & k0;
+    const uint32_t hi = k1a | k1b;  // n2 | n3
+    const uint32_t o = n1 & (n0 | self) & ~hi;
+    return (hm & self) | (~hm & o);
+  };
+  RowSums P2[K], P1[K], Cs[K];  // level l = 1..K at index l - 1: 3-sums of rows q-2 / q-1, row q-1
+  uint32_t Xp[K];
+#pragma unroll
+  for (int l = 0; l < K; ++l) {
+    P2[l] = P1[l] = Cs[l] = RowSums{0, 0, 0, 0};
+    Xp[l] = 0;
+  }
+  {
+    const uint32_t a = ld(zs - K - 1), b = ld(zs - K);
+    P2[0] = sums(a);
+    P1[0] = Cs[0] = sums(b);
+    Xp[0] = b;
+  }
+  uint32_t nxt = ld(zs - K + 1);
+  double acc = 0.0;
+  for (int64_t q = zs - K + 1; q <= ze - 1 + K; ++q) {
+    uint32_t X = nxt;  // u0(q)
+    nxt = ld(q + 1);
+    const int64_t lz = q - K;
+#pragma unroll
+    for (int l = 1; l <= K; ++l) {
+      const RowSums sq = sums(X);
+      const uint32_t self = Xp[l - 1];
+      const int64_t row = q - l;  // the row this level finishes
+      const int64_t gz = row + g.gz_off;
+      const bool bnd = l < K ? (gz <= 0 || gz >= g.gnz - 1) : (gz == 0 || gz == g.gnz - 1);
+      const uint32_t o = bnd ? self : gen(P2[l - 1], sq, Cs[l - 1], self);
+      P2[l - 1] = P1[l - 1];
+      P1[l - 1] = Cs[l - 1] = sq;
+      Xp[l - 1] = X;
+      if (l < K) {
+        X = o;
+      } else if (lz >= zs && own) {
+        uint4 qa, qb;
+        qa.x = life_unpack4(o, 0);
+        qa.y = life_unpack4(o, 1);
+        qa.z = life_unpack4(o, 2);
+        qa.w = life_unpack4(o, 3);
+        qb.x = life_unpack4(o, 4);
+        qb.y = life_unpack4(o, 5);
+        qb.z = life_unpack4(o, 6);
+        qb.w = life_unpack4(o, 7);
+        uint4* p = (uint4*)(out + lz * plane + x);
+        dcheck(g, (const uint8_t*)out, (const uint8_t*)p, CW);
+        p[0] = qa;
+        p[1] = qb;
+        if (RES) acc += (double)__builtin_popcount((o ^ self) & vm);
+      }
+    }
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <int K>
+static void launch_life_bits_k(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s) {
+  const int64_t planes = g.lz_end - g.lz_begin;
+  if (planes <= 0) return;
+  constexpr int SEG = 62 * 32;
+  const int XT = (int)((g.nx + SEG - 1) / SEG);
+  int zc = knobs().zc;
+  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const int ntasks = XT * ZT;
+  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((life_bits<K, true>), grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
+  else
+    hipLaunchKernelGGL((life_bits<K, false>), grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
+}
+
 void launch_life_tbk(const Geo& g, const uint8_t* in, uint8_t* out, int steps, double* resid, hipStream_t s) {
+  // the bit-sliced kernel by default (MDFX_LIFE_BITS=0: the SWAR one, depths up to 8)
+  if (knobs().life_bits || steps > 8) {
+    switch (steps) {
+      case 2: launch_life_bits_k<2>(g, in, out, resid, s); return;
+      case 3: launch_life_bits_k<3>(g, in, out, resid, s); return;
+      case 4: launch_life_bits_k<4>(g, in, out, resid, s); return;
+      case 6: launch_life_bits_k<6>(g, in, out, resid, s); return;
+      case 8: launch_life_bits_k<8>(g, in, out, resid, s); return;
+      case 12: launch_life_bits_k<12>(g, in, out, resid, s); return;
+      case 16: launch_life_bits_k<16>(g, in, out, resid, s); return;
+      default: return;
+    }
+  }
   switch (steps) {
     case 2: launch_life_tbk_k<2>(g, in, out, resid, s); break;
     case 3: launch_life_tbk_k<3>(g, in, out, resid, s); break;

@@ -152,7 +152,7 @@ def advance(problem: Problem, grid: torch.Tensor, steps: int, temporal: int = 0)
                          (tuple(grid.shape), problem.nz, problem.ny, problem.nx))
     dev = g.device
     if temporal <= 0:
-        want = {"jacobi5": 8, "life": 6}.get(problem.kind, 2)
+        want = {"jacobi5": 8, "life": 12}.get(problem.kind, 2)
         while want > 1 and problem.nz < want:
             want //= 2
         temporal = 1

@@ -295,7 +295,7 @@ def test_temporal2_checkpoint_roundtrip(mdfx, tmp_path):
 
 def test_temporal_depth_validated(mdfx):
     with pytest.raises(RuntimeError):
-        m.Simulation(m.heat3d(n=8), device="cpu", temporal=9)
+        m.Simulation(m.heat3d(n=8), device="cpu", temporal=17)  # 1..16 (16: the bit-sliced Life)
     with pytest.raises(RuntimeError, match="ghost planes"):  # slabs thinner than the exchanged halo
         m.Simulation(m.mdf2d(h=20, w=16), device="cpu", ranks=4, temporal=8)
 

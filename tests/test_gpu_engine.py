@@ -208,12 +208,12 @@ def test_auto_temporal_on_gpu(hip):
     assert auto_temporal(m.heat3d(n=64), 1, "hip") == 2
     assert auto_temporal(m.mdf2d(h=4096, w=64), 4, "hip") == 8
     assert auto_temporal(m.mdf2d(h=40, w=64), 4, "hip") == 2  # 40 rows over 4 slabs: shallower sweeps
-    assert auto_temporal(m.life2d(h=4096, w=64), 2, "hip") == 6
-    assert auto_temporal(m.life2d(h=40, w=64), 2, "hip") == 3  # 40 rows over 2 slabs: 6 -> 3
+    assert auto_temporal(m.life2d(h=4096, w=64), 2, "hip") == 12
+    assert auto_temporal(m.life2d(h=40, w=64), 2, "hip") == 3  # 40 rows over 2 slabs: 12 -> 6 -> 3
     prob = m.life2d(h=400, w=1000)
     ref, _ = _sim_gather(prob, 21, temporal=1)
     got, t = _sim_gather(prob, 21, temporal=0, ranks=3)
-    assert t == 6 and np.array_equal(ref, got)
+    assert t == 12 and np.array_equal(ref, got)
 
 
 def _sim_gather(prob, steps, **kw):

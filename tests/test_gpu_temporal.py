@@ -219,8 +219,45 @@ def test_deep_fused_steps_bitwise(hip, prob, k, knob):
         assert abs(res.item() - ref_res.item()) <= 1e-9 * max(1.0, ref_res.item())
 
 
+LIFE_DEEP = [models.life2d(h=50, w=3000), models.life2d(h=19, w=100), models.life2d(h=40, w=2049),
+             models.life2d(h=70, w=64, density=0.4)]
+
+
+@pytest.mark.parametrize("prob", LIFE_DEEP, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("k", [2, 3, 4, 6, 8, 12, 16])
+def test_life_kernels_bitwise(hip, prob, k, knob):
+    """K Life generations per sweep through the bit-sliced kernel (life_bits, up to 16) and the SWAR
+    one (life_tbk, up to 8) == K naive generations, bitwise, with the change count of the last."""
+    knob("MDFX_LIFE_TBK", 1)
+    for bits in ((1, 0) if k <= 8 else (1,)):
+        knob("MDFX_LIFE_BITS", bits)
+        lay = FieldLayout.make(prob, halo=k)
+        src = alloc_field(lay, "cuda")
+        init_field(prob, lay, src)
+        fused = alloc_field(lay, "cuda")
+        res = torch.zeros((), dtype=torch.float64, device="cuda")
+        apply_stencil(prob, lay, src, fused, steps=k, resid=res)
+        set_kernel_variant("naive")
+        try:
+            cur = alloc_field(lay, "cuda")
+            cur.copy_(src)
+            ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+            for i in range(k):
+                nxt = alloc_field(lay, "cuda")
+                nxt.copy_(cur)
+                apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+                cur = nxt
+        finally:
+            set_kernel_variant("auto")
+        torch.cuda.synchronize()
+        o = lay.owned
+        assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, bits)
+        assert res.item() == ref_res.item(), (k, bits)
+
+
 @pytest.mark.parametrize("prob,k", [(mm.mdf2d(h=400, w=1500), 8), (mm.mdf2d(h=200, w=700, dtype="f64"), 4),
-                                    (mm.life2d(h=300, w=5000), 4), (mm.life2d(h=300, w=2000), 6)])
+                                    (mm.life2d(h=300, w=5000), 4), (mm.life2d(h=300, w=2000), 6),
+                                    (mm.life2d(h=300, w=4100), 16), (mm.life2d(h=200, w=1000), 12)])
 def test_engine_deep_temporal_2d(hip, prob, k):
     ref, rr = _sim(prob, 37, ranks=1, residual_every=9)
     got, rg = _sim(prob, 37, ranks=4, temporal=k, residual_every=9)
