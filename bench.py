@@ -174,11 +174,14 @@ def pick_temporal(a, prob, nslab, hip):
 
     if a.temporal > 0:
         return a.temporal
-    # fused depth where a kernel exists: 2 for the 3D stencils, 8 (MDF) / 12 (Life) for the 2D ones
-    # (profiles/r02_mdf2d/, profiles/r02_life.txt), capped so every slab is at least 4 sweeps deep
-    want = {"jacobi5": 8, "life": 12}.get(a.stencil, 2)
+    # the deepest measured-win fused depth (native hip_fused_depth: 3 for the 3D 7-point at
+    # 1024-cell rows through heat7_wtk, else 2 for the 3D stencils; 8 (MDF) / 12 (Life) for the 2D
+    # ones; profiles/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt), made shallower until every slab is at
+    # least 4 sweeps deep
+    want = native().hip_fused_depth(prob.kind, prob.dtype, prob.nx, prob.ref_precision) if hip else \
+        {"jacobi5": 8, "life": 12}.get(a.stencil, 2)
     while want > 1 and prob.nz < 4 * want * nslab:
-        want //= 2
+        want = 2 if want == 3 else want // 2
     if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz,
                                                             want, want, prob.ref_precision)):
         return want

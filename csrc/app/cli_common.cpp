@@ -283,8 +283,8 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
       MDFX_FAIL("unknown transport " + tname);
     }
     if (o.temporal <= 0) {  // auto: deepest fused sweep with a kernel, slabs >= 4 sweeps deep
-      int want = kind == StencilKind::Jacobi5 ? 8 : (kind == StencilKind::Life ? 12 : 2);
-      while (want > 1 && g.nz < 4 * (int64_t)want * nranks) want /= 2;
+      int want = hip ? hip_fused_depth(spec, g.nx) : 1;
+      while (want > 1 && g.nz < 4 * (int64_t)want * nranks) want = shallower_depth(want);
       o.temporal = (hip && want > 1 &&
                     hip_supports_steps(spec, FieldLayout::make(g, 0, g.nz, want, spec.dtype), want))
                        ? want

@@ -46,6 +46,13 @@ template <class T>
 void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
 template <class T>
 bool heat7_tbk_supported(const Geo& g, int steps);
+template <class T>
+void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
+bool heat7_wtk_supported(int steps);
+double heat7_wtk_xeff(int64_t nx, int esize, int steps);
+// 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
+// 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
+static bool use_wtk(int steps) { return knobs().h7_wtk >= 0 && heat7_wtk_supported(steps); }
 
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -60,6 +67,7 @@ static Knobs read_knobs() {
   k.ry = env_int("MDFX_RY", 0);
   k.tb_ry = env_int("MDFX_TB_RY", 0);
   k.tbk_ry = env_int("MDFX_TBK_RY", 0);
+  k.h7_wtk = env_int("MDFX_H7_WTK", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
   k.b27_tbk = env_int("MDFX_B27_TBK", 0);
@@ -223,6 +231,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
     return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d && !spec.coef.ref_precision;
   if (spec.kind == StencilKind::Life) return k2d || steps == 12 || steps == 16;  // 12 / 16: life_bits
   if (spec.kind == StencilKind::Heat7 && steps > 2) {  // deep temporal blocking (rows within one block)
+    if (dev::use_wtk(steps)) return true;
     const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
     return spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, steps)
                                     : dev::heat7_tbk_supported<double>(g, steps);
@@ -235,6 +244,24 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   if (spec.kind != StencilKind::Heat7) return false;
   const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
   return spec.dtype == DType::F32 ? dev::heat7_tb2_supported<float>(g) : dev::heat7_tb2_supported<double>(g);
+}
+
+int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
+  switch (spec.kind) {
+    case StencilKind::Jacobi5: return 8;
+    case StencilKind::Life: return 12;
+    case StencilKind::Box27: return 2;
+    case StencilKind::Heat7:
+      // K = 3 wins at 1024-cell rows (fp32 1443 vs 1226 GCells/s, fp64 594-605 vs 543-565, the
+      // N = 8 slab shape 1267-1295 vs 1146-1155) and loses where the x segments waste lanes (512^3
+      // fp32: 958-965 vs 1113-1125) or the K = 2 x tiles are at the copy roof (2048^3 fp64: 506 vs
+      // 556); wider rows are unmeasured and keep K = 2
+      if (dev::knobs().h7_wtk >= 0 && nx > 512 && nx <= 1024 &&
+          dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.79)
+        return 3;
+      return 2;
+  }
+  return 1;
 }
 
 void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
@@ -268,6 +295,11 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
       }
+    } else if (dev::use_wtk(a.steps)) {
+      if (spec.dtype == DType::F32)
+        dev::launch_heat7_wtk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
+      else
+        dev::launch_heat7_wtk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
     } else if (a.steps > 2 || (spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, 2)
                                                         : dev::heat7_tbk_supported<double>(g, 2))) {
       // rows within one block: the streaming K-step kernel; wider rows (K = 2): heat7_tb2 x tiles

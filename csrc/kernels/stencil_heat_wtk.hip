@@ -1,0 +1,229 @@
+// Deep temporal blocking for the 3D 7-point stencil with wave-independent tiles (heat7_wtk):
+// K = 3 or 4 fused steps per sweep, rows of any width, no block barriers.
+//
+// heat7_tbk (stencil_heat_tbk.hip) spreads one row over the 4 waves of a block and hands the x
+// seams of every level between them through LDS: K-1 block barriers per plane, and at K >= 3 the
+// barrier-coupled waves are latency-bound at two waves per SIMD. Here every wave is
+// a task of its own -- jacobi5_tbk's overlapping wave segments carried into 3D:
+//   x: a wave covers 64 lanes x N cells but owns only lanes OV..63-OV (OV = ceil(K / N)); the
+//      outer lanes carry the neighbouring segments' edge columns through the same instructions and
+//      go wrong one cell per level from the outside, so after K levels the owned lanes are exact.
+//      x neighbours inside the wave are DPP lane shifts, nothing crosses a wave.
+//   y: the wave owns RY output rows; level k computes the RY + 2(K-k) rows the levels above it
+//      need (the y halo is recomputed, as in heat7_tbk).
+//   z: every level is heat7_tbk's streaming recurrence: per row only the partial sum
+//      S_k = (((xm + xp) + ym) + yp) + zm of plane p and the centre C_k = u_{k-1}(p) live between
+//      planes; when u_{k-1}(p+1) arrives the level finishes u_k(p) = fma(r, fma(-6, C, S + zp), C),
+//      sm::heat7's operation order, so the sweep is bitwise equal to K single steps.
+//   u0: the next plane's RY + 2K rows stream by LDS DMA into the wave's private LDS slot one plane
+//      ahead (no VGPRs held by the prefetch; no other wave reads the slot, so no barrier).
+//   Boundaries: held cells get a zero coefficient (fma(0, t, u) = u for finite t): per lane for x,
+//   per level and plane for z, per row only in tiles that reach y = 0 / ny-1. Loads outside the
+//   grid read the nearest valid row / vector, so every value a lane carries is finite.
+//
+// Region contract (as heat7_tbk): output storage planes [lz_begin, lz_end) need u0 valid on
+// [lz_begin - K, lz_end + K) (the engine keeps K ghost planes per side).
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <type_traits>
+
+#include "kcommon.hpp"
+#include "rowops.hpp"
+#include "mdfx/kernels.hpp"
+#include "mdfx/stencil_math.hpp"
+
+namespace mdfx {
+namespace dev {
+
+int64_t resident_blocks(const void* kfn);
+int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
+
+template <class T, int RY, int K, bool RES>
+__global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
+                                                 int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  using RO = RowOps<T>;
+  using Row = typename RO::Row;
+  constexpr int N = VT<T>::N;
+  constexpr int OV = (K + N - 1) / N;         // overlap lanes per side
+  constexpr int SEG = (64 - 2 * OV) * N;      // owned columns per wave
+  constexpr int R0 = RY + 2 * K;              // u0 window rows y0-K .. y0+RY+K-1
+  constexpr int TOT = tbk_off<RY, K>(K + 1);  // state rows over all levels
+  const int lane = threadIdx.x & 63;
+  // wave-uniform task in an SGPR: row bases and row / plane tests below are scalar
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (task >= ntasks) return;  // wave-uniform; no block barriers in this kernel
+  // task order: x segments fastest, then y tiles, then z chunks (y tiles fastest, so that a block's
+  // 4 waves are y neighbours of one x segment, measured slower: profiles/r02_wtk/README.txt)
+  const int xt = task % XT;
+  const int yz = task / XT;
+  const int yt = yz % YT, zt = yz / YT;
+  const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
+  const int64_t x = xs + (int64_t)lane * N;
+  const int64_t y0 = (int64_t)yt * RY;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const bool xin = x >= 0 && x < pitch;
+  const bool own = lane >= OV && lane <= 63 - OV && xin;
+
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  const Row rx = RO::coef(r, xb);
+  const Row r0 = RO::zero();
+  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= g.ny - 2;
+
+  // u0 plane lz -> this wave's private LDS slot by LDS DMA (global_load_lds, no VGPR destination):
+  // rows outside [0, ny) and lanes outside the row read the nearest valid row / vector (finite
+  // values that only meet held or unowned cells). Per lane a 32-bit byte offset from the
+  // wave-uniform row start, so the loads take the SGPR-base + VGPR-offset form.
+  __shared__ V slot[4][R0][64];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
+  auto issue = [&](int64_t lz) {
+    const int64_t lzc = lz < 0 ? 0 : lz >= g.lz_max ? g.lz_max - 1 : lz;
+#pragma unroll
+    for (int k = 0; k < R0; ++k) {
+      const int64_t y = y0 - K + k;
+      const int64_t yc = y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y;
+      const T* a = (const T*)((const char*)(in + lzc * plane + yc * pitch) + xcb);
+      dcheck(g, in, a, N);
+      glds16(a, &slot[w][k][0]);
+    }
+  };
+
+  Row S[TOT], C[TOT];
+#pragma unroll
+  for (int i = 0; i < TOT; ++i) {
+    S[i] = RO::zero();
+    C[i] = RO::zero();
+  }
+  const int64_t qlast = ze - 1 + K;  // last u0 plane of the march
+  issue(zs - K);
+  double acc = 0.0;
+  T* ob = out + y0 * pitch;
+  const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
+
+  auto march = [&](auto edge) __attribute__((always_inline)) {
+    constexpr bool EDGE = decltype(edge)::value;
+    // newest u0 plane q; level k finishes plane q - k (its first planes are priming garbage that
+    // no stored plane depends on)
+    for (int64_t q = zs - K; q <= qlast; ++q) {
+      // this wave's DMA of plane q has landed (a second slot with two planes in flight measured
+      // no faster: the wave is not waiting on DMA latency, profiles/r02_wtk/README.txt)
+      wait_vm0();
+      Row X[R0];
+#pragma unroll
+      for (int k = 0; k < R0; ++k) X[k] = RO::lds((const T*)&slot[w][k][lane]);
+      wait_lgkm0();  // slot consumed: refill it while the levels compute
+      asm volatile("" ::: "memory");
+      if (q < qlast) issue(q + 1);
+#pragma unroll
+      for (int l = 1; l <= K; ++l) {
+        const int ROUT = RY + 2 * (K - l);
+        const int off = tbk_off<RY, K>(l);
+        const int64_t gz = q - l + g.gz_off;
+        const Row rl = (gz <= 0 || gz >= g.gnz - 1) ? r0 : rx;
+        Row Y[R0];
+#pragma unroll
+        for (int i = 0; i < ROUT; ++i) {
+          Row ri = rl;
+          if (EDGE) {
+            const int64_t y = y0 - (K - l) + i;
+            if (y == 0 || y == g.ny - 1) ri = r0;
+          }
+          const Row cen = X[i + 1];
+          const Row cold = C[off + i];
+          const Row o = RO::fin(S[off + i], cen, cold, ri);
+          const T lft = lane_up1(RO::last(cen));
+          const T rgt = lane_down1(RO::first(cen));
+          S[off + i] = RO::partial(cen, lft, rgt, X[i], X[i + 2], cold);
+          C[off + i] = cen;
+          Y[i] = o;
+          if (RES && l == K && q - K >= zs && y0 + i < g.ny && own) {
+#pragma unroll
+            for (int e = 0; e < N; ++e)
+              if (x + e < g.nx) {
+                const double d = (double)RO::get(o, e) - (double)RO::get(cold, e);
+                acc += d * d;
+              }
+          }
+        }
+        if (l < K) {
+#pragma unroll
+          for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
+        } else if (q - K >= zs) {  // u_K(q - K) is an owned output plane
+          const int64_t lz = q - K;
+#pragma unroll
+          for (int i = 0; i < RY; ++i) {
+            if (y0 + i < g.ny && own) {
+              T* a = (T*)((char*)(ob + lz * plane + (int64_t)i * pitch) + xob);
+              dcheck(g, (const T*)out, a, N);
+              store_nt((V*)a, RO::vec(Y[i]));
+            }
+          }
+        }
+      }
+    }
+  };
+  if (yint)
+    march(std::integral_constant<bool, false>{});
+  else
+    march(std::integral_constant<bool, true>{});
+  wait_vm0();  // no DMA may outlive the wave
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T, int RY, int K>
+static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int XT = (int)((g.nx + SEG - 1) / SEG);
+  const int YT = (int)((g.ny + RY - 1) / RY);
+  const void* kfn = (const void*)&heat7_wtk<T, RY, K, false>;
+  int zc = knobs().zc;
+  const int64_t tiles = ((int64_t)XT * YT + 3) / 4;  // blocks per z chunk
+  if (zc <= 0) zc = tbk_zc(planes, tiles, resident_blocks(kfn), K);
+  if (knobs().debug_zc)
+    fprintf(stderr, "[mdfx] wtk K=%d RY=%d: %lld planes x %d x %d tasks -> zc %d\n", K, RY, (long long)planes, XT, YT, zc);
+  const int ZT = (int)((planes + zc - 1) / zc);
+  const int64_t ntasks = (int64_t)XT * YT * ZT;
+  MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wtk: too many tasks");
+  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
+  if (resid)
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  else
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+}
+
+bool heat7_wtk_supported(int steps) { return steps == 3 || steps == 4; }
+
+// fraction of the lanes' cells inside the row: x segments overlap by OV lanes per side, and the
+// last one is ragged (1024 fp32: 5 segments of 256 cells, 0.8)
+double heat7_wtk_xeff(int64_t nx, int esize, int steps) {
+  const int N = 16 / esize, OV = (steps + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  const int64_t XT = (nx + SEG - 1) / SEG;
+  return (double)nx / (double)(XT * 64 * N);
+}
+
+// K = 3: 3 rows per wave (2 rows: 1146 vs 1415-1582 GCells/s at 1024^3 fp32; 4 rows do not fit
+// two waves per SIMD); K = 4: 1 row (K = 4 with 2 rows needs > 256 VGPRs)
+template <class T>
+void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  MDFX_CHECK((steps == 3 || steps == 4) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+             format("heat7_wtk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
+                    (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
+  MDFX_CHECK(g.pitch % VT<T>::N == 0, "heat7_wtk: the row pitch must be a whole number of vectors");
+  if (steps == 3)
+    launch_wtk_k<T, 3, 3>(g, in, out, r, resid, s);
+  else
+    launch_wtk_k<T, 1, 4>(g, in, out, r, resid, s);
+}
+template void launch_heat7_wtk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
+template void launch_heat7_wtk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
+
+}  // namespace dev
+}  // namespace mdfx

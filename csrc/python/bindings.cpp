@@ -326,6 +326,10 @@ PYBIND11_MODULE(_mdfx, m) {
     return hip_supports_steps(s, FieldLayout::make(Extent3{nx, ny, nz}, 0, nz, halo, dtype_from_name(dtype)), steps);
   }, py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ny"), py::arg("nz"), py::arg("halo"),
      py::arg("steps"), py::arg("ref_precision") = false);
+  m.def("hip_fused_depth", [](const std::string& kind, const std::string& dtype, int64_t nx, bool ref_precision) {
+    StencilSpec s = make_spec(kind, dtype, -1, 0, 0, 0, 0, ref_precision);
+    return hip_fused_depth(s, nx);
+  }, py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ref_precision") = false);
   m.def("life_compat_init", [](int64_t h, int64_t w, double density, unsigned seed) {
     py::array_t<uint8_t> a({h, w});
     cpu_life_compat_init(a.mutable_data(), h, w, density, seed);

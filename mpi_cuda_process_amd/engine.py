@@ -37,13 +37,14 @@ from .parallel.dist import ControlPlane, TorchP2PTransport, broadcast_bytes, is_
 
 def auto_temporal(problem: Problem, nranks: int, device: str) -> int:
     """Fused steps per sweep chosen like the CLIs' auto mode: the deepest fused kernel that exists on
-    this device (2 for the 3D stencils, 8 for the 2D MDF, 12 for Life), halved until every slab is
-    at least 4 sweeps deep; 1 on the CPU, where fused sweeps bring nothing."""
+    this device (``hip_fused_depth``: 3 for the 3D 7-point at 1024-cell rows, else 2 for the 3D
+    stencils, 8 for the 2D MDF, 12 for Life), made shallower until every slab is at least 4 sweeps
+    deep; 1 on the CPU, where fused sweeps bring nothing."""
     if device != "hip":
         return 1
-    want = {"jacobi5": 8, "life": 12}.get(problem.kind, 2)
+    want = native().hip_fused_depth(problem.kind, problem.dtype, problem.nx, problem.ref_precision)
     while want > 1 and problem.nz < 4 * want * nranks:
-        want //= 2
+        want = 2 if want == 3 else want // 2
     if want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                                 want, want, problem.ref_precision):
         return want

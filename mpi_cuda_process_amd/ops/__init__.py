@@ -152,9 +152,9 @@ def advance(problem: Problem, grid: torch.Tensor, steps: int, temporal: int = 0)
                          (tuple(grid.shape), problem.nz, problem.ny, problem.nx))
     dev = g.device
     if temporal <= 0:
-        want = {"jacobi5": 8, "life": 12}.get(problem.kind, 2)
+        want = native().hip_fused_depth(problem.kind, problem.dtype, problem.nx, problem.ref_precision)
         while want > 1 and problem.nz < want:
-            want //= 2
+            want = 2 if want == 3 else want // 2
         temporal = 1
         if dev.type == "cuda" and want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx,
                                                                          problem.ny, problem.nz, want, want,

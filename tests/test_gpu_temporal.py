@@ -276,8 +276,10 @@ DEEP3D = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=
 @pytest.mark.parametrize("k", [2, 3, 4])
 @pytest.mark.parametrize("ry", ["1", "2", "4"])
 def test_heat7_deep_fused_bitwise(hip, prob, k, ry, knob):
-    """K fused 3D steps per sweep == K naive single steps, bitwise, with the residual of step K."""
+    """heat7_tbk's K fused 3D steps per sweep == K naive single steps, bitwise, with the residual of
+    step K (K >= 3 through heat7_tbk only with MDFX_H7_WTK=-1; the default is heat7_wtk)."""
     knob("MDFX_TBK_RY", ry)
+    knob("MDFX_H7_WTK", "-1")
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -372,6 +374,100 @@ def test_kernels_never_read_stale_lds(hip, prob, k):
     coefficient that cannot cancel NaN) would now differ from the naive single steps."""
     from mpi_cuda_process_amd import native
 
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    out = alloc_field(lay, "cuda")
+    torch.cuda.synchronize()
+    native().poison_lds()
+    apply_stencil(prob, lay, src, out, steps=k)
+    set_kernel_variant("naive")
+    try:
+        cur = alloc_field(lay, "cuda")
+        cur.copy_(src)
+        for _ in range(k):
+            nxt = alloc_field(lay, "cuda")
+            nxt.copy_(cur)
+            apply_stencil(prob, lay, cur, nxt)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(out[o, :, :lay.nx], cur[o, :, :lay.nx])
+
+
+# heat7_wtk (wave-independent tiles: overlapping wave segments in x, recomputed y halo, streaming
+# z levels, per-wave LDS-DMA slots): any row width, including rows wider than one block
+WTK3D = DEEP3D + [models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, ny=9, nz=9, dtype="f64"),
+                  models.heat3d(nx=1030, ny=7, nz=8), models.heat3d(nx=8, ny=6, nz=9)]
+
+
+@pytest.mark.parametrize("prob", WTK3D, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("k", [3, 4])
+def test_heat7_wtk_bitwise(hip, prob, k):
+    """heat7_wtk's K fused steps (the default 3D 7-point kernel for K >= 3) == K naive single
+    steps, bitwise, with the residual of step K."""
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res)
+    set_kernel_variant("naive")
+    try:
+        cur = alloc_field(lay, "cuda")
+        cur.copy_(src)
+        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+        for i in range(k):
+            nxt = alloc_field(lay, "cuda")
+            nxt.copy_(cur)
+            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), k
+    assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_heat7_wtk_regions_on_a_slab(hip, k):
+    """heat7_wtk on a middle slab with K ghost planes: boundary + interior regions == whole grid."""
+    prob = models.heat3d(nx=1024, ny=20, nz=40)
+    full = FieldLayout.make(prob, halo=k)
+    g = alloc_field(full, "cuda")
+    init_field(prob, full, g)
+    ref = alloc_field(full, "cuda")
+    apply_stencil(prob, full, g, ref, steps=k)
+    lay = FieldLayout.make(prob, 12, 30, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    out = alloc_field(lay, "cuda")
+    h = lay.halo
+    apply_stencil(prob, lay, src, out, h, h + k, steps=k)
+    apply_stencil(prob, lay, src, out, h + 18 - k, h + 18, steps=k)
+    apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k)
+    torch.cuda.synchronize()
+    assert torch.equal(out[h:h + 18, :, :1024], ref[12 + k:30 + k, :, :1024])
+
+
+@pytest.mark.parametrize("k,ranks", [(3, 1), (3, 3), (4, 2)])
+def test_engine_wtk_temporal_3d(hip, k, ranks):
+    prob = mm.heat3d(nx=1024, ny=24, nz=60)
+    ref, rr = _sim(prob, 23, ranks=1, temporal=1, residual_every=10)
+    got, rg = _sim(prob, 23, ranks=ranks, temporal=k, residual_every=10)
+    assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
+
+
+@pytest.mark.parametrize("prob", [models.heat3d(nx=1024, ny=12, nz=11), models.heat3d(nx=500, ny=21, nz=11, dtype="f64")],
+                         ids=lambda p: p.describe().replace(" ", "_"))
+def test_wtk_never_reads_stale_lds(hip, prob):
+    """heat7_wtk reads only LDS its own DMA filled: NaN-poisoned LDS does not change the result."""
+    from mpi_cuda_process_amd import native
+
+    k = 3
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
