@@ -68,6 +68,7 @@ static Knobs read_knobs() {
   k.tb_ry = env_int("MDFX_TB_RY", 0);
   k.tbk_ry = env_int("MDFX_TBK_RY", 0);
   k.h7_wtk = env_int("MDFX_H7_WTK", 0);
+  k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
   k.b27_tbk = env_int("MDFX_B27_TBK", 0);
@@ -252,12 +253,11 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
     case StencilKind::Life: return 12;
     case StencilKind::Box27: return 2;
     case StencilKind::Heat7:
-      // K = 3 wins at 1024-cell rows (fp32 1443 vs 1226 GCells/s, fp64 594-605 vs 543-565, the
-      // N = 8 slab shape 1267-1295 vs 1146-1155) and loses where the x segments waste lanes (512^3
-      // fp32: 958-965 vs 1113-1125) or the K = 2 x tiles are at the copy roof (2048^3 fp64: 506 vs
-      // 556); wider rows are unmeasured and keep K = 2
-      if (dev::knobs().h7_wtk >= 0 && nx > 512 && nx <= 1024 &&
-          dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.79)
+      // K = 3 through heat7_wtk wherever its x segments cover the row well (>= 79% of the lane
+      // cells): 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2, 2048^3 fp32 1666 vs 1136,
+      // 1024^3 fp64 823-825 vs 546, 2048^3 fp64 818 vs 556; at 512^3 fp32 (3 segments of 256 for
+      // 512 cells) K = 2 stays
+      if (dev::knobs().h7_wtk >= 0 && nx > 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.79)
         return 3;
       return 2;
   }

@@ -39,8 +39,14 @@ namespace dev {
 int64_t resident_blocks(const void* kfn);
 int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
 
-template <class T, int RY, int K, bool RES>
-__global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
+// A block is one task: WB = 4 or 8 waves stacked along y on one x segment (a y band of WB * RY
+// rows). The band's u0 window (WB * RY + 2K rows) streams into a shared double-buffered LDS
+// window, each row fetched once for the band instead of once per wave (9 rows per 3 output rows
+// -> 18 per 12 / 30 per 24), at one block barrier per plane. (The first version ran every wave as
+// an independent task with a private LDS slot and no barrier: 1.565 fields fetched per sweep
+// against 1.444 / 1.108 for bands of 4 / 8, and slower on every shape, profiles/r02_wtk/README.txt.)
+template <class T, int RY, int K, int WB, bool RES>
+__global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                  int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
@@ -50,18 +56,19 @@ __global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __
   constexpr int SEG = (64 - 2 * OV) * N;      // owned columns per wave
   constexpr int R0 = RY + 2 * K;              // u0 window rows y0-K .. y0+RY+K-1
   constexpr int TOT = tbk_off<RY, K>(K + 1);  // state rows over all levels
+  constexpr int RB = WB * RY + 2 * K;         // shared window rows of a band
   const int lane = threadIdx.x & 63;
-  // wave-uniform task in an SGPR: row bases and row / plane tests below are scalar
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (task >= ntasks) return;  // wave-uniform; no block barriers in this kernel
-  // task order: x segments fastest, then y tiles, then z chunks (y tiles fastest, so that a block's
-  // 4 waves are y neighbours of one x segment, measured slower: profiles/r02_wtk/README.txt)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // block-uniform task; order: x segments fastest, then y bands, then z chunks
+  const int task = (int)xcd_remap(blockIdx.x, gridDim.x);
+  if (task >= ntasks) return;  // block-uniform (the grid has exactly ntasks blocks)
   const int xt = task % XT;
   const int yz = task / XT;
   const int yt = yz % YT, zt = yz / YT;
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
   const int64_t x = xs + (int64_t)lane * N;
-  const int64_t y0 = (int64_t)yt * RY;
+  const int64_t yb = (int64_t)yt * RY * WB;  // first row of the band
+  const int64_t y0 = yb + (int64_t)w * RY;   // first row of this wave
   const int64_t zs = g.lz_begin + (int64_t)zt * zc;
   const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
   const int64_t pitch = g.pitch, plane = g.plane;
@@ -75,23 +82,25 @@ __global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __
   const Row r0 = RO::zero();
   const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= g.ny - 2;
 
-  // u0 plane lz -> this wave's private LDS slot by LDS DMA (global_load_lds, no VGPR destination):
-  // rows outside [0, ny) and lanes outside the row read the nearest valid row / vector (finite
-  // values that only meet held or unowned cells). Per lane a 32-bit byte offset from the
-  // wave-uniform row start, so the loads take the SGPR-base + VGPR-offset form.
-  __shared__ V slot[4][R0][64];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // u0 plane lz -> LDS by LDS DMA (global_load_lds, no VGPR destination): rows outside [0, ny) and
+  // lanes outside the row read the nearest valid row / vector (finite values that only meet held
+  // or unowned cells). Per lane a 32-bit byte offset from the wave-uniform row start. Wave w
+  // fetches rows w, w + WB, ... of the band's window.
+  __shared__ V slot[2][RB][64];
   const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
-  auto issue = [&](int64_t lz) {
+  auto issue = [&](int64_t lz, int buf) {
     const int64_t lzc = lz < 0 ? 0 : lz >= g.lz_max ? g.lz_max - 1 : lz;
 #pragma unroll
-    for (int k = 0; k < R0; ++k) {
-      const int64_t y = y0 - K + k;
-      const int64_t yc = y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y;
-      const T* a = (const T*)((const char*)(in + lzc * plane + yc * pitch) + xcb);
-      dcheck(g, in, a, N);
-      glds16(a, &slot[w][k][0]);
-    }
+      for (int j = 0; j < (RB + WB - 1) / WB; ++j) {
+        const int k = w + j * WB;
+        if (k < RB) {
+          const int64_t y = yb - K + k;
+          const int64_t yc = y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y;
+          const T* a = (const T*)((const char*)(in + lzc * plane + yc * pitch) + xcb);
+          dcheck(g, in, a, N);
+          glds16(a, &slot[buf][k][0]);
+        }
+      }
   };
 
   Row S[TOT], C[TOT];
@@ -101,7 +110,7 @@ __global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __
     C[i] = RO::zero();
   }
   const int64_t qlast = ze - 1 + K;  // last u0 plane of the march
-  issue(zs - K);
+  issue(zs - K, 0);
   double acc = 0.0;
   T* ob = out + y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
@@ -111,15 +120,18 @@ __global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __
     // newest u0 plane q; level k finishes plane q - k (its first planes are priming garbage that
     // no stored plane depends on)
     for (int64_t q = zs - K; q <= qlast; ++q) {
-      // this wave's DMA of plane q has landed (a second slot with two planes in flight measured
-      // no faster: the wave is not waiting on DMA latency, profiles/r02_wtk/README.txt)
+      // the DMA of plane q has landed: every wave waits for its own rows, then one barrier
+      // publishes them and also certifies that every wave has finished reading the other buffer
+      // (plane q-1), which the next DMA overwrites
       wait_vm0();
+      const int buf = (int)((q - (zs - K)) & 1);
+      lds_barrier();
+      if (q < qlast) issue(q + 1, buf ^ 1);
+      // level 1 reads its u0 rows from the window as it goes (three rows live, not R0; plane q
+      // stays in its buffer for the whole iteration)
+      const T* xw = (const T*)&slot[buf][w * RY][lane];
+      auto u0row = [&](int k) -> Row { return RO::lds(xw + k * 64 * N); };
       Row X[R0];
-#pragma unroll
-      for (int k = 0; k < R0; ++k) X[k] = RO::lds((const T*)&slot[w][k][lane]);
-      wait_lgkm0();  // slot consumed: refill it while the levels compute
-      asm volatile("" ::: "memory");
-      if (q < qlast) issue(q + 1);
 #pragma unroll
       for (int l = 1; l <= K; ++l) {
         const int ROUT = RY + 2 * (K - l);
@@ -133,6 +145,13 @@ __global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __
           if (EDGE) {
             const int64_t y = y0 - (K - l) + i;
             if (y == 0 || y == g.ny - 1) ri = r0;
+          }
+          if (l == 1) {  // sliding three-row window over the u0 rows in LDS
+            if (i == 0) {
+              X[0] = u0row(0);
+              X[1] = u0row(1);
+            }
+            X[i + 2] = u0row(i + 2);
           }
           const Row cen = X[i + 1];
           const Row cold = C[off + i];
@@ -168,7 +187,9 @@ __global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __
       }
     }
   };
-  if (yint)
+  // (fp64: only the copy with the per-row y test; a second copy costs the registers that keep
+  // the 8-wave bands at two waves per SIMD without spilling)
+  if (yint && sizeof(T) == 4)
     march(std::integral_constant<bool, false>{});
   else
     march(std::integral_constant<bool, true>{});
@@ -176,26 +197,31 @@ __global__ __launch_bounds__(256) void heat7_wtk(const T* __restrict__ in, T* __
   if (RES) wave_atomic_add(resid, acc);
 }
 
-template <class T, int RY, int K>
+template <class T, int RY, int K, int WB>
 static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
-  const int YT = (int)((g.ny + RY - 1) / RY);
-  const void* kfn = (const void*)&heat7_wtk<T, RY, K, false>;
+  const int YT = (int)((g.ny + RY * WB - 1) / (RY * WB));  // y bands
+  const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false>;
   int zc = knobs().zc;
-  const int64_t tiles = ((int64_t)XT * YT + 3) / 4;  // blocks per z chunk
+  const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
   if (zc <= 0) zc = tbk_zc(planes, tiles, resident_blocks(kfn), K);
   if (knobs().debug_zc)
     fprintf(stderr, "[mdfx] wtk K=%d RY=%d: %lld planes x %d x %d tasks -> zc %d\n", K, RY, (long long)planes, XT, YT, zc);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int64_t ntasks = (int64_t)XT * YT * ZT;
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wtk: too many tasks");
-  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
-  if (resid)
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
-  else
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  const dim3 grd((unsigned)ntasks), blk(64 * WB);
+  if constexpr (WB == 8 || RY == 3) {  // no residual instance (spills / one wave per SIMD): residual
+    // sweeps use 2-row bands of 4 waves
+    MDFX_CHECK(!resid, "heat7_wtk: no residual variant of this shape");
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  } else if (resid) {
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  } else {
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  }
 }
 
 bool heat7_wtk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -208,8 +234,7 @@ double heat7_wtk_xeff(int64_t nx, int esize, int steps) {
   return (double)nx / (double)(XT * 64 * N);
 }
 
-// K = 3: 3 rows per wave (2 rows: 1146 vs 1415-1582 GCells/s at 1024^3 fp32; 4 rows do not fit
-// two waves per SIMD); K = 4: 1 row (K = 4 with 2 rows needs > 256 VGPRs)
+// K = 4: 1 row per wave (2 rows need > 256 VGPRs)
 template <class T>
 void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
@@ -217,10 +242,24 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
              format("heat7_wtk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.pitch % VT<T>::N == 0, "heat7_wtk: the row pitch must be a whole number of vectors");
-  if (steps == 3)
-    launch_wtk_k<T, 3, 3>(g, in, out, r, resid, s);
-  else
-    launch_wtk_k<T, 1, 4>(g, in, out, r, resid, s);
+  // bands of 8 waves (one 512-thread block per CU) only for deep regions: 1024^3 1632-1674 vs
+  // 1593-1612 GCells/s for bands of 4, but on 128..512-plane slabs the few large blocks leave CUs
+  // idle (8 slabs of 128 planes: 1188-1223 vs 1347-1385); the residual sweeps use bands of 4 (the
+  // 8-wave residual variant spills)
+  int wb = knobs().wtk_wb;
+  if (wb != 4 && wb != 8) wb = (g.lz_end - g.lz_begin >= 768 && !resid) ? 8 : 4;
+  if (resid) wb = 4;
+  // rows per wave at K = 3: fp32 3 (1024^3: 1679 vs 1447 GCells/s for 2 rows), fp64 2 (3 rows need
+  // more than 256 VGPRs in fp64: 823-825 vs 732-734 with the spills)
+  constexpr int RY3 = sizeof(T) == 4 ? 3 : 2;
+  if (steps == 3 && resid) {
+    launch_wtk_k<T, 2, 3, 4>(g, in, out, r, resid, s);  // the fp32 3-row residual variant: one wave per SIMD
+  } else if (steps == 3) {
+    if (wb == 8) launch_wtk_k<T, RY3, 3, 8>(g, in, out, r, resid, s);
+    else launch_wtk_k<T, RY3, 3, 4>(g, in, out, r, resid, s);
+  } else {
+    launch_wtk_k<T, 1, 4, 4>(g, in, out, r, resid, s);
+  }
 }
 template void launch_heat7_wtk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
 template void launch_heat7_wtk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);

@@ -404,16 +404,17 @@ WTK3D = DEEP3D + [models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, n
 
 
 @pytest.mark.parametrize("prob", WTK3D, ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("k", [3, 4])
-def test_heat7_wtk_bitwise(hip, prob, k):
+@pytest.mark.parametrize("k,wb", [(3, "4"), (3, "8"), (4, "4")])
+def test_heat7_wtk_bitwise(hip, prob, k, wb, knob):
     """heat7_wtk's K fused steps (the default 3D 7-point kernel for K >= 3) == K naive single
-    steps, bitwise, with the residual of step K."""
+    steps, bitwise, with the residual of step K (bands of 4 waves) or without (bands of 8)."""
+    knob("MDFX_WTK_WB", wb)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
     fused = alloc_field(lay, "cuda")
     res = torch.zeros((), dtype=torch.float64, device="cuda")
-    apply_stencil(prob, lay, src, fused, steps=k, resid=res)
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res if wb == "4" else None)
     set_kernel_variant("naive")
     try:
         cur = alloc_field(lay, "cuda")
@@ -428,8 +429,9 @@ def test_heat7_wtk_bitwise(hip, prob, k):
         set_kernel_variant("auto")
     torch.cuda.synchronize()
     o = lay.owned
-    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), k
-    assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb)
+    if wb == "4":
+        assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
 @pytest.mark.parametrize("k", [3, 4])
