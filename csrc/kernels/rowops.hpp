@@ -45,7 +45,7 @@ struct RowOps<float> {
     const unsigned a = (unsigned)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
     Row r;
     asm volatile("ds_read2_b32 %0, %2 offset0:1 offset1:2\n\tds_read2_b32 %1, %2 offset1:3"
-                 : "=v"(r.a), "=v"(r.b)
+                 : "=&v"(r.a), "=&v"(r.b)
                  : "v"(a));
     return r;
   }
