@@ -262,13 +262,16 @@ namespace dev {
 // best of 3 x 20): zc 128 / 64 / 43 -> 1025 / 1358 / 1082 GCells/s.
 static std::atomic<int> g_min_rounds{1};
 
+// Every chunk also pays 2K planes of pipeline fill, so a region is never split into chunks shorter
+// than 4K planes: under the 2-round policy of multi-slab runs the K-plane boundary regions were
+// split in two (8 slabs of 1024^2 x 128 at K = 3: 1369 vs 1491 GCells/s, profiles/r02_wtk/README.txt).
 int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
-  (void)K;
   const double per_slot = (double)planes * (double)tiles / (double)resident;
   const int64_t rounds = std::max<int64_t>(g_min_rounds.load(std::memory_order_relaxed),
                                            std::min<int64_t>(4, (int64_t)(per_slot / 128.0 + 0.5)));
   const int64_t zt = std::max<int64_t>(1, std::min<int64_t>(planes, (rounds * resident + tiles / 2) / tiles));
-  return (int)((planes + zt - 1) / zt);
+  const int64_t zc = (planes + zt - 1) / zt;
+  return (int)std::max<int64_t>(zc, std::min<int64_t>(planes, 4 * (int64_t)K));
 }
 
 template <class T>

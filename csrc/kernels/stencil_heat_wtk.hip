@@ -206,13 +206,7 @@ static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, 
   const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false>;
   int zc = knobs().zc;
   const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
-  if (zc <= 0) {
-    zc = tbk_zc(planes, tiles, resident_blocks(kfn), K);
-    // every chunk pays 2K planes of pipeline fill: never split a region into chunks shorter than
-    // 4K planes (the K planes of a boundary region were split in two under the 2-round policy:
-    // 8 slabs 1369 vs 1475 GCells/s with whole boundary regions, profiles/r02_wtk/README.txt)
-    zc = std::max<int64_t>(zc, std::min<int64_t>(planes, 4 * K));
-  }
+  if (zc <= 0) zc = tbk_zc(planes, tiles, resident_blocks(kfn), K);  // chunks >= 4K planes
   if (knobs().debug_zc)
     fprintf(stderr, "[mdfx] wtk K=%d RY=%d: %lld planes x %d x %d tasks -> zc %d\n", K, RY, (long long)planes, XT, YT, zc);
   const int ZT = (int)((planes + zc - 1) / zc);
