@@ -67,10 +67,13 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   const int yt = yz % YT, zt = yz / YT;
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
   const int64_t x = xs + (int64_t)lane * N;
-  const int64_t yb = (int64_t)yt * RY * WB;  // first row of the band
-  const int64_t y0 = yb + (int64_t)w * RY;   // first row of this wave
-  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
-  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  // row / plane indices in 32 bits (extents < 2^31; the launcher checks): fewer SGPRs, so the
+  // scalar tests stay scalar
+  const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
+  const int yb = yt * RY * WB;  // first row of the band
+  const int y0 = yb + w * RY;   // first row of this wave
+  const int zs = (int)g.lz_begin + zt * zc;
+  const int ze = min((int)g.lz_end, zs + zc);
   const int64_t pitch = g.pitch, plane = g.plane;
   const bool xin = x >= 0 && x < pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
   const Row rx = RO::coef(r, xb);
   const Row r0 = RO::zero();
-  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= g.ny - 2;
+  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= ny - 2;
 
   // u0 plane lz -> LDS by LDS DMA (global_load_lds, no VGPR destination): rows outside [0, ny) and
   // lanes outside the row read the nearest valid row / vector (finite values that only meet held
@@ -88,15 +91,15 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   // fetches rows w, w + WB, ... of the band's window.
   __shared__ V slot[2][RB][64];
   const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
-  auto issue = [&](int64_t lz, int buf) {
-    const int64_t lzc = lz < 0 ? 0 : lz >= g.lz_max ? g.lz_max - 1 : lz;
+  auto issue = [&](int lz, int buf) {
+    const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
 #pragma unroll
       for (int j = 0; j < (RB + WB - 1) / WB; ++j) {
         const int k = w + j * WB;
         if (k < RB) {
-          const int64_t y = yb - K + k;
-          const int64_t yc = y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y;
-          const T* a = (const T*)((const char*)(in + lzc * plane + yc * pitch) + xcb);
+          const int y = yb - K + k;
+          const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
+          const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xcb);
           dcheck(g, in, a, N);
           glds16(a, &slot[buf][k][0]);
         }
@@ -109,17 +112,17 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
     S[i] = RO::zero();
     C[i] = RO::zero();
   }
-  const int64_t qlast = ze - 1 + K;  // last u0 plane of the march
+  const int qlast = ze - 1 + K;  // last u0 plane of the march
   issue(zs - K, 0);
   double acc = 0.0;
-  T* ob = out + y0 * pitch;
+  T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
 
   auto march = [&](auto edge) __attribute__((always_inline)) {
     constexpr bool EDGE = decltype(edge)::value;
     // newest u0 plane q; level k finishes plane q - k (its first planes are priming garbage that
     // no stored plane depends on)
-    for (int64_t q = zs - K; q <= qlast; ++q) {
+    for (int q = zs - K; q <= qlast; ++q) {
       // the DMA of plane q has landed: every wave waits for its own rows, then one barrier
       // publishes them and also certifies that every wave has finished reading the other buffer
       // (plane q-1), which the next DMA overwrites
@@ -136,15 +139,15 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
       for (int l = 1; l <= K; ++l) {
         const int ROUT = RY + 2 * (K - l);
         const int off = tbk_off<RY, K>(l);
-        const int64_t gz = q - l + g.gz_off;
-        const Row rl = (gz <= 0 || gz >= g.gnz - 1) ? r0 : rx;
+        const int gz = q - l + gzoff;
+        const Row rl = (gz <= 0 || gz >= gnz - 1) ? r0 : rx;
         Row Y[R0];
 #pragma unroll
         for (int i = 0; i < ROUT; ++i) {
           Row ri = rl;
           if (EDGE) {
-            const int64_t y = y0 - (K - l) + i;
-            if (y == 0 || y == g.ny - 1) ri = r0;
+            const int y = y0 - (K - l) + i;
+            if (y == 0 || y == ny - 1) ri = r0;
           }
           if (l == 1) {  // sliding three-row window over the u0 rows in LDS
             if (i == 0) {
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
           S[off + i] = RO::partial(cen, lft, rgt, X[i], X[i + 2], cold);
           C[off + i] = cen;
           Y[i] = o;
-          if (RES && l == K && q - K >= zs && y0 + i < g.ny && own) {
+          if (RES && l == K && q - K >= zs && y0 + i < ny && own) {
 #pragma unroll
             for (int e = 0; e < N; ++e)
               if (x + e < g.nx) {
@@ -174,11 +177,11 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
 #pragma unroll
           for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
         } else if (q - K >= zs) {  // u_K(q - K) is an owned output plane
-          const int64_t lz = q - K;
+          const int lz = q - K;
 #pragma unroll
           for (int i = 0; i < RY; ++i) {
-            if (y0 + i < g.ny && own) {
-              T* a = (T*)((char*)(ob + lz * plane + (int64_t)i * pitch) + xob);
+            if (y0 + i < ny && own) {
+              T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
               dcheck(g, (const T*)out, a, N);
               store_nt((V*)a, RO::vec(Y[i]));
             }
@@ -242,6 +245,9 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
              format("heat7_wtk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.pitch % VT<T>::N == 0, "heat7_wtk: the row pitch must be a whole number of vectors");
+  MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
+                 g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
+             "heat7_wtk: row / plane counts must fit 32-bit indices");
   // bands of 8 waves (one 512-thread block per CU) only for deep regions: 1024^3 1632-1674 vs
   // 1593-1612 GCells/s for bands of 4, but on 128..512-plane slabs the few large blocks leave CUs
   // idle (8 slabs of 128 planes: 1188-1223 vs 1347-1385); the residual sweeps use bands of 4 (the
