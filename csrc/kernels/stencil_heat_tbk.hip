@@ -76,9 +76,11 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
   const int64_t xw = (int64_t)wx * WX;
   const uint32_t xo = (uint32_t)lane * N;
   const int64_t x = xw + xo;
-  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
-  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
-  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  // row / plane indices in 32 bits (the launcher checks the extents): fewer SGPRs
+  const int ny = (int)g.ny, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
+  const int y0 = (yt * WYN + wy) * RY;
+  const int zs = (int)g.lz_begin + zt * zc;
+  const int ze = min((int)g.lz_end, zs + zc);
   const bool xin = x < g.pitch;
   const int64_t pitch = g.pitch, plane = g.plane;
   T* ob = out + y0 * pitch + xw;
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
   for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
   const Row rx = RO::coef(r, xb);
   const Row r0 = RO::zero();
-  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= g.ny - 2;
+  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= ny - 2;
 
   // ---- u0 streaming: rows + seam vectors of plane lz into this wave's slot ----------------------
   // All lanes of every DMA are active: rows outside [0, ny) and lanes beyond the row read a
@@ -106,21 +108,21 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
   const uint32_t xcb = (uint32_t)((xin ? x : pitch - N) * (int64_t)sizeof(T));
   const uint32_t socb = son ? (uint32_t)((lane < 32 ? xw - N : xw + WX) * (int64_t)sizeof(T)) : xcb;
   const T* ib0 = in + (y0 - K) * pitch;  // u0 window row k, column 0
-  auto rowc = [&](int k) -> int64_t {  // window row k, clamped into [0, ny)
-    const int64_t y = y0 - K + k;
-    return (y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y) - (y0 - K);
+  auto rowc = [&](int k) -> int {  // window row k, clamped into [0, ny)
+    const int y = y0 - K + k;
+    return (y < 0 ? 0 : y >= ny ? ny - 1 : y) - (y0 - K);
   };
-  const int64_t srowc = rowc(srow < R0 ? srow : 0);
-  auto issue = [&](int64_t lz) {
-    const T* pb = ib0 + lz * plane;
+  const int srowc = rowc(srow < R0 ? srow : 0);
+  auto issue = [&](int lz) {
+    const T* pb = ib0 + (int64_t)lz * plane;
 #pragma unroll
     for (int k = 0; k < R0; ++k) {
-      const T* a = (const T*)((const char*)(pb + rowc(k) * pitch) + xcb);
+      const T* a = (const T*)((const char*)(pb + (int64_t)rowc(k) * pitch) + xcb);
       dcheck(g, in, a, N);
       glds16(a, &slot[w][k][0]);
     }
     if (WXN > 1) {  // srowc is per lane: the row term stays in the 64-bit address
-      const T* a = (const T*)((const char*)(pb + srowc * pitch) + socb);
+      const T* a = (const T*)((const char*)(pb + (int64_t)srowc * pitch) + socb);
       dcheck(g, in, a, N);
       glds16(a, &slot[w][R0][0]);
     }
@@ -141,9 +143,9 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
     C[i] = RO::zero();
   }
   double acc = 0.0;
-  const int64_t cend = ze + K;
+  const int cend = ze + K;
   issue(zs - K);
-  for (int64_t c = zs - K; c < cend; ++c) {
+  for (int c = zs - K; c < cend; ++c) {
     const int par = (int)(c & 1);
     wait_vm0();  // this wave's DMA of plane c has landed
     Row X[R0];
@@ -179,8 +181,8 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
             HI[j] = b1[j * TB_ROW + 1];
           }
         }
-        const int64_t gz = c - k + g.gz_off;  // plane finished by this level: c - k
-        const Row rl = (gz <= 0 || gz >= g.gnz - 1) ? r0 : rx;
+        const int gz = c - k + gzoff;  // plane finished by this level: c - k
+        const Row rl = (gz <= 0 || gz >= gnz - 1) ? r0 : rx;
         Row Y[R0];
         auto rows = [&](auto edge) __attribute__((always_inline)) {
           constexpr bool EDGE = decltype(edge)::value;
@@ -188,8 +190,8 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
           for (int i = 0; i < ROUT; ++i) {
             Row ri = rl;
             if (EDGE) {
-              const int64_t y = y0 - (K - k) + i;
-              if (y == 0 || y == g.ny - 1) ri = r0;
+              const int y = y0 - (K - k) + i;
+              if (y == 0 || y == ny - 1) ri = r0;
             }
             const Row cen = X[i + 1];
             const Row cold = C[off + i];
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
             S[off + i] = RO::partial(cen, l, rr, X[i], X[i + 2], cold);
             C[off + i] = cen;
             Y[i] = o;
-            if (RES && k == K && c >= zs + K && y0 + i < g.ny && xin) {
+            if (RES && k == K && c >= zs + K && y0 + i < ny && xin) {
 #pragma unroll
               for (int e = 0; e < N; ++e)
                 if (x + e < g.nx) {
@@ -229,11 +231,11 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
 #pragma unroll
           for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
         } else if (c >= zs + K) {  // u_K(c - K) is an owned output plane
-          const int64_t lz = c - K;
+          const int lz = c - K;
 #pragma unroll
           for (int i = 0; i < RY; ++i) {
-            if (y0 + i < g.ny && xin) {
-              T* a = (T*)((char*)(ob + lz * plane + (int64_t)i * pitch) + xo * (uint32_t)sizeof(T));
+            if (y0 + i < ny && xin) {
+              T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xo * (uint32_t)sizeof(T));
               dcheck(g, (const T*)out, a, N);
               store_nt((V*)a, RO::vec(Y[i]));
             }
@@ -323,6 +325,9 @@ void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double*
              format("heat7_tbk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.pitch <= 4 * 64 * VT<T>::N, "heat7_tbk: the row must fit one block");
+  MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
+                 g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
+             "heat7_tbk: row / plane counts must fit 32-bit indices");
   int ry = knobs().tbk_ry;
   if (ry <= 0) ry = steps == 2 ? 4 : 2;
   if (g.ny < 8) ry = 1;
