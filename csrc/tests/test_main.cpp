@@ -129,8 +129,8 @@ static void test_graph() {
   }
 }
 
-// fused two-step sweeps (halo 2) == single steps, every stencil, several slab counts, ragged and
-// x-tiled (wider than one block) rows
+// fused two- and three-step sweeps (halo 2 / 3; heat7_wtk for the 3D 7-point at K = 3) == single
+// steps, every stencil, several slab counts, ragged and x-tiled (wider than one block) rows
 static void test_temporal(bool gpu) {
   struct C {
     StencilKind k;
@@ -144,7 +144,8 @@ static void test_temporal(bool gpu) {
   for (auto& c : cs)
     for (int p : {1, 3}) {
       std::vector<std::vector<char>> outs;
-      for (int t : {1, 2}) {
+      for (int t : {1, 2, 3}) {
+        if (t == 3 && c.k == StencilKind::Box27) continue;  // the 27-point fuses 2 steps at most
         StencilSpec s;
         s.kind = c.k;
         s.dtype = c.d;
@@ -171,7 +172,7 @@ static void test_temporal(bool gpu) {
         }
         outs.push_back(out);
       }
-      EXPECT(outs[0] == outs[1]);
+      for (size_t i = 1; i < outs.size(); ++i) EXPECT(outs[0] == outs[i]);
     }
 }
 
