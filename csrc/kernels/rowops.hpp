@@ -97,6 +97,8 @@ struct RowOps<float> {
   static __device__ __forceinline__ V vec(const Row& c) { return V{c.b.x, c.a.x, c.a.y, c.b.y}; }
   // ---- 27-point helpers (box27_tbk) ----
   static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.a + y.a, x.b + y.b}; }
+  // x * s for a wave-uniform s (2 packed multiplies instead of 8 selects for a 0 / 1 choice)
+  static __device__ __forceinline__ Row scale(const Row& x, float s) { return Row{x.a * T2{s, s}, x.b * T2{s, s}}; }
   // xm + xp of every cell; l / rr are the cells beyond the slice's ends
   static __device__ __forceinline__ Row hsum(const Row& c, float l, float rr) {
     Row h;
@@ -162,6 +164,7 @@ struct RowOps<double> {
   }
   static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
   static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.v + y.v}; }
+  static __device__ __forceinline__ Row scale(const Row& x, double s) { return Row{x.v * T2{s, s}}; }
   static __device__ __forceinline__ Row hsum(const Row& c, double l, double rr) {
     return Row{T2{l + c.v.y, c.v.x + rr}};
   }

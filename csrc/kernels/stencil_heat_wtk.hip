@@ -140,7 +140,9 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
         const int ROUT = RY + 2 * (K - l);
         const int off = tbk_off<RY, K>(l);
         const int gz = q - l + gzoff;
-        const Row rl = (gz <= 0 || gz >= gnz - 1) ? r0 : rx;
+        // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact: r * 1 = r,
+        // r * 0 = +0 for r >= 0)
+        const Row rl = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
         Row Y[R0];
 #pragma unroll
         for (int i = 0; i < ROUT; ++i) {
