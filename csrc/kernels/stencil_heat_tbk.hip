@@ -182,7 +182,8 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
           }
         }
         const int gz = c - k + gzoff;  // plane finished by this level: c - k
-        const Row rl = (gz <= 0 || gz >= gnz - 1) ? r0 : rx;
+        // z-held planes through a wave-uniform 0 / 1 factor (2 packed multiplies, not 8 selects)
+        const Row rl = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
         Row Y[R0];
         auto rows = [&](auto edge) __attribute__((always_inline)) {
           constexpr bool EDGE = decltype(edge)::value;
