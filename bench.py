@@ -22,10 +22,11 @@ The grid is fixed as N grows (strong scaling, the BASELINE.json config "3D 7-pt 
 slab-decomposed across 8xMI355X"). Data is synthetic: a uniform random initial grid generated on
 the device from a counter-based hash of the global cell index (seed 1). Every timed step is a full
 Jacobi update of every cell (boundary planes + halo exchange + interior), nothing is skipped or
-cached. By default two consecutive Jacobi steps are fused into one pass over memory (temporal
-blocking, --temporal 2; bitwise identical to two single steps, tests/test_gpu_temporal.py): every
-step is still computed in full, the fused kernel keeps u^{t+1} on chip. --temporal 1 measures one
-sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
+cached. By default three consecutive Jacobi steps are fused into one pass over memory (temporal
+blocking, --temporal 3 through heat7_wtk; bitwise identical to three single steps,
+tests/test_gpu_temporal.py): every step is still computed in full, the fused kernel keeps u^{t+1}
+and u^{t+2} on chip. A step count that is not a multiple of 3 ends with a shorter fused sweep.
+--temporal 1 measures one sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
 torch.cuda.synchronize() on both sides; the slowest rank's time is reported. GCells/s =
 nx*ny*nz*K / t / 1e9 for the whole job. Rank 0 prints one JSON line. The DRAM fields report the
 traffic actually required per time step (one read + one write of every cell per fused sweep, i.e.
@@ -74,8 +75,9 @@ def parse(argv=None):
     p.add_argument("--trial-steps", type=int, default=16,
                    help="steps of each short timed trial that picks transport / graph mode (auto)")
     p.add_argument("--temporal", type=int, default=0,
-                   help="time steps fused per memory sweep (temporal blocking); 0 = auto: 2 for the 3D "
-                        "stencils, 8 (2D MDF) / 4 (Life) for the 2D ones, where a fused kernel exists")
+                   help="time steps fused per memory sweep (temporal blocking); 0 = auto: 3 for the 3D "
+                        "7-point at 1024-cell rows, else 2 for the 3D stencils, 8 (2D MDF) / 12 (Life) "
+                        "for the 2D ones, where a fused kernel exists")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
