@@ -89,7 +89,7 @@ def _reference(prob, steps, temporal=1):
 
 
 @pytest.mark.parametrize("world,temporal,graph", [(2, 1, False), (3, 1, False), (2, 2, False), (3, 2, False),
-                                                  (3, 2, True)])
+                                                  (3, 2, True), (2, 3, False), (3, 3, True)])
 def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
     import mpi_cuda_process_amd as m
 

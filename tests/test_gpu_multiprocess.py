@@ -71,7 +71,7 @@ def _spawn(world, src, env_extra=None, timeout=300):
     return outs
 
 
-@pytest.mark.parametrize("world,temporal", [(2, 1), (3, 1), (2, 2), (3, 2)])
+@pytest.mark.parametrize("world,temporal", [(2, 1), (3, 1), (2, 2), (3, 2), (3, 3)])
 def test_multiprocess_gpu_matches_single(hip, tmp_path, world, temporal):
     import mpi_cuda_process_amd as m
 
