@@ -69,6 +69,7 @@ static Knobs read_knobs() {
   k.tbk_ry = env_int("MDFX_TBK_RY", 0);
   k.h7_wtk = env_int("MDFX_H7_WTK", 0);
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
+  k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
   k.b27_tbk = env_int("MDFX_B27_TBK", 0);

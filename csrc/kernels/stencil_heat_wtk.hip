@@ -257,13 +257,27 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
   int wb = knobs().wtk_wb;
   if (wb != 4 && wb != 8) wb = (g.lz_end - g.lz_begin >= 768 && !resid) ? 8 : 4;
   if (resid) wb = 4;
-  // rows per wave at K = 3: fp32 3 (1024^3: 1679 vs 1447 GCells/s for 2 rows), fp64 2 (3 rows need
-  // more than 256 VGPRs in fp64: 823-825 vs 732-734 with the spills)
+  // rows per wave at K = 3: fp32 3 (1024^3: 1679 vs 1447 GCells/s for 2 rows); fp64 2 in bands of
+  // 4 (3 rows need more than 256 VGPRs there), see below for bands of 8
   constexpr int RY3 = sizeof(T) == 4 ? 3 : 2;
   if (steps == 3 && resid) {
     launch_wtk_k<T, 2, 3, 4>(g, in, out, r, resid, s);  // the fp32 3-row residual variant: one wave per SIMD
   } else if (steps == 3) {
-    if (wb == 8) launch_wtk_k<T, RY3, 3, 8>(g, in, out, r, resid, s);
+    if (wb == 8) {
+      // fp64 8-wave bands: 3 rows per wave at rows up to 1024 cells (1024^3 923-925 vs 849-852
+      // GCells/s), 2 rows on wider rows (2048^3 835 vs 802); MDFX_WTK_RY8 = 2 / 3 forces
+      bool ry2 = false;
+      if constexpr (sizeof(T) == 8) {
+        const int k = knobs().wtk_ry8;
+        ry2 = k == 2 || (k != 3 && g.nx > 1024);
+      }
+      if constexpr (sizeof(T) == 8) {
+        if (ry2) launch_wtk_k<T, 2, 3, 8>(g, in, out, r, resid, s);
+        else launch_wtk_k<T, 3, 3, 8>(g, in, out, r, resid, s);
+      } else {
+        launch_wtk_k<T, 3, 3, 8>(g, in, out, r, resid, s);
+      }
+    }
     else launch_wtk_k<T, RY3, 3, 4>(g, in, out, r, resid, s);
   } else {
     launch_wtk_k<T, 1, 4, 4>(g, in, out, r, resid, s);
