@@ -1,22 +1,23 @@
-// Deep temporal blocking for the 3D 7-point stencil with wave-independent tiles (heat7_wtk):
-// K = 3 or 4 fused steps per sweep, rows of any width, no block barriers.
+// Deep temporal blocking for the 3D 7-point stencil in y bands of wave tiles (heat7_wtk):
+// K = 3 or 4 fused steps per sweep, rows of any width, one block barrier per plane.
 //
 // heat7_tbk (stencil_heat_tbk.hip) spreads one row over the 4 waves of a block and hands the x
 // seams of every level between them through LDS: K-1 block barriers per plane, and at K >= 3 the
-// barrier-coupled waves are latency-bound at two waves per SIMD. Here every wave is
-// a task of its own -- jacobi5_tbk's overlapping wave segments carried into 3D:
+// barrier-coupled waves are latency-bound at two waves per SIMD. Here no level seam
+// crosses a wave -- jacobi5_tbk's overlapping wave segments carried into 3D:
 //   x: a wave covers 64 lanes x N cells but owns only lanes OV..63-OV (OV = ceil(K / N)); the
 //      outer lanes carry the neighbouring segments' edge columns through the same instructions and
 //      go wrong one cell per level from the outside, so after K levels the owned lanes are exact.
-//      x neighbours inside the wave are DPP lane shifts, nothing crosses a wave.
+//      x neighbours inside the wave are DPP lane shifts.
 //   y: the wave owns RY output rows; level k computes the RY + 2(K-k) rows the levels above it
 //      need (the y halo is recomputed, as in heat7_tbk).
 //   z: every level is heat7_tbk's streaming recurrence: per row only the partial sum
 //      S_k = (((xm + xp) + ym) + yp) + zm of plane p and the centre C_k = u_{k-1}(p) live between
 //      planes; when u_{k-1}(p+1) arrives the level finishes u_k(p) = fma(r, fma(-6, C, S + zp), C),
 //      sm::heat7's operation order, so the sweep is bitwise equal to K single steps.
-//   u0: the next plane's RY + 2K rows stream by LDS DMA into the wave's private LDS slot one plane
-//      ahead (no VGPRs held by the prefetch; no other wave reads the slot, so no barrier).
+//   u0: the waves of a block form a y band; the band's rows of the next plane stream by LDS DMA into
+//      a shared double-buffered window one plane ahead (no VGPRs held by the prefetch), and the one
+//      barrier per plane both publishes a plane and frees the other buffer (below).
 //   Boundaries: held cells get a zero coefficient (fma(0, t, u) = u for finite t): per lane for x,
 //   per level and plane for z, per row only in tiles that reach y = 0 / ny-1. Loads outside the
 //   grid read the nearest valid row / vector, so every value a lane carries is finite.
