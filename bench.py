@@ -214,6 +214,7 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False):
         with Simulation(prob, distributed=True, transport=transport, graph=graph, **kw) as sim:
             trace("gate: engine up")
             sim.init()
+            sim.prepare_graphs()  # the timed run's path: cycles captured before any step
             sim.run(steps)
             trace("gate: steps enqueued")
             sim.synchronize()
@@ -257,7 +258,10 @@ def main(argv=None):
     from mpi_cuda_process_amd.parallel.dist import init_distributed
 
     force = os.environ.get("MDFX_FORCE_DIST", "") == "1"  # distributed path even at WORLD_SIZE 1 (tests)
-    env = init_distributed("gloo", force=force) if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or force) else None
+    # the control plane's collectives are bounded too: a rank that hangs (e.g. never joins RCCL)
+    # makes its peers' gloo calls raise after the watchdog plus a margin, and the run exits non-zero
+    env = init_distributed("gloo", timeout_s=max(60.0, a.timeout + 60.0), force=force) \
+        if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or force) else None
     world = dist.get_world_size() if env else 1
     rank = dist.get_rank() if env else 0
     if env and world > 1 and a.gpus != world:
@@ -380,6 +384,7 @@ def main(argv=None):
                 sim, sim_t = make_sim(t, g, rr, ov), t
                 sim.init()
             sim.set_options(graph=g, min_rounds=rr, overlap=ov)
+            sim.prepare_graphs()  # capture before timing (no-op with graphs off)
             sim.run(max(2, min(a.warmup, 4)))
             dt = timed(sim, n_trial)
             trace("trial %s graph=%s rounds=%s overlap=%s: %.3f ms/step" % (t, g, rr, ov, dt / n_trial * 1e3))
@@ -396,12 +401,14 @@ def main(argv=None):
     sim.set_options(graph=chosen[1], min_rounds=chosen[2], overlap=chosen[3])
     trace("engine up (%s, graph=%s, rounds=%s, overlap=%s)" % (sim.transport, chosen[1], chosen[2], chosen[3]))
     sim.init()  # every timed run starts from the same initial grid
-    trace("init done")
+    # capture both parities' graph cycles now: whatever --warmup is, the timed region only replays
+    n_graphs = sim.prepare_graphs()
+    trace("init done (%d graph cycles captured)" % n_graphs)
     sim.run(a.warmup)
     trace("warmup enqueued")
     timed(sim, 0)
     trace("warmup done")
-    replays0 = sim.graph_replays
+    replays0, captures0 = sim.graph_replays, sim.graph_captures
     best = None
     for _ in range(max(1, a.repeats)):
         dt = timed(sim, a.steps)
@@ -457,8 +464,11 @@ def main(argv=None):
                 "transport": sim_transport,
                 "comm_size": nproc if sim_transport == "rccl" else 0,
                 "kernel_variant": native().kernel_variant(),
-                "graph": chosen[1],
+                # effective mode: true only if captured cycles actually replayed in the timed region
+                "graph": (sim.graph_replays - replays0) > 0,
+                "graph_requested": chosen[1],
                 "graph_replays_timed": sim.graph_replays - replays0,
+                "graph_captures_timed": sim.graph_captures - captures0,
                 "min_rounds": chosen[2] or ("2 (auto)" if nproc > 1 or a.virtual_ranks > 1 else "1 (auto)"),
                 "trials": trials,
                 "overlap": chosen[3],

@@ -20,6 +20,8 @@
 // on the slab's halo stream, after the boundary kernels that wrote the faces of buffer b:
 //
 //   for each neighbour n:  wait(n.pulled[mine] >= e - 2)   n is done with mailbox slot b (exchange e-2)
+//                          (>= e - 1 when exchange e-1 used the same parity b: a re-send of the
+//                          current buffer after init() / write_owned(), so slot b was used last)
 //   copy my faces of b -> mailbox[b][side]               (local)
 //   signal(ready)                                        exchange e published
 //   for each neighbour n:  wait(n.ready >= e)
@@ -47,6 +49,8 @@ namespace mdfx {
     hipError_t e_ = (x);                                                                 \
     if (e_ != hipSuccess) ::mdfx::throw_error(__FILE__, __LINE__, std::string("HIP: ") + #x + " -> " + hipGetErrorString(e_)); \
   } while (0)
+
+void ipc_enable_peer(int mine, int peer, int peer_rank);
 
 namespace {
 
@@ -79,6 +83,7 @@ class IpcTransport final : public Transport {
     }
     if (mbox_) (void)hipFree(mbox_);
     hip_free_uncached(ctr_);
+    hip_words_free(words_);
   }
   const char* name() const override { return "ipc"; }
   bool in_process_only() const override { return false; }
@@ -92,6 +97,7 @@ class IpcTransport final : public Transport {
     MDFX_CHECK(self_.be->kind() == DeviceKind::HIP, "ipc transport needs a HIP backend");
     self_.be->activate();
     ctr_ = (uint64_t*)hip_alloc_uncached(kCounterBytes);
+    words_ = hip_words_alloc();  // this transport's own abort / wait-error words
     const uint64_t two = 2;  // exchanges 1 and 2 find their mailbox slot free
     HIPC(hipMemcpy(ctr_ + kPulled + 0, &two, 8, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(ctr_ + kPulled + 1, &two, 8, hipMemcpyHostToDevice));
@@ -122,9 +128,13 @@ class IpcTransport final : public Transport {
       IpcRecord r;
       MDFX_CHECK(all[p.rank].size() == sizeof(IpcRecord), "ipc: malformed handle record");
       std::memcpy(&r, all[p.rank].data(), sizeof(r));
-      MDFX_CHECK(std::memcmp(r.magic, "MDFXIPC2", 8) == 0 && r.rank == p.rank, "ipc: handle record mismatch");
-      MDFX_CHECK(r.pid != mine.pid, "ipc transport: neighbouring slabs must live in different processes");
-      MDFX_CHECK(r.face_bytes == face_, "ipc: neighbour face size does not match this slab's");
+      IpcPeerInfo me{mine.rank, mine.device, mine.pid, mine.face_bytes, true};
+      IpcPeerInfo them{r.rank, r.device, r.pid, r.face_bytes, std::memcmp(r.magic, "MDFXIPC2", 8) == 0};
+      int can = 1;
+      if (r.device != mine.device) HIPC(hipDeviceCanAccessPeer(&can, mine.device, r.device));
+      const std::string why = ipc_peer_problem(me, them, p.rank, can != 0);
+      MDFX_CHECK(why.empty(), why);
+      ipc_enable_peer(mine.device, r.device, p.rank);
       HIPC(hipIpcOpenMemHandle(&p.mbox, r.mbox, hipIpcMemLazyEnablePeerAccess));
       HIPC(hipIpcOpenMemHandle(&p.ctr, r.ctr, hipIpcMemLazyEnablePeerAccess));
       p.device = r.device;
@@ -138,13 +148,20 @@ class IpcTransport final : public Transport {
   void exchange(int b) override {
     self_.be->activate();
     hipStream_t hs = (hipStream_t)self_.halo_stream;
+    // inside a graph capture the pair alternates parities and the engine replays it only after an
+    // exchange of the other parity: no look-ahead, and last_b_ tracks real (eager) exchanges only
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPC(hipStreamIsCapturing(hs, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    const uint64_t ahead = (!capturing && last_b_ == b) ? 1 : 0;
     // publish: the neighbour on `side` must be done with slot b (exchange e-2) before it is reused
     for (int side = 0; side < 2; ++side) {
       const Peer& p = peers_[side];
       if (p.rank < 0) continue;
       const HaloSpan mine = halo_span(self_, b, side, nranks_);
       MDFX_CHECK(mine.bytes == face_ && mine.peer == p.rank, "ipc: face geometry mismatch");
-      hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs);
+      hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs,
+                       ahead, &words_);
       HIPC(hipMemcpyAsync(slot(mbox_, b, side), mine.send, face_, hipMemcpyDeviceToDevice, hs));
     }
     hip_counter_signal(ctr_ + kReady, hs);
@@ -153,11 +170,16 @@ class IpcTransport final : public Transport {
       const Peer& p = peers_[side];
       if (p.rank < 0) continue;
       const HaloSpan mine = halo_span(self_, b, side, nranks_);
-      hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs);
+      hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
       HIPC(hipMemcpyAsync(mine.recv, slot(p.mbox, b, 1 - side), face_, hipMemcpyDeviceToDevice, hs));
       hip_counter_signal(ctr_ + kPulled + side, hs);
     }
+    if (!capturing) last_b_ = b;
   }
+  void set_last_parity(int b) override { last_b_ = b; }
+  // a captured 2-exchange cycle bakes the look-ahead of its first wait: the engine replays one only
+  // when the exchange before it used the other parity (Solver::run)
+  int last_parity() const override { return last_b_; }
 
   double allreduce_sum(double v) override { return f_.allreduce_sum ? f_.allreduce_sum(v) : v; }
   double allreduce_max(double v) override { return f_.allreduce_max ? f_.allreduce_max(v) : v; }
@@ -165,11 +187,16 @@ class IpcTransport final : public Transport {
     if (f_.barrier) f_.barrier();
   }
   void check() override {
-    if (hip_wait_error())
+    if (!words_.host) return;
+    if (words_.wait_error())
       MDFX_FAIL(format("ipc transport: rank %d timed out after %.0f s waiting for a neighbour's halo counter "
                        "(a peer process died or hung)", self_.rank, timeout_s_));
+    if (words_.abort_raised())
+      MDFX_FAIL(format("ipc transport: rank %d was aborted; its halo copies are no longer ordered", self_.rank));
   }
-  void abort() override { hip_set_abort(1); }
+  void abort() override {
+    if (words_.host) words_.set_abort(1);
+  }
 
  private:
   struct Peer {
@@ -182,6 +209,8 @@ class IpcTransport final : public Transport {
   LocalSlab self_;
   int nranks_ = 1;
   uint64_t* ctr_ = nullptr;
+  HipWords words_;
+  int last_b_ = -1;  // parity of the previous exchange
   void* mbox_ = nullptr;
   size_t face_ = 0;
   bool dev_ok_ = false;
@@ -190,6 +219,37 @@ class IpcTransport final : public Transport {
 };
 
 }  // namespace
+
+std::string ipc_peer_problem(const IpcPeerInfo& mine, const IpcPeerInfo& peer, int expect_rank, bool peer_access) {
+  if (!peer.magic_ok || peer.rank != expect_rank)
+    return format("ipc: handle record mismatch (expected rank %d, got %d)", expect_rank, peer.rank);
+  if (peer.pid == mine.pid) return "ipc transport: neighbouring slabs must live in different processes";
+  if (peer.face_bytes != mine.face_bytes)
+    return format("ipc: neighbour face size %llu does not match this slab's %llu", (unsigned long long)peer.face_bytes,
+                  (unsigned long long)mine.face_bytes);
+  if (peer.device != mine.device && !peer_access)
+    return format("ipc transport: device %d cannot access device %d (rank %d's) with peer copies over xGMI / PCIe; "
+                  "use --transport rccl", mine.device, peer.device, peer.rank);
+  return "";
+}
+
+// A neighbour on another GPU is reached by peer copies over xGMI: enable peer access explicitly
+// (an already-enabled pair is fine) instead of relying on the lazy mapping of the IPC open.
+void ipc_enable_peer(int mine, int peer, int peer_rank) {
+  if (mine == peer) return;
+  int cur = 0;
+  HIPC(hipGetDevice(&cur));
+  HIPC(hipSetDevice(mine));
+  const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  (void)hipSetDevice(cur);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();  // clear the "already enabled" status
+    return;
+  }
+  if (e != hipSuccess)
+    MDFX_FAIL(format("ipc transport: enabling peer access from device %d to device %d (rank %d) failed: %s", mine,
+                     peer, peer_rank, hipGetErrorString(e)));
+}
 
 std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns) {
   return std::unique_ptr<Transport>(new IpcTransport(std::move(fns)));

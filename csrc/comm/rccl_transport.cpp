@@ -15,6 +15,8 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -79,6 +81,10 @@ class RcclTransport final : public Transport {
       if (c) (void)ncclCommAbort(c);
   }
 
+  // Bounded bootstrap: the communicators are created non-blocking and polled under the watchdog
+  // bound (timeout_s, or 600 s when the watchdog is off), so a rank that never joins makes every
+  // other rank abort its half-built communicator and fail with a message instead of blocking in
+  // ncclCommInitRank forever (the reference's D4 hang class starts at its MPI_Init / first send).
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
     locals_ = locals;
     nranks_ = nranks;
@@ -86,17 +92,21 @@ class RcclTransport final : public Transport {
     scratch_.assign(locals_.size(), nullptr);
     aux_.assign(locals_.size(), nullptr);
     for (auto& s : locals_) MDFX_CHECK(s.be->kind() == DeviceKind::HIP, "rccl transport needs HIP backends");
+    maybe_hang_before_init();
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
     if (locals_.size() == 1) {
       locals_[0].be->activate();
-      NCCLC(ncclCommInitRank(&comms_[0], nranks_, id_, locals_[0].rank));
+      accept(ncclCommInitRankConfig(&comms_[0], nranks_, id_, locals_[0].rank, &cfg), "ncclCommInitRankConfig");
     } else {
       NCCLC(ncclGroupStart());
       for (size_t i = 0; i < locals_.size(); ++i) {
         locals_[i].be->activate();
-        NCCLC(ncclCommInitRank(&comms_[i], nranks_, id_, locals_[i].rank));
+        accept(ncclCommInitRankConfig(&comms_[i], nranks_, id_, locals_[i].rank, &cfg), "ncclCommInitRankConfig");
       }
-      NCCLC(ncclGroupEnd());
+      accept(ncclGroupEnd(), "ncclGroupEnd (init)");
     }
+    wait_ready("bootstrap (ncclCommInitRankConfig)", 1000);
     for (size_t i = 0; i < locals_.size(); ++i) {
       locals_[i].be->activate();
       HIPC(hipMalloc(&scratch_[i], 2 * sizeof(double)));
@@ -111,11 +121,13 @@ class RcclTransport final : public Transport {
       for (int side = 0; side < 2; ++side) {
         const HaloSpan h = halo_span(s, b, side, nranks_);
         if (h.peer < 0) continue;
-        NCCLC(ncclRecv(h.recv, h.bytes, ncclUint8, h.peer, comms_[i], (hipStream_t)s.halo_stream));
-        NCCLC(ncclSend(h.send, h.bytes, ncclUint8, h.peer, comms_[i], (hipStream_t)s.halo_stream));
+        accept(ncclRecv(h.recv, h.bytes, ncclUint8, h.peer, comms_[i], (hipStream_t)s.halo_stream), "ncclRecv");
+        accept(ncclSend(h.send, h.bytes, ncclUint8, h.peer, comms_[i], (hipStream_t)s.halo_stream), "ncclSend");
       }
     }
-    NCCLC(ncclGroupEnd());
+    // non-blocking communicators: a group whose p2p connections are still being set up (the first
+    // exchange with a peer) returns ncclInProgress; wait for the launch before anything else
+    if (accept(ncclGroupEnd(), "ncclGroupEnd (exchange)") == ncclInProgress) wait_ready("halo exchange launch", 50);
   }
 
   double allreduce(double v, ncclRedOp_t op) {
@@ -128,9 +140,9 @@ class RcclTransport final : public Transport {
     }
     NCCLC(ncclGroupStart());
     for (size_t i = 0; i < locals_.size(); ++i)
-      NCCLC(ncclAllReduce(scratch_[i], (char*)scratch_[i] + sizeof(double), 1, ncclFloat64, op,
-                          comms_[i], aux_[i]));
-    NCCLC(ncclGroupEnd());
+      accept(ncclAllReduce(scratch_[i], (char*)scratch_[i] + sizeof(double), 1, ncclFloat64, op, comms_[i], aux_[i]),
+             "ncclAllReduce");
+    if (accept(ncclGroupEnd(), "ncclGroupEnd (all-reduce)") == ncclInProgress) wait_ready("all-reduce launch", 50);
     const auto t0 = std::chrono::steady_clock::now();
     for (size_t i = 0; i < locals_.size(); ++i) {
       locals_[i].be->activate();
@@ -169,6 +181,57 @@ class RcclTransport final : public Transport {
   }
 
  private:
+  // ncclSuccess or (non-blocking communicator) ncclInProgress; anything else throws
+  static ncclResult_t accept(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess && r != ncclInProgress)
+      ::mdfx::throw_error(__FILE__, __LINE__, std::string("RCCL: ") + what + " -> " + ncclGetErrorString(r));
+    return r;
+  }
+  // Poll every communicator until no operation is in progress, bounded by the watchdog (600 s when
+  // it is off); on expiry or error abort the communicators and throw.
+  void wait_ready(const char* what, int poll_us) {
+    const double limit = timeout_s_ > 0 ? timeout_s_ : 600.0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      bool busy = false;
+      for (auto c : comms_) {
+        if (!c) continue;
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+        if (q != ncclSuccess && q != ncclInProgress) {
+          abort();
+          MDFX_FAIL(std::string("RCCL ") + what + ": ncclCommGetAsyncError -> " + ncclGetErrorString(q));
+        }
+        if (st == ncclInProgress) busy = true;
+        else if (st != ncclSuccess) {
+          abort();
+          MDFX_FAIL(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(st));
+        }
+      }
+      if (!busy) return;
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > limit) {
+        abort();
+        MDFX_FAIL(format("RCCL %s not complete after %.1f s on rank %d of %d: a peer rank never joined or hung "
+                         "(communicators aborted)", what, el, locals_.empty() ? -1 : locals_[0].rank, nranks_));
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
+    }
+  }
+  // Fault injection for the bootstrap tests: MDFX_FAULT=inithang@<rank> makes that rank stop
+  // before it joins the communicator (it sleeps until killed, at most an hour).
+  void maybe_hang_before_init() const {
+    const char* v = std::getenv("MDFX_FAULT");
+    int rk = -1;
+    if (!v || std::sscanf(v, "inithang@%d", &rk) != 1) return;
+    for (auto& s : locals_)
+      if (s.rank == rk) {
+        std::fprintf(stderr, "[mdfx] injecting fault 'inithang' on rank %d before ncclCommInitRankConfig\n", rk);
+        std::fflush(stderr);
+        for (int i = 0; i < 3600; ++i) std::this_thread::sleep_for(std::chrono::seconds(1));
+      }
+  }
+
   ncclUniqueId id_;
   std::vector<LocalSlab> locals_;
   int nranks_ = 1;

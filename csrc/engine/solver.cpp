@@ -158,14 +158,16 @@ void Solver::set_options(const SolverOptions& o) {
 }
 
 void Solver::init(const InitSpec& is) {
-  destroy_graph();
+  // captured cycles stay valid: init rewrites the buffers in place, it does not move them
   for (auto& s : slabs_) {
     s.be->init(is, s.lay, s.buf[0], s.hs);
     s.be->init(is, s.lay, s.buf[1], s.hs);
   }
   sync_all();
   cur_ = 0;
+  const int64_t caps = stats_.graph_captures;
   stats_ = StepStats();
+  stats_.graph_captures = caps;
   ghosts_dirty_ = false;  // ghosts are generated from the global index too
 }
 
@@ -243,7 +245,6 @@ void Solver::synchronize() {
 }
 
 void Solver::exchange_ghosts() {
-  destroy_graph();
   // make the current buffer's owned planes visible to the exchange (ordered on the halo stream)
   for (auto& s : slabs_) {
     s.be->wait(s.hs, s.ev_int);
@@ -478,10 +479,12 @@ void Solver::run(int64_t steps) {
     // binary and capture replay bitwise under 7.2 (csrc/tests/test_main.cpp test_graph run against
     // both runtimes: profiles/r02_graph_runtime.txt). One slab per process (the production layout)
     // replays under both.
-    if (opt_.graph && hip && !res && !opt_.sync_debug && !opt_.profile && transport_->graph_capturable() &&
-        (slabs_.size() == 1 || multislab_graph_ok())) {
+    // A captured cycle's first exchange sends buffer 1 - cur_; it is replayed only when the exchange
+    // before it sent the other parity (a repeated parity needs the ipc transport's eager look-ahead
+    // wait, ipc_transport.cpp).
+    if (!res && graph_eligible() && transport_->last_parity() != 1 - cur_) {
       const int64_t plain = std::min<int64_t>(steps - done, to_res - 1);
-      const int64_t pairs = fault().rank >= 0 ? 0 : plain / (2 * k);
+      const int64_t pairs = plain / (2 * k);
       if (pairs > 0) {
         run_graph(pairs, k);
         done += 2 * k * pairs;
@@ -497,13 +500,48 @@ void Solver::run(int64_t steps) {
 // ---- hipGraph replay of a 2-step cycle --------------------------------------------------------
 // Captured from the halo stream of slab 0; every other stream joins the capture through event
 // waits (fork) and is joined back at the end, so the replay carries exactly the eager schedule's
-// dependencies. The captured cycle starts at buffer `graph_parity_`.
+// dependencies. graph_exec_[p] is the cycle that starts at buffer p; both are kept until an option
+// change alters the captured work (init() rewrites the buffers in place and keeps them).
 void Solver::destroy_graph() {
-  if (graph_exec_) {
-    (void)hipGraphExecDestroy((hipGraphExec_t)graph_exec_);
-    graph_exec_ = nullptr;
+  for (int p = 0; p < 2; ++p) {
+    if (graph_exec_[p]) (void)hipGraphExecDestroy((hipGraphExec_t)graph_exec_[p]);
+    graph_exec_[p] = nullptr;
+    graph_k_[p] = 0;
   }
-  graph_parity_ = -1;
+}
+
+bool Solver::graph_eligible() const {
+  const bool hip = slabs_[0].be->kind() == DeviceKind::HIP;
+  return opt_.graph && hip && !opt_.sync_debug && !opt_.profile && transport_->graph_capturable() &&
+         (slabs_.size() == 1 || multislab_graph_ok()) && fault().rank < 0 && !poisoned_;
+}
+
+int Solver::prepare_graphs() {
+  MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
+  if (!graph_eligible()) return 0;
+  int k = 1;
+  for (int kk = opt_.temporal; kk > 1; --kk)
+    if (depth_ok_[kk]) {
+      k = kk;
+      break;
+    }
+  // one eager exchange first (it re-sends the current faces, so it changes nothing): transports
+  // that set up peer connections on first use (RCCL p2p) do so outside the capture
+  exchange_ghosts();
+  const int saved = cur_;
+  for (int p = 0; p < 2; ++p) {
+    if (graph_exec_[p] && graph_k_[p] == k) continue;
+    cur_ = p;
+    capture_graph(p, k);
+  }
+  cur_ = saved;
+  // the captures recorded the per-slab events inside the graphs: re-arm them for eager work
+  for (auto& s : slabs_) {
+    s.be->activate();
+    s.be->record(s.ev_bnd, s.hs);
+    s.be->record(s.ev_int, s.cs);
+  }
+  return (graph_exec_[0] ? 1 : 0) + (graph_exec_[1] ? 1 : 0);
 }
 
 static bool graph_debug() {
@@ -518,70 +556,89 @@ static bool graph_debug() {
     if (graph_debug()) std::fprintf(stderr, "[mdfx graph] %s\n", msg); \
   } while (0)
 
-void Solver::run_graph(int64_t pairs, int k) {
-  if (!graph_exec_ || graph_parity_ != cur_ || graph_k_ != k) {
-    GDBG("capture begin");
-    destroy_graph();
-    Slab& o = slabs_[0];
-    o.be->activate();
-    hipStream_t origin = (hipStream_t)o.hs;
-    std::vector<hipEvent_t> fork(slabs_.size() * 2), join(slabs_.size() * 2);
-    for (auto& e : fork) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto& e : join) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPC(hipStreamBeginCapture(origin, hipStreamCaptureModeRelaxed));
-    HIPC(hipEventRecord(fork[0], origin));
-    size_t ei = 0;
-    for (auto& s : slabs_) {
-      s.be->activate();
-      for (void* st : {s.hs, s.cs}) {
-        if (st != (void*)origin) HIPC(hipStreamWaitEvent((hipStream_t)st, fork[0], 0));
-        ++ei;
+// Capture the cycle starting at buffer `parity` (== cur_): two sweeps of depth k. Nothing runs.
+void Solver::capture_graph(int parity, int k) {
+  GDBG("capture begin");
+  if (graph_exec_[parity]) {
+    (void)hipGraphExecDestroy((hipGraphExec_t)graph_exec_[parity]);
+    graph_exec_[parity] = nullptr;
+  }
+  Slab& o = slabs_[0];
+  o.be->activate();
+  hipStream_t origin = (hipStream_t)o.hs;
+  std::vector<hipEvent_t> fork(slabs_.size() * 2), join(slabs_.size() * 2);
+  for (auto& e : fork) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : join) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPC(hipStreamBeginCapture(origin, hipStreamCaptureModeRelaxed));
+  HIPC(hipEventRecord(fork[0], origin));
+  for (auto& s : slabs_) {
+    s.be->activate();
+    for (void* st : {s.hs, s.cs})
+      if (st != (void*)origin) HIPC(hipStreamWaitEvent((hipStream_t)st, fork[0], 0));
+  }
+  // every event the captured steps wait on must itself be recorded inside the capture
+  for (auto& s : slabs_) {
+    s.be->activate();
+    s.be->record(s.ev_bnd, s.hs);
+    s.be->record(s.ev_int, s.cs);
+  }
+  const StepStats saved = stats_;
+  GDBG("capture: steps");
+  step(false, k);
+  step(false, k);
+  GDBG("capture: join");
+  stats_ = saved;  // replay accounts for them
+  ++stats_.graph_captures;
+  size_t ei = 0;
+  for (auto& s : slabs_) {
+    s.be->activate();
+    for (void* st : {s.hs, s.cs}) {
+      if (st != (void*)origin) {
+        HIPC(hipEventRecord(join[ei], (hipStream_t)st));
+        o.be->activate();
+        HIPC(hipStreamWaitEvent(origin, join[ei], 0));
+        s.be->activate();
       }
+      ++ei;
     }
-    // every event the captured steps wait on must itself be recorded inside the capture
+  }
+  o.be->activate();
+  hipGraph_t g;
+  GDBG("capture: end");
+  HIPC(hipStreamEndCapture(origin, &g));
+  GDBG("instantiate");
+  hipGraphExec_t ex;
+  HIPC(hipGraphInstantiateWithFlags(&ex, g, 0));
+  HIPC(hipGraphDestroy(g));
+  for (auto& e : fork) (void)hipEventDestroy(e);
+  for (auto& e : join) (void)hipEventDestroy(e);
+  graph_exec_[parity] = ex;
+  graph_k_[parity] = k;
+  MDFX_CHECK(cur_ == parity, "graph capture must leave the buffer parity unchanged");
+  GDBG("instantiated");
+}
+
+void Solver::run_graph(int64_t pairs, int k) {
+  if (!graph_exec_[cur_] || graph_k_[cur_] != k) {
+    capture_graph(cur_, k);
+    // the capture recorded the per-slab events inside the graph: re-arm them before the launch
     for (auto& s : slabs_) {
       s.be->activate();
       s.be->record(s.ev_bnd, s.hs);
       s.be->record(s.ev_int, s.cs);
     }
-    const int64_t saved = stats_.steps;
-    GDBG("capture: steps");
-    step(false, k);
-    step(false, k);
-    GDBG("capture: join");
-    stats_.steps = saved;  // replay accounts for them
-    ei = 0;
-    for (auto& s : slabs_) {
-      s.be->activate();
-      for (void* st : {s.hs, s.cs}) {
-        if (st != (void*)origin) {
-          HIPC(hipEventRecord(join[ei], (hipStream_t)st));
-          o.be->activate();
-          HIPC(hipStreamWaitEvent(origin, join[ei], 0));
-          s.be->activate();
-        }
-        ++ei;
-      }
-    }
-    o.be->activate();
-    hipGraph_t g;
-    GDBG("capture: end");
-    HIPC(hipStreamEndCapture(origin, &g));
-    GDBG("instantiate");
-    hipGraphExec_t ex;
-    HIPC(hipGraphInstantiateWithFlags(&ex, g, 0));
-    HIPC(hipGraphDestroy(g));
-    for (auto& e : fork) (void)hipEventDestroy(e);
-    for (auto& e : join) (void)hipEventDestroy(e);
-    graph_exec_ = ex;
-    graph_parity_ = cur_;  // step() x2 leaves cur_ unchanged
-    graph_k_ = k;
-    GDBG("instantiated");
   }
   GDBG("launch");
   Slab& o = slabs_[0];
   o.be->activate();
-  for (int64_t i = 0; i < pairs; ++i) HIPC(hipGraphLaunch((hipGraphExec_t)graph_exec_, (hipStream_t)o.hs));
+  // the replay starts after all eager work on every slab's streams
+  for (auto& s : slabs_) {
+    if (&s == &o) continue;
+    o.be->wait(o.hs, s.ev_bnd);
+    o.be->wait(o.hs, s.ev_int);
+  }
+  o.be->wait(o.hs, o.ev_int);
+  for (int64_t i = 0; i < pairs; ++i) HIPC(hipGraphLaunch((hipGraphExec_t)graph_exec_[cur_], (hipStream_t)o.hs));
   // later eager work on the other streams must follow the replay
   HIPC(hipEventRecord((hipEvent_t)o.ev_bnd, (hipStream_t)o.hs));
   for (auto& s : slabs_) {
@@ -595,6 +652,8 @@ void Solver::run_graph(int64_t pairs, int k) {
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
   }
+  // a replayed cycle ends with the exchange of buffer cur_ (the parity is unchanged)
+  transport_->set_last_parity(cur_);
   stats_.steps += 2 * (int64_t)k * pairs;
   stats_.graph_replays += pairs;
   GDBG("replayed");
@@ -621,7 +680,6 @@ void Solver::read_owned(int i, void* host) {
 }
 
 void Solver::write_owned(int i, const void* host) {
-  destroy_graph();
   Slab& s = slabs_[i];
   sync_all();
   const FieldLayout& l = s.lay;

@@ -27,9 +27,24 @@ void hip_free_uncached(void* p);
 // Stream-ordered: *ctr += 1 (system-scope release: everything earlier on `stream` is visible to
 // any agent that then observes the new value). Single writer per counter.
 void hip_counter_signal(uint64_t* ctr, void* stream);
-// Stream-ordered: ++*expect (a private device counter), then wait until *remote >= *expect with a
-// system-scope acquire. Bounded by timeout_s and the abort word.
-void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream);
+// An abort word ([0]) and a wait-error word ([16]) of one owner (a transport), host-mapped and
+// coherent, so one engine's watchdog releases only its own device waits and reports only its own
+// timeouts (the process-wide words above serve the fault-injection spin and owners without a pair).
+struct HipWords {
+  int* host = nullptr;
+  int* dev = nullptr;
+  void set_abort(int v) const { __atomic_store_n(&host[0], v, __ATOMIC_SEQ_CST); }
+  int abort_raised() const { return __atomic_load_n(&host[0], __ATOMIC_SEQ_CST); }
+  int wait_error() const { return __atomic_load_n(&host[16], __ATOMIC_SEQ_CST); }
+};
+HipWords hip_words_alloc();
+void hip_words_free(HipWords& w);
+
+// Stream-ordered: ++*expect (a private device counter), then wait until *remote >= *expect + ahead
+// with a system-scope acquire. Bounded by timeout_s and the abort word (the owner's pair when
+// `own` is given, else the process-wide one); a timeout raises the matching error word.
+void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream,
+                      uint64_t ahead = 0, const HipWords* own = nullptr);
 
 // Tests: leave a quiet-NaN pattern in every CU's LDS (synchronous, current device), so a kernel
 // that reads LDS it never wrote produces NaN instead of silently using stale finite data.

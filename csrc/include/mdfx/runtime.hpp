@@ -90,6 +90,11 @@ class Transport {
   // Watchdog escalation: make every outstanding transport operation return (ncclCommAbort, the
   // device abort word) so the streams drain and the process can exit instead of hanging.
   virtual void abort() {}
+  // Parity of the buffer the last exchange() sent (-1: none yet, or the transport does not track
+  // it). The ipc transport uses it to reuse a mailbox slot safely when a parity repeats.
+  virtual int last_parity() const { return -1; }
+  // The engine replayed captured exchanges (which bypass exchange()); the last one sent parity b.
+  virtual void set_last_parity(int) {}
 };
 
 // CPU, all subdomains in this process: memcpy.
@@ -114,5 +119,16 @@ std::unique_ptr<Transport> make_callback_transport(CallbackFns fns);
 // neighbours' mapped buffers by the copy engines, ordered by device-side counters
 // (csrc/comm/ipc_transport.cpp). Needs fns.allgather; residual / barrier go through fns too.
 std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns);
+// What the ipc transport knows about one process's slab when it maps a neighbour (the host-side
+// part of its handle record).
+struct IpcPeerInfo {
+  int rank = -1, device = -1, pid = 0;
+  uint64_t face_bytes = 0;
+  bool magic_ok = true;
+};
+// Host-only validation of a neighbour's record (CPU-testable): "" if the pair can exchange, else
+// why not. `peer_access` is hipDeviceCanAccessPeer(mine.device -> peer.device) for devices that
+// differ (ignored on one device).
+std::string ipc_peer_problem(const IpcPeerInfo& mine, const IpcPeerInfo& peer, int expect_rank, bool peer_access);
 
 }  // namespace mdfx

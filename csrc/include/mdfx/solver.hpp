@@ -53,6 +53,7 @@ struct StepStats {
   double last_residual = -1.0;  // sqrt(sum over the grid of (u_new - u_old)^2), -1 if never
   int64_t residual_step = -1;
   int64_t graph_replays = 0;  // 2-sweep cycles replayed from a captured hipGraph
+  int64_t graph_captures = 0;  // cycles captured + instantiated (prepare_graphs() or on demand)
 };
 
 class Solver {
@@ -67,6 +68,14 @@ class Solver {
 
   void init(const InitSpec& s);
   void run(int64_t steps);
+  // Capture the 2-sweep hipGraph cycles of both buffer parities now (graph option on and the
+  // configuration capturable), so a later run() only replays: a benchmark calls this before its
+  // warmup and no capture or instantiation ever falls inside a timed region. Returns the number of
+  // cycles held (0 if graphs are off or not capturable here). init() keeps them (buffers do not
+  // move); option changes that alter the captured work drop them.
+  int prepare_graphs();
+  // Whether run() would replay captured cycles in this configuration.
+  bool graph_eligible() const;
   void synchronize();
   // Refresh ghost planes of the current buffer (after write_owned / resume).
   void exchange_ghosts();
@@ -119,6 +128,7 @@ class Solver {
   [[noreturn]] void poison(const std::string& why);  // watchdog escalation, then throw
   void finish_residual();
   void run_graph(int64_t pairs, int k);
+  void capture_graph(int parity, int k);
   void destroy_graph();
 
   StencilSpec spec_;
@@ -134,9 +144,9 @@ class Solver {
   void* pev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // timing events (slab 0)
   bool ghosts_dirty_ = false;
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
-  void* graph_exec_ = nullptr;  // hipGraphExec_t for the 2-step cycle starting at buffer 0
-  int graph_parity_ = -1;
-  int graph_k_ = 0;
+  // hipGraphExec_t of the 2-sweep cycle starting at buffer p (index p), and its fused depth
+  void* graph_exec_[2] = {nullptr, nullptr};
+  int graph_k_[2] = {0, 0};
   // depth_ok_[k]: every slab can run a k-step fused sweep (k <= temporal); 1 always can
   bool depth_ok_[17] = {false, true};
 };

@@ -90,6 +90,23 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
 
 // Raw waits: s_waitcnt encodings for gfx9 (vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]).
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// vmcnt(n) for a wave-uniform n in 0..7 (an immediate per case): wait until at most the wave's n
+// youngest vector-memory operations are outstanding. The streaming kernels issue the next plane's
+// LDS DMA first and the output stores of the plane after it; waiting with n = the stores issued
+// since the DMA leaves those stores in flight across the next plane's barrier instead of
+// exposing a full store round trip per plane (an out-of-range n waits for everything).
+__device__ __forceinline__ void wait_vm_le(int n) {
+  switch (n) {
+    case 1: __builtin_amdgcn_s_waitcnt(0x0F71); break;
+    case 2: __builtin_amdgcn_s_waitcnt(0x0F72); break;
+    case 3: __builtin_amdgcn_s_waitcnt(0x0F73); break;
+    case 4: __builtin_amdgcn_s_waitcnt(0x0F74); break;
+    case 5: __builtin_amdgcn_s_waitcnt(0x0F75); break;
+    case 6: __builtin_amdgcn_s_waitcnt(0x0F76); break;
+    case 7: __builtin_amdgcn_s_waitcnt(0x0F77); break;
+    default: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+  }
+}
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 // Workgroup barrier that does NOT drain outstanding vector-memory operations (a __syncthreads
 // makes hipcc wait for vmcnt(0), which would also wait for an in-flight LDS DMA). LDS writes are
@@ -190,6 +207,8 @@ struct Knobs {
   int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
   int life_bits = 1;   // MDFX_LIFE_BITS: Life sweeps of K > 2 generations bit-sliced (0: SWAR life_tbk)
   int b27_tbk = 0;     // MDFX_B27_TBK: 27-point fused kernel (0: per dtype, -1: box27_tb2, 1/2/4: box27_tbk rows)
+  int vm_lag = 1;      // MDFX_VM_LAG: streaming kernels leave the last plane's stores in flight across the
+                       // next plane's DMA wait (0: wait for every vector-memory operation, round 2)
   int debug_zc = 0;    // MDFX_DEBUG_ZC: print the z chunking of the streaming kernels
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
 };

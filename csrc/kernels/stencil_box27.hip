@@ -411,7 +411,8 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
 // one barrier per level and plane. Region contract as heat7_tbk: u0 valid on [lz_begin - K, lz_end + K).
 template <class T, int RY, int K, int WXN, bool RES>
 __global__ __launch_bounds__(256) void box27_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
-                                                 T c2, T c3, int zc, int YT, double* __restrict__ resid) {
+                                                 T c2, T c3, int zc, int YT, double* __restrict__ resid,
+                                                 int lag) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
   using Row = typename RO::Row;
@@ -486,13 +487,16 @@ __global__ __launch_bounds__(256) void box27_tbk(const T* __restrict__ in, T* __
     S[i] = RO::zero();
     C[i] = RO::zero();
   }
+  // output stores per stored plane (wave-uniform; a wave with no lane in the row issues none)
+  const int nsto = (lag && __builtin_amdgcn_ballot_w64(xin) != 0) ? (int)max((int64_t)0, min((int64_t)RY, g.ny - y0)) : 0;
+  int nst = 0;  // stores issued since this wave's last DMA
   double acc = 0.0;
   const int64_t cend = ze + K;
   const T* base0 = (const T*)&slot[w][R0][0] + (lane < 32 ? N - 1 : 0);
   issue(zs - K);
   for (int64_t c = zs - K; c < cend; ++c) {
     const int par = (int)(c & 1);
-    wait_vm0();  // this wave's DMA of plane c has landed
+    wait_vm_le(nst);  // this wave's DMA of plane c has landed (its later stores may not have)
     Row X[R0];
     T LO[R0], HI[R0];
 #pragma unroll
@@ -579,6 +583,7 @@ __global__ __launch_bounds__(256) void box27_tbk(const T* __restrict__ in, T* __
 #pragma unroll
           for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
         } else if (c >= zs + K) {  // u_K(c - K) is an owned output plane
+          nst = nsto;
           const int64_t lz = c - K;
 #pragma unroll
           for (int i = 0; i < RY; ++i) {
@@ -608,9 +613,9 @@ static void launch_box27_tbk_w(const Geo& g, const T* in, T* out, const StencilC
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
   if (resid)
-    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid, knobs().vm_lag);
   else
-    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid, knobs().vm_lag);
 }
 
 template <class T, int RY, int K>

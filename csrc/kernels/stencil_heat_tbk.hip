@@ -50,7 +50,7 @@ int64_t resident_blocks(const void* kfn);
 
 template <class T, int RY, int K, int WXN, bool RES>
 __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                 int zc, int YT, double* __restrict__ resid) {
+                                                 int zc, int YT, double* __restrict__ resid, int lag) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
   using Row = typename RO::Row;
@@ -142,12 +142,15 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
     S[i] = RO::zero();
     C[i] = RO::zero();
   }
+  // output stores per stored plane (wave-uniform; a wave with no lane in the row issues none)
+  const int nsto = (lag && __builtin_amdgcn_ballot_w64(xin) != 0) ? max(0, min(RY, ny - y0)) : 0;
+  int nst = 0;  // stores issued since this wave's last DMA
   double acc = 0.0;
   const int cend = ze + K;
   issue(zs - K);
   for (int c = zs - K; c < cend; ++c) {
     const int par = (int)(c & 1);
-    wait_vm0();  // this wave's DMA of plane c has landed
+    wait_vm_le(nst);  // this wave's DMA of plane c has landed (its later stores may not have)
     Row X[R0];
     T LO[R0], HI[R0];
     auto ld0 = [&](int k) __attribute__((always_inline)) {
@@ -232,6 +235,7 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
 #pragma unroll
           for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
         } else if (c >= zs + K) {  // u_K(c - K) is an owned output plane
+          nst = nsto;
           const int lz = c - K;
 #pragma unroll
           for (int i = 0; i < RY; ++i) {
@@ -299,9 +303,9 @@ static void launch_tbk_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
-    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid, knobs().vm_lag);
   else
-    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid, knobs().vm_lag);
 }
 
 template <class T, int RY, int K>

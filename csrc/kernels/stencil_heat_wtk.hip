@@ -48,7 +48,8 @@ int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
 // against 1.444 / 1.108 for bands of 4 / 8, and slower on every shape, profiles/r02_wtk/README.txt.)
 template <class T, int RY, int K, int WB, bool RES>
 __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                 int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
+                                                 int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
+                                                 int lag) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
   using Row = typename RO::Row;
@@ -84,7 +85,14 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
   const Row rx = RO::coef(r, xb);
   const Row r0 = RO::zero();
-  const bool yint = y0 - (K - 1) >= 1 && y0 + RY + K - 2 <= ny - 2;
+  // block-uniform: all rows the band computes at any level are y-interior. Every wave of the block
+  // then runs the same march() copy, so all of them reach the per-plane barrier from one code path
+  // (bands at y = 0 / ny-1 take the per-row tested copy as a whole)
+  const bool yint = yb - (K - 1) >= 1 && yb + WB * RY + K - 2 <= ny - 2;
+  // output stores this wave issues per stored plane (wave-uniform; a store whose lanes are all
+  // masked may be skipped by the compiler, so a wave without owned lanes counts none)
+  const int nsto = (lag && __builtin_amdgcn_ballot_w64(own) != 0) ? max(0, min(RY, ny - y0)) : 0;
+  int nst = 0;  // stores issued since this wave's last DMA
 
   // u0 plane lz -> LDS by LDS DMA (global_load_lds, no VGPR destination): rows outside [0, ny) and
   // lanes outside the row read the nearest valid row / vector (finite values that only meet held
@@ -124,10 +132,10 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
     // newest u0 plane q; level k finishes plane q - k (its first planes are priming garbage that
     // no stored plane depends on)
     for (int q = zs - K; q <= qlast; ++q) {
-      // the DMA of plane q has landed: every wave waits for its own rows, then one barrier
-      // publishes them and also certifies that every wave has finished reading the other buffer
-      // (plane q-1), which the next DMA overwrites
-      wait_vm0();
+      // the DMA of plane q has landed: every wave waits for its own rows (the stores it issued
+      // after that DMA stay in flight), then one barrier publishes them and also certifies that
+      // every wave has finished reading the other buffer (plane q-1), which the next DMA overwrites
+      wait_vm_le(nst);
       const int buf = (int)((q - (zs - K)) & 1);
       lds_barrier();
       if (q < qlast) issue(q + 1, buf ^ 1);
@@ -181,6 +189,7 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
           for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
         } else if (q - K >= zs) {  // u_K(q - K) is an owned output plane
           const int lz = q - K;
+          nst = nsto;
 #pragma unroll
           for (int i = 0; i < RY; ++i) {
             if (y0 + i < ny && own) {
@@ -222,11 +231,11 @@ static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, 
   if constexpr (WB == 8 || RY == 3) {  // no residual instance (spills / one wave per SIMD): residual
     // sweeps use 2-row bands of 4 waves
     MDFX_CHECK(!resid, "heat7_wtk: no residual variant of this shape");
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
   } else if (resid) {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
   } else {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
   }
 }
 

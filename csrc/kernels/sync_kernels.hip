@@ -64,11 +64,12 @@ __global__ __launch_bounds__(64) void counter_signal_kernel(uint64_t* ctr) {
   __hip_atomic_store(ctr, v + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(64) void counter_wait_kernel(const uint64_t* remote, uint64_t* expect, uint64_t ticks,
-                                                          const int* abort_w, int* err_w) {
+__global__ __launch_bounds__(64) void counter_wait_kernel(const uint64_t* remote, uint64_t* expect, uint64_t ahead,
+                                                          uint64_t ticks, const int* abort_w, int* err_w) {
   if (threadIdx.x != 0) return;
-  const uint64_t want = __hip_atomic_load(expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  __hip_atomic_store(expect, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t next = __hip_atomic_load(expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __hip_atomic_store(expect, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t want = next + ahead;
   // once one wait has timed out the exchange is broken: later waits return at once, so the queued
   // steps drain in microseconds and the host reports the error (Transport::check)
   if (__hip_atomic_load(err_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
@@ -129,11 +130,29 @@ void hip_counter_signal(uint64_t* ctr, void* stream) {
   check_launch("counter_signal");
 }
 
-void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream) {
-  int* w = dev_words();
-  hipLaunchKernelGGL(counter_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, remote, expect,
+void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream, uint64_t ahead,
+                      const HipWords* own) {
+  int* w = own ? own->dev : dev_words();
+  hipLaunchKernelGGL(counter_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, remote, expect, ahead,
                      ticks_for(timeout_s), (const int*)w, w + 16);
   check_launch("counter_wait");
+}
+
+HipWords hip_words_alloc() {
+  HipWords h;
+  void* p = nullptr;
+  HIPC(hipHostMalloc(&p, 4096, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+  std::fill((int*)p, (int*)p + 1024, 0);
+  h.host = (int*)p;
+  void* d = nullptr;
+  HIPC(hipHostGetDevicePointer(&d, p, 0));
+  h.dev = (int*)d;
+  return h;
+}
+
+void hip_words_free(HipWords& h) {
+  if (h.host) (void)hipHostFree(h.host);
+  h.host = h.dev = nullptr;
 }
 
 void hip_poison_lds() {

@@ -258,6 +258,21 @@ PYBIND11_MODULE(_mdfx, m) {
 
   m.def("hip_device_count", &hip_device_count);
   m.def("hip_wait_error", &hip_wait_error, "1 after a device-side halo wait timed out");
+  m.def(
+      "ipc_peer_problem",
+      [](py::dict mine, py::dict peer, int expect_rank, bool peer_access) {
+        auto info = [](py::dict d) {
+          IpcPeerInfo i;
+          i.rank = d["rank"].cast<int>();
+          i.device = d["device"].cast<int>();
+          i.pid = d["pid"].cast<int>();
+          i.face_bytes = d["face_bytes"].cast<uint64_t>();
+          i.magic_ok = d.contains("magic_ok") ? d["magic_ok"].cast<bool>() : true;
+          return i;
+        };
+        return ipc_peer_problem(info(mine), info(peer), expect_rank, peer_access);
+      },
+      "host-side check of an ipc neighbour record: '' if usable, else the reason");
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("set_kernel_variant", [](const std::string& v) { hip_set_kernel_variant(v.c_str()); });
   m.def("reload_knobs", &hip_reload_knobs, "re-read the MDFX_* kernel tuning knobs from the environment");
@@ -423,6 +438,10 @@ PYBIND11_MODULE(_mdfx, m) {
       .def_property_readonly("residual", [](PySolver& p) { return p.chk().stats().last_residual; })
       .def_property_readonly("residual_step", [](PySolver& p) { return p.chk().stats().residual_step; })
       .def_property_readonly("graph_replays", [](PySolver& p) { return p.chk().stats().graph_replays; })
+      .def_property_readonly("graph_captures", [](PySolver& p) { return p.chk().stats().graph_captures; })
+      .def("prepare_graphs", [](PySolver& p) { return p.chk().prepare_graphs(); },
+           "capture both parities' 2-sweep hipGraph cycles now (0 if graphs are off / not capturable)")
+      .def_property_readonly("graph_eligible", [](PySolver& p) { return p.chk().graph_eligible(); })
       .def_property_readonly("current_index", [](PySolver& p) { return p.chk().current_index(); })
       .def_property_readonly("transport_name", [](PySolver& p) { return std::string(p.chk().transport().name()); })
       .def("local_rank", [](PySolver& p, int i) { return p.chk().local_rank(i); })

@@ -202,6 +202,23 @@ class Simulation:
         options not named keep their values."""
         self._s.set_options(**kw)
 
+    def prepare_graphs(self) -> int:
+        """Capture the hipGraph cycles of both buffer parities now (graph=True and capturable), so
+        that later run() calls only replay them: benchmarks call this before their warmup so no
+        capture or instantiation lands in a timed region. init() keeps the captured cycles. Returns
+        the number of cycles held (0: graphs off or not capturable in this configuration)."""
+        return int(self._s.prepare_graphs())
+
+    @property
+    def graph_captures(self) -> int:
+        """hipGraph cycles captured and instantiated so far (prepare_graphs() or on demand in run())."""
+        return int(self._s.graph_captures)
+
+    @property
+    def graph_eligible(self) -> bool:
+        """Whether run() replays captured cycles in the current configuration."""
+        return bool(self._s.graph_eligible)
+
     @property
     def graph_replays(self) -> int:
         """2-sweep cycles replayed from a captured hipGraph so far (0: every step ran eagerly, e.g.

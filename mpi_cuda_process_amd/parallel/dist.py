@@ -73,6 +73,11 @@ class ControlPlane:
     over a CPU (gloo) process group."""
 
     def __init__(self, group=None, timeout_s: float = 300.0):
+        # the control plane moves CPU tensors: on a non-gloo group (e.g. a torchrun default NCCL
+        # group) it makes its own gloo group over the same ranks instead of failing on CPU tensors
+        if dist.get_backend(group) != "gloo":
+            group = dist.new_group(backend="gloo") if group is None else \
+                dist.new_group(ranks=dist.get_process_group_ranks(group), backend="gloo")
         self.group = group
         self.timeout_s = timeout_s
 

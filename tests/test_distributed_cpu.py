@@ -134,6 +134,19 @@ def test_bench_self_launches_ranks_cpu(mdfx):
     assert gate["passed"] and run["transport"] == "torch" and run["grid"][2] % 3 == 0
 
 
+def test_bench_json_reports_effective_graph_mode(mdfx):
+    """--graph on where nothing can replay (CPU): the JSON's graph flag is false, the request is
+    reported separately, and no capture or replay is counted in the timed region."""
+    import json
+
+    rc, out, err = _bench(["--device", "cpu", "--graph", "on", "--n", "24", "--steps", "4", "--warmup", "1"])
+    assert rc == 0, err
+    rec = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    cfg = rec["config"]
+    assert cfg["graph"] is False and cfg["graph_requested"] is True
+    assert cfg["graph_replays_timed"] == 0 and cfg["graph_captures_timed"] == 0
+
+
 def test_bench_refuses_more_gpus_than_visible(mdfx):
     """No GPU here: asking for 2 HIP ranks fails fast instead of running on fewer devices."""
     rc, out, err = _bench(["--device", "hip", "--gpus", "2", "--n", "32", "--steps", "1"], timeout=120)
@@ -157,6 +170,14 @@ import torch.distributed as dist
 from mpi_cuda_process_amd.parallel.dist import init_distributed, ControlPlane
 env = init_distributed("gloo")
 cp = ControlPlane()
+# a control plane handed a non-gloo group (torchrun's default NCCL group) builds its own gloo group
+_real = dist.get_backend
+dist.get_backend = lambda g=None: "nccl" if g is None else _real(g)
+cp2 = ControlPlane()
+dist.get_backend = _real
+own_gloo = cp2.group is not None and _real(cp2.group) == "gloo"
+cb2 = cp2.callbacks()
+s2 = cb2["allreduce_sum"](1.0)
 cb = cp.callbacks()
 # an IpcRecord-shaped byte string: magic, ints, embedded NULs, two 64-byte handles
 rec = b"MDFXIPC2" + struct.pack("<iiiiQ", env.rank, 0, 1000 + env.rank, 0, 8 << 20) + bytes(64) + bytes([env.rank]) * 64
@@ -165,7 +186,8 @@ ok = [len(x) == len(rec) and struct.unpack("<i", x[8:12])[0] == r and x[-1] == r
 s = cb["allreduce_sum"](float(env.rank + 1))
 mx = cb["allreduce_max"](float(env.rank))
 cb["barrier"]()
-json.dump({"ok": all(ok) and len(allr) == env.world, "sum": s, "max": mx}, open(%(out)r + str(env.rank), "w"))
+json.dump({"ok": all(ok) and len(allr) == env.world and own_gloo and s2 == env.world, "sum": s, "max": mx},
+          open(%(out)r + str(env.rank), "w"))
 dist.destroy_process_group()
 """
 
@@ -190,6 +212,24 @@ def test_ipc_control_plane_marshalling_cpu(mdfx, tmp_path):
     for r in range(3):
         rec = json.load(open(out + str(r)))
         assert rec == {"ok": True, "sum": 6.0, "max": 2.0}
+
+
+def test_ipc_peer_record_checks_cpu(mdfx):
+    """The ipc transport's host-side checks of a neighbour's record, including the cross-device
+    case (no GPU needed): same pid refused, face size mismatch refused, another device accepted only
+    with peer access."""
+    nat = mdfx.native()
+    me = dict(rank=0, device=0, pid=100, face_bytes=4 << 20)
+    ok = dict(rank=1, device=0, pid=101, face_bytes=4 << 20)
+    assert nat.ipc_peer_problem(me, ok, 1, False) == ""
+    assert "different processes" in nat.ipc_peer_problem(me, dict(ok, pid=100), 1, True)
+    assert "face size" in nat.ipc_peer_problem(me, dict(ok, face_bytes=1 << 20), 1, True)
+    assert "mismatch" in nat.ipc_peer_problem(me, dict(ok, rank=2), 1, True)
+    assert "mismatch" in nat.ipc_peer_problem(me, dict(ok, magic_ok=False), 1, True)
+    other = dict(ok, device=3)
+    assert nat.ipc_peer_problem(me, other, 1, True) == ""
+    why = nat.ipc_peer_problem(me, other, 1, False)
+    assert "cannot access device 3" in why and "rccl" in why
 
 
 def test_ipc_transport_needs_hip(mdfx):

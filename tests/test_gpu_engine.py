@@ -61,6 +61,35 @@ def test_graph_replay_equals_eager(hip, prob):
     assert np.array_equal(a, e)
 
 
+@pytest.mark.parametrize("prob", [PROBS[0], m.heat3d(nx=256, ny=20, nz=40)], ids=_ids)
+def test_prepared_graphs_replay_without_capture(hip, prob):
+    """prepare_graphs() captures both parities up front; later runs (any warmup parity, across
+    init()) only replay, and the result equals eager stepping bitwise."""
+    t = 3 if prob.nx >= 256 else 1
+    eager = {}
+    for steps in (5, 20):
+        with m.Simulation(prob, device="hip", temporal=t) as sim:
+            sim.init()
+            sim.run(steps)
+            eager[steps] = sim.gather()
+    with m.Simulation(prob, device="hip", graph=True, temporal=t) as sim:
+        sim.init()
+        assert sim.prepare_graphs() == 2
+        caps = sim.graph_captures
+        sim.run(5)  # the driver's warmup: leaves the buffer parity odd
+        r0 = sim.graph_replays
+        sim.run(20)
+        assert sim.graph_captures == caps, "a capture happened inside the timed run"
+        assert sim.graph_replays - r0 == 20 // (2 * t)
+        sim.init()  # keeps the captured cycles
+        sim.run(20)
+        assert sim.graph_captures == caps
+        assert np.array_equal(sim.gather(), eager[20])
+        sim.init()
+        sim.run(5)
+        assert np.array_equal(sim.gather(), eager[5])
+
+
 def test_graph_with_residual_interleave(hip):
     prob = m.heat3d(nx=64, ny=16, nz=18)
     with m.Simulation(prob, device="hip", graph=True, residual_every=4) as sim:

@@ -105,3 +105,71 @@ def test_bench_staged_two_processes(hip):
                   env_extra={"HIP_VISIBLE_DEVICES": "0"})
     lines = [l for l in outs[0].splitlines() if l.startswith("{")]
     assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
+
+
+INITHANG = r"""
+import os, sys, time
+sys.path.insert(0, %(root)r)
+import torch
+import mpi_cuda_process_amd as m
+from mpi_cuda_process_amd.parallel.dist import init_distributed
+env = init_distributed("gloo", timeout_s=120)
+torch.cuda.set_device(0)
+t0 = time.time()
+try:
+    m.Simulation(m.heat3d(n=64), device="hip", distributed=True, transport="rccl", timeout_s=%(t)f, devices=[0])
+except Exception as e:  # the bounded bootstrap gave up: report and exit non-zero
+    print("BOOTSTRAP-FAILED after %%.1f s: %%s" %% (time.time() - t0, e), flush=True)
+    os._exit(3)
+print("BOOTSTRAP-OK", flush=True)
+os._exit(0)
+"""
+
+
+def test_rccl_bootstrap_is_bounded(hip):
+    """A rank that never joins the RCCL communicator (MDFX_FAULT=inithang@1: rank 1 stops right
+    before ncclCommInitRankConfig) makes rank 0 abort its half-built communicator and exit non-zero
+    within the watchdog bound instead of blocking in ncclCommInitRank forever."""
+    import time
+
+    t = 8.0
+    port = _port()
+    procs = []
+    code = INITHANG % dict(root=ROOT, t=t)
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), MDFX_FAULT="inithang@1")
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, cwd=ROOT))
+    try:
+        t0 = time.time()
+        o, _ = procs[0].communicate(timeout=t + 60)
+        took = time.time() - t0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            p.wait()
+    out = o.decode()
+    assert procs[0].returncode == 3, out
+    assert "BOOTSTRAP-FAILED" in out and "never joined" in out, out
+    assert took < t + 45, "rank 0 took %.1f s to give up" % took
+
+
+@pytest.mark.timeout(360)
+def test_bench_rccl_bootstrap_hang_exits_nonzero(hip):
+    """bench.py --gpus 2 --transport auto with a rank that never joins RCCL: the gate marks rccl
+    failed, and the run ends non-zero (no usable transport with a hung peer) instead of hanging."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["MDFX_FAULT"] = "inithang@1"
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--n", "128",
+                        "--steps", "4", "--warmup", "2", "--timeout", "8"], env=env, capture_output=True, timeout=400,
+                       cwd=ROOT)
+    took = time.time() - t0
+    assert p.returncode != 0, p.stdout.decode()
+    assert not [l for l in p.stdout.decode().splitlines() if l.startswith("{")]
+    assert took < 300, took
