@@ -58,6 +58,9 @@ $(OBJ)/%.o: csrc/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX_HOST) $(HOSTFLAGS) -c $< -o $@
 
+# heat7_wtk's natural-layout rows need the scalar x adds left unpacked (RowOpsN, rowops.hpp)
+$(OBJ)/kernels/stencil_heat_wtk.o $(ASAN_DIR)/kernels/stencil_heat_wtk.o $(DCK_DIR)/kernels/stencil_heat_wtk.o: HIPFLAGS += -fno-slp-vectorize
+
 # the AVX2 + FMA copy of the CPU stencils (selected at run time by cpu_kernels.cpp)
 $(OBJ)/cpu/cpu_kernels_avx2.o $(ASAN_DIR)/cpu/cpu_kernels_avx2.o $(DCK_DIR)/cpu/cpu_kernels_avx2.o: HOSTFLAGS += -mavx2 -mfma
 $(OBJ)/cpu/cpu_kernels.o $(OBJ)/cpu/cpu_kernels_avx2.o: csrc/cpu/cpu_stencils.inc

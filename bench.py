@@ -89,6 +89,12 @@ def parse(argv=None):
     p.add_argument("--gate-n", type=int, default=0, help="edge of the correctness-gate grid (0 = auto)")
     p.add_argument("--no-gate", action="store_true", help="skip the N > 1 correctness gate")
     p.add_argument("--verbose", action="store_true", help="per-rank phase trace on stderr")
+    p.add_argument("--rank-proxy", type=int, default=0, metavar="N",
+                   help="per-GPU proxy of an N-GPU run on ONE GPU: only rank --proxy-rank's slab of the N-way "
+                        "split, its halo exchange looped back through the ipc mailbox copies and counters; "
+                        "reports per-GPU GCells/s (a proxy, never the headline)")
+    p.add_argument("--proxy-rank", type=int, default=-1,
+                   help="which slab the proxy runs (default: a middle rank, two neighbours)")
     p.add_argument("--share-gpu", action="store_true",
                    help="allow more ranks than GPUs (processes share devices; tests of the ipc/staged paths)")
     return p.parse_args(argv)
@@ -244,11 +250,105 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False):
     return bad == 0, rec
 
 
+def run_proxy(a):
+    """--rank-proxy N: time exactly one rank's per-step work of an N-GPU strong-scaling run on one
+    GPU (its slab plus K ghost planes per side, both boundary regions on the halo stream, the
+    interior on the compute stream, the ipc exchange sequence looped back onto itself). Prints one
+    JSON line labelled as a proxy: per-GPU GCells/s of that slab and the implied N-GPU figure."""
+    from mpi_cuda_process_amd import Simulation, native
+
+    if not torch.cuda.is_available():
+        print("bench: --rank-proxy needs a HIP device", file=sys.stderr)
+        return 2
+    n = a.rank_proxy
+    r = a.proxy_rank if a.proxy_rank >= 0 else (n // 2 if n > 1 else 0)
+    torch.cuda.set_device(0)
+    native().set_kernel_variant(a.variant)
+    nx, ny, nz = a.nx or a.n, a.ny or a.n, a.nz or a.n
+    if a.stencil in ("jacobi5", "life"):
+        ny = 1
+    prob = make_problem(a, nx, ny, nz)
+    temporal = pick_temporal(a, prob, max(1, n), True)
+    graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True])
+    overlaps = [True, False] if (n > 1 and not a.no_overlap) else [not a.no_overlap]
+    rounds = [int(a.rounds)] if a.rounds != "auto" else ([2, 1] if n > 1 else [0])
+    sim = Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graphs[0],
+                     residual_every=a.residual_every, timeout_s=a.timeout)
+    lay = sim.layout(0)
+    slab_cells = (lay["z1"] - lay["z0"]) * prob.nx * prob.ny
+
+    def timed(steps):
+        sim.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sim.run(steps)
+        sim.synchronize()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    trials = []
+    cands = [(g, rr, ov) for g in graphs for rr in rounds for ov in overlaps]
+    chosen = cands[0]
+    if len(cands) > 1:
+        n_trial = max(2, min(a.trial_steps, a.steps))
+        for g, rr, ov in cands:
+            sim.set_options(graph=g, min_rounds=rr, overlap=ov)
+            sim.init()
+            sim.prepare_graphs()
+            sim.run(max(2, min(a.warmup, 4)))
+            dt = timed(n_trial)
+            trials.append({"graph": g, "min_rounds": rr, "overlap": ov, "ms_per_step": round(dt / n_trial * 1e3, 4)})
+        chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
+    sim.set_options(graph=chosen[0], min_rounds=chosen[1], overlap=chosen[2])
+    sim.init()
+    sim.prepare_graphs()
+    sim.run(a.warmup)
+    timed(0)
+    replays0, captures0 = sim.graph_replays, sim.graph_captures
+    best = None
+    for _ in range(max(1, a.repeats)):
+        dt = timed(a.steps)
+        best = dt if best is None else min(best, dt)
+    per_gpu = slab_cells * a.steps / best / 1e9
+    model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF", "life": "2D Game of Life"}[a.stencil]
+    dram_tbps = per_gpu * prob.bytes_per_cell_per_step / temporal / 1e3
+    rec = {
+        "metric": "PROXY per-GPU GCells/s, rank %d of a %d-GPU slab split, %s %dx%dx%d %s (one GPU; not a "
+                  "whole-node measurement)" % (r, n, model, nx, ny, nz, a.dtype),
+        "value": round(per_gpu, 3),
+        "unit": "GCells/s per GPU",
+        "proxy": True,
+        "n_gpus": 1,
+        "proxied_n_gpus": n,
+        "proxy_rank": r,
+        "implied_node_gcells": round(per_gpu * n, 3),
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(best / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "dtype": {"f32": "fp32", "f64": "fp64", "u8": "u8"}[a.dtype],
+        "data": "synthetic (uniform random grid from a counter hash of the global index, seed 1)",
+        "config": {"model": "%s %dx%dx%d %s" % (model, nx, ny, nz, a.dtype), "slab_planes": [lay["z0"], lay["z1"]],
+                   "ghost_planes": lay["halo"], "temporal_block": temporal, "transport": sim.transport,
+                   "graph": (sim.graph_replays - replays0) > 0, "graph_requested": chosen[0],
+                   "graph_replays_timed": sim.graph_replays - replays0,
+                   "graph_captures_timed": sim.graph_captures - captures0,
+                   "min_rounds": chosen[1], "overlap": chosen[2], "trials": trials},
+        "achieved_dram_TBps": round(dram_tbps, 3),
+        "pct_of_hbm_copy_roof": round(100.0 * dram_tbps / HBM_MEASURED_TBPS, 1),
+    }
+    print(json.dumps(rec), flush=True)
+    sim.close()
+    return 0
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
     global _VERBOSE
     _VERBOSE = a.verbose
+    if a.rank_proxy > 0:
+        return run_proxy(a)
     if a.gpus > 1 and not launched() and not os.environ.get("MDFX_FORCE_DIST"):
         return self_launch(a, argv)
 

@@ -1,0 +1,128 @@
+// Rank-proxy halo transport: ONE slab of an N-way slab decomposition, alone on one GPU, exchanging
+// with itself through the ipc transport's machinery.
+//
+// Purpose: measure on a single MI355X what each GPU of an N-GPU run does per step, which the
+// one-GPU pool cannot otherwise show (the whole-node bench is the driver's). The slab is exactly
+// rank r's (its owned planes of the global grid plus K ghost planes per side), the engine runs its
+// real schedule (both boundary regions on the halo stream, the interior on the compute stream,
+// event joins, graph replay), and every exchange moves the same bytes through the same stream work
+// as an ipc exchange between processes: per face a publish copy into a mailbox slot, a "ready"
+// counter signal, a device counter wait, a pull copy from the mailbox into the ghost planes and a
+// "pulled" signal (ipc_transport.cpp). The only difference is where the pulled face comes from:
+// the slab's own mailbox (its own face, copied into its own ghost) instead of the neighbour's, so
+// the copies run at local HBM speed instead of over xGMI, and the ghost values are not the
+// neighbour's. Results are therefore exact only at planes farther from a proxied boundary than the
+// steps run (tests/test_gpu_proxy.py), and every number measured this way is labelled a proxy.
+//
+// Reference parity: the per-rank generation loop of MDF_kernel.cu:155-188 (C12/C13) with its
+// halo exchange MDF_kernel.cu:166-172,180-183, measured for one rank at a time.
+#include <hip/hip_runtime_api.h>
+
+#include "mdfx/devsync.hpp"
+#include "mdfx/runtime.hpp"
+
+namespace mdfx {
+
+#define HIPC(x)                                                                          \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) ::mdfx::throw_error(__FILE__, __LINE__, std::string("HIP: ") + #x + " -> " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+// counter block layout as the ipc transport's (64-bit words on separate 128-B lines)
+constexpr int kReady = 0, kPulled = 16, kExpReady = 48, kExpPulled = 64;
+constexpr size_t kCounterBytes = 128 * 8;
+
+class ProxyTransport final : public Transport {
+ public:
+  ~ProxyTransport() override {
+    if (!ok_) return;
+    (void)hipSetDevice(self_.be->device());
+    if (mbox_) (void)hipFree(mbox_);
+    hip_free_uncached(ctr_);
+    hip_words_free(words_);
+  }
+  const char* name() const override { return "proxy"; }
+  bool graph_capturable() const override { return true; }
+  void set_timeout(double s) override { timeout_s_ = s > 0 ? s : 300.0; }
+
+  void setup(const std::vector<LocalSlab>& locals, int nranks) override {
+    MDFX_CHECK(locals.size() == 1, "proxy transport: exactly one slab (rank r of an N-way split) per process");
+    self_ = locals[0];
+    nranks_ = nranks;
+    MDFX_CHECK(self_.be->kind() == DeviceKind::HIP, "proxy transport needs a HIP backend");
+    self_.be->activate();
+    ctr_ = (uint64_t*)hip_alloc_uncached(kCounterBytes);
+    words_ = hip_words_alloc();
+    const uint64_t two = 2;
+    HIPC(hipMemcpy(ctr_ + kPulled + 0, &two, 8, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(ctr_ + kPulled + 1, &two, 8, hipMemcpyHostToDevice));
+    face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
+    HIPC(hipMalloc(&mbox_, 4 * face_));
+    HIPC(hipMemset(mbox_, 0, 4 * face_));
+    HIPC(hipDeviceSynchronize());
+    ok_ = true;
+  }
+
+  char* slot(int b, int s) const { return (char*)mbox_ + (size_t)(2 * b + s) * face_; }
+
+  void exchange(int b) override {
+    self_.be->activate();
+    hipStream_t hs = (hipStream_t)self_.halo_stream;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPC(hipStreamIsCapturing(hs, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    const uint64_t ahead = (!capturing && last_b_ == b) ? 1 : 0;
+    // publish (the ipc sequence, with this slab as its own neighbour on both sides)
+    for (int side = 0; side < 2; ++side) {
+      const HaloSpan h = halo_span(self_, b, side, nranks_);
+      if (h.peer < 0) continue;
+      MDFX_CHECK(h.bytes == face_, "proxy: face geometry mismatch");
+      hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, ahead, &words_);
+      HIPC(hipMemcpyAsync(slot(b, side), h.send, face_, hipMemcpyDeviceToDevice, hs));
+    }
+    hip_counter_signal(ctr_ + kReady, hs);
+    // pull
+    for (int side = 0; side < 2; ++side) {
+      const HaloSpan h = halo_span(self_, b, side, nranks_);
+      if (h.peer < 0) continue;
+      hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
+      HIPC(hipMemcpyAsync(h.recv, slot(b, side), face_, hipMemcpyDeviceToDevice, hs));
+      hip_counter_signal(ctr_ + kPulled + side, hs);
+    }
+    if (!capturing) last_b_ = b;
+  }
+  int last_parity() const override { return last_b_; }
+  void set_last_parity(int b) override { last_b_ = b; }
+
+  double allreduce_sum(double v) override { return v; }
+  double allreduce_max(double v) override { return v; }
+  void barrier() override {}
+  void check() override {
+    if (!words_.host) return;
+    if (words_.wait_error()) MDFX_FAIL(format("proxy transport: a halo counter wait timed out after %.0f s", timeout_s_));
+    if (words_.abort_raised()) MDFX_FAIL("proxy transport was aborted");
+  }
+  void abort() override {
+    if (words_.host) words_.set_abort(1);
+  }
+
+ private:
+  LocalSlab self_;
+  int nranks_ = 1;
+  uint64_t* ctr_ = nullptr;
+  HipWords words_;
+  void* mbox_ = nullptr;
+  size_t face_ = 0;
+  bool ok_ = false;
+  int last_b_ = -1;
+  double timeout_s_ = 300.0;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_proxy_transport() { return std::unique_ptr<Transport>(new ProxyTransport()); }
+
+}  // namespace mdfx

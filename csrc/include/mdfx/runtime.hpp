@@ -119,6 +119,11 @@ std::unique_ptr<Transport> make_callback_transport(CallbackFns fns);
 // neighbours' mapped buffers by the copy engines, ordered by device-side counters
 // (csrc/comm/ipc_transport.cpp). Needs fns.allgather; residual / barrier go through fns too.
 std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns);
+// Rank proxy (HIP): ONE slab of an N-way decomposition alone on a GPU, exchanging with itself
+// through the ipc transport's mailbox copies and device counters (csrc/comm/proxy_transport.cpp):
+// the per-GPU schedule of an N-GPU run, measurable on one GPU. Ghost values are the slab's own
+// faces, so results are exact only away from the proxied boundaries.
+std::unique_ptr<Transport> make_proxy_transport();
 // What the ipc transport knows about one process's slab when it maps a neighbour (the host-side
 // part of its handle record).
 struct IpcPeerInfo {

@@ -27,7 +27,8 @@ void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipSt
 template <class T>
 void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s);
 template <class T>
-void launch_jacobi5_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
+void launch_jacobi5_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s,
+                        bool ref_precision);
 template <class T>
 void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid, hipStream_t s);
 template <class T>
@@ -75,6 +76,7 @@ static Knobs read_knobs() {
   k.b27_tbk = env_int("MDFX_B27_TBK", 0);
   k.life_bits = env_int("MDFX_LIFE_BITS", 1);
   k.vm_lag = env_int("MDFX_VM_LAG", 1);
+  k.wtk_nat = env_int("MDFX_WTK_NAT", 2);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
@@ -231,7 +233,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   if (steps < 2 || lay.halo < steps) return false;
   const bool k2d = steps == 2 || steps == 3 || steps == 4 || steps == 6 || steps == 8;
   if (spec.kind == StencilKind::Jacobi5)  // deep temporal blocking of the 2D problems
-    return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d && !spec.coef.ref_precision;
+    return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d;  // ref precision too (jacobi5_tbk REF)
   if (spec.kind == StencilKind::Life) return k2d || steps == 12 || steps == 16;  // 12 / 16: life_bits
   if (spec.kind == StencilKind::Heat7 && steps > 2) {  // deep temporal blocking (rows within one block)
     if (dev::use_wtk(steps)) return true;
@@ -287,11 +289,13 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       else
         dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
     } else if (spec.kind == StencilKind::Jacobi5) {
-      if (a.steps > 2 || dev::knobs().j5_tbk) {
+      if (a.steps > 2 || dev::knobs().j5_tbk || spec.coef.ref_precision) {
         if (spec.dtype == DType::F32)
-          dev::launch_jacobi5_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
+          dev::launch_jacobi5_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s,
+                                         spec.coef.ref_precision);
         else
-          dev::launch_jacobi5_tbk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
+          dev::launch_jacobi5_tbk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s,
+                                          spec.coef.ref_precision);
       } else if (spec.dtype == DType::F32) {
         dev::launch_jacobi5_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
       } else {

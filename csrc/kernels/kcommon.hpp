@@ -201,6 +201,7 @@ struct Knobs {
   int tb_ry = 0;       // MDFX_TB_RY: rows per tile of heat7_tb2 (x-tiled rows) / box27_tb2 (0: 2)
   int tbk_ry = 0;      // MDFX_TBK_RY: rows per tile of heat7_tbk (0: 4 at K = 2, 2 deeper)
   int wtk_ry8 = 0;     // MDFX_WTK_RY8: fp64 rows per wave in 8-wave bands (2 / 3; 0: 3 up to 1024-cell rows, else 2)
+  int wtk_nat = 2;     // MDFX_WTK_NAT: heat7_wtk fp32 rows: 2 natural pair layout + 2-plane unroll, 1 natural, 0 round 2's
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)
   int j5_tbk = 0;      // MDFX_J5_TBK: 2D MDF two-step sweeps through the K-step kernel

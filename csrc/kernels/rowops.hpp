@@ -50,6 +50,7 @@ struct RowOps<float> {
     return r;
   }
   static __device__ __forceinline__ void fence(Row& r) { asm volatile("" : "+v"(r.a), "+v"(r.b)); }
+  static __device__ __forceinline__ void pin(Row&) {}
   static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}, T2{0.f, 0.f}}; }
   static __device__ __forceinline__ float first(const Row& c) { return c.b.x; }
   static __device__ __forceinline__ float last(const Row& c) { return c.b.y; }
@@ -80,6 +81,18 @@ struct RowOps<float> {
     Row o;
     o.a = __builtin_elementwise_fma(rc.a, __builtin_elementwise_fma(m4, c.a, S.a + zp.a), c.a);
     o.b = __builtin_elementwise_fma(rc.b, __builtin_elementwise_fma(m4, c.b, S.b + zp.b), c.b);
+    return o;
+  }
+  // sm::jacobi5_ref: t = fma(-4, c, S + zp) in fp32, then (float)fma((double)r, (double)t, (double)c)
+  static __device__ __forceinline__ Row fin4_ref(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m4 = T2{-4.f, -4.f};
+    const T2 ta = __builtin_elementwise_fma(m4, c.a, S.a + zp.a);
+    const T2 tb = __builtin_elementwise_fma(m4, c.b, S.b + zp.b);
+    Row o;
+    o.a.x = (float)__builtin_fma((double)rc.a.x, (double)ta.x, (double)c.a.x);
+    o.a.y = (float)__builtin_fma((double)rc.a.y, (double)ta.y, (double)c.a.y);
+    o.b.x = (float)__builtin_fma((double)rc.b.x, (double)tb.x, (double)c.b.x);
+    o.b.y = (float)__builtin_fma((double)rc.b.y, (double)tb.y, (double)c.b.y);
     return o;
   }
   static __device__ __forceinline__ Row coef(float r, const bool* held) {
@@ -135,6 +148,7 @@ struct RowOps<double> {
   static __device__ __forceinline__ Row lds(const double* p) { return Row{*(const T2*)p}; }
   static __device__ __forceinline__ Row lds_pairs(const double* p) { return lds(p); }
   static __device__ __forceinline__ void fence(Row&) {}
+  static __device__ __forceinline__ void pin(Row&) {}
   static __device__ __forceinline__ Row zero() { return Row{T2{0.0, 0.0}}; }
   static __device__ __forceinline__ double first(const Row& c) { return c.v.x; }
   static __device__ __forceinline__ double last(const Row& c) { return c.v.y; }
@@ -153,6 +167,9 @@ struct RowOps<double> {
   static __device__ __forceinline__ Row fin4(const Row& S, const Row& zp, const Row& c, const Row& rc) {
     const T2 m4 = T2{-4.0, -4.0};
     return Row{__builtin_elementwise_fma(rc.v, __builtin_elementwise_fma(m4, c.v, S.v + zp.v), c.v)};
+  }
+  static __device__ __forceinline__ Row fin4_ref(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    return fin4(S, zp, c, rc);  // fp64 fields: the reference's widening is the identity
   }
   static __device__ __forceinline__ Row coef(double r, const bool* held) {
     return Row{T2{held[0] ? 0.0 : r, held[1] ? 0.0 : r}};
@@ -176,6 +193,61 @@ struct RowOps<double> {
   static __device__ __forceinline__ Row sel(const bool* held, const Row& h, const Row& o) {
     return Row{T2{held[0] ? h.v.x : o.v.x, held[1] ? h.v.y : o.v.y}};
   }
+};
+
+// fp32 rows in the NATURAL pair layout p = (e0, e1), q = (e2, e3): a 16-B LDS or global vector is
+// already two aligned register pairs, so nothing is regrouped after a ds_read_b128. The x sums are
+// four scalar adds, two of them with the neighbour lane's cell as a DPP operand
+// (v_add_f32_dpp wave_shr / wave_shl: the lane shift costs no instruction of its own), and every
+// y / z / update operation is one packed op per pair. Issue slots per row update: 4 scalar x adds
+// + 12 packed ops, against 2 DPP moves + 14 packed ops + about 5 regrouping moves in RowOps<float>.
+// Needs -fno-slp-vectorize on the translation unit, or the two plain x adds get packed into one
+// v_pk_add_f32 whose halves then have to be moved apart (Makefile / CMakeLists.txt).
+struct RowOpsN {
+  typedef float T2 __attribute__((ext_vector_type(2)));
+  typedef float V __attribute__((ext_vector_type(4)));
+  struct Row {
+    T2 p, q;
+  };
+  static __device__ __forceinline__ Row lds(const float* a) {
+    const V v = *(const V*)a;
+    return Row{T2{v.x, v.y}, T2{v.z, v.w}};
+  }
+  static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}, T2{0.f, 0.f}}; }
+  static __device__ __forceinline__ float first(const Row& c) { return c.p.x; }
+  static __device__ __forceinline__ float last(const Row& c) { return c.q.y; }
+  // (((xm + xp) + ym) + yp) + zm; l / rr are the cells beyond the slice's ends (lane shifts the
+  // compiler folds into the adds as DPP operands)
+  static __device__ __forceinline__ Row partial(const Row& c, float l, float rr, const Row& ym, const Row& yp,
+                                                const Row& zm) {
+    Row s;
+    s.p.x = l + c.p.y;    // e0: xm + xp
+    s.p.y = c.p.x + c.q.x;  // e1
+    s.q.x = c.p.y + c.q.y;  // e2
+    s.q.y = rr + c.q.x;   // e3
+    s.p = ((s.p + ym.p) + yp.p) + zm.p;
+    s.q = ((s.q + ym.q) + yp.q) + zm.q;
+    return s;
+  }
+  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m6 = T2{-6.f, -6.f};
+    Row o;
+    o.p = __builtin_elementwise_fma(rc.p, __builtin_elementwise_fma(m6, c.p, S.p + zp.p), c.p);
+    o.q = __builtin_elementwise_fma(rc.q, __builtin_elementwise_fma(m6, c.q, S.q + zp.q), c.q);
+    return o;
+  }
+  static __device__ __forceinline__ Row coef(float r, const bool* held) {
+    return Row{T2{held[0] ? 0.f : r, held[1] ? 0.f : r}, T2{held[2] ? 0.f : r, held[3] ? 0.f : r}};
+  }
+  static __device__ __forceinline__ Row scale(const Row& x, float s) { return Row{x.p * T2{s, s}, x.q * T2{s, s}}; }
+  static __device__ __forceinline__ float get(const Row& c, int e) {
+    return e == 0 ? c.p.x : e == 1 ? c.p.y : e == 2 ? c.q.x : c.q.y;
+  }
+  static __device__ __forceinline__ V vec(const Row& c) { return V{c.p.x, c.p.y, c.q.x, c.q.y}; }
+  // materialise a loop-carried row where it is computed: otherwise hipcc carries the INPUTS of the
+  // partial sum across the back edge and forms it in the next iteration, where the lane-shift
+  // moves can no longer fold into the adds as DPP operands (DPP combining works inside a block)
+  static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.p), "+v"(r.q)); }
 };
 
 }  // namespace dev

@@ -489,7 +489,10 @@ template void launch_jacobi5_tb2<double>(const Geo&, const double*, double*, dou
 // bitwise equal to K single steps -- and replaces S / C with row p+1's. No register rotation, and
 // held cells take a zero coefficient (fma(0, t, u) = u for finite t; every lane, inside the grid or
 // not, holds finite data) instead of a select. One read and one write of the field per K steps.
-template <class T, int K, bool RES>
+// REF: the reference program's own evaluation of every level (sm::jacobi5_ref, MDF_kernel.cu:20,
+// SURVEY D17): the fp32 sum and -4u term as usual, then r * t + u as ONE fp64 fma of the widened
+// values, rounded back to fp32. Held cells stay exact (fma(0, t, u) = u). fp64 fields: identical.
+template <class T, int K, bool RES, bool REF>
 __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                    int zc, int XT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
       const int64_t gz = row + g.gz_off;
       const Row rc = (ZT && (gz <= 0 || gz >= g.gnz - 1)) ? r0 : rx;
       const Row c = C[l - 1];
-      const Row o = RO::fin4(S[l - 1], X, c, rc);
+      const Row o = REF ? RO::fin4_ref(S[l - 1], X, c, rc) : RO::fin4(S[l - 1], X, c, rc);
       // row + 1's partial from the arriving row X: (xm + xp) + zm
       const T lft = lane_up1(RO::last(X));
       const T rgt = lane_down1(RO::first(X));
@@ -581,7 +584,7 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   if (RES) wave_atomic_add(resid, acc);
 }
 
-template <class T, int K>
+template <class T, int K, bool REF>
 static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   const int64_t planes = g.lz_end - g.lz_begin;
   if (planes <= 0) return;
@@ -593,24 +596,34 @@ static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double*
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
   if (resid)
-    hipLaunchKernelGGL((jacobi5_tbk<T, K, true>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+    hipLaunchKernelGGL((jacobi5_tbk<T, K, true, REF>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
   else
-    hipLaunchKernelGGL((jacobi5_tbk<T, K, false>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+    hipLaunchKernelGGL((jacobi5_tbk<T, K, false, REF>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
 }
 
-template <class T>
-void launch_jacobi5_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
+template <class T, bool REF>
+static void launch_jacobi5_tbk_r(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   switch (steps) {
-    case 2: launch_jacobi5_tbk_k<T, 2>(g, in, out, r, resid, s); break;
-    case 3: launch_jacobi5_tbk_k<T, 3>(g, in, out, r, resid, s); break;
-    case 4: launch_jacobi5_tbk_k<T, 4>(g, in, out, r, resid, s); break;
-    case 6: launch_jacobi5_tbk_k<T, 6>(g, in, out, r, resid, s); break;
-    case 8: launch_jacobi5_tbk_k<T, 8>(g, in, out, r, resid, s); break;
+    case 2: launch_jacobi5_tbk_k<T, 2, REF>(g, in, out, r, resid, s); break;
+    case 3: launch_jacobi5_tbk_k<T, 3, REF>(g, in, out, r, resid, s); break;
+    case 4: launch_jacobi5_tbk_k<T, 4, REF>(g, in, out, r, resid, s); break;
+    case 6: launch_jacobi5_tbk_k<T, 6, REF>(g, in, out, r, resid, s); break;
+    case 8: launch_jacobi5_tbk_k<T, 8, REF>(g, in, out, r, resid, s); break;
     default: break;
   }
 }
-template void launch_jacobi5_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
-template void launch_jacobi5_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
+
+// ref_precision (fp32 only; an fp64 field evaluates the reference's update exactly as sm::jacobi5)
+template <class T>
+void launch_jacobi5_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s,
+                        bool ref_precision) {
+  if (sizeof(T) == 4 && ref_precision)
+    launch_jacobi5_tbk_r<T, true>(g, in, out, r, steps, resid, s);
+  else
+    launch_jacobi5_tbk_r<T, false>(g, in, out, r, steps, resid, s);
+}
+template void launch_jacobi5_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t, bool);
+template void launch_jacobi5_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t, bool);
 
 }  // namespace dev
 }  // namespace mdfx

@@ -46,12 +46,12 @@ int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
 // -> 18 per 12 / 30 per 24), at one block barrier per plane. (The first version ran every wave as
 // an independent task with a private LDS slot and no barrier: 1.565 fields fetched per sweep
 // against 1.444 / 1.108 for bands of 4 / 8, and slower on every shape, profiles/r02_wtk/README.txt.)
-template <class T, int RY, int K, int WB, bool RES>
+template <class T, int RY, int K, int WB, bool RES, int MODE>
 __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                  int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
                                                  int lag) {
   using V = typename VT<T>::type;
-  using RO = RowOps<T>;
+  using RO = typename std::conditional<sizeof(T) == 4 && MODE >= 1, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
   constexpr int N = VT<T>::N;
   constexpr int OV = (K + N - 1) / N;         // overlap lanes per side
@@ -115,11 +115,15 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
       }
   };
 
-  Row S[TOT], C[TOT];
+  // MODE 2 unrolls the plane loop by two with the loop-carried centres in two arrays that swap
+  // roles (plane q reads CA and writes CB, plane q+1 the reverse), so a new centre is produced
+  // straight into the register the next plane reads instead of being copied there every plane
+  Row S[TOT], CA[TOT], CB[TOT];
 #pragma unroll
   for (int i = 0; i < TOT; ++i) {
     S[i] = RO::zero();
-    C[i] = RO::zero();
+    CA[i] = RO::zero();
+    CB[i] = RO::zero();
   }
   const int qlast = ze - 1 + K;  // last u0 plane of the march
   issue(zs - K, 0);
@@ -127,79 +131,92 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
 
-  auto march = [&](auto edge) __attribute__((always_inline)) {
+  // one u0 plane q: level k finishes plane q - k (its first planes are priming garbage that no
+  // stored plane depends on); centres of the previous plane come from Cin, this plane's go to Cout
+  auto plane_step = [&](int q, Row(&Cin)[TOT], Row(&Cout)[TOT], auto edge) __attribute__((always_inline)) {
     constexpr bool EDGE = decltype(edge)::value;
-    // newest u0 plane q; level k finishes plane q - k (its first planes are priming garbage that
-    // no stored plane depends on)
-    for (int q = zs - K; q <= qlast; ++q) {
-      // the DMA of plane q has landed: every wave waits for its own rows (the stores it issued
-      // after that DMA stay in flight), then one barrier publishes them and also certifies that
-      // every wave has finished reading the other buffer (plane q-1), which the next DMA overwrites
-      wait_vm_le(nst);
-      const int buf = (int)((q - (zs - K)) & 1);
-      lds_barrier();
-      if (q < qlast) issue(q + 1, buf ^ 1);
-      // level 1 reads its u0 rows from the window as it goes (three rows live, not R0; plane q
-      // stays in its buffer for the whole iteration)
-      const T* xw = (const T*)&slot[buf][w * RY][lane];
-      auto u0row = [&](int k) -> Row { return RO::lds(xw + k * 64 * N); };
-      Row X[R0];
+    // the DMA of plane q has landed: every wave waits for its own rows (the stores it issued
+    // after that DMA stay in flight), then one barrier publishes them and also certifies that
+    // every wave has finished reading the other buffer (plane q-1), which the next DMA overwrites
+    // no instruction moves across a plane boundary: the two planes of an unrolled trip would
+    // otherwise be interleaved by the scheduler, with both planes' rows live at once
+    if constexpr (MODE == 2) __builtin_amdgcn_sched_barrier(0);
+    wait_vm_le(nst);
+    const int buf = (int)((q - (zs - K)) & 1);
+    lds_barrier();
+    if (q < qlast) issue(q + 1, buf ^ 1);
+    // level 1 reads its u0 rows from the window as it goes (three rows live, not R0; plane q
+    // stays in its buffer for the whole iteration)
+    const T* xw = (const T*)&slot[buf][w * RY][lane];
+    auto u0row = [&](int k) -> Row { return RO::lds(xw + k * 64 * N); };
+    Row X[R0];
 #pragma unroll
-      for (int l = 1; l <= K; ++l) {
-        const int ROUT = RY + 2 * (K - l);
-        const int off = tbk_off<RY, K>(l);
-        const int gz = q - l + gzoff;
-        // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact: r * 1 = r,
-        // r * 0 = +0 for r >= 0)
-        const Row rl = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
-        Row Y[R0];
+    for (int l = 1; l <= K; ++l) {
+      const int ROUT = RY + 2 * (K - l);
+      const int off = tbk_off<RY, K>(l);
+      const int gz = q - l + gzoff;
+      // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact: r * 1 = r,
+      // r * 0 = +0 for r >= 0)
+      const Row rl = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
+      Row Y[R0];
 #pragma unroll
-        for (int i = 0; i < ROUT; ++i) {
-          Row ri = rl;
-          if (EDGE) {
-            const int y = y0 - (K - l) + i;
-            if (y == 0 || y == ny - 1) ri = r0;
-          }
-          if (l == 1) {  // sliding three-row window over the u0 rows in LDS
-            if (i == 0) {
-              X[0] = u0row(0);
-              X[1] = u0row(1);
-            }
-            X[i + 2] = u0row(i + 2);
-          }
-          const Row cen = X[i + 1];
-          const Row cold = C[off + i];
-          const Row o = RO::fin(S[off + i], cen, cold, ri);
-          const T lft = lane_up1(RO::last(cen));
-          const T rgt = lane_down1(RO::first(cen));
-          S[off + i] = RO::partial(cen, lft, rgt, X[i], X[i + 2], cold);
-          C[off + i] = cen;
-          Y[i] = o;
-          if (RES && l == K && q - K >= zs && y0 + i < ny && own) {
-#pragma unroll
-            for (int e = 0; e < N; ++e)
-              if (x + e < g.nx) {
-                const double d = (double)RO::get(o, e) - (double)RO::get(cold, e);
-                acc += d * d;
-              }
-          }
+      for (int i = 0; i < ROUT; ++i) {
+        Row ri = rl;
+        if (EDGE) {
+          const int y = y0 - (K - l) + i;
+          if (y == 0 || y == ny - 1) ri = r0;
         }
-        if (l < K) {
+        if (l == 1) {  // sliding three-row window over the u0 rows in LDS
+          if (i == 0) {
+            X[0] = u0row(0);
+            X[1] = u0row(1);
+          }
+          X[i + 2] = u0row(i + 2);
+        }
+        const Row cen = X[i + 1];
+        const Row cold = Cin[off + i];
+        const Row o = RO::fin(S[off + i], cen, cold, ri);
+        const T lft = lane_up1(RO::last(cen));
+        const T rgt = lane_down1(RO::first(cen));
+        S[off + i] = RO::partial(cen, lft, rgt, X[i], X[i + 2], cold);
+        RO::pin(S[off + i]);
+        Cout[off + i] = cen;
+        Y[i] = o;
+        if (RES && l == K && q - K >= zs && q <= qlast && y0 + i < ny && own) {
 #pragma unroll
-          for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
-        } else if (q - K >= zs) {  // u_K(q - K) is an owned output plane
-          const int lz = q - K;
-          nst = nsto;
-#pragma unroll
-          for (int i = 0; i < RY; ++i) {
-            if (y0 + i < ny && own) {
-              T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
-              dcheck(g, (const T*)out, a, N);
-              store_nt((V*)a, RO::vec(Y[i]));
+          for (int e = 0; e < N; ++e)
+            if (x + e < g.nx) {
+              const double d = (double)RO::get(o, e) - (double)RO::get(cold, e);
+              acc += d * d;
             }
+        }
+      }
+      if (l < K) {
+#pragma unroll
+        for (int j = 0; j < ROUT; ++j) X[j] = Y[j];
+      } else if (q - K >= zs && q <= qlast) {  // u_K(q - K) is an owned output plane
+        const int lz = q - K;
+        nst = nsto;
+#pragma unroll
+        for (int i = 0; i < RY; ++i) {
+          if (y0 + i < ny && own) {
+            T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
+            dcheck(g, (const T*)out, a, N);
+            store_nt((V*)a, RO::vec(Y[i]));
           }
         }
       }
+    }
+  };
+  auto march = [&](auto edge) __attribute__((always_inline)) {
+    if constexpr (MODE == 2) {
+      // an odd plane count ends with one extra plane (q = qlast + 1): no DMA, nothing stored
+      for (int q = zs - K; q <= qlast; q += 2) {
+        plane_step(q, CA, CB, edge);
+        plane_step(q + 1, CB, CA, edge);
+      }
+    } else {
+      for (int q = zs - K; q <= qlast; ++q) plane_step(q, CA, CA, edge);
     }
   };
   // (fp64: only the copy with the per-row y test; a second copy costs the registers that keep
@@ -212,13 +229,13 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   if (RES) wave_atomic_add(resid, acc);
 }
 
-template <class T, int RY, int K, int WB>
-static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+template <class T, int RY, int K, int WB, int NAT>
+static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
   const int YT = (int)((g.ny + RY * WB - 1) / (RY * WB));  // y bands
-  const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false>;
+  const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, NAT>;
   int zc = knobs().zc;
   const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
   if (zc <= 0) zc = tbk_zc(planes, tiles, resident_blocks(kfn), K);  // chunks >= 4K planes
@@ -231,12 +248,30 @@ static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, 
   if constexpr (WB == 8 || RY == 3) {  // no residual instance (spills / one wave per SIMD): residual
     // sweeps use 2-row bands of 4 waves
     MDFX_CHECK(!resid, "heat7_wtk: no residual variant of this shape");
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
   } else if (resid) {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
   } else {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
   }
+}
+
+// fp32 rows: MDFX_WTK_NAT = 2 (default) natural pair layout (RowOpsN) with the plane loop unrolled
+// by two; 1 the same without the unroll; 0 round 2's regrouped layout (RowOps<float>). fp64 has one
+// layout (mode 0)
+template <class T, int RY, int K, int WB>
+static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  if constexpr (sizeof(T) == 4) {
+    if (knobs().wtk_nat == 2) {
+      launch_wtk_kn<T, RY, K, WB, 2>(g, in, out, r, resid, s);
+      return;
+    }
+    if (knobs().wtk_nat == 1) {
+      launch_wtk_kn<T, RY, K, WB, 1>(g, in, out, r, resid, s);
+      return;
+    }
+  }
+  launch_wtk_kn<T, RY, K, WB, 0>(g, in, out, r, resid, s);
 }
 
 bool heat7_wtk_supported(int steps) { return steps == 3 || steps == 4; }

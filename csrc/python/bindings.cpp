@@ -222,8 +222,10 @@ class PySolver {
       CallbackFns f = callback_fns(callbacks);
       if (!f.allgather) throw Error("ipc transport needs an allgather callback");
       tr = make_ipc_transport(std::move(f));
+    } else if (transport == "proxy") {
+      tr = make_proxy_transport();
     } else {
-      throw Error("unknown transport '" + transport + "' (host|loopback|rccl|ipc|callback)");
+      throw Error("unknown transport '" + transport + "' (host|loopback|rccl|ipc|callback|proxy)");
     }
     SolverOptions o;
     o.overlap = overlap;

@@ -67,7 +67,7 @@ class Simulation:
                  devices: Optional[Sequence[int]] = None, transport: str = "auto",
                  distributed: Optional[bool] = None, overlap: bool = True, sync_debug: bool = False,
                  residual_every: int = 0, graph: bool = False, timeout_s: float = 0.0,
-                 temporal: int = 1, group=None):
+                 temporal: int = 1, group=None, proxy_rank: Optional[int] = None):
         self.problem = problem
         if device == "auto":
             device = "hip" if hip_available() else "cpu"
@@ -119,6 +119,17 @@ class Simulation:
                 args = dict(transport="callback", callbacks=self._torch_transport.callbacks())
             else:
                 raise ValueError("distributed transport must be rccl|ipc|torch|staged|auto")
+        elif proxy_rank is not None:
+            # rank proxy: only slab `proxy_rank` of a `ranks`-way split, on one GPU, its halo
+            # exchange looped back through the ipc mailbox machinery (proxy_transport.cpp)
+            if device != "hip":
+                raise ValueError("the rank proxy needs a HIP device")
+            nranks = int(ranks or 1)
+            if not 0 <= proxy_rank < nranks:
+                raise ValueError("proxy_rank must be in [0, ranks)")
+            local_ranks = [int(proxy_rank)]
+            dev_list = [devices[0] if devices else torch.cuda.current_device()]
+            args = dict(transport="proxy")
         else:
             nranks = ranks or 1
             local_ranks = list(range(nranks))

@@ -1,0 +1,58 @@
+"""Rank proxy on ONE MI355X (bench.py --rank-proxy, csrc/comm/proxy_transport.cpp): one slab of an
+N-way split runs the engine's real per-rank schedule with its halo exchange looped back through the
+ipc mailbox copies and device counters. Its ghosts hold the slab's own faces instead of the
+neighbours', so a plane is exact only if no wrong ghost value can reach it: after S steps, the
+planes more than S away from a proxied boundary equal the full-grid run bitwise."""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import mpi_cuda_process_amd as m  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _full(prob, steps, temporal):
+    with m.Simulation(prob, device="hip", temporal=temporal) as sim:
+        sim.init()
+        sim.run(steps)
+        return sim.gather()
+
+
+@pytest.mark.parametrize("n,r,temporal,graph", [(2, 0, 1, False), (2, 1, 3, True), (4, 1, 3, False),
+                                                (4, 2, 2, True), (8, 3, 3, True), (8, 7, 3, False)])
+def test_proxy_slab_matches_full_grid_away_from_boundaries(hip, n, r, temporal, graph):
+    prob = m.heat3d(nx=1024 if temporal == 3 else 256, ny=24, nz=36 * n)
+    steps = 6
+    full = _full(prob, steps, temporal)
+    with m.Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graph) as sim:
+        assert sim.transport == "proxy"
+        sim.init()
+        sim.prepare_graphs()
+        sim.run(steps)
+        got = sim.read_local(0)
+        lay = sim.layout(0)
+        if graph:
+            assert sim.graph_replays >= 1
+    z0, z1 = lay["z0"], lay["z1"]
+    lo = steps if r > 0 else 0          # planes a wrong lo ghost may have reached
+    hi = steps if r < n - 1 else 0
+    assert np.array_equal(got[lo:(z1 - z0) - hi], full[z0 + lo:z1 - hi])
+
+
+def test_bench_rank_proxy_json(hip):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--rank-proxy", "4", "--n", "256",
+                        "--steps", "6", "--warmup", "3"], capture_output=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr.decode()
+    rec = json.loads([l for l in p.stdout.decode().splitlines() if l.startswith("{")][0])
+    assert rec["proxy"] is True and "PROXY" in rec["metric"] and rec["proxied_n_gpus"] == 4
+    assert rec["proxy_rank"] == 2 and rec["config"]["slab_planes"] == [128, 192]
+    assert rec["implied_node_gcells"] == pytest.approx(4 * rec["value"], rel=1e-3)
+    assert rec["config"]["graph_captures_timed"] == 0

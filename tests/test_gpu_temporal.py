@@ -184,7 +184,9 @@ def test_engine_temporal2_box27(hip, dtype):
 
 
 DEEP = [models.mdf2d(h=45, w=1000), models.mdf2d(h=33, w=300, dtype="f64"), models.life2d(h=50, w=3000),
-        models.life2d(h=19, w=100)]
+        models.life2d(h=19, w=100),
+        # the reference's mixed fp32 / fp64 evaluation (MDF_kernel.cu:20, jacobi5_tbk REF)
+        models.mdf2d(h=45, w=1000, ref_precision=True), models.mdf2d(h=23, w=130, ref_precision=True)]
 
 
 @pytest.mark.parametrize("prob", DEEP, ids=lambda p: p.describe().replace(" ", "_"))
@@ -217,6 +219,21 @@ def test_deep_fused_steps_bitwise(hip, prob, k, knob):
         o = lay.owned
         assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, force)
         assert abs(res.item() - ref_res.item()) <= 1e-9 * max(1.0, ref_res.item())
+
+
+def test_fused_ref_precision_is_the_reference_arithmetic(hip):
+    """The fused ref-precision sweep really evaluates the mixed-precision update: on random data
+    it differs from the pure-fp32 sweep in some cells, and equals the naive ref-precision steps."""
+    out = {}
+    for ref in (False, True):
+        prob = models.mdf2d(h=64, w=1000, ref_precision=ref)
+        lay = FieldLayout.make(prob, halo=8)
+        src = alloc_field(lay, "cuda")
+        init_field(prob, lay, src)
+        dst = alloc_field(lay, "cuda")
+        apply_stencil(prob, lay, src, dst, steps=8)
+        out[ref] = dst[lay.owned, :, :lay.nx].clone()
+    assert not torch.equal(out[False], out[True])
 
 
 LIFE_DEEP = [models.life2d(h=50, w=3000), models.life2d(h=19, w=100), models.life2d(h=40, w=2049),
