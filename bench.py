@@ -78,6 +78,8 @@ def parse(argv=None):
                    help="time steps fused per memory sweep (temporal blocking); 0 = auto: 3 for the 3D "
                         "7-point at 1024-cell rows, else 2 for the 3D stencils, 8 (2D MDF) / 12 (Life) "
                         "for the 2D ones, where a fused kernel exists")
+    p.add_argument("--ref-precision", action="store_true",
+                   help="jacobi5: the reference program's mixed fp32/fp64 update (MDF_kernel.cu:20)")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
@@ -173,7 +175,7 @@ def make_problem(a, nx, ny, nz):
     if a.stencil == "box27":
         return box27(nx=nx, ny=ny, nz=nz, dtype=a.dtype)
     if a.stencil == "jacobi5":
-        return mdf2d(h=nz, w=nx, dtype=a.dtype)
+        return mdf2d(h=nz, w=nx, dtype=a.dtype, ref_precision=a.ref_precision)
     return life2d(h=nz, w=nx)
 
 

@@ -204,6 +204,7 @@ struct Knobs {
   int wtk_nat = 2;     // MDFX_WTK_NAT: heat7_wtk fp32 rows: 2 natural pair layout + 2-plane unroll, 1 natural, 0 round 2's
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)
+  int j5_nat = 2;      // MDFX_J5_NAT: jacobi5_tbk fp32 rows: 2 natural layout + 2-row unroll, 1 natural, 0 round 2's pair layout
   int j5_tbk = 0;      // MDFX_J5_TBK: 2D MDF two-step sweeps through the K-step kernel
   int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
   int life_bits = 1;   // MDFX_LIFE_BITS: Life sweeps of K > 2 generations bit-sliced (0: SWAR life_tbk)

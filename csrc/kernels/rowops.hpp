@@ -75,6 +75,9 @@ struct RowOps<float> {
     o.b = __builtin_elementwise_fma(rc.b, __builtin_elementwise_fma(m6, c.b, S.b + zp.b), c.b);
     return o;
   }
+  static __device__ __forceinline__ Row partial5(const Row& c, float l, float rr, const Row& zm) {
+    return add(hsum(c, l, rr), zm);
+  }
   // fma(r, fma(-4, c, S + zp), c): sm::jacobi5 with S = (xm + xp) + zm
   static __device__ __forceinline__ Row fin4(const Row& S, const Row& zp, const Row& c, const Row& rc) {
     const T2 m4 = T2{-4.f, -4.f};
@@ -171,6 +174,9 @@ struct RowOps<double> {
   static __device__ __forceinline__ Row fin4_ref(const Row& S, const Row& zp, const Row& c, const Row& rc) {
     return fin4(S, zp, c, rc);  // fp64 fields: the reference's widening is the identity
   }
+  static __device__ __forceinline__ Row partial5(const Row& c, double l, double rr, const Row& zm) {
+    return Row{T2{l + c.v.y, c.v.x + rr} + zm.v};
+  }
   static __device__ __forceinline__ Row coef(double r, const bool* held) {
     return Row{T2{held[0] ? 0.0 : r, held[1] ? 0.0 : r}};
   }
@@ -214,6 +220,13 @@ struct RowOpsN {
     return Row{T2{v.x, v.y}, T2{v.z, v.w}};
   }
   static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}, T2{0.f, 0.f}}; }
+  // one scalar add the backend cannot pair with its neighbour into a v_pk_add_f32 (e0 + e2 and
+  // e1 + e3 would pack, and their halves then need two moves to reach (e0,e1) / (e2,e3))
+  static __device__ __forceinline__ float add1(float a, float b) {
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+  }
   static __device__ __forceinline__ float first(const Row& c) { return c.p.x; }
   static __device__ __forceinline__ float last(const Row& c) { return c.q.y; }
   // (((xm + xp) + ym) + yp) + zm; l / rr are the cells beyond the slice's ends (lane shifts the
@@ -222,8 +235,8 @@ struct RowOpsN {
                                                 const Row& zm) {
     Row s;
     s.p.x = l + c.p.y;    // e0: xm + xp
-    s.p.y = c.p.x + c.q.x;  // e1
-    s.q.x = c.p.y + c.q.y;  // e2
+    s.p.y = add1(c.p.x, c.q.x);  // e1
+    s.q.x = add1(c.p.y, c.q.y);  // e2
     s.q.y = rr + c.q.x;   // e3
     s.p = ((s.p + ym.p) + yp.p) + zm.p;
     s.q = ((s.q + ym.q) + yp.q) + zm.q;
@@ -238,6 +251,36 @@ struct RowOpsN {
   }
   static __device__ __forceinline__ Row coef(float r, const bool* held) {
     return Row{T2{held[0] ? 0.f : r, held[1] ? 0.f : r}, T2{held[2] ? 0.f : r, held[3] ? 0.f : r}};
+  }
+  // 2D 5-point: (xm + xp) + zm, and fma(r, fma(-4, c, S + zp), c) (sm::jacobi5)
+  static __device__ __forceinline__ Row partial5(const Row& c, float l, float rr, const Row& zm) {
+    Row s;
+    s.p.x = l + c.p.y;
+    s.p.y = add1(c.p.x, c.q.x);
+    s.q.x = add1(c.p.y, c.q.y);
+    s.q.y = rr + c.q.x;
+    s.p = s.p + zm.p;
+    s.q = s.q + zm.q;
+    return s;
+  }
+  static __device__ __forceinline__ Row fin4(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m4 = T2{-4.f, -4.f};
+    Row o;
+    o.p = __builtin_elementwise_fma(rc.p, __builtin_elementwise_fma(m4, c.p, S.p + zp.p), c.p);
+    o.q = __builtin_elementwise_fma(rc.q, __builtin_elementwise_fma(m4, c.q, S.q + zp.q), c.q);
+    return o;
+  }
+  // sm::jacobi5_ref: t = fma(-4, c, S + zp) in fp32, then (float)fma((double)r, (double)t, (double)c)
+  static __device__ __forceinline__ Row fin4_ref(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m4 = T2{-4.f, -4.f};
+    const T2 tp = __builtin_elementwise_fma(m4, c.p, S.p + zp.p);
+    const T2 tq = __builtin_elementwise_fma(m4, c.q, S.q + zp.q);
+    Row o;
+    o.p.x = (float)__builtin_fma((double)rc.p.x, (double)tp.x, (double)c.p.x);
+    o.p.y = (float)__builtin_fma((double)rc.p.y, (double)tp.y, (double)c.p.y);
+    o.q.x = (float)__builtin_fma((double)rc.q.x, (double)tq.x, (double)c.q.x);
+    o.q.y = (float)__builtin_fma((double)rc.q.y, (double)tq.y, (double)c.q.y);
+    return o;
   }
   static __device__ __forceinline__ Row scale(const Row& x, float s) { return Row{x.p * T2{s, s}, x.q * T2{s, s}}; }
   static __device__ __forceinline__ float get(const Row& c, int e) {

@@ -492,11 +492,15 @@ template void launch_jacobi5_tb2<double>(const Geo&, const double*, double*, dou
 // REF: the reference program's own evaluation of every level (sm::jacobi5_ref, MDF_kernel.cu:20,
 // SURVEY D17): the fp32 sum and -4u term as usual, then r * t + u as ONE fp64 fma of the widened
 // values, rounded back to fp32. Held cells stay exact (fma(0, t, u) = u). fp64 fields: identical.
-template <class T, int K, bool RES, bool REF>
+// MODE (fp32): 2 = rows in the natural pair layout (RowOpsN: no regrouping after a 16-B load, x
+// sums as scalar adds with DPP-folded lane shifts) and the row loop unrolled by two with the
+// loop-carried centres ping-ponged between two arrays (no per-row centre copies); 0 = round 2's
+// pair layout (RowOps<float>). fp64 runs mode 0.
+template <class T, int K, bool RES, bool REF, int MODE>
 __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                    int zc, int XT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
-  using RO = RowOps<T>;
+  using RO = typename std::conditional<sizeof(T) == 4 && MODE >= 1, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
   constexpr int N = VT<T>::N;
   constexpr int OV = (K + N - 1) / N;  // overlap lanes per side
@@ -512,13 +516,11 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   const bool xin = x >= 0 && x < g.pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
   const int64_t plane = g.plane;
-  // rows live in RowOps' pair layout (fp32: packed ops without register moves between levels);
   // per-cell coefficient 0 on the held columns x = 0, x >= nx - 1
   bool held[N];
 #pragma unroll
   for (int e = 0; e < N; ++e) held[e] = (x + e == 0) || (x + e >= g.nx - 1);
   const Row rx = RO::coef(r, held);
-  const Row r0 = RO::zero();
   // Loads without lane predication: lanes outside the row read the nearest in-row vector and rows
   // past the storage read its last row. Those values are finite and only ever meet held or unowned
   // cells (the left halo lane of the first segment feeds only x = 0, which is held; lanes beyond
@@ -527,41 +529,45 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   auto ld = [&](int64_t lz) -> Row {
     const int64_t lzc = lz < 0 ? 0 : lz >= g.lz_max ? g.lz_max - 1 : lz;
     dcheck(g, in, ib + lzc * plane, N);
-    return RO::lds(ib + lzc * plane);  // a 16-B vector regrouped into the pair layout
+    return RO::lds(ib + lzc * plane);  // one 16-B vector
   };
-  Row S[K], C[K];  // level l = 1..K at index l - 1
+  Row S[K], CA[K], CB[K];  // level l = 1..K at index l - 1
 #pragma unroll
   for (int l = 0; l < K; ++l) {
     S[l] = RO::zero();
-    C[l] = RO::zero();
+    CA[l] = RO::zero();
+    CB[l] = RO::zero();
   }
   Row nx = ld(zs - K);
   double acc = 0.0;
+  const int64_t qlast = ze - 1 + K;
   // newest u0 row q; level l finishes row q - l (each level's first two rows are priming garbage
-  // that no level needs)
-  // rows of the chunk's pipeline (zs - K - 1 .. ze + K - 1) that are all interior in z need no
-  // z test: one loop copy without it, one with the per-level test for chunks at the z boundary
+  // that no level needs). Rows of the chunk's pipeline (zs - K - 1 .. ze + K - 1) that are all
+  // interior in z need no z test: one loop copy without it, one with the per-level test for chunks
+  // at the z boundary.
   const bool zint = zs - K - 1 + g.gz_off >= 1 && ze + K - 1 + g.gz_off <= g.gnz - 2;
-  auto march = [&](auto ztest) __attribute__((always_inline)) {
-  constexpr bool ZT = decltype(ztest)::value;
-  for (int64_t q = zs - K; q <= ze - 1 + K; ++q) {
+  auto row_step = [&](int64_t q, Row(&Cin)[K], Row(&Cout)[K], auto ztest) __attribute__((always_inline)) {
+    constexpr bool ZT = decltype(ztest)::value;
     Row X = nx;
     nx = ld(q + 1);
 #pragma unroll
     for (int l = 1; l <= K; ++l) {
       const int64_t row = q - l;
       const int64_t gz = row + g.gz_off;
-      const Row rc = (ZT && (gz <= 0 || gz >= g.gnz - 1)) ? r0 : rx;
-      const Row c = C[l - 1];
+      // z-held rows through a wave-uniform 0 / 1 factor (r * 1 = r, r * 0 = +0; a Row-valued select
+      // here was lowered to a scratch-memory table)
+      const Row rc = ZT ? RO::scale(rx, (gz <= 0 || gz >= g.gnz - 1) ? T(0) : T(1)) : rx;
+      const Row c = Cin[l - 1];
       const Row o = REF ? RO::fin4_ref(S[l - 1], X, c, rc) : RO::fin4(S[l - 1], X, c, rc);
       // row + 1's partial from the arriving row X: (xm + xp) + zm
       const T lft = lane_up1(RO::last(X));
       const T rgt = lane_down1(RO::first(X));
-      S[l - 1] = RO::add(RO::hsum(X, lft, rgt), c);
-      C[l - 1] = X;
+      S[l - 1] = RO::partial5(X, lft, rgt, c);
+      RO::pin(S[l - 1]);
+      Cout[l - 1] = X;
       if (l < K) {
         X = o;
-      } else if (row >= zs && own) {
+      } else if (row >= zs && q <= qlast && own) {
         dcheck(g, (const T*)out, out + row * plane + x, N);
         store_nt((V*)(out + row * plane + x), RO::vec(o));
         if (RES) {
@@ -574,7 +580,17 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
         }
       }
     }
-  }
+  };
+  auto march = [&](auto ztest) __attribute__((always_inline)) {
+    if constexpr (MODE == 2) {
+      // an odd row count ends with one extra row (q = qlast + 1): loads clamp, nothing is stored
+      for (int64_t q = zs - K; q <= qlast; q += 2) {
+        row_step(q, CA, CB, ztest);
+        row_step(q + 1, CB, CA, ztest);
+      }
+    } else {
+      for (int64_t q = zs - K; q <= qlast; ++q) row_step(q, CA, CA, ztest);
+    }
   };
   // (fp64: one loop copy with the test; the second copy costs the VGPRs of occupancy 4 at K = 8)
   if (zint && sizeof(T) == 4)
@@ -584,8 +600,8 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   if (RES) wave_atomic_add(resid, acc);
 }
 
-template <class T, int K, bool REF>
-static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+template <class T, int K, bool REF, int MODE>
+static void launch_jacobi5_tbk_km(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   const int64_t planes = g.lz_end - g.lz_begin;
   if (planes <= 0) return;
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
@@ -596,9 +612,26 @@ static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double*
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
   if (resid)
-    hipLaunchKernelGGL((jacobi5_tbk<T, K, true, REF>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+    hipLaunchKernelGGL((jacobi5_tbk<T, K, true, REF, MODE>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
   else
-    hipLaunchKernelGGL((jacobi5_tbk<T, K, false, REF>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+    hipLaunchKernelGGL((jacobi5_tbk<T, K, false, REF, MODE>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
+}
+
+// fp32: MDFX_J5_NAT = 2 (default) natural layout + 2-row unroll, 1 natural layout, 0 round 2's
+// pair layout; fp64: mode 0
+template <class T, int K, bool REF>
+static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  if constexpr (sizeof(T) == 4) {
+    if (knobs().j5_nat == 2) {
+      launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
+      return;
+    }
+    if (knobs().j5_nat == 1) {
+      launch_jacobi5_tbk_km<T, K, REF, 1>(g, in, out, r, resid, s);
+      return;
+    }
+  }
+  launch_jacobi5_tbk_km<T, K, REF, 0>(g, in, out, r, resid, s);
 }
 
 template <class T, bool REF>

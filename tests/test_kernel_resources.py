@@ -54,6 +54,9 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 1>", 2),              # natural layout, no unroll
     ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0>", 2),
     ("mdfx::dev::heat7_wtk<float, 2, 3, 4, true, 2>", 2),               # residual sweeps
+    ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 2>", 3),           # 2D MDF, 8 steps per sweep
+    ("mdfx::dev::jacobi5_tbk<float, 8, false, true, 2>", 2),            # reference precision
+    ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 1>", 4),
     ("mdfx::dev::heat7_tbk<float, 4, 2, 4, false>", 2),                 # K = 2 fused sweep
     ("mdfx::dev::heat7_tbk<double, 4, 2, 4, false>", 2),
     ("mdfx::dev::heat7_tb2<float, 2, 4, false, 1, true>", 3),           # x-tiled rows
