@@ -464,13 +464,16 @@ def test_mdf_ref_precision_matches_reference_arithmetic(mdfx, ranks):
     assert np.abs(other - want).max() < 1e-3  # same update up to rounding
 
 
-def test_mdf_ref_precision_has_no_fused_kernel(mdfx):
+def test_mdf_ref_precision_runs_fused(mdfx):
+    """The reference's mixed-precision MDF update has fused kernels (jacobi5_tbk REF), so the
+    reference-compatible dialogue gets the deep temporal blocking too."""
     import mpi_cuda_process_amd as m
 
-    assert not m.native().hip_supports_steps("jacobi5", "f32", 64, 1, 64, 2, 2, True)
+    for k in (2, 3, 4, 6, 8):
+        assert m.native().hip_supports_steps("jacobi5", "f32", 64, 1, 64, k, k, True)
     from mpi_cuda_process_amd.engine import auto_temporal
 
-    assert auto_temporal(m.mdf2d(h=4096, w=512, ref_precision=True), 1, "hip") == 1
+    assert auto_temporal(m.mdf2d(h=4096, w=512, ref_precision=True), 1, "hip") == 8
     assert auto_temporal(m.mdf2d(h=4096, w=512), 1, "hip") == 8
 
 
