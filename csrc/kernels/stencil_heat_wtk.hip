@@ -245,8 +245,10 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
   const int64_t ntasks = (int64_t)XT * YT * ZT;
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wtk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
-  if constexpr (WB == 8 || RY == 3) {  // no residual instance (spills / one wave per SIMD): residual
-    // sweeps use 2-row bands of 4 waves
+  // residual instances exist where they fit 256 VGPRs without spills: every fp64 shape, fp32 in
+  // mode 1 (the fp32 mode-0 / mode-2 3-row residual instances spill), and 2-row waves
+  constexpr bool kRes = sizeof(T) == 8 || NAT == 1 || RY <= 2;
+  if constexpr (!kRes) {
     MDFX_CHECK(!resid, "heat7_wtk: no residual variant of this shape");
     hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
   } else if (resid) {
@@ -262,6 +264,10 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
 template <class T, int RY, int K, int WB>
 static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if constexpr (sizeof(T) == 4) {
+    if (resid && RY == 3 && knobs().wtk_nat != 0) {  // the spill-free 3-row residual instance
+      launch_wtk_kn<T, RY, K, WB, 1>(g, in, out, r, resid, s);
+      return;
+    }
     if (knobs().wtk_nat == 2) {
       launch_wtk_kn<T, RY, K, WB, 2>(g, in, out, r, resid, s);
       return;
@@ -297,16 +303,17 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
              "heat7_wtk: row / plane counts must fit 32-bit indices");
   // bands of 8 waves (one 512-thread block per CU) only for deep regions: 1024^3 1632-1674 vs
   // 1593-1612 GCells/s for bands of 4, but on 128..512-plane slabs the few large blocks leave CUs
-  // idle (8 slabs of 128 planes: 1188-1223 vs 1347-1385); the residual sweeps use bands of 4 (the
-  // 8-wave residual variant spills)
+  // idle (8 slabs of 128 planes: 1188-1223 vs 1347-1385). Residual sweeps run the same band shape
+  // as plain ones (round 2 forced 2-row bands of 4 waves on them: MDFX_WTK_RES_SHAPE=1)
+  const bool old_res = resid && knobs().wtk_res_shape == 1;
   int wb = knobs().wtk_wb;
-  if (wb != 4 && wb != 8) wb = (g.lz_end - g.lz_begin >= 768 && !resid) ? 8 : 4;
-  if (resid) wb = 4;
+  if (wb != 4 && wb != 8) wb = (g.lz_end - g.lz_begin >= 768 && !old_res) ? 8 : 4;
+  if (old_res) wb = 4;
   // rows per wave at K = 3: fp32 3 (1024^3: 1679 vs 1447 GCells/s for 2 rows); fp64 2 in bands of
   // 4 (3 rows need more than 256 VGPRs there), see below for bands of 8
   constexpr int RY3 = sizeof(T) == 4 ? 3 : 2;
-  if (steps == 3 && resid) {
-    launch_wtk_k<T, 2, 3, 4>(g, in, out, r, resid, s);  // the fp32 3-row residual variant: one wave per SIMD
+  if (steps == 3 && old_res) {
+    launch_wtk_k<T, 2, 3, 4>(g, in, out, r, resid, s);
   } else if (steps == 3) {
     if (wb == 8) {
       // fp64 8-wave bands: 3 rows per wave at rows up to 1024 cells (1024^3 923-925 vs 849-852
