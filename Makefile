@@ -58,9 +58,10 @@ $(OBJ)/%.o: csrc/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX_HOST) $(HOSTFLAGS) -c $< -o $@
 
-# the natural-layout rows (heat7_wtk, jacobi5_tbk) need the scalar x adds left unpacked (RowOpsN, rowops.hpp)
+# the natural-layout rows (heat7_wtk, jacobi5_tbk, box27_tb2n) need the scalar x adds left unpacked (RowOpsN, rowops.hpp)
 $(OBJ)/kernels/stencil_heat_wtk.o $(ASAN_DIR)/kernels/stencil_heat_wtk.o $(DCK_DIR)/kernels/stencil_heat_wtk.o: HIPFLAGS += -fno-slp-vectorize
 $(OBJ)/kernels/stencil_heat_tb.o $(ASAN_DIR)/kernels/stencil_heat_tb.o $(DCK_DIR)/kernels/stencil_heat_tb.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJ)/kernels/stencil_box27.o $(ASAN_DIR)/kernels/stencil_box27.o $(DCK_DIR)/kernels/stencil_box27.o: HIPFLAGS += -fno-slp-vectorize
 
 # the AVX2 + FMA copy of the CPU stencils (selected at run time by cpu_kernels.cpp)
 $(OBJ)/cpu/cpu_kernels_avx2.o $(ASAN_DIR)/cpu/cpu_kernels_avx2.o $(DCK_DIR)/cpu/cpu_kernels_avx2.o: HOSTFLAGS += -mavx2 -mfma

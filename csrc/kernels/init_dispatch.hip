@@ -79,6 +79,7 @@ static Knobs read_knobs() {
   k.wtk_nat = env_int("MDFX_WTK_NAT", 2);
   k.j5_nat = env_int("MDFX_J5_NAT", 2);
   k.wtk_res_shape = env_int("MDFX_WTK_RES_SHAPE", 0);
+  k.b27_nat = env_int("MDFX_B27_NAT", 1);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;

@@ -108,6 +108,17 @@ __device__ __forceinline__ void wait_vm_le(int n) {
   }
 }
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+// An LDS pointer whose (wave-uniform) address is pinned in a VGPR: ds_read / ds_write take a VGPR
+// address, and a uniform address kept in an SGPR is otherwise copied into a VGPR at every access
+// (v_mov + access). Accesses through the result at compile-time indices use the instruction's
+// offset field.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(3))) T* lds_vptr(T* p) {
+  unsigned a = (unsigned)(uintptr_t)((__attribute__((address_space(3))) T*)p);
+  asm volatile("" : "+v"(a));
+  return (__attribute__((address_space(3))) T*)(uintptr_t)a;
+}
+
 // Workgroup barrier that does NOT drain outstanding vector-memory operations (a __syncthreads
 // makes hipcc wait for vmcnt(0), which would also wait for an in-flight LDS DMA). LDS writes are
 // completed first; the empty asm statements keep the compiler from moving memory accesses across.
@@ -209,6 +220,7 @@ struct Knobs {
   int j5_tbk = 0;      // MDFX_J5_TBK: 2D MDF two-step sweeps through the K-step kernel
   int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
   int life_bits = 1;   // MDFX_LIFE_BITS: Life sweeps of K > 2 generations bit-sliced (0: SWAR life_tbk)
+  int b27_nat = 1;     // MDFX_B27_NAT: fp32 box27_tb2 in the natural layout with the 2-plane unroll (0: round 2's)
   int b27_tbk = 0;     // MDFX_B27_TBK: 27-point fused kernel (0: per dtype, -1: box27_tb2, 1/2/4: box27_tbk rows)
   int vm_lag = 1;      // MDFX_VM_LAG: streaming kernels leave the last plane's stores in flight across the
                        // next plane's DMA wait (0: wait for every vector-memory operation, round 2)

@@ -252,6 +252,34 @@ struct RowOpsN {
   static __device__ __forceinline__ Row coef(float r, const bool* held) {
     return Row{T2{held[0] ? 0.f : r, held[1] ? 0.f : r}, T2{held[2] ? 0.f : r, held[3] ? 0.f : r}};
   }
+  // ---- 27-point helpers (box27_tb2n) ----
+  static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.p + y.p, x.q + y.q}; }
+  // xm + xp of every cell; l / rr are the cells beyond the slice's ends
+  static __device__ __forceinline__ Row hsum(const Row& c, float l, float rr) {
+    Row h;
+    h.p.x = l + c.p.y;
+    h.p.y = add1(c.p.x, c.q.x);
+    h.q.x = add1(c.p.y, c.q.y);
+    h.q.y = rr + c.q.x;
+    return h;
+  }
+  // fma(k2, d, fma(k1, x, k0 * c)): sm::box27_A / box27_B
+  static __device__ __forceinline__ Row lin3(const Row& c, const Row& x, const Row& d, float k0, float k1, float k2) {
+    const T2 K0{k0, k0}, K1{k1, k1}, K2{k2, k2};
+    Row o;
+    o.p = __builtin_elementwise_fma(K2, d.p, __builtin_elementwise_fma(K1, x.p, K0 * c.p));
+    o.q = __builtin_elementwise_fma(K2, d.q, __builtin_elementwise_fma(K1, x.q, K0 * c.q));
+    return o;
+  }
+  // per cell: held ? h : o
+  static __device__ __forceinline__ Row sel(const bool* held, const Row& h, const Row& o) {
+    Row r;
+    r.p.x = held[0] ? h.p.x : o.p.x;
+    r.p.y = held[1] ? h.p.y : o.p.y;
+    r.q.x = held[2] ? h.q.x : o.q.x;
+    r.q.y = held[3] ? h.q.y : o.q.y;
+    return r;
+  }
   // 2D 5-point: (xm + xp) + zm, and fma(r, fma(-4, c, S + zp), c) (sm::jacobi5)
   static __device__ __forceinline__ Row partial5(const Row& c, float l, float rr, const Row& zm) {
     Row s;

@@ -395,6 +395,175 @@ __global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __
   if (RES) wave_atomic_add(resid, acc);
 }
 
+// box27_tb2 for fp32 in the natural pair layout (RowOpsN: (e0,e1),(e2,e3) straight from a 16-B
+// load, x sums as scalar adds) with the plane loop unrolled by two: every loop-carried row (the
+// running sums, the last A, the centres, the pending u1 plane and the prefetched u0 plane) lives in
+// two copies that swap roles between the planes of a trip, so no carried row is ever copied (the
+// pair-layout kernel spent 161 of its 400 VALU instructions per plane on register moves). Same
+// arithmetic and order as box27_tb2, so bitwise equal to it and to two box27_zw steps. An odd
+// plane count ends with one extra plane that stores nothing.
+template <int RY, int WXN, bool RES>
+__global__ __launch_bounds__(256) void box27_tb2n(const float* __restrict__ in, float* __restrict__ out, Geo g,
+                                                  float c0, float c1, float c2, float c3, int zc, int YT,
+                                                  double* __restrict__ resid) {
+  using T = float;
+  using V = typename VT<T>::type;
+  using RO = RowOpsN;
+  using Row = RO::Row;
+  constexpr int N = 4;
+  constexpr int WX = 64 * N;
+  constexpr int WYN = 4 / WXN;
+  constexpr int R0 = RY + 4;  // u0 rows y0-2 .. y0+RY+1
+  constexpr int R1 = RY + 2;  // u1 rows y0-1 .. y0+RY
+  __shared__ T edge[2][4][R0 + R1][2];
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int yt = t % YT;
+  const int zt = t / YT;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wx = w % WXN, wy = w / WXN;
+  const int64_t xw = (int64_t)wx * WX;
+  const uint32_t xo = (uint32_t)lane * N;
+  const int64_t x = xw + xo;
+  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
+  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
+  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
+  const bool xin = x < g.pitch;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  T* ob = out + y0 * pitch + xw;
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+
+  // Unpredicated loads from clamped addresses (rows outside [0, ny), planes outside the storage and
+  // lanes beyond the row read the nearest valid vector): those values are finite and only ever
+  // feed held cells (the selects keep the centre there) or unstored lanes. The plane / row part of
+  // the address is wave-uniform, the lane part a 32-bit byte offset.
+  const int ny32 = (int)g.ny;
+  const uint32_t xcb = (uint32_t)((xin ? x : pitch - N) * (int64_t)sizeof(T));
+  auto ld = [&](int64_t lz, int k) -> Row {
+    const int y = (int)y0 - 2 + k;
+    const int yc = y < 0 ? 0 : y >= ny32 ? ny32 - 1 : y;
+    const int64_t lzc = lz < 0 ? 0 : lz >= g.lz_max ? g.lz_max - 1 : lz;
+    const T* a = (const T*)((const char*)(in + lzc * plane + (int64_t)yc * pitch) + xcb);
+    dcheck(g, in, a, N);
+    return RO::lds(a);
+  };
+  // Seam cells of the neighbouring waves in the row, read by every lane (broadcast) from VGPR-held
+  // LDS bases. A wave at the row's left / right end reads its own entry instead of a neighbour's:
+  // that value only reaches the x = 0 / x >= nx - 1 cells, which the selects hold, so any finite
+  // value serves (round 2 branched to substitute 0).
+  constexpr int SL = R0 + R1;  // seam slots per wave and parity
+  const int wl = wx > 0 ? w - 1 : w, wr = wx < WXN - 1 ? w + 1 : w;
+  const auto eL = lds_vptr(&edge[0][wl][0][1]);
+  const auto eR = lds_vptr(&edge[0][wr][0][0]);
+  const auto eW = lds_vptr(&edge[0][w][0][lane == 0 ? 0 : 1]);
+  auto hsum = [&](const Row& v, int buf, int slot) -> Row {
+    const T le = eL[(buf * 4 * SL + slot) * 2];
+    const T re = eR[(buf * 4 * SL + slot) * 2];
+    return RO::hsum(v, lane_up1_or(le, RO::last(v)), lane_down1_or(re, RO::first(v)));
+  };
+  struct St {
+    Row Rw[R0];                   // u0 plane k
+    Row A0p[R1], S0[R1], C0[R1];  // A0(k-1); A0(k-2) + B0(k-1); u0 plane k-1 (u1 window rows)
+    Row U1[R1];                   // u1 plane k-2
+    Row A1p[RY], S1[RY], C1[RY];  // A1(k-3); A1(k-4) + B1(k-3); u1 plane k-3 (owned rows)
+  };
+  St sa, sb;
+#pragma unroll
+  for (int j = 0; j < R0; ++j) {
+    sa.Rw[j] = ld(zs - 2, j);
+    sb.Rw[j] = RO::zero();
+  }
+#pragma unroll
+  for (int j = 0; j < R1; ++j) sa.A0p[j] = sa.S0[j] = sa.C0[j] = sa.U1[j] = sb.A0p[j] = sb.S0[j] = sb.C0[j] = sb.U1[j] = RO::zero();
+#pragma unroll
+  for (int i = 0; i < RY; ++i) sa.A1p[i] = sa.S1[i] = sa.C1[i] = sb.A1p[i] = sb.S1[i] = sb.C1[i] = RO::zero();
+  double acc = 0.0;
+  const int64_t klast = ze + 2;
+
+  auto plane_step = [&](int64_t k, int buf, St& si, St& so) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < R0; ++j) so.Rw[j] = ld(k + 1, j);  // next plane, in flight over this one
+    if (lane == 0 || lane == 63) {  // lane 0 publishes each row's first cell, lane 63 its last
+#pragma unroll
+      for (int j = 0; j < R0; ++j) eW[(buf * 4 * SL + j) * 2] = lane == 0 ? RO::first(si.Rw[j]) : RO::last(si.Rw[j]);
+#pragma unroll
+      for (int j = 0; j < R1; ++j)
+        eW[(buf * 4 * SL + R0 + j) * 2] = lane == 0 ? RO::first(si.U1[j]) : RO::last(si.U1[j]);
+    }
+    lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
+
+    // ---- level 1: partials of u1 plane k-2, u2(k-3) ------------------------------------------
+    if (k >= zs + 1) {
+      Row Hm = hsum(si.U1[0], buf, R0), Hc = hsum(si.U1[1], buf, R0 + 1);
+      const int64_t lz = k - 3;
+      const int64_t gz = lz + g.gz_off;
+      const bool zb = gz == 0 || gz == g.gnz - 1;
+#pragma unroll
+      for (int i = 0; i < RY; ++i) {
+        const int j = i + 1;
+        const Row Hp = hsum(si.U1[j + 1], buf, R0 + j + 1);
+        const Row cross = RO::add(Hc, RO::add(si.U1[j - 1], si.U1[j + 1]));
+        const Row diag = RO::add(Hm, Hp);
+        const Row A = RO::lin3(si.U1[j], cross, diag, c1, c2, c3);  // sm::box27_A
+        const Row B = RO::lin3(si.U1[j], cross, diag, c0, c1, c2);  // sm::box27_B
+        Hm = Hc;
+        Hc = Hp;
+        const int64_t y = y0 + i;
+        if (k >= zs + 3 && k <= klast && y < g.ny) {
+          Row o = si.C1[i];
+          if (!zb && y != 0 && y != g.ny - 1) o = RO::sel(xb, si.C1[i], RO::add(si.S1[i], A));
+          if (xin) {
+            dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
+            store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), RO::vec(o));
+            if (RES) {
+#pragma unroll
+              for (int e = 0; e < N; ++e)
+                if (x + e < g.nx) {
+                  const double d = (double)RO::get(o, e) - (double)RO::get(si.C1[i], e);
+                  acc += d * d;
+                }
+            }
+          }
+        }
+        so.S1[i] = RO::add(si.A1p[i], B);
+        so.A1p[i] = A;
+        so.C1[i] = si.U1[j];
+      }
+    }
+    // ---- level 0: partials of u0 plane k, u1(k-1) ----------------------------------------------
+    {
+      const int64_t gz = k - 1 + g.gz_off;
+      const bool zb = gz <= 0 || gz >= g.gnz - 1;
+      Row Hm = hsum(si.Rw[0], buf, 0), Hc = hsum(si.Rw[1], buf, 1);
+#pragma unroll
+      for (int jj = 0; jj < R1; ++jj) {
+        const int j = jj + 1;
+        const Row Hp = hsum(si.Rw[j + 1], buf, j + 1);
+        const Row cross = RO::add(Hc, RO::add(si.Rw[j - 1], si.Rw[j + 1]));
+        const Row diag = RO::add(Hm, Hp);
+        const Row A = RO::lin3(si.Rw[j], cross, diag, c1, c2, c3);
+        const Row B = RO::lin3(si.Rw[j], cross, diag, c0, c1, c2);
+        Hm = Hc;
+        Hc = Hp;
+        const int64_t y = y0 - 1 + jj;
+        Row u = si.C0[jj];
+        if (!zb && y > 0 && y < g.ny - 1) u = RO::sel(xb, si.C0[jj], RO::add(si.S0[jj], A));
+        so.U1[jj] = u;
+        so.S0[jj] = RO::add(si.A0p[jj], B);
+        so.A0p[jj] = A;
+        so.C0[jj] = si.Rw[j];
+      }
+    }
+  };
+  for (int64_t k = zs - 2; k <= klast; k += 2) {
+    plane_step(k, 0, sa, sb);
+    plane_step(k + 1, 1, sb, sa);
+  }
+  if (RES) wave_atomic_add(resid, acc);
+}
+
 // ---- K steps per sweep, streaming levels (box27_tbk) ---------------------------------------------
 //
 // heat7_tbk's organisation applied to the 27-point update: u0 planes arrive by LDS DMA (each wave
@@ -656,6 +825,16 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
+  // fp32: the natural-layout unrolled kernel unless MDFX_B27_NAT=0
+  if constexpr (std::is_same<T, float>::value) {
+    if (knobs().b27_nat) {
+      if (resid)
+        hipLaunchKernelGGL((box27_tb2n<RY, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+      else
+        hipLaunchKernelGGL((box27_tb2n<RY, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+      return;
+    }
+  }
   // next-plane prefetch always: fp32 985.7 vs 773.3 GCells/s without, fp64 491.8 vs 479.8 (512^3,
   // profiles/r01_box27_tb2.txt)
   if (resid)

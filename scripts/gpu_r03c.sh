@@ -11,6 +11,9 @@ for r in a b; do
   for m in 0 1 2; do steps+=("mdf_nat${m}_$r=MDFX_J5_NAT=$m $M"); done
   for m in 0 1 2; do steps+=("mdfref_nat${m}_$r=MDFX_J5_NAT=$m $M --ref-precision"); done
 done
+for r in a b; do
+  for m in 0 1; do steps+=("b27f32_nat${m}_$r=MDFX_B27_NAT=$m $B --stencil box27 --n 512"); done
+done
 steps+=("mdf_f64=$M --dtype f64" "mdf_dialogue=printf '100\n16384\n16384\n' | ./build/bin/mdf --json")
 steps+=("h1024_a=$B" "h1024_drv=python bench.py --steps 20 --warmup 5")
 for n in 2 4 8; do steps+=("proxy$n=python bench.py --rank-proxy $n --steps 48 --warmup 12"); done

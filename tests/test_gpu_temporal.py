@@ -77,11 +77,13 @@ BOX27 = [models.box27(nx=1024, ny=11, nz=9), models.box27(nx=512, ny=21, nz=15),
 
 
 @pytest.mark.parametrize("prob", BOX27, ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("kernel", ["-1", "1", "2", "4"])
+@pytest.mark.parametrize("kernel", ["-1", "-1n", "1", "2", "4"])
 def test_box27_fused_kernels_bitwise(hip, prob, kernel, knob):
-    """Both fused 27-point kernels (MDFX_B27_TBK=-1: box27_tb2; 1 / 2 / 4: box27_tbk with that
-    many rows per tile) == two naive single steps, bitwise, with the residual of step 2."""
-    knob("MDFX_B27_TBK", kernel)
+    """Both fused 27-point kernels (MDFX_B27_TBK=-1: box27_tb2, fp32 in the natural layout with
+    the 2-plane unroll (box27_tb2n) or, -1n here, round 2's pair layout; 1 / 2 / 4: box27_tbk with
+    that many rows per tile) == two naive single steps, bitwise, with the residual of step 2."""
+    knob("MDFX_B27_TBK", kernel.rstrip("n"))
+    knob("MDFX_B27_NAT", "0" if kernel.endswith("n") else "1")
     lay = FieldLayout.make(prob, halo=2)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
