@@ -80,6 +80,7 @@ static Knobs read_knobs() {
   k.j5_nat = env_int("MDFX_J5_NAT", 2);
   k.wtk_res_shape = env_int("MDFX_WTK_RES_SHAPE", 0);
   k.b27_nat = env_int("MDFX_B27_NAT", 1);
+  k.wtk_split = env_int("MDFX_WTK_SPLIT", 0);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;

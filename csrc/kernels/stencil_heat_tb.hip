@@ -263,21 +263,23 @@ bool heat7_tb2_supported(const Geo& g) {
 template bool heat7_tb2_supported<float>(const Geo&);
 template bool heat7_tb2_supported<double>(const Geo&);
 
-// Blocks of kernel `kfn` (256 threads) the whole device holds at once, cached per kernel.
-int64_t resident_blocks(const void* kfn) {
+// Blocks of kernel `kfn` (of `block` threads, default 256) the whole device holds at once, cached
+// per kernel and block size.
+int64_t resident_blocks(const void* kfn, int block) {
   static std::mutex mu;
-  static std::map<std::pair<int, const void*>, int64_t> cache;
+  static std::map<std::pair<int, std::pair<const void*, int>>, int64_t> cache;
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find({dev, kfn});
+  auto it = cache.find({dev, {kfn, block}});
   if (it != cache.end()) return it->second;
   int cus = 0, nb = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 256, 0) != hipSuccess || nb <= 0) nb = 2;
-  if (knobs().debug_zc) fprintf(stderr, "[mdfx] tb2 residency: %d CUs x %d blocks\n", cus, nb);
-  return cache[{dev, kfn}] = (int64_t)cus * nb;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, block, 0) != hipSuccess || nb <= 0) nb = block > 256 ? 1 : 2;
+  if (knobs().debug_zc) fprintf(stderr, "[mdfx] residency: %d CUs x %d blocks of %d threads\n", cus, nb, block);
+  return cache[{dev, {kfn, block}}] = (int64_t)cus * nb;
 }
+int64_t resident_blocks(const void* kfn) { return resident_blocks(kfn, 256); }
 
 // z-chunk of a fused sweep over `planes` planes and `tiles` xy tiles: balanced chunks of about 43
 // planes (equal up to one plane), shortened while the grid would not fill the device once.

@@ -272,6 +272,8 @@ static std::atomic<int> g_min_rounds{1};
 // Every chunk also pays 2K planes of pipeline fill, so a region is never split into chunks shorter
 // than 4K planes: under the 2-round policy of multi-slab runs the K-plane boundary regions were
 // split in two (8 slabs of 1024^2 x 128 at K = 3: 1369 vs 1491 GCells/s, profiles/r02_wtk/README.txt).
+int hip_min_rounds_now() { return g_min_rounds.load(std::memory_order_relaxed); }
+
 int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
   const double per_slot = (double)planes * (double)tiles / (double)resident;
   const int64_t rounds = std::max<int64_t>(g_min_rounds.load(std::memory_order_relaxed),

@@ -25,6 +25,7 @@
 // Region contract (as heat7_tbk): output storage planes [lz_begin, lz_end) need u0 valid on
 // [lz_begin - K, lz_end + K) (the engine keeps K ghost planes per side).
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <type_traits>
@@ -37,8 +38,52 @@
 namespace mdfx {
 namespace dev {
 
-int64_t resident_blocks(const void* kfn);
-int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
+int64_t resident_blocks(const void* kfn, int block);
+int hip_min_rounds_now();
+
+// Schedule of one streaming sweep over `planes` planes of `tiles` tiles on `resident` block slots,
+// every block paying 2K planes of pipeline fill per segment it marches:
+//  chunked: z chunks of zc planes, tiles x chunks blocks, dealt in rounds of `resident`; the chunk
+//           count minimises rounds x (zc + 2K) (chunks of at least 4K planes; at least `min_rounds`
+//           rounds when several slabs leave CUs for exchange kernels). 1024^3 fp32 in 8-wave bands:
+//           7 chunks of 147 planes (5.9 rounds), the measured optimum of round 2's zc sweep, where 6
+//           or 4 chunks (171, 256 planes) end on a nearly empty round.
+//  split:   one round of blocks, block b marching the b-th equal share of the tile-major
+//           (tile, plane) work: no ragged last round, at most two segments (two fills) per block,
+//           but neighbouring y bands no longer march in lockstep, so bands of 8 waves lose their
+//           L2 sharing of the y-halo rows (priced at +6%). Thin slabs: the interior of a 1024^2 x
+//           128 slab at K = 3 (430 tiles, 512 slots) is 128 plane-times chunked (one 84%-full
+//           round), 115 split.
+struct WtkPlan {
+  int zc = 0;
+  bool split = false;
+};
+static WtkPlan wtk_plan(int64_t planes, int64_t tiles, int64_t resident, int K, int WB, int min_rounds, int knob) {
+  WtkPlan p;
+  const int64_t fill = 2 * K;
+  const int64_t zmax = std::max<int64_t>(1, planes / (4 * K));
+  double best = 1e300;
+  int64_t bz = 1;
+  for (int64_t zt = 1; zt <= zmax; ++zt) {
+    const int64_t rounds = (tiles * zt + resident - 1) / resident;
+    if (rounds < min_rounds && zt < zmax) continue;
+    const double t = (double)rounds * (double)((planes + zt - 1) / zt + fill);
+    if (t < best * 0.999) {
+      best = t;
+      bz = zt;
+    }
+  }
+  p.zc = (int)((planes + bz - 1) / bz);
+  const double share = (double)planes * (double)tiles / (double)resident;
+  if (knob == 1) {
+    p.split = true;  // forced (tests: any size, blocks with an empty share included)
+  } else if (knob == 0 && min_rounds <= 1 && tiles * planes > resident) {
+    const double segs = std::ceil(share / (double)planes) + 1.0;
+    const double ts = (share + (double)fill * segs) * (WB == 8 ? 1.06 : 1.0);
+    p.split = ts < best;
+  }
+  return p;
+}
 
 // A block is one task: WB = 4 or 8 waves stacked along y on one x segment (a y band of WB * RY
 // rows). The band's u0 window (WB * RY + 2K rows) streams into a shared double-buffered LDS
@@ -49,7 +94,7 @@ int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
 template <class T, int RY, int K, int WB, bool RES, int MODE>
 __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                  int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
-                                                 int lag) {
+                                                 int lag, int64_t split_w) {
   using V = typename VT<T>::type;
   using RO = typename std::conditional<sizeof(T) == 4 && MODE >= 1, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
@@ -61,12 +106,33 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   constexpr int RB = WB * RY + 2 * K;         // shared window rows of a band
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // block-uniform task; order: x segments fastest, then y bands, then z chunks
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x);
-  if (task >= ntasks) return;  // block-uniform (the grid has exactly ntasks blocks)
-  const int xt = task % XT;
-  const int yz = task / XT;
-  const int yt = yz % YT, zt = yz / YT;
+  // Work: tile t = (x segment, y band) x planes of the region, flattened tile-major (index
+  // t * P + plane). Chunked schedule (split_w == 0): block-uniform task = one z chunk of one tile;
+  // order x segments fastest, then y bands, then z chunks. Balanced schedule (split_w = tiles * P):
+  // the grid is one round of resident blocks and block b takes the equal share
+  // [b * W / B, (b+1) * W / B) of the flattened work, i.e. the tail of one tile's planes and the
+  // head of the next (each segment pays its own 2K-plane pipeline fill), so no round ends ragged.
+  const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int P = (int)(g.lz_end - g.lz_begin);
+  int64_t wlo, whi;
+  if (split_w == 0) {
+    if (b >= ntasks) return;  // block-uniform (the grid has exactly ntasks blocks)
+    const int t = b % (XT * YT), zt = b / (XT * YT);
+    wlo = (int64_t)t * P + (int64_t)zt * zc;
+    whi = (int64_t)t * P + min(P, (zt + 1) * zc);
+  } else {
+    wlo = split_w * b / gridDim.x;
+    whi = split_w * (b + 1) / gridDim.x;
+  }
+  __shared__ V slot[2][RB][64];
+  double acc = 0.0;
+  for (int64_t cur = wlo; cur < whi;) {  // block-uniform segment loop
+  const int tile = (int)(cur / P), z0 = (int)(cur - (int64_t)tile * P);
+  const int z1 = (int)min((int64_t)P, (int64_t)z0 + (whi - cur));
+  if (cur > wlo) lds_barrier();  // a block's next segment reuses the LDS window
+  cur += z1 - z0;
+  const int xt = tile % XT;
+  const int yt = tile / XT;
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
   const int64_t x = xs + (int64_t)lane * N;
   // row / plane indices in 32 bits (extents < 2^31; the launcher checks): fewer SGPRs, so the
@@ -74,8 +140,8 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
   const int yb = yt * RY * WB;  // first row of the band
   const int y0 = yb + w * RY;   // first row of this wave
-  const int zs = (int)g.lz_begin + zt * zc;
-  const int ze = min((int)g.lz_end, zs + zc);
+  const int zs = (int)g.lz_begin + z0;
+  const int ze = (int)g.lz_begin + z1;
   const int64_t pitch = g.pitch, plane = g.plane;
   const bool xin = x >= 0 && x < pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
@@ -98,7 +164,6 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   // lanes outside the row read the nearest valid row / vector (finite values that only meet held
   // or unowned cells). Per lane a 32-bit byte offset from the wave-uniform row start. Wave w
   // fetches rows w, w + WB, ... of the band's window.
-  __shared__ V slot[2][RB][64];
   const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
   auto issue = [&](int lz, int buf) {
     const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
@@ -127,7 +192,6 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   }
   const int qlast = ze - 1 + K;  // last u0 plane of the march
   issue(zs - K, 0);
-  double acc = 0.0;
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
 
@@ -225,7 +289,8 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
     march(std::integral_constant<bool, false>{});
   else
     march(std::integral_constant<bool, true>{});
-  wait_vm0();  // no DMA may outlive the wave
+  wait_vm0();  // no DMA may outlive the wave (or the segment)
+  }  // segments
   if (RES) wave_atomic_add(resid, acc);
 }
 
@@ -236,13 +301,21 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
   const int XT = (int)((g.nx + SEG - 1) / SEG);
   const int YT = (int)((g.ny + RY * WB - 1) / (RY * WB));  // y bands
   const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, NAT>;
-  int zc = knobs().zc;
   const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
-  if (zc <= 0) zc = tbk_zc(planes, tiles, resident_blocks(kfn), K);  // chunks >= 4K planes
-  if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] wtk K=%d RY=%d: %lld planes x %d x %d tasks -> zc %d\n", K, RY, (long long)planes, XT, YT, zc);
+  const int64_t resident = resident_blocks(kfn, 64 * WB);
+  WtkPlan plan = wtk_plan(planes, tiles, resident, K, WB, hip_min_rounds_now(), knobs().wtk_split);
+  if (knobs().zc > 0) {
+    plan.zc = knobs().zc;
+    plan.split = false;
+  }
+  const int zc = plan.zc;
   const int ZT = (int)((planes + zc - 1) / zc);
-  const int64_t ntasks = (int64_t)XT * YT * ZT;
+  const int64_t ntasks = plan.split ? resident : (int64_t)XT * YT * ZT;
+  const int64_t split_w = plan.split ? tiles * planes : 0;
+  if (knobs().debug_zc)
+    fprintf(stderr, "[mdfx] wtk K=%d RY=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> %s\n", K, RY, WB,
+            (long long)planes, XT, YT, (long long)resident,
+            plan.split ? "split" : format("zc %d (%lld blocks)", zc, (long long)ntasks).c_str());
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wtk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   // residual instances exist where they fit 256 VGPRs without spills: every fp64 shape, fp32 in
@@ -250,11 +323,11 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
   constexpr bool kRes = sizeof(T) == 8 || NAT == 1 || RY <= 2;
   if constexpr (!kRes) {
     MDFX_CHECK(!resid, "heat7_wtk: no residual variant of this shape");
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag, split_w);
   } else if (resid) {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag, split_w);
   } else {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag, split_w);
   }
 }
 

@@ -423,17 +423,20 @@ WTK3D = DEEP3D + [models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, n
 
 
 @pytest.mark.parametrize("prob", WTK3D, ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("k,wb", [(3, "4"), (3, "8"), (4, "4")])
-def test_heat7_wtk_bitwise(hip, prob, k, wb, knob):
+@pytest.mark.parametrize("k,wb,split", [(3, "4", "-1"), (3, "8", "-1"), (4, "4", "-1"), (3, "4", "1"), (3, "8", "1")])
+@pytest.mark.parametrize("resid", [False, True])
+def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
     """heat7_wtk's K fused steps (the default 3D 7-point kernel for K >= 3) == K naive single
-    steps, bitwise, with the residual of step K (bands of 4 waves) or without (bands of 8)."""
+    steps, bitwise, with or without the residual of step K, in bands of 4 or 8 waves, under the
+    chunked and the balanced one-round (MDFX_WTK_SPLIT=1) schedules."""
     knob("MDFX_WTK_WB", wb)
+    knob("MDFX_WTK_SPLIT", split)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
     fused = alloc_field(lay, "cuda")
     res = torch.zeros((), dtype=torch.float64, device="cuda")
-    apply_stencil(prob, lay, src, fused, steps=k, resid=res if wb == "4" else None)
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res if resid else None)
     set_kernel_variant("naive")
     try:
         cur = alloc_field(lay, "cuda")
@@ -448,8 +451,8 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, knob):
         set_kernel_variant("auto")
     torch.cuda.synchronize()
     o = lay.owned
-    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb)
-    if wb == "4":
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb, split)
+    if resid:
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
@@ -474,8 +477,9 @@ def test_heat7_wtk_regions_on_a_slab(hip, k):
     assert torch.equal(out[h:h + 18, :, :1024], ref[12 + k:30 + k, :, :1024])
 
 
-@pytest.mark.parametrize("k,ranks", [(3, 1), (3, 3), (4, 2)])
-def test_engine_wtk_temporal_3d(hip, k, ranks):
+@pytest.mark.parametrize("k,ranks,split", [(3, 1, "0"), (3, 3, "0"), (4, 2, "0"), (3, 1, "1"), (3, 3, "1")])
+def test_engine_wtk_temporal_3d(hip, k, ranks, split, knob):
+    knob("MDFX_WTK_SPLIT", split)
     prob = mm.heat3d(nx=1024, ny=24, nz=60)
     ref, rr = _sim(prob, 23, ranks=1, temporal=1, residual_every=10)
     got, rg = _sim(prob, 23, ranks=ranks, temporal=k, residual_every=10)
