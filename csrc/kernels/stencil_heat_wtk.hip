@@ -91,7 +91,7 @@ static WtkPlan wtk_plan(int64_t planes, int64_t tiles, int64_t resident, int K, 
 // -> 18 per 12 / 30 per 24), at one block barrier per plane. (The first version ran every wave as
 // an independent task with a private LDS slot and no barrier: 1.565 fields fetched per sweep
 // against 1.444 / 1.108 for bands of 4 / 8, and slower on every shape, profiles/r02_wtk/README.txt.)
-template <class T, int RY, int K, int WB, bool RES, int MODE>
+template <class T, int RY, int K, int WB, bool RES, int MODE, bool SPLIT>
 __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                  int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
                                                  int lag, int64_t split_w) {
@@ -126,11 +126,8 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   }
   __shared__ V slot[2][RB][64];
   double acc = 0.0;
-  for (int64_t cur = wlo; cur < whi;) {  // block-uniform segment loop
-  const int tile = (int)(cur / P), z0 = (int)(cur - (int64_t)tile * P);
-  const int z1 = (int)min((int64_t)P, (int64_t)z0 + (whi - cur));
-  if (cur > wlo) lds_barrier();  // a block's next segment reuses the LDS window
-  cur += z1 - z0;
+  // one segment: planes [z0, z1) of the region for tile `tile`
+  auto segment = [&](const int tile, const int z0, const int z1) __attribute__((always_inline)) {
   const int xt = tile % XT;
   const int yt = tile / XT;
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
@@ -290,8 +287,36 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   else
     march(std::integral_constant<bool, true>{});
   wait_vm0();  // no DMA may outlive the wave (or the segment)
-  }  // segments
+  };
+  if constexpr (SPLIT) {
+    for (int64_t cur = wlo; cur < whi;) {  // block-uniform segment loop
+      const int tile = (int)(cur / P), z0 = (int)(cur - (int64_t)tile * P);
+      const int z1 = (int)min((int64_t)P, (int64_t)z0 + (whi - cur));
+      if (cur > wlo) lds_barrier();  // a block's next segment reuses the LDS window
+      cur += z1 - z0;
+      segment(tile, z0, z1);
+    }
+  } else {
+    const int tile = (int)(wlo / P), z0 = (int)(wlo - (int64_t)tile * P);
+    segment(tile, z0, z0 + (int)(whi - wlo));
+  }
   if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T, int RY, int K, int WB, bool RES, int NAT>
+static void launch_split(bool split, dim3 grd, dim3 blk, hipStream_t s, const T* in, T* out, const Geo& g, T r, int zc,
+                         int XT, int YT, int ntasks, double* resid, int64_t split_w) {
+  // the segment loop's scalar state does not fit beside the 2-plane unroll (SGPR spills, scratch):
+  // split sweeps run the natural layout without the unroll (mode 1)
+  // (fp32 always mode 1; fp64 3-row 8-wave bands have no split instance: they need scratch for it)
+  constexpr int NS = sizeof(T) == 4 ? 1 : NAT;
+  constexpr bool kSplit = !(sizeof(T) == 8 && RY == 3 && WB == 8);
+  if (kSplit && split)
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, RES, NS, kSplit>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, ntasks,
+                       resid, knobs().vm_lag, split_w);
+  else
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, RES, NAT, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, ntasks, resid,
+                       knobs().vm_lag, split_w);
 }
 
 template <class T, int RY, int K, int WB, int NAT>
@@ -300,12 +325,12 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
   const int YT = (int)((g.ny + RY * WB - 1) / (RY * WB));  // y bands
-  const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, NAT>;
+  const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, NAT, false>;
   const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
   const int64_t resident = resident_blocks(kfn, 64 * WB);
   WtkPlan plan = wtk_plan(planes, tiles, resident, K, WB, hip_min_rounds_now(), knobs().wtk_split);
-  if (knobs().zc > 0) {
-    plan.zc = knobs().zc;
+  if (knobs().zc > 0 || (sizeof(T) == 8 && RY == 3 && WB == 8)) {  // (no split instance of that shape)
+    if (knobs().zc > 0) plan.zc = knobs().zc;
     plan.split = false;
   }
   const int zc = plan.zc;
@@ -323,11 +348,11 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
   constexpr bool kRes = sizeof(T) == 8 || NAT == 1 || RY <= 2;
   if constexpr (!kRes) {
     MDFX_CHECK(!resid, "heat7_wtk: no residual variant of this shape");
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag, split_w);
+    launch_split<T, RY, K, WB, false, NAT>(plan.split, grd, blk, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, split_w);
   } else if (resid) {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag, split_w);
+    launch_split<T, RY, K, WB, true, NAT>(plan.split, grd, blk, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, split_w);
   } else {
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, NAT>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, knobs().vm_lag, split_w);
+    launch_split<T, RY, K, WB, false, NAT>(plan.split, grd, blk, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, split_w);
   }
 }
 

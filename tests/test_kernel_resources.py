@@ -49,11 +49,13 @@ def test_lds_never_limits_occupancy(recs):
 
 
 @pytest.mark.parametrize("name,min_waves", [
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 2>", 2),              # headline K = 3 sweep (8-wave bands)
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 2>", 2),              # thin slabs (4-wave bands)
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 1>", 2),              # natural layout, no unroll
-    ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0>", 2),
-    ("mdfx::dev::heat7_wtk<float, 2, 3, 4, true, 2>", 2),               # residual sweeps
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 2, false>", 2),       # headline K = 3 sweep (8-wave bands)
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 2, false>", 2),       # thin slabs (4-wave bands)
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 1, false>", 2),       # natural layout, no unroll
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 1, true>", 2),        # balanced one-round schedule
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 1, true>", 2),
+    ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0, false>", 2),
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, true, 1, false>", 2),        # residual sweeps
     ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 2>", 3),           # 2D MDF, 8 steps per sweep
     ("mdfx::dev::jacobi5_tbk<float, 8, false, true, 2>", 2),            # reference precision
     ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 1>", 4),
