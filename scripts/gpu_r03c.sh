@@ -21,7 +21,8 @@ steps+=("proxy8_nosplit=MDFX_WTK_SPLIT=-1 python bench.py --rank-proxy 8 --steps
         "proxy4_nosplit=MDFX_WTK_SPLIT=-1 python bench.py --rank-proxy 4 --steps 48 --warmup 12"
         "v8=$B --virtual-ranks 8" "v8_nosplit=MDFX_WTK_SPLIT=-1 $B --virtual-ranks 8")
 steps+=("proxy8_r0=python bench.py --rank-proxy 8 --proxy-rank 0 --steps 48 --warmup 12"
-        "slab128=python bench.py --nz 128 --steps 48 --warmup 12" "h1024_b=$B")
+        "slab128=python bench.py --nz 128 --steps 48 --warmup 12" "h1024_b=$B"
+        "h512_k2=$B --n 512" "h512_k3=$B --n 512 --temporal 3")
 LIMIT=400 scripts/gpu_session.sh "${steps[@]}" || exit $?
 PMC_TAG=h1024 scripts/gpu_session.sh pmc_fetch pmc_write || exit $?
 PMC_TAG=proxy8 BENCH_ARGS="--rank-proxy 8" scripts/gpu_session.sh pmc_fetch pmc_write || exit $?
