@@ -28,6 +28,15 @@ using cpu_base::pl_of;
 static void cpu_region(const StencilSpec& spec, const RegionArgs& a);
 
 void cpu_stencil(const StencilSpec& spec, const RegionArgs& a) {
+  if (a.lz2_end > a.lz2_begin) {  // two regions: one after the other
+    RegionArgs r1 = a, r2 = a;
+    r1.lz2_begin = r1.lz2_end = r2.lz2_begin = r2.lz2_end = 0;
+    r2.lz_begin = a.lz2_begin;
+    r2.lz_end = a.lz2_end;
+    cpu_stencil(spec, r1);
+    cpu_stencil(spec, r2);
+    return;
+  }
   if (a.lz_end <= a.lz_begin) return;
   MDFX_CHECK(a.lz_begin >= a.lay.halo && a.lz_end <= a.lay.halo + a.lay.nzl(),
              "region must lie inside the owned planes");

@@ -279,12 +279,19 @@ void Solver::step(bool want_resid, int k) {
     s.be->wait(s.hs, s.ev_int);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)s.hs));
     a.resid = want_resid ? s.resid : nullptr;
-    if (s.lo_e > s.lo_b) {
+    if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
+      // both boundary regions in one call (one launch where the kernel supports it)
+      a.lz_begin = s.lo_b;
+      a.lz_end = s.lo_e;
+      a.lz2_begin = s.hi_b;
+      a.lz2_end = s.hi_e;
+      s.be->stencil(spec_, a, s.hs);
+      a.lz2_begin = a.lz2_end = 0;
+    } else if (s.lo_e > s.lo_b) {
       a.lz_begin = s.lo_b;
       a.lz_end = s.lo_e;
       s.be->stencil(spec_, a, s.hs);
-    }
-    if (s.hi_e > s.hi_b) {
+    } else if (s.hi_e > s.hi_b) {
       a.lz_begin = s.hi_b;
       a.lz_end = s.hi_e;
       s.be->stencil(spec_, a, s.hs);

@@ -23,6 +23,9 @@ struct RegionArgs {
   void* out = nullptr;
   FieldLayout lay;
   int64_t lz_begin = 0, lz_end = 0;  // storage planes to write
+  // optional second region written by the same call (the engine passes both K-plane boundary
+  // regions of a slab at once; heat7_wtk runs them as one launch, other kernels as two)
+  int64_t lz2_begin = 0, lz2_end = 0;
   double* resid = nullptr;           // optional accumulator of sum((out-in)^2) over the region
   // Time steps fused into this sweep (temporal blocking). 2 needs lay.halo >= 2 and reads
   // in[lz_begin-2, lz_end+2); the residual then covers the second step only.

@@ -81,6 +81,7 @@ static Knobs read_knobs() {
   k.wtk_res_shape = env_int("MDFX_WTK_RES_SHAPE", 0);
   k.b27_nat = env_int("MDFX_B27_NAT", 1);
   k.wtk_split = env_int("MDFX_WTK_SPLIT", 0);
+  k.fuse_regions = env_int("MDFX_FUSE_REGIONS", 1);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
@@ -273,10 +274,29 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
 }
 
 void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
+  if (a.lz2_end > a.lz2_begin) {
+    // two regions in one call: heat7_wtk sweeps them in ONE launch (both boundary regions of a
+    // slab: one fill of the device, one launch gap); every other kernel runs them one after the other
+    const bool fuse = a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps) && a.lz_end > a.lz_begin &&
+                      dev::knobs().fuse_regions;
+    if (!fuse) {
+      RegionArgs r1 = a, r2 = a;
+      r1.lz2_begin = r1.lz2_end = r2.lz2_begin = r2.lz2_end = 0;
+      r2.lz_begin = a.lz2_begin;
+      r2.lz_end = a.lz2_end;
+      hip_stencil(spec, r1, stream);
+      hip_stencil(spec, r2, stream);
+      return;
+    }
+    MDFX_CHECK(a.lz2_begin >= a.lay.halo && a.lz2_end <= a.lay.halo + a.lay.nzl() && a.lz2_begin >= a.lz_end,
+               "second region must lie inside the owned planes, after the first");
+  }
   if (a.lz_end <= a.lz_begin) return;
   MDFX_CHECK(a.lz_begin >= a.lay.halo && a.lz_end <= a.lay.halo + a.lay.nzl(),
              "region must lie inside the owned planes");
-  const dev::Geo g = dev::make_geo(a.lay, a.lz_begin, a.lz_end);
+  dev::Geo g = dev::make_geo(a.lay, a.lz_begin, a.lz_end);
+  g.lz2_begin = a.lz2_begin;
+  g.lz2_end = a.lz2_end;
   hipStream_t s = (hipStream_t)stream;
   if (a.steps != 1) {
     MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),

@@ -33,6 +33,7 @@ struct Geo {
   int64_t lz_end;    // one past the last storage plane to write
   int64_t gz_off;    // global z = lz + gz_off
   int64_t lz_max;    // storage planes allocated (loads outside [0,lz_max) return 0)
+  int64_t lz2_begin = 0, lz2_end = 0;  // optional second region of the same launch (heat7_wtk)
   int64_t alloc = 0;                 // elements allocated (planes + slack), for device checks
   unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };
@@ -214,6 +215,7 @@ struct Knobs {
   int wtk_ry8 = 0;     // MDFX_WTK_RY8: fp64 rows per wave in 8-wave bands (2 / 3; 0: 3 up to 1024-cell rows, else 2)
   int wtk_nat = 2;     // MDFX_WTK_NAT: heat7_wtk fp32 rows: 2 natural pair layout + 2-plane unroll, 1 natural, 0 round 2's
   int wtk_res_shape = 0;  // MDFX_WTK_RES_SHAPE: 1 = residual sweeps in round 2's 2-row 4-wave bands
+  int fuse_regions = 1;  // MDFX_FUSE_REGIONS: both boundary regions of a slab in one heat7_wtk launch (0: two)
   int wtk_split = 0;   // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: 0 auto (cost model), 1 always, -1 never
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)

@@ -112,22 +112,21 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   // the grid is one round of resident blocks and block b takes the equal share
   // [b * W / B, (b+1) * W / B) of the flattened work, i.e. the tail of one tile's planes and the
   // head of the next (each segment pays its own 2K-plane pipeline fill), so no round ends ragged.
+  // A second region (g.lz2_*: the other boundary region of a slab) adds its own z chunks after the
+  // first region's, chunked schedule only.
   const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   const int P = (int)(g.lz_end - g.lz_begin);
-  int64_t wlo, whi;
-  if (split_w == 0) {
-    if (b >= ntasks) return;  // block-uniform (the grid has exactly ntasks blocks)
-    const int t = b % (XT * YT), zt = b / (XT * YT);
-    wlo = (int64_t)t * P + (int64_t)zt * zc;
-    whi = (int64_t)t * P + min(P, (zt + 1) * zc);
-  } else {
+  int64_t wlo = 0, whi = 0;
+  if constexpr (SPLIT) {
     wlo = split_w * b / gridDim.x;
     whi = split_w * (b + 1) / gridDim.x;
+  } else {
+    if (b >= ntasks) return;  // block-uniform (the grid has exactly ntasks blocks)
   }
   __shared__ V slot[2][RB][64];
   double acc = 0.0;
-  // one segment: planes [z0, z1) of the region for tile `tile`
-  auto segment = [&](const int tile, const int z0, const int z1) __attribute__((always_inline)) {
+  // one segment: storage planes [zs, ze) for tile `tile`
+  auto segment = [&](const int tile, const int zs, const int ze) __attribute__((always_inline)) {
   const int xt = tile % XT;
   const int yt = tile / XT;
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
@@ -137,8 +136,6 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
   const int yb = yt * RY * WB;  // first row of the band
   const int y0 = yb + w * RY;   // first row of this wave
-  const int zs = (int)g.lz_begin + z0;
-  const int ze = (int)g.lz_begin + z1;
   const int64_t pitch = g.pitch, plane = g.plane;
   const bool xin = x >= 0 && x < pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
@@ -294,11 +291,18 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
       const int z1 = (int)min((int64_t)P, (int64_t)z0 + (whi - cur));
       if (cur > wlo) lds_barrier();  // a block's next segment reuses the LDS window
       cur += z1 - z0;
-      segment(tile, z0, z1);
+      segment(tile, (int)g.lz_begin + z0, (int)g.lz_begin + z1);
     }
   } else {
-    const int tile = (int)(wlo / P), z0 = (int)(wlo - (int64_t)tile * P);
-    segment(tile, z0, z0 + (int)(whi - wlo));
+    const int t = b % (XT * YT), zt = b / (XT * YT);
+    const int zt1 = (P + zc - 1) / zc;  // chunks of the first region
+    if (zt < zt1) {
+      const int zs = (int)g.lz_begin + zt * zc;
+      segment(t, zs, min((int)g.lz_end, zs + zc));
+    } else {
+      const int zs = (int)g.lz2_begin + (zt - zt1) * zc;
+      segment(t, zs, min((int)g.lz2_end, zs + zc));
+    }
   }
   if (RES) wave_atomic_add(resid, acc);
 }
@@ -333,8 +337,13 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
     if (knobs().zc > 0) plan.zc = knobs().zc;
     plan.split = false;
   }
+  const int64_t planes2 = g.lz2_end - g.lz2_begin;  // a second region (boundary pair): chunked
+  if (planes2 > 0) {
+    plan.split = false;
+    plan.zc = (int)std::max(planes, planes2);
+  }
   const int zc = plan.zc;
-  const int ZT = (int)((planes + zc - 1) / zc);
+  const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = plan.split ? resident : (int64_t)XT * YT * ZT;
   const int64_t split_w = plan.split ? tiles * planes : 0;
   if (knobs().debug_zc)
@@ -395,6 +404,8 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
   MDFX_CHECK((steps == 3 || steps == 4) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_wtk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
+  MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
+             "heat7_wtk: the second region must follow the first and have its planes + ghosts allocated");
   MDFX_CHECK(g.pitch % VT<T>::N == 0, "heat7_wtk: the row pitch must be a whole number of vectors");
   MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),

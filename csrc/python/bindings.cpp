@@ -300,8 +300,10 @@ PYBIND11_MODULE(_mdfx, m) {
       [](const std::string& kind, const std::string& dtype, uintptr_t in, uintptr_t out, int64_t nx,
          int64_t ny, int64_t nz, int64_t z0, int64_t z1, int halo, int64_t lz_begin, int64_t lz_end,
          int device, uintptr_t stream, uintptr_t resid, double r, double c0, double c1, double c2,
-         double c3, int steps, bool ref_precision) {
+         double c3, int steps, bool ref_precision, int64_t lz2_begin, int64_t lz2_end) {
         RegionArgs a;
+        a.lz2_begin = lz2_begin;
+        a.lz2_end = lz2_end;
         a.in = (const void*)in;
         a.out = (void*)out;
         a.lay = FieldLayout::make(Extent3{nx, ny, nz}, z0, z1, halo, dtype_from_name(dtype));
@@ -319,7 +321,8 @@ PYBIND11_MODULE(_mdfx, m) {
       py::arg("ny"), py::arg("nz"), py::arg("z0"), py::arg("z1"), py::arg("halo"),
       py::arg("lz_begin"), py::arg("lz_end"), py::arg("device"), py::arg("stream") = 0,
       py::arg("resid_ptr") = 0, py::arg("r") = -1.0, py::arg("c0") = 0.25, py::arg("c1") = 0.05,
-      py::arg("c2") = 0.025, py::arg("c3") = 3.0 / 160.0, py::arg("steps") = 1, py::arg("ref_precision") = false);
+      py::arg("c2") = 0.025, py::arg("c3") = 3.0 / 160.0, py::arg("steps") = 1, py::arg("ref_precision") = false,
+      py::arg("lz2_begin") = 0, py::arg("lz2_end") = 0);
   m.def(
       "init_field",
       [](const std::string& kind, const std::string& dtype, uintptr_t buf, int64_t nx, int64_t ny,

@@ -82,13 +82,15 @@ def init_field(problem: Problem, layout: FieldLayout, t: torch.Tensor, init=None
 
 def apply_stencil(problem: Problem, layout: FieldLayout, src: torch.Tensor, dst: torch.Tensor,
                   lz_begin: Optional[int] = None, lz_end: Optional[int] = None,
-                  resid: Optional[torch.Tensor] = None, steps: int = 1) -> None:
+                  resid: Optional[torch.Tensor] = None, steps: int = 1,
+                  second: Optional[tuple] = None) -> None:
     """One update of storage planes [lz_begin, lz_end) (default: all owned planes) src -> dst.
 
     ``resid`` (float64 scalar tensor on the same device), when given, accumulates
     sum((dst - src)^2) over the region. ``steps`` > 1 fuses that many time steps into one sweep
     (temporal blocking; needs ``layout.halo >= steps`` and valid ghosts that deep); the residual
-    then covers the last step.
+    then covers the last step. ``second`` = (lz_begin, lz_end) of a second region updated by the
+    same call (the engine's pair of boundary regions; one launch for the fused 3D 7-point sweep).
     """
     _check(src, layout)
     _check(dst, layout)
@@ -107,7 +109,8 @@ def apply_stencil(problem: Problem, layout: FieldLayout, src: torch.Tensor, dst:
     stream = torch.cuda.current_stream(src.device).cuda_stream if dev >= 0 else 0
     native().stencil(problem.kind, layout.dtype, src.data_ptr(), dst.data_ptr(), layout.nx, layout.ny,
                      layout.nz, layout.z0, layout.z1, layout.halo, lb, le, dev, stream, rp,
-                     steps=steps, **problem.coef_kwargs())
+                     steps=steps, lz2_begin=second[0] if second else 0, lz2_end=second[1] if second else 0,
+                     **problem.coef_kwargs())
 
 
 def dense_to_field(problem: Problem, dense: torch.Tensor, layout: FieldLayout, t: torch.Tensor):

@@ -475,6 +475,18 @@ def test_heat7_wtk_regions_on_a_slab(hip, k):
     apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k)
     torch.cuda.synchronize()
     assert torch.equal(out[h:h + 18, :, :1024], ref[12 + k:30 + k, :, :1024])
+    # both boundary regions in ONE call (one heat7_wtk launch), with their residual
+    out2 = alloc_field(lay, "cuda")
+    res2 = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, out2, h, h + k, steps=k, second=(h + 18 - k, h + 18), resid=res2)
+    res1 = torch.zeros((), dtype=torch.float64, device="cuda")
+    out3 = alloc_field(lay, "cuda")
+    apply_stencil(prob, lay, src, out3, h, h + k, steps=k, resid=res1)
+    apply_stencil(prob, lay, src, out3, h + 18 - k, h + 18, steps=k, resid=res1)
+    torch.cuda.synchronize()
+    for lo, hi in ((h, h + k), (h + 18 - k, h + 18)):
+        assert torch.equal(out2[lo:hi, :, :1024], out[lo:hi, :, :1024])
+    assert res2.item() > 0 and abs(res2.item() - res1.item()) <= 1e-9 * res1.item()
 
 
 @pytest.mark.parametrize("k,ranks,split", [(3, 1, "0"), (3, 3, "0"), (4, 2, "0"), (3, 1, "1"), (3, 3, "1")])
