@@ -19,6 +19,7 @@ steps+=("h1024_a=$B" "h1024_drv=python bench.py --steps 20 --warmup 5")
 for n in 2 4 8; do steps+=("proxy$n=python bench.py --rank-proxy $n --steps 48 --warmup 12"); done
 steps+=("proxy8_nosplit=MDFX_WTK_SPLIT=-1 python bench.py --rank-proxy 8 --steps 48 --warmup 12"
         "proxy4_nosplit=MDFX_WTK_SPLIT=-1 python bench.py --rank-proxy 4 --steps 48 --warmup 12"
+        "proxy8_nofuse=MDFX_FUSE_REGIONS=0 python bench.py --rank-proxy 8 --steps 48 --warmup 12"
         "v8=$B --virtual-ranks 8" "v8_nosplit=MDFX_WTK_SPLIT=-1 $B --virtual-ranks 8")
 steps+=("proxy8_r0=python bench.py --rank-proxy 8 --proxy-rank 0 --steps 48 --warmup 12"
         "slab128=python bench.py --nz 128 --steps 48 --warmup 12" "h1024_b=$B"
