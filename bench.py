@@ -72,8 +72,9 @@ def parse(argv=None):
     p.add_argument("--rounds", default="auto", choices=["auto", "1", "2"],
                    help="minimum rounds of resident blocks per fused sweep; auto = 1 on one GPU, timed "
                         "trial of 1 and 2 with several ranks (2 leaves CUs for exchange kernels mid-sweep)")
-    p.add_argument("--trial-steps", type=int, default=16,
-                   help="steps of each short timed trial that picks transport / graph mode (auto)")
+    p.add_argument("--trial-steps", type=int, default=48,
+                   help="steps of each short timed trial that picks transport / graph mode / rounds / "
+                        "overlap (auto); every candidate is timed twice, interleaved, and its faster run counts")
     p.add_argument("--temporal", type=int, default=0,
                    help="time steps fused per memory sweep (temporal blocking); 0 = auto: 3 for the 3D "
                         "7-point at 1024-cell rows, else 2 for the 3D stencils, 8 (2D MDF) / 12 (Life) "
@@ -292,14 +293,18 @@ def run_proxy(a):
     cands = [(g, rr, ov) for g in graphs for rr in rounds for ov in overlaps]
     chosen = cands[0]
     if len(cands) > 1:
-        n_trial = max(2, min(a.trial_steps, a.steps))
+        n_trial = max(2, a.trial_steps)
+        best_t = {}
+        for _pass in range(2):
+            for c in cands:
+                g, rr, ov = c
+                sim.set_options(graph=g, min_rounds=rr, overlap=ov)
+                sim.init()
+                sim.prepare_graphs()
+                sim.run(max(2, min(a.warmup, 6)))
+                best_t[c] = min(best_t.get(c, 1e30), timed(n_trial) / n_trial * 1e3)
         for g, rr, ov in cands:
-            sim.set_options(graph=g, min_rounds=rr, overlap=ov)
-            sim.init()
-            sim.prepare_graphs()
-            sim.run(max(2, min(a.warmup, 4)))
-            dt = timed(n_trial)
-            trials.append({"graph": g, "min_rounds": rr, "overlap": ov, "ms_per_step": round(dt / n_trial * 1e3, 4)})
+            trials.append({"graph": g, "min_rounds": rr, "overlap": ov, "ms_per_step": round(best_t[(g, rr, ov)], 4)})
         chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
     sim.set_options(graph=chosen[0], min_rounds=chosen[1], overlap=chosen[2])
     sim.init()
@@ -477,21 +482,28 @@ def main(argv=None):
     trials = []
     sim, sim_t = None, None
     if len(cands) > 1:
-        n_trial = max(2, min(a.trial_steps, a.steps))
+        # two interleaved passes over the candidates (sorted by transport, so each transport's engine
+        # is built once per pass); a candidate's faster pass counts
+        n_trial = max(2, a.trial_steps)
+        best_t = {}
+        for _pass in range(2):
+            for t, g, rr, ov in cands:
+                if sim is not None and sim_t != t:
+                    sim.close()
+                    sim = None
+                if sim is None:
+                    sim, sim_t = make_sim(t, g, rr, ov), t
+                    sim.init()
+                sim.set_options(graph=g, min_rounds=rr, overlap=ov)
+                sim.prepare_graphs()  # capture before timing (no-op with graphs off)
+                sim.run(max(2, min(a.warmup, 6)))
+                dt = timed(sim, n_trial)
+                trace("trial %s graph=%s rounds=%s overlap=%s: %.3f ms/step" % (t, g, rr, ov, dt / n_trial * 1e3))
+                key = (t, g, rr, ov)
+                best_t[key] = min(best_t.get(key, 1e30), dt / n_trial * 1e3)
         for t, g, rr, ov in cands:
-            if sim is not None and sim_t != t:
-                sim.close()
-                sim = None
-            if sim is None:
-                sim, sim_t = make_sim(t, g, rr, ov), t
-                sim.init()
-            sim.set_options(graph=g, min_rounds=rr, overlap=ov)
-            sim.prepare_graphs()  # capture before timing (no-op with graphs off)
-            sim.run(max(2, min(a.warmup, 4)))
-            dt = timed(sim, n_trial)
-            trace("trial %s graph=%s rounds=%s overlap=%s: %.3f ms/step" % (t, g, rr, ov, dt / n_trial * 1e3))
-            trials.append({"transport": sim.transport, "graph": g, "min_rounds": rr, "overlap": ov,
-                           "ms_per_step": round(dt / n_trial * 1e3, 4)})
+            trials.append({"transport": t, "graph": g, "min_rounds": rr, "overlap": ov,
+                           "ms_per_step": round(best_t[(t, g, rr, ov)], 4)})
         chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
         if sim_t != chosen[0]:
             sim.close()

@@ -80,8 +80,8 @@ static Knobs read_knobs() {
   k.j5_nat = env_int("MDFX_J5_NAT", 2);
   k.wtk_res_shape = env_int("MDFX_WTK_RES_SHAPE", 0);
   k.b27_nat = env_int("MDFX_B27_NAT", 1);
-  k.wtk_split = env_int("MDFX_WTK_SPLIT", 0);
-  k.fuse_regions = env_int("MDFX_FUSE_REGIONS", 1);
+  k.wtk_split = env_int("MDFX_WTK_SPLIT", -1);
+  k.fuse_regions = env_int("MDFX_FUSE_REGIONS", 0);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
@@ -262,11 +262,11 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
     case StencilKind::Life: return 12;
     case StencilKind::Box27: return 2;
     case StencilKind::Heat7:
-      // K = 3 through heat7_wtk wherever its x segments cover the row well (>= 79% of the lane
-      // cells): 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2, 2048^3 fp32 1666 vs 1136,
-      // 1024^3 fp64 823-825 vs 546, 2048^3 fp64 818 vs 556; at 512^3 fp32 (3 segments of 256 for
-      // 512 cells) K = 2 stays
-      if (dev::knobs().h7_wtk >= 0 && nx > 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.79)
+      // K = 3 through heat7_wtk wherever its x segments cover at least 2/3 of the lane cells:
+      // 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2 (round 2), 2048^3 fp32 1666 vs 1136,
+      // 1024^3 fp64 823-825 vs 546, 2048^3 fp64 818 vs 556; since the natural-layout rows also
+      // 512^3 fp32 (3 segments of 256 for 512 cells): 1311 vs 1230 (profiles/r03_wtk/)
+      if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
         return 3;
       return 2;
   }

@@ -215,8 +215,8 @@ struct Knobs {
   int wtk_ry8 = 0;     // MDFX_WTK_RY8: fp64 rows per wave in 8-wave bands (2 / 3; 0: 3 up to 1024-cell rows, else 2)
   int wtk_nat = 2;     // MDFX_WTK_NAT: heat7_wtk fp32 rows: 2 natural pair layout + 2-plane unroll, 1 natural, 0 round 2's
   int wtk_res_shape = 0;  // MDFX_WTK_RES_SHAPE: 1 = residual sweeps in round 2's 2-row 4-wave bands
-  int fuse_regions = 1;  // MDFX_FUSE_REGIONS: both boundary regions of a slab in one heat7_wtk launch (0: two)
-  int wtk_split = 0;   // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: 0 auto (cost model), 1 always, -1 never
+  int fuse_regions = 0;  // MDFX_FUSE_REGIONS: 1 = both boundary regions of a slab in one heat7_wtk launch (measured slower)
+  int wtk_split = -1;  // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: -1 never (default, measured slower), 0 cost model, 1 always
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)
   int j5_nat = 2;      // MDFX_J5_NAT: jacobi5_tbk fp32 rows: 2 natural layout + 2-row unroll, 1 natural, 0 round 2's pair layout

@@ -624,8 +624,14 @@ static void launch_jacobi5_tbk_km(const Geo& g, const T* in, T* out, T r, double
 template <class T, int K, bool REF>
 static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if constexpr (sizeof(T) == 4) {
-    if (knobs().j5_nat == 2) {
+    // the reference-precision instance keeps 4 waves per SIMD without the unroll (16384^2 K = 8:
+    // 3346-3368 GCells/s vs 3131-3145 unrolled at 2 waves per SIMD; plain fp32 ties, 4147-4212)
+    if (knobs().j5_nat == 2 && !REF) {
       launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
+      return;
+    }
+    if (knobs().j5_nat == 2 && REF) {
+      launch_jacobi5_tbk_km<T, K, REF, 1>(g, in, out, r, resid, s);
       return;
     }
     if (knobs().j5_nat == 1) {

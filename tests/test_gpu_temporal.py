@@ -188,7 +188,8 @@ def test_engine_temporal2_box27(hip, dtype):
 DEEP = [models.mdf2d(h=45, w=1000), models.mdf2d(h=33, w=300, dtype="f64"), models.life2d(h=50, w=3000),
         models.life2d(h=19, w=100),
         # the reference's mixed fp32 / fp64 evaluation (MDF_kernel.cu:20, jacobi5_tbk REF)
-        models.mdf2d(h=45, w=1000, ref_precision=True), models.mdf2d(h=23, w=130, ref_precision=True)]
+        models.mdf2d(h=45, w=1000, ref_precision=True).with_init(kind="random", seed=5, lo=-50.0, hi=150.0),
+        models.mdf2d(h=23, w=130, ref_precision=True)]
 
 
 @pytest.mark.parametrize("prob", DEEP, ids=lambda p: p.describe().replace(" ", "_"))
@@ -228,7 +229,7 @@ def test_fused_ref_precision_is_the_reference_arithmetic(hip):
     it differs from the pure-fp32 sweep in some cells, and equals the naive ref-precision steps."""
     out = {}
     for ref in (False, True):
-        prob = models.mdf2d(h=64, w=1000, ref_precision=ref)
+        prob = models.mdf2d(h=64, w=1000, ref_precision=ref).with_init(kind="random", seed=3, lo=-50.0, hi=150.0)
         lay = FieldLayout.make(prob, halo=8)
         src = alloc_field(lay, "cuda")
         init_field(prob, lay, src)
