@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <stdexcept>
+#include <cmath>
 #include <string>
 
 namespace mdfx {
@@ -61,7 +62,7 @@ struct StencilCoef {
   double c0 = 0.25, c1 = 1.0 / 20.0, c2 = 1.0 / 40.0, c3 = 3.0 / 160.0;
   // 2D MDF only: evaluate the update exactly as the reference does (sm::jacobi5_ref: fp32 sum and
   // -4u, fp64 scale and add, one more rounding at the store) instead of wholly in the field type.
-  // Single-step sweeps only (no fused kernel implements it).
+  // See StencilSpec::mixed_update() for when the two can differ at all.
   bool ref_precision = false;
 };
 
@@ -72,6 +73,22 @@ struct StencilSpec {
   double rate() const {  // effective r for 5/7-pt
     if (coef.r >= 0) return coef.r;
     return kind == StencilKind::Jacobi5 ? 0.25 : 1.0 / 6.0;
+  }
+  // Whether ref_precision can change a single bit of the result. The reference evaluates
+  // round_f32(round_f64(r*t + u)) with t = fma_f32(-4, u, s); the field-type update is fma_f32(r, t, u)
+  // = round_f32(r*t + u), one rounding of the exact value. When r is a power of two, r*t is exact
+  // with 24 significant bits, so r*t + u is exact in fp64 unless the two exponents are more than 28
+  // apart; then the smaller term is under 2^-28 of the larger, both the exact and the fp64-rounded
+  // sum lie strictly inside the larger term's half-ulp interval, and both round to it. So with a
+  // power-of-two r (the reference's 0.25) the two evaluations are bitwise identical for every input
+  // (subnormals included: fp64 holds every fp32 subnormal product exactly), and the fused field-type
+  // kernels serve ref_precision. An fp64 field evaluates the reference's update in one fp64 fma
+  // either way. Only fp32 with another r needs the mixed kernels (tests/test_cpu_engine.py).
+  bool mixed_update() const {
+    if (!coef.ref_precision || kind != StencilKind::Jacobi5 || dtype != DType::F32) return false;
+    int e = 0;
+    const float r = (float)rate();
+    return !(r > 0.0f && std::frexp(r, &e) == 0.5f);
   }
 };
 

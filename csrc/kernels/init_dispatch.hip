@@ -313,13 +313,15 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       else
         dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
     } else if (spec.kind == StencilKind::Jacobi5) {
-      if (a.steps > 2 || dev::knobs().j5_tbk || spec.coef.ref_precision) {
+      // ref_precision takes the mixed kernels only where it can change a bit (mixed_update())
+      const bool mixed = spec.mixed_update();
+      if (a.steps > 2 || dev::knobs().j5_tbk || mixed) {
         if (spec.dtype == DType::F32)
           dev::launch_jacobi5_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s,
-                                         spec.coef.ref_precision);
+                                         mixed);
         else
           dev::launch_jacobi5_tbk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s,
-                                          spec.coef.ref_precision);
+                                          false);
       } else if (spec.dtype == DType::F32) {
         dev::launch_jacobi5_tb2<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s);
       } else {
@@ -364,10 +366,9 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       case StencilKind::Jacobi5:
         if (spec.dtype == DType::F32)
           dev::launch_jacobi5<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.resid, s,
-                                     spec.coef.ref_precision);
+                                     spec.mixed_update());
         else
-          dev::launch_jacobi5<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s,
-                                      spec.coef.ref_precision);
+          dev::launch_jacobi5<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s, false);
         break;
       case StencilKind::Box27:
         if (spec.dtype == DType::F32)

@@ -42,9 +42,11 @@ for s in "$@"; do
     bench_ipc4) run 300 bench_ipc4 python bench.py --gpus 4 --share-gpu --transport ipc ;;
     bench_refuse) run 120 bench_refuse bash -c 'python bench.py --gpus 2 --n 256; test $? -eq 2' ;;  # must refuse
     rccl2) run 150 rccl2 python bench.py --gpus 2 --share-gpu --transport rccl --n 256 --steps 4 --warmup 2 ;;
-    prof) (cd /tmp && export TMPDIR=/tmp && run_dir="$R" && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
-            --output-format csv -d "$R/gpurun_out/prof" -o bench -- python "$R/bench.py" --steps 20 --warmup 5 \
-            > "$R/gpurun_out/prof.log" 2>&1); rc=$?; echo "== prof rc=$rc"; [[ $rc -le 1 ]] || exit $rc ;;
+    prof)  # kernel trace + stats of one bench run (PROF_TAG names it, BENCH_ARGS replaces the bench flags)
+      out="prof${PROF_TAG:+_$PROF_TAG}"
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "$R/gpurun_out/$out" -o bench -- python3 "$R/bench.py" ${BENCH_ARGS:---steps 20 --warmup 5} \
+          > "$R/gpurun_out/$out.log" 2>&1); rc=$?; echo "== $out rc=$rc"; tail -2 "gpurun_out/$out.log"; [[ $rc -le 1 ]] || exit $rc ;;
     pmc_fetch|pmc_write)  # one counter per pass (FETCH_SIZE and WRITE_SIZE cannot share one)
       ctr=$([[ $s == pmc_fetch ]] && echo FETCH_SIZE || echo WRITE_SIZE)
       out="$s${PMC_TAG:+_$PMC_TAG}"

@@ -51,7 +51,12 @@ def main():
     print("%-52s %5s %9s %10s %10s %8s %7s %s" % ("kernel", "n", "ms", "fetch GB", "write GB", "TB/s", "%roof",
                                                   "fetch+write / field" if a.field_bytes else ""))
     for k in sorted(set(fetch) | set(write)):
-        if k not in fetch or k not in write:
+        if k not in fetch:
+            continue
+        if k not in write:  # a fetch-only pass: bytes fetched per dispatch and the kernel time
+            fb, fns, n = big(fetch[k])
+            extra = "%.3f fetched" % (2.0 * fb / a.field_bytes) if a.field_bytes else ""
+            print("%-52s %5d %9.3f %10.3f %10s %8s %7s %s" % (k[:52], n, fns / 1e6, 2.0 * fb / 1e9, "-", "-", "-", extra))
             continue
         fb, fns, n = big(fetch[k])
         wb, wns, _ = big(write[k])

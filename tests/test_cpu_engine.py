@@ -477,6 +477,27 @@ def test_mdf_ref_precision_runs_fused(mdfx):
     assert auto_temporal(m.mdf2d(h=4096, w=512), 1, "hip") == 8
 
 
+@pytest.mark.parametrize("r", [0.25, 0.5, 0.125])
+def test_mdf_ref_precision_at_power_of_two_rate_is_bitwise_fp32(mdfx, r):
+    """StencilSpec::mixed_update: with a power-of-two r the reference's round_f32(round_f64(r*t + u))
+    equals fma_f32(r, t, u) for every input, so ref_precision and the plain update agree bit for
+    bit (the CPU oracle evaluates both literally; values spanning 2^-30..2^30 exercise wide
+    exponent gaps, where fp64 itself rounds)."""
+    import mpi_cuda_process_amd as m
+
+    out = []
+    for ref in (False, True):
+        prob = m.mdf2d(h=41, w=67, r=r, ref_precision=ref).with_init(kind="random", seed=11, lo=-50.0, hi=150.0)
+        with m.Simulation(prob, device="cpu") as sim:
+            sim.init()
+            g = sim.gather()
+            g[:, 0, :] *= np.exp2(np.random.default_rng(3).integers(-30, 30, g[:, 0, :].shape)).astype(np.float32)
+            sim.write_local(0, g)
+            sim.run(5)
+            out.append(sim.gather())
+    assert np.array_equal(out[0], out[1])
+
+
 def test_fused_depth_policy(mdfx):
     """hip_fused_depth: the measured-win fused depth per stencil and row width (host-side policy,
     profiles/r02_wtk/README.txt, r03_wtk/): K = 3 for the 3D 7-point where heat7_wtk's x segments

@@ -187,9 +187,12 @@ def test_engine_temporal2_box27(hip, dtype):
 
 DEEP = [models.mdf2d(h=45, w=1000), models.mdf2d(h=33, w=300, dtype="f64"), models.life2d(h=50, w=3000),
         models.life2d(h=19, w=100),
-        # the reference's mixed fp32 / fp64 evaluation (MDF_kernel.cu:20, jacobi5_tbk REF)
+        # the reference's mixed fp32 / fp64 evaluation (MDF_kernel.cu:20): at its r = 0.25 through the
+        # plain kernels (StencilSpec::mixed_update), at other r through jacobi5_tbk REF
         models.mdf2d(h=45, w=1000, ref_precision=True).with_init(kind="random", seed=5, lo=-50.0, hi=150.0),
-        models.mdf2d(h=23, w=130, ref_precision=True)]
+        models.mdf2d(h=23, w=130, ref_precision=True),
+        models.mdf2d(h=45, w=1000, r=0.2, ref_precision=True).with_init(kind="random", seed=5, lo=-50.0, hi=150.0),
+        models.mdf2d(h=23, w=130, r=0.15, ref_precision=True)]
 
 
 @pytest.mark.parametrize("prob", DEEP, ids=lambda p: p.describe().replace(" ", "_"))
@@ -224,9 +227,10 @@ def test_deep_fused_steps_bitwise(hip, prob, k, knob):
         assert abs(res.item() - ref_res.item()) <= 1e-9 * max(1.0, ref_res.item())
 
 
-def test_fused_ref_precision_is_the_reference_arithmetic(hip):
-    """The fused ref-precision sweep really evaluates the mixed-precision update: on random data
-    it differs from the pure-fp32 sweep in some cells, and equals the naive ref-precision steps."""
+def test_ref_precision_at_power_of_two_rate_is_the_field_type_update(hip):
+    """At the reference's r = 0.25 its mixed fp32 / fp64 update rounds exactly like the fp32 fma
+    update (proof: StencilSpec::mixed_update), so ref_precision runs the plain fused kernels; the
+    naive kernel evaluates the reference's expression literally and must agree bit for bit."""
     out = {}
     for ref in (False, True):
         prob = models.mdf2d(h=64, w=1000, ref_precision=ref).with_init(kind="random", seed=3, lo=-50.0, hi=150.0)
@@ -236,7 +240,18 @@ def test_fused_ref_precision_is_the_reference_arithmetic(hip):
         dst = alloc_field(lay, "cuda")
         apply_stencil(prob, lay, src, dst, steps=8)
         out[ref] = dst[lay.owned, :, :lay.nx].clone()
-    assert not torch.equal(out[False], out[True])
+        if ref:
+            set_kernel_variant("naive")
+            try:
+                cur = src.clone()
+                for _ in range(8):
+                    nxt = cur.clone()
+                    apply_stencil(prob, lay, cur, nxt)
+                    cur = nxt
+            finally:
+                set_kernel_variant("auto")
+            out["naive"] = cur[lay.owned, :, :lay.nx].clone()
+    assert torch.equal(out[False], out[True]) and torch.equal(out[True], out["naive"])
 
 
 LIFE_DEEP = [models.life2d(h=50, w=3000), models.life2d(h=19, w=100), models.life2d(h=40, w=2049),
