@@ -50,10 +50,16 @@ bool heat7_tbk_supported(const Geo& g, int steps);
 template <class T>
 void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
 bool heat7_wtk_supported(int steps);
+template <class T>
+void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
 double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
 // 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
 static bool use_wtk(int steps) { return knobs().h7_wtk >= 0 && heat7_wtk_supported(steps); }
+// ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
+// 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
+// 0 / 1 forces it off / on (fp64 on: K = 3 only, heat7_wtk's K = 4)
+static bool use_wxk(DType dt) { return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && dt == DType::F32); }
 
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -70,6 +76,8 @@ static Knobs read_knobs() {
   k.tbk_ry = env_int("MDFX_TBK_RY", 0);
   k.h7_wtk = env_int("MDFX_H7_WTK", 0);
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
+  k.h7_wxk = env_int("MDFX_H7_WXK", -1);
+  k.wxk_ry = env_int("MDFX_WXK_RY", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
@@ -265,9 +273,11 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // K = 3 through heat7_wtk wherever its x segments cover at least 2/3 of the lane cells:
       // 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2 (round 2), 2048^3 fp32 1666 vs 1136,
       // 1024^3 fp64 823-825 vs 546, 2048^3 fp64 818 vs 556; since the natural-layout rows also
-      // 512^3 fp32 (3 segments of 256 for 512 cells): 1311 vs 1230 (profiles/r03_wtk/)
+      // 512^3 fp32 (3 segments of 256 for 512 cells): 1311 vs 1230 (profiles/r03_wtk/). K = 4
+      // where heat7_wxk runs (fp32): its per-wave rows no longer grow with K, so the fourth step
+      // per pass costs less than the HBM pass it saves
       if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
-        return 3;
+        return dev::use_wxk(spec.dtype) ? 4 : 3;
       return 2;
   }
   return 1;
@@ -278,7 +288,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
     // two regions in one call: heat7_wtk sweeps them in ONE launch (both boundary regions of a
     // slab: one fill of the device, one launch gap); every other kernel runs them one after the other
     const bool fuse = a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps) && a.lz_end > a.lz_begin &&
-                      dev::knobs().fuse_regions;
+                      (dev::knobs().fuse_regions || dev::use_wxk(spec.dtype));
     if (!fuse) {
       RegionArgs r1 = a, r2 = a;
       r1.lz2_begin = r1.lz2_end = r2.lz2_begin = r2.lz2_end = 0;
@@ -327,6 +337,11 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
       }
+    } else if (dev::use_wtk(a.steps) && dev::use_wxk(spec.dtype)) {
+      if (spec.dtype == DType::F32)
+        dev::launch_heat7_wxk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
+      else
+        dev::launch_heat7_wxk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
     } else if (dev::use_wtk(a.steps)) {
       if (spec.dtype == DType::F32)
         dev::launch_heat7_wtk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);

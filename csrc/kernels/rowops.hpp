@@ -149,6 +149,7 @@ struct RowOps<double> {
     T2 v;
   };
   static __device__ __forceinline__ Row lds(const double* p) { return Row{*(const T2*)p}; }
+  static __device__ __forceinline__ Row fromv(const V& v) { return Row{v}; }
   static __device__ __forceinline__ Row lds_pairs(const double* p) { return lds(p); }
   static __device__ __forceinline__ void fence(Row&) {}
   static __device__ __forceinline__ void pin(Row&) {}
@@ -219,6 +220,7 @@ struct RowOpsN {
     const V v = *(const V*)a;
     return Row{T2{v.x, v.y}, T2{v.z, v.w}};
   }
+  static __device__ __forceinline__ Row fromv(const V& v) { return Row{T2{v.x, v.y}, T2{v.z, v.w}}; }
   static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}, T2{0.f, 0.f}}; }
   // one scalar add the backend cannot pair with its neighbour into a v_pk_add_f32 (e0 + e2 and
   // e1 + e3 would pack, and their halves then need two moves to reach (e0,e1) / (e2,e3))

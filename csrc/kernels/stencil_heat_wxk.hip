@@ -1,0 +1,385 @@
+// Deep temporal blocking for the 3D 7-point stencil with the y halo EXCHANGED between the waves of
+// a band instead of recomputed (heat7_wxk): K = 3 or 4 fused steps per sweep, one block barrier
+// per plane, bitwise equal to K single steps.
+//
+// heat7_wtk (stencil_heat_wtk.hip) makes every wave of a y band compute the RY + 2(K-l) rows that
+// its own level l+1 needs: at K = 3, 3-row waves, 15 row updates per plane for 9 output rows. Most
+// of those extra rows are rows the neighbouring wave of the same band computes anyway. Here a
+// wave computes only its own RY rows at every level; the rows just above and below it come from
+// its neighbours through a small LDS seam table. Only the band's first and last waves still
+// compute a one-sided trapezoid of K-l extra rows (the rows outside the band). Row updates per
+// output row, 8-wave bands: 1.06 (K = 3, 4-row waves) / 1.13 (K = 4, 3-row waves), against 1.67
+// for heat7_wtk's 3-row waves at K = 3.
+//
+// Why one barrier per plane is still enough: the plane loop streams u0 plane q in and finishes
+// level l at plane m = q - l. The z neighbours of u_l(m) are the wave's own rows
+// (u_{l-1}(m-1), u_{l-1}(m+1): the latter is computed earlier in the same step), and its in-plane
+// neighbours are u_{l-1}(m), which every wave computed in the PREVIOUS step. So a wave publishes
+// the first and last of its own rows of levels 1..K-1 into the seam table as it computes them
+// (parity q & 1), and after the next plane's barrier the neighbours read them. The in-plane
+// partial sum S = (((xm + xp) + ym) + yp) + zm of u_l(m) is therefore formed at the top of the
+// step, from the two stored planes m-1, m of level l-1 and the seam rows, and the step finishes
+// u_l(m) = fma(r, fma(-6, C, S + zp), C) with zp = u_{l-1}(m+1) the moment that row is computed:
+// one row cascades through all K levels (sm::heat7's operation order, so the result is bitwise
+// that of K single steps).
+//
+// Per row and level the state is two stored planes of level l-1 (ping-ponged between the two
+// halves of a 2-plane unrolled loop, so no row is ever copied); level 1 keeps heat7_wtk's
+// (S, C) pair fed straight from the u0 window. x: overlapping segments of 64 lanes x N cells
+// (OV lanes per side), DPP lane shifts -- as heat7_wtk. u0: the band's rows stream by LDS DMA into
+// a double-buffered window one plane ahead -- as heat7_wtk. Boundaries: held cells get a zero
+// coefficient; the band-edge waves' trapezoid rows outside the grid read clamped (finite) rows and
+// never feed an unheld cell.
+//
+// Region contract (as heat7_wtk): output storage planes [lz_begin, lz_end) (and optionally a
+// second region [lz2_begin, lz2_end)) need u0 valid on [lz_begin - K, lz_end + K).
+//
+// Reference parity: the generation update MDF_kernel.cu:10-22 (here in 3D, K generations per
+// pass over HBM instead of one generation per host round trip, MDF_kernel.cu:155-188).
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <type_traits>
+
+#include "kcommon.hpp"
+#include "rowops.hpp"
+#include "mdfx/kernels.hpp"
+#include "mdfx/stencil_math.hpp"
+
+namespace mdfx {
+namespace dev {
+
+int64_t resident_blocks(const void* kfn, int block);
+int hip_min_rounds_now();
+
+// rows of level l (1..K) a wave computes, relative to its first own row y0: [lo, hi)
+// ROLE 0 = the band's first wave (trapezoid above), 1 = inner waves, 2 = the band's last wave
+template <int ROLE, int RY, int K>
+struct WxRows {
+  static constexpr int lo(int l) { return ROLE == 0 ? -(K - l) : 0; }
+  static constexpr int hi(int l) { return RY + (ROLE == 2 ? K - l : 0); }
+  static constexpr int n(int l) { return hi(l) - lo(l); }
+};
+
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+template <class T, int RY, int K, int WB, bool RES>
+__global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
+                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
+  using Row = typename RO::Row;
+  constexpr int N = VT<T>::N;
+  constexpr int OV = (K + N - 1) / N;     // overlap lanes per side
+  constexpr int SEG = (64 - 2 * OV) * N;  // owned columns per wave
+  constexpr int RB = WB * RY + 2 * K;     // u0 window rows of a band: yb-K .. yb+WB*RY+K-1
+  constexpr int NM = RY + K - 1;          // most rows any wave computes at level 1
+  static_assert(WB >= 2 && K >= 2, "heat7_wxk: bands of at least two waves, at least two levels");
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // work: block-uniform task = one z chunk of one (x segment, y band) tile; x segments fastest, then
+  // y bands, then z chunks (the first region's chunks, then the second region's)
+  const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
+  if (b >= ntasks) return;
+  __shared__ V win[2][RB][64];
+  // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
+  __shared__ V seam[2][K - 1][WB - 1][2][64];
+  const int tiles = XT * YT;
+  const int t = b % tiles, zt = b / tiles;
+  const int P0 = (int)(g.lz_end - g.lz_begin);
+  const int zt1 = (P0 + zc - 1) / zc;
+  int zs, ze;
+  if (zt < zt1) {
+    zs = (int)g.lz_begin + zt * zc;
+    ze = min((int)g.lz_end, zs + zc);
+  } else {
+    zs = (int)g.lz2_begin + (zt - zt1) * zc;
+    ze = min((int)g.lz2_end, zs + zc);
+  }
+  const int xt = t % XT, yt = t / XT;
+  const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
+  const int64_t x = xs + (int64_t)lane * N;
+  const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
+  const int yb = yt * RY * WB;  // first row of the band
+  const int y0 = yb + w * RY;   // first own row of this wave
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const bool xin = x >= 0 && x < pitch;
+  const bool own = lane >= OV && lane <= 63 - OV && xin;
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
+  const Row rx = RO::coef(r, xb);
+  const Row r0 = RO::zero();
+  // block-uniform: every row the band computes at any level is y-interior, so no wave needs the
+  // per-row held test (bands at y = 0 / ny-1 run the tested copy, all their waves together)
+  const bool yint = yb - (K - 1) >= 1 && yb + WB * RY + K - 2 <= ny - 2;
+  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(RY, ny - y0)) : 0;
+  int nst = 0;  // output stores issued since this wave's last DMA
+
+  // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
+  // read the nearest valid row / vector. Wave w fetches rows w, w + WB, ... of the window.
+  const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
+  auto issue = [&](int lz, int buf) {
+    const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
+#pragma unroll
+    for (int j = 0; j < (RB + WB - 1) / WB; ++j) {
+      const int k = w + j * WB;
+      if (k < RB) {
+        const int y = yb - K + k;
+        const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
+        const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xcb);
+        dcheck(g, in, a, N);
+        glds16(a, &win[buf][k][0]);
+      }
+    }
+  };
+
+  const int qlast = ze - 1 + K;  // last u0 plane of the march
+  issue(zs - K, 0);
+  T* ob = out + (int64_t)y0 * pitch;
+  const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
+  double acc = 0.0;
+  // LDS addresses pinned in VGPRs with the wave-uniform parts folded in; compile-time parts go to
+  // the instructions' offset fields. Window rows from y0 - K (so every offset is non-negative).
+  typedef __attribute__((address_space(3))) V LV;
+  LV* const wrow = lds_vptr(&win[0][w * RY][lane]);
+  const int wu = w > 0 ? w - 1 : 0, wd = w < WB - 1 ? w : WB - 2;
+  // (the seam reads index `seam` itself: through a laundered pointer hipcc cannot tell them from
+  // the window's in-flight DMA and drains it with vmcnt(0) first)
+  LV* const s_first = lds_vptr(&seam[0][0][wu][0][lane]);  // my first row (write, w > 0)
+  LV* const s_last = lds_vptr(&seam[0][0][wd][1][lane]);   // my last row (write, w < WB-1)
+  constexpr int WIN_BUF = RB * 64;  // V elements per window buffer
+  constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
+  auto st = [](LV* p, const V& v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+  };
+
+  auto march = [&](auto role_c, auto edge_c) __attribute__((always_inline)) {
+    constexpr int ROLE = decltype(role_c)::value;
+    constexpr bool EDGE = decltype(edge_c)::value;
+    using SH = WxRows<ROLE, RY, K>;
+    // level 1: running partial S1 and centre of u0 (ping-pong CA / CB); levels 2..K: the two
+    // stored planes of the level below, H[l-2][0 / 1] (which is which alternates with the parity)
+    Row S1[NM], CA[NM], CB[NM], H[K - 1][2][NM];
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      S1[i] = RO::zero();
+      CA[i] = RO::zero();
+      CB[i] = RO::zero();
+#pragma unroll
+      for (int l = 0; l < K - 1; ++l) H[l][0][i] = H[l][1][i] = RO::zero();
+    }
+    auto step = [&](int q, auto par_c) __attribute__((always_inline)) {
+      constexpr int P = decltype(par_c)::value;
+      Row(&Cin)[NM] = P == 0 ? CA : CB;
+      Row(&Cout)[NM] = P == 0 ? CB : CA;
+      // no instruction moves across a plane boundary (the two planes of an unrolled trip would
+      // otherwise interleave, with both planes' rows live at once)
+      __builtin_amdgcn_sched_barrier(0);
+      // plane q's DMA has landed (the stores issued after it stay in flight); the barrier
+      // publishes it and last step's seam rows, and certifies that every wave is done with the
+      // other window buffer and the other seam parity
+      wait_vm_le(nst);
+      lds_barrier();
+      if (q < qlast) issue(q + 1, P ^ 1);
+      // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact)
+      Row rl[K + 1];
+#pragma unroll
+      for (int l = 1; l <= K; ++l) {
+        const int gz = q - l + gzoff;
+        rl[l] = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
+      }
+      // (1) levels 2..K: S_l(m), m = q - l, into the slot of u_{l-1}(m-1) (its zm, consumed here)
+#pragma unroll
+      for (int l = 2; l <= K; ++l) {
+        const int j = l - 1;  // level of the inputs
+        Row up = RO::zero(), dn = RO::zero();
+        if (ROLE != 0) up = RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
+        if (ROLE != 2) dn = RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
+#pragma unroll
+        for (int i = SH::lo(l); i < SH::hi(l); ++i) {
+          const int ij = i - SH::lo(j);
+          const Row& c = H[j - 1][P ^ 1][ij];
+          const Row& ym = (i - 1 < SH::lo(j)) ? up : H[j - 1][P ^ 1][ij - 1];
+          const Row& yp = (i + 1 >= SH::hi(j)) ? dn : H[j - 1][P ^ 1][ij + 1];
+          const T lft = lane_up1(RO::last(c));
+          const T rgt = lane_down1(RO::first(c));
+          Row& a = H[j - 1][P][ij];
+          a = RO::partial(c, lft, rgt, ym, yp, a);
+          RO::pin(a);
+        }
+      }
+      // (2) level 1 row by row from the u0 window, each new row cascading up through the levels
+      auto u0row = [&](int i) -> Row { return RO::fromv(V(wrow[P * WIN_BUF + (i + K) * 64])); };
+      Row X[3];
+      X[0] = u0row(SH::lo(1) - 1);
+      X[1] = u0row(SH::lo(1));
+      const bool valid = q - K >= zs && q <= qlast;  // u_K(q - K) is an owned output plane
+      const int lz = q - K;
+#pragma unroll
+      for (int i = SH::lo(1); i < SH::hi(1); ++i) {
+        const int i1 = i - SH::lo(1);
+        X[(i1 + 2) % 3] = u0row(i + 1);
+        const Row& xm = X[i1 % 3];
+        const Row& cen = X[(i1 + 1) % 3];
+        const Row& xp = X[(i1 + 2) % 3];
+        const bool yh = EDGE && (y0 + i == 0 || y0 + i == ny - 1);
+        Row ri = rl[1];
+        if (yh) ri = r0;
+        const Row cold = Cin[i1];
+        Row cur = RO::fin(S1[i1], cen, cold, ri);  // u_1(q - 1), row i
+        const T lft = lane_up1(RO::last(cen));
+        const T rgt = lane_down1(RO::first(cen));
+        S1[i1] = RO::partial(cen, lft, rgt, xm, xp, cold);
+        RO::pin(S1[i1]);
+        Cout[i1] = cen;
+        // cascade: cur = u_j(q - j) for j = 1, 2, ...
+#pragma unroll
+        for (int j = 1; j <= K; ++j) {
+          if (j == K) {  // the sweep's output row
+            if (valid && i >= 0 && i < RY && y0 + i < ny && own) {
+              T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
+              dcheck(g, (const T*)out, a, N);
+              store_nt((V*)a, RO::vec(cur));
+            }
+            break;
+          }
+          const int ij = i - SH::lo(j);
+          const bool next = i >= SH::lo(j + 1) && i < SH::hi(j + 1);  // row i exists at level j + 1
+          Row nxt = cur;
+          if (next) {
+            Row rj = rl[j + 1];
+            if (yh) rj = r0;
+            const Row& bc = H[j - 1][P ^ 1][ij];  // u_j(q - j - 1): the centre of u_{j+1}(q - j - 1)
+            nxt = RO::fin(H[j - 1][P][ij], cur, bc, rj);
+            if (RES && j + 1 == K && valid && i >= 0 && i < RY && y0 + i < ny && own) {
+#pragma unroll
+              for (int e = 0; e < N; ++e)
+                if (x + e < g.nx) {
+                  const double d = (double)RO::get(nxt, e) - (double)RO::get(bc, e);
+                  acc += d * d;
+                }
+            }
+          }
+          H[j - 1][P][ij] = cur;  // next step's centre plane of level j
+          // seam rows of level j for the neighbours' next step
+          if (ROLE != 0 && i == 0) st(s_first + P * SEAM_PAR + (j - 1) * SEAM_LVL, RO::vec(cur));
+          if (ROLE != 2 && i == RY - 1) st(s_last + P * SEAM_PAR + (j - 1) * SEAM_LVL, RO::vec(cur));
+          if (!next) break;
+          cur = nxt;
+        }
+      }
+      nst = valid ? nsto : 0;
+    };
+    // an odd plane count ends with one extra step (q = qlast + 1): no DMA, nothing stored
+    for (int q = zs - K; q <= qlast; q += 2) {
+      step(q, IC<0>{});
+      step(q + 1, IC<1>{});
+    }
+  };
+  if (w == 0) {
+    if (yint) march(IC<0>{}, std::false_type{});
+    else march(IC<0>{}, std::true_type{});
+  } else if (w == WB - 1) {
+    if (yint) march(IC<2>{}, std::false_type{});
+    else march(IC<2>{}, std::true_type{});
+  } else {
+    if (yint) march(IC<1>{}, std::false_type{});
+    else march(IC<1>{}, std::true_type{});
+  }
+  wait_vm0();  // no DMA may outlive the wave
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+struct WxkPlan {
+  int zc = 0;
+};
+// chunked schedule: z chunks minimising rounds x (zc + 2K) (as heat7_wtk's wtk_plan, chunked)
+static int wxk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int min_rounds) {
+  const int64_t fill = 2 * K;
+  const int64_t zmax = std::max<int64_t>(1, planes / (4 * K));
+  double best = 1e300;
+  int64_t bz = 1;
+  for (int64_t zt = 1; zt <= zmax; ++zt) {
+    const int64_t rounds = (tiles * zt + resident - 1) / resident;
+    if (rounds < min_rounds && zt < zmax) continue;
+    const double t = (double)rounds * (double)((planes + zt - 1) / zt + fill);
+    if (t < best * 0.999) {
+      best = t;
+      bz = zt;
+    }
+  }
+  return (int)((planes + bz - 1) / bz);
+}
+
+template <class T, int RY, int K, int WB>
+static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int64_t planes2 = g.lz2_end > g.lz2_begin ? g.lz2_end - g.lz2_begin : 0;
+  const int XT = (int)((g.nx + SEG - 1) / SEG);
+  const int YT = (int)((g.ny + RY * WB - 1) / (RY * WB));
+  const int64_t tiles = (int64_t)XT * YT;
+  const void* kfn = (const void*)&heat7_wxk<T, RY, K, WB, false>;
+  const int64_t resident = resident_blocks(kfn, 64 * WB);
+  int zc = knobs().zc > 0 ? knobs().zc : wxk_zc(planes, tiles, resident, K, hip_min_rounds_now());
+  if (planes2 > 0) zc = (int)std::max(planes, planes2);
+  const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
+  const int64_t ntasks = tiles * ZT;
+  if (knobs().debug_zc)
+    fprintf(stderr, "[mdfx] wxk K=%d RY=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n", K,
+            RY, WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
+  MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
+  const dim3 grd((unsigned)ntasks), blk(64 * WB);
+  if (resid)
+    hipLaunchKernelGGL((heat7_wxk<T, RY, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  else
+    hipLaunchKernelGGL((heat7_wxk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+}
+
+bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
+
+template <class T>
+void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
+
+// fp32: K = 3 in 4-row waves (MDFX_WXK_RY = 3: 3 rows), K = 4 in 2-row waves, bands of 8 waves
+// (MDFX_WTK_WB = 4: bands of 4 with 4 / 3 rows); fp64: K = 3 in 2-row waves, K = 4 stays on
+// heat7_wtk. The shapes that would spill (fp32 K = 4 3-row waves in 8-wave bands, fp64 K = 4 and
+// 3-row waves) are not built (tests/test_kernel_resources.py).
+template <class T>
+void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  if (sizeof(T) == 8 && steps == 4) {
+    launch_heat7_wtk<T>(g, in, out, r, steps, resid, s);
+    return;
+  }
+  MDFX_CHECK((steps == 3 || steps == 4) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+             format("heat7_wxk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
+                    (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
+  MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
+             "heat7_wxk: the second region must follow the first and have its planes + ghosts allocated");
+  MDFX_CHECK(g.pitch % VT<T>::N == 0, "heat7_wxk: the row pitch must be a whole number of vectors");
+  MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
+                 g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
+             "heat7_wxk: row / plane counts must fit 32-bit indices");
+  const int wb = knobs().wtk_wb == 4 ? 4 : 8;
+  const int ry = knobs().wxk_ry;
+  if constexpr (sizeof(T) == 4) {
+    if (steps == 3) {
+      if (wb == 4) launch_wxk<T, 4, 3, 4>(g, in, out, r, resid, s);
+      else if (ry == 3) launch_wxk<T, 3, 3, 8>(g, in, out, r, resid, s);
+      else launch_wxk<T, 4, 3, 8>(g, in, out, r, resid, s);
+    } else {
+      if (wb == 4) launch_wxk<T, 3, 4, 4>(g, in, out, r, resid, s);
+      else launch_wxk<T, 2, 4, 8>(g, in, out, r, resid, s);
+    }
+  } else {
+    launch_wxk<T, 2, 3, 8>(g, in, out, r, resid, s);
+  }
+}
+template void launch_heat7_wxk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
+template void launch_heat7_wxk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
+
+}  // namespace dev
+}  // namespace mdfx

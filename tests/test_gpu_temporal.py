@@ -472,6 +472,68 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
+@pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=300, ny=33, nz=9, dtype="f64")],
+                         ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("k,wb,ry", [(3, "8", "0"), (3, "8", "3"), (3, "4", "0"), (4, "8", "0"), (4, "4", "0")])
+@pytest.mark.parametrize("resid", [False, True])
+def test_heat7_wxk_bitwise(hip, prob, k, wb, ry, resid, knob):
+    """heat7_wxk (y halo exchanged between the waves of a band through the LDS seam table, one
+    barrier per plane) == K naive single steps, bitwise, with the residual of step K, for every
+    band shape and row count, including bands taller than the grid and waves wholly outside it."""
+    knob("MDFX_H7_WXK", 1)
+    knob("MDFX_WTK_WB", wb)
+    knob("MDFX_WXK_RY", ry)
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res if resid else None)
+    set_kernel_variant("naive")
+    try:
+        cur = src.clone()
+        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+        for i in range(k):
+            nxt = cur.clone()
+            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb, ry)
+    if resid:
+        assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_heat7_wxk_regions_and_engine(hip, k, knob):
+    """heat7_wxk on a middle slab: both boundary regions in one launch + the interior == the whole
+    grid; and an engine run over 3 slabs with the wxk sweeps == single steps."""
+    knob("MDFX_H7_WXK", 1)
+    prob = models.heat3d(nx=1024, ny=20, nz=40)
+    full = FieldLayout.make(prob, halo=k)
+    g = alloc_field(full, "cuda")
+    init_field(prob, full, g)
+    ref = alloc_field(full, "cuda")
+    apply_stencil(prob, full, g, ref, steps=k)
+    lay = FieldLayout.make(prob, 12, 30, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    out = alloc_field(lay, "cuda")
+    h = lay.halo
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, out, h, h + k, steps=k, second=(h + 18 - k, h + 18), resid=res)
+    apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k, resid=res)
+    torch.cuda.synchronize()
+    assert torch.equal(out[h:h + 18, :, :1024], ref[12 + k:30 + k, :, :1024])
+    assert res.item() > 0
+    p3 = models.heat3d(nx=600, ny=37, nz=45)
+    a, _ = _sim(p3, 2 * k, ranks=1)
+    b, _ = _sim(p3, 2 * k, ranks=3, temporal=k)
+    assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("k", [3, 4])
 def test_heat7_wtk_regions_on_a_slab(hip, k):
     """heat7_wtk on a middle slab with K ghost planes: boundary + interior regions == whole grid."""
