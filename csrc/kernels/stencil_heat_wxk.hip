@@ -53,18 +53,22 @@ int64_t resident_blocks(const void* kfn, int block);
 int hip_min_rounds_now();
 
 // rows of level l (1..K) a wave computes, relative to its first own row y0: [lo, hi)
-// ROLE 0 = the band's first wave (trapezoid above), 1 = inner waves, 2 = the band's last wave
-template <int ROLE, int RY, int K>
+// ROLE 0 = the band's first wave (trapezoid above), 1 = inner waves, 2 = the band's last wave.
+// Inner waves own RY rows, the two edge waves RE: an edge wave also computes the K-l trapezoid
+// rows outside the band at level l, so RE < RY evens out the waves' work per plane (every wave
+// waits for the slowest at the plane barrier)
+template <int ROLE, int RY, int RE, int K>
 struct WxRows {
+  static constexpr int R = ROLE == 1 ? RY : RE;  // own rows
   static constexpr int lo(int l) { return ROLE == 0 ? -(K - l) : 0; }
-  static constexpr int hi(int l) { return RY + (ROLE == 2 ? K - l : 0); }
+  static constexpr int hi(int l) { return R + (ROLE == 2 ? K - l : 0); }
   static constexpr int n(int l) { return hi(l) - lo(l); }
 };
 
 template <int V>
 using IC = std::integral_constant<int, V>;
 
-template <class T, int RY, int K, int WB, bool RES>
+template <class T, int RY, int RE, int K, int WB, bool RES>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
@@ -73,8 +77,9 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   constexpr int N = VT<T>::N;
   constexpr int OV = (K + N - 1) / N;     // overlap lanes per side
   constexpr int SEG = (64 - 2 * OV) * N;  // owned columns per wave
-  constexpr int RB = WB * RY + 2 * K;     // u0 window rows of a band: yb-K .. yb+WB*RY+K-1
-  constexpr int NM = RY + K - 1;          // most rows any wave computes at level 1
+  constexpr int BR = 2 * RE + (WB - 2) * RY;  // output rows of a band
+  constexpr int RB = BR + 2 * K;              // u0 window rows of a band: yb-K .. yb+BR+K-1
+  constexpr int NM = RY > RE + K - 1 ? RY : RE + K - 1;  // most rows any wave computes at level 1
   static_assert(WB >= 2 && K >= 2, "heat7_wxk: bands of at least two waves, at least two levels");
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -101,8 +106,9 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
   const int64_t x = xs + (int64_t)lane * N;
   const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
-  const int yb = yt * RY * WB;  // first row of the band
-  const int y0 = yb + w * RY;   // first own row of this wave
+  const int yb = yt * BR;                              // first row of the band
+  const int y0 = yb + (w == 0 ? 0 : RE + (w - 1) * RY);  // first own row of this wave
+  const int rown = (w == 0 || w == WB - 1) ? RE : RY;    // own rows of this wave
   const int64_t pitch = g.pitch, plane = g.plane;
   const bool xin = x >= 0 && x < pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
@@ -113,8 +119,8 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const Row r0 = RO::zero();
   // block-uniform: every row the band computes at any level is y-interior, so no wave needs the
   // per-row held test (bands at y = 0 / ny-1 run the tested copy, all their waves together)
-  const bool yint = yb - (K - 1) >= 1 && yb + WB * RY + K - 2 <= ny - 2;
-  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(RY, ny - y0)) : 0;
+  const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
+  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(rown, ny - y0)) : 0;
   int nst = 0;  // output stores issued since this wave's last DMA
 
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
@@ -143,7 +149,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // LDS addresses pinned in VGPRs with the wave-uniform parts folded in; compile-time parts go to
   // the instructions' offset fields. Window rows from y0 - K (so every offset is non-negative).
   typedef __attribute__((address_space(3))) V LV;
-  LV* const wrow = lds_vptr(&win[0][w * RY][lane]);
+  LV* const wrow = lds_vptr(&win[0][y0 - yb][lane]);
   const int wu = w > 0 ? w - 1 : 0, wd = w < WB - 1 ? w : WB - 2;
   // (the seam reads index `seam` itself: through a laundered pointer hipcc cannot tell them from
   // the window's in-flight DMA and drains it with vmcnt(0) first)
@@ -158,7 +164,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   auto march = [&](auto role_c, auto edge_c) __attribute__((always_inline)) {
     constexpr int ROLE = decltype(role_c)::value;
     constexpr bool EDGE = decltype(edge_c)::value;
-    using SH = WxRows<ROLE, RY, K>;
+    using SH = WxRows<ROLE, RY, RE, K>;
     // level 1: running partial S1 and centre of u0 (ping-pong CA / CB); levels 2..K: the two
     // stored planes of the level below, H[l-2][0 / 1] (which is which alternates with the parity)
     Row S1[NM], CA[NM], CB[NM], H[K - 1][2][NM];
@@ -238,7 +244,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
 #pragma unroll
         for (int j = 1; j <= K; ++j) {
           if (j == K) {  // the sweep's output row
-            if (valid && i >= 0 && i < RY && y0 + i < ny && own) {
+            if (valid && i >= 0 && i < SH::R && y0 + i < ny && own) {
               T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
               dcheck(g, (const T*)out, a, N);
               store_nt((V*)a, RO::vec(cur));
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
             if (yh) rj = r0;
             const Row& bc = H[j - 1][P ^ 1][ij];  // u_j(q - j - 1): the centre of u_{j+1}(q - j - 1)
             nxt = RO::fin(H[j - 1][P][ij], cur, bc, rj);
-            if (RES && j + 1 == K && valid && i >= 0 && i < RY && y0 + i < ny && own) {
+            if (RES && j + 1 == K && valid && i >= 0 && i < SH::R && y0 + i < ny && own) {
 #pragma unroll
               for (int e = 0; e < N; ++e)
                 if (x + e < g.nx) {
@@ -265,7 +271,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
           H[j - 1][P][ij] = cur;  // next step's centre plane of level j
           // seam rows of level j for the neighbours' next step
           if (ROLE != 0 && i == 0) st(s_first + P * SEAM_PAR + (j - 1) * SEAM_LVL, RO::vec(cur));
-          if (ROLE != 2 && i == RY - 1) st(s_last + P * SEAM_PAR + (j - 1) * SEAM_LVL, RO::vec(cur));
+          if (ROLE != 2 && i == SH::R - 1) st(s_last + P * SEAM_PAR + (j - 1) * SEAM_LVL, RO::vec(cur));
           if (!next) break;
           cur = nxt;
         }
@@ -313,29 +319,30 @@ static int wxk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int mi
   return (int)((planes + bz - 1) / bz);
 }
 
-template <class T, int RY, int K, int WB>
+template <class T, int RY, int RE, int K, int WB>
 static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int64_t planes2 = g.lz2_end > g.lz2_begin ? g.lz2_end - g.lz2_begin : 0;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
-  const int YT = (int)((g.ny + RY * WB - 1) / (RY * WB));
+  constexpr int BR = 2 * RE + (WB - 2) * RY;
+  const int YT = (int)((g.ny + BR - 1) / BR);
   const int64_t tiles = (int64_t)XT * YT;
-  const void* kfn = (const void*)&heat7_wxk<T, RY, K, WB, false>;
+  const void* kfn = (const void*)&heat7_wxk<T, RY, RE, K, WB, false>;
   const int64_t resident = resident_blocks(kfn, 64 * WB);
   int zc = knobs().zc > 0 ? knobs().zc : wxk_zc(planes, tiles, resident, K, hip_min_rounds_now());
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = tiles * ZT;
   if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] wxk K=%d RY=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n", K,
-            RY, WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
+    fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
+            K, RY, RE, WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   if (resid)
-    hipLaunchKernelGGL((heat7_wxk<T, RY, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
   else
-    hipLaunchKernelGGL((heat7_wxk<T, RY, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -367,15 +374,17 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   const int ry = knobs().wxk_ry;
   if constexpr (sizeof(T) == 4) {
     if (steps == 3) {
-      if (wb == 4) launch_wxk<T, 4, 3, 4>(g, in, out, r, resid, s);
-      else if (ry == 3) launch_wxk<T, 3, 3, 8>(g, in, out, r, resid, s);
-      else launch_wxk<T, 4, 3, 8>(g, in, out, r, resid, s);
+      if (wb == 4) launch_wxk<T, 4, 4, 3, 4>(g, in, out, r, resid, s);
+      else if (ry == 3) launch_wxk<T, 3, 3, 3, 8>(g, in, out, r, resid, s);
+      else launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
     } else {
-      if (wb == 4) launch_wxk<T, 3, 4, 4>(g, in, out, r, resid, s);
-      else launch_wxk<T, 2, 4, 8>(g, in, out, r, resid, s);
+      if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
+      else if (ry == 2) launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 21) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
+      else launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
     }
   } else {
-    launch_wxk<T, 2, 3, 8>(g, in, out, r, resid, s);
+    launch_wxk<T, 2, 2, 3, 8>(g, in, out, r, resid, s);
   }
 }
 template void launch_heat7_wxk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
