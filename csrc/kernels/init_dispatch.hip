@@ -55,11 +55,15 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
 double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
 // 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
-static bool use_wtk(int steps) { return knobs().h7_wtk >= 0 && heat7_wtk_supported(steps); }
+static bool use_wxk(DType dt);
+static bool use_wtk(int steps, DType dt) {
+  return knobs().h7_wtk >= 0 && (heat7_wtk_supported(steps) || (steps == 5 && dt == DType::F32 && use_wxk(dt)));
+}
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
 // 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
 // 0 / 1 forces it off / on (fp64 on: K = 3 only, heat7_wtk's K = 4)
 static bool use_wxk(DType dt) { return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && dt == DType::F32); }
+// (K = 5: fp32 heat7_wxk only)
 
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -249,7 +253,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
     return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d;  // ref precision too (jacobi5_tbk REF)
   if (spec.kind == StencilKind::Life) return k2d || steps == 12 || steps == 16;  // 12 / 16: life_bits
   if (spec.kind == StencilKind::Heat7 && steps > 2) {  // deep temporal blocking (rows within one block)
-    if (dev::use_wtk(steps)) return true;
+    if (dev::use_wtk(steps, spec.dtype)) return true;
     const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
     return spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, steps)
                                     : dev::heat7_tbk_supported<double>(g, steps);
@@ -287,7 +291,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   if (a.lz2_end > a.lz2_begin) {
     // two regions in one call: heat7_wtk sweeps them in ONE launch (both boundary regions of a
     // slab: one fill of the device, one launch gap); every other kernel runs them one after the other
-    const bool fuse = a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps) && a.lz_end > a.lz_begin &&
+    const bool fuse = a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps, spec.dtype) && a.lz_end > a.lz_begin &&
                       (dev::knobs().fuse_regions || dev::use_wxk(spec.dtype));
     if (!fuse) {
       RegionArgs r1 = a, r2 = a;
@@ -337,12 +341,12 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
       }
-    } else if (dev::use_wtk(a.steps) && dev::use_wxk(spec.dtype)) {
+    } else if (dev::use_wtk(a.steps, spec.dtype) && dev::use_wxk(spec.dtype)) {
       if (spec.dtype == DType::F32)
         dev::launch_heat7_wxk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
       else
         dev::launch_heat7_wxk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
-    } else if (dev::use_wtk(a.steps)) {
+    } else if (dev::use_wtk(a.steps, spec.dtype)) {
       if (spec.dtype == DType::F32)
         dev::launch_heat7_wtk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
       else

@@ -218,7 +218,8 @@ struct Knobs {
   int fuse_regions = 0;  // MDFX_FUSE_REGIONS: 1 = both boundary regions of a slab in one heat7_wtk launch (measured slower)
   int wtk_split = -1;  // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: -1 never (default, measured slower), 0 cost model, 1 always
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
-  int wxk_ry = 0;      // MDFX_WXK_RY: heat7_wxk fp32 rows per wave (0: 4 at K = 3, 3 at K = 4)    // MDFX_WTK_K4RY: fp32 rows per wave of the K = 4 sweeps (1 or 2)
+  int wxk_ry = 0;      // MDFX_WXK_RY: heat7_wxk fp32 band shape (K = 3: 3 = 3-row waves; K = 4: 31 = 3-row inner /
+                       // 1-row edge waves, 21 = 2 / 1; 0: by row width)
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)
   int j5_nat = 2;      // MDFX_J5_NAT: jacobi5_tbk fp32 rows: 2 natural layout + 2-row unroll, 1 natural, 0 round 2's pair layout

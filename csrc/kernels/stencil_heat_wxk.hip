@@ -339,10 +339,13 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
             K, RY, RE, WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
-  if (resid)
+  if constexpr (K == 5) {  // (its residual instance needs more than 256 VGPRs)
+    MDFX_CHECK(!resid, "heat7_wxk: no residual variant of the 5-step sweep (use --temporal 4 with a residual)");
+  } else if (resid) {
     hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
-  else
-    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+    return;
+  }
+  hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -361,7 +364,7 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
     launch_heat7_wtk<T>(g, in, out, r, steps, resid, s);
     return;
   }
-  MDFX_CHECK((steps == 3 || steps == 4) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+  MDFX_CHECK((steps == 3 || steps == 4 || (steps == 5 && sizeof(T) == 4)) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_wxk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
@@ -377,11 +380,16 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
       if (wb == 4) launch_wxk<T, 4, 4, 3, 4>(g, in, out, r, resid, s);
       else if (ry == 3) launch_wxk<T, 3, 3, 3, 8>(g, in, out, r, resid, s);
       else launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
+    } else if (steps == 5) {
+      launch_wxk<T, 2, 1, 5, 8>(g, in, out, r, resid, s);
     } else {
+      // 2-row waves (1024^3: 2212-2262 GCells/s vs 2150-2162 for 3-row inner waves with 1-row edge
+      // waves); at rows of 512 cells and less the 3 + 1 band (512^3: 1863 vs 1746)
       if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
-      else if (ry == 2) launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 31 || (ry == 0 && g.nx <= 512)) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
       else if (ry == 21) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
-      else launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 32) launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
+      else launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
     }
   } else {
     launch_wxk<T, 2, 2, 3, 8>(g, in, out, r, resid, s);
