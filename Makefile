@@ -61,6 +61,7 @@ $(OBJ)/%.o: csrc/%.cpp $(HEADERS)
 # the natural-layout rows (heat7_wtk, jacobi5_tbk, box27_tb2n) need the scalar x adds left unpacked (RowOpsN, rowops.hpp)
 $(OBJ)/kernels/stencil_heat_wtk.o $(ASAN_DIR)/kernels/stencil_heat_wtk.o $(DCK_DIR)/kernels/stencil_heat_wtk.o: HIPFLAGS += -fno-slp-vectorize
 $(OBJ)/kernels/stencil_heat_wxk.o $(ASAN_DIR)/kernels/stencil_heat_wxk.o $(DCK_DIR)/kernels/stencil_heat_wxk.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJ)/kernels/stencil_box27_wxk.o $(ASAN_DIR)/kernels/stencil_box27_wxk.o $(DCK_DIR)/kernels/stencil_box27_wxk.o: HIPFLAGS += -fno-slp-vectorize
 $(OBJ)/kernels/stencil_heat_tb.o $(ASAN_DIR)/kernels/stencil_heat_tb.o $(DCK_DIR)/kernels/stencil_heat_tb.o: HIPFLAGS += -fno-slp-vectorize
 $(OBJ)/kernels/stencil_box27.o $(ASAN_DIR)/kernels/stencil_box27.o $(DCK_DIR)/kernels/stencil_box27.o: HIPFLAGS += -fno-slp-vectorize
 

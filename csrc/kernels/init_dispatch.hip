@@ -52,6 +52,9 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 bool heat7_wtk_supported(int steps);
 template <class T>
 void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
+template <class T>
+void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, int steps, double* resid,
+                      hipStream_t s);
 double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
 // 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
@@ -81,6 +84,7 @@ static Knobs read_knobs() {
   k.h7_wtk = env_int("MDFX_H7_WTK", 0);
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
+  k.b27_wxk = env_int("MDFX_B27_WXK", 0);
   k.wxk_ry = env_int("MDFX_WXK_RY", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
@@ -258,6 +262,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
     return spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, steps)
                                     : dev::heat7_tbk_supported<double>(g, steps);
   }
+  if (spec.kind == StencilKind::Box27 && steps == 3) return true;  // box27_wxk (any row width)
   if (steps != 2) return false;
   if (spec.kind == StencilKind::Box27) {
     const dev::Geo g = dev::make_geo(lay, lay.halo, lay.halo + lay.nzl());
@@ -272,7 +277,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
   switch (spec.kind) {
     case StencilKind::Jacobi5: return 8;
     case StencilKind::Life: return 12;
-    case StencilKind::Box27: return 2;
+    case StencilKind::Box27: return dev::knobs().b27_wxk == 1 ? 3 : 2;
     case StencilKind::Heat7:
       // K = 3 through heat7_wtk wherever its x segments cover at least 2/3 of the lane cells:
       // 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2 (round 2), 2048^3 fp32 1666 vs 1136,
@@ -291,8 +296,10 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   if (a.lz2_end > a.lz2_begin) {
     // two regions in one call: heat7_wtk sweeps them in ONE launch (both boundary regions of a
     // slab: one fill of the device, one launch gap); every other kernel runs them one after the other
-    const bool fuse = a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps, spec.dtype) && a.lz_end > a.lz_begin &&
-                      (dev::knobs().fuse_regions || dev::use_wxk(spec.dtype));
+    const bool fuse = a.lz_end > a.lz_begin &&
+                      ((a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps, spec.dtype) &&
+                        (dev::knobs().fuse_regions || dev::use_wxk(spec.dtype))) ||
+                       (spec.kind == StencilKind::Box27 && a.steps == 3));
     if (!fuse) {
       RegionArgs r1 = a, r2 = a;
       r1.lz2_begin = r1.lz2_end = r2.lz2_begin = r2.lz2_end = 0;
@@ -316,7 +323,12 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
     MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),
                format("no fused %d-step kernel for %s %s at nx=%lld (halo %d)", a.steps, stencil_name(spec.kind),
                       dtype_name(spec.dtype), (long long)a.lay.global.nx, a.lay.halo));
-    if (spec.kind == StencilKind::Box27) {
+    if (spec.kind == StencilKind::Box27 && a.steps == 3) {
+      if (spec.dtype == DType::F32)
+        dev::launch_box27_wxk<float>(g, (const float*)a.in, (float*)a.out, spec.coef, 3, a.resid, s);
+      else
+        dev::launch_box27_wxk<double>(g, (const double*)a.in, (double*)a.out, spec.coef, 3, a.resid, s);
+    } else if (spec.kind == StencilKind::Box27) {
       if (spec.dtype == DType::F32)
         dev::launch_box27_tb2<float>(g, (const float*)a.in, (float*)a.out, spec.coef, a.resid, s);
       else

@@ -217,6 +217,7 @@ struct Knobs {
   int wtk_res_shape = 0;  // MDFX_WTK_RES_SHAPE: 1 = residual sweeps in round 2's 2-row 4-wave bands
   int fuse_regions = 0;  // MDFX_FUSE_REGIONS: 1 = both boundary regions of a slab in one heat7_wtk launch (measured slower)
   int wtk_split = -1;  // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: -1 never (default, measured slower), 0 cost model, 1 always
+  int b27_wxk = 0;     // MDFX_B27_WXK: 1 = the 27-point's fused depth is 3 (box27_wxk, y halo exchanged)
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
   int wxk_ry = 0;      // MDFX_WXK_RY: heat7_wxk fp32 band shape (K = 3: 3 = 3-row waves; K = 4: 31 = 3-row inner /
                        // 1-row edge waves, 21 = 2 / 1; 0: by row width)

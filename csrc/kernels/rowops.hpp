@@ -192,6 +192,17 @@ struct RowOps<double> {
   static __device__ __forceinline__ Row hsum(const Row& c, double l, double rr) {
     return Row{T2{l + c.v.y, c.v.x + rr}};
   }
+  static __device__ __forceinline__ Row lin3r(const Row& c, const Row& x, const Row& d, const Row& k0, const Row& k1,
+                                              const Row& k2) {
+    return Row{__builtin_elementwise_fma(k2.v, d.v, __builtin_elementwise_fma(k1.v, x.v, k0.v * c.v))};
+  }
+  static __device__ __forceinline__ Row fmaz(double z, const Row& a, const Row& s) {
+    return Row{__builtin_elementwise_fma(T2{z, z}, a.v, s.v)};
+  }
+  static __device__ __forceinline__ Row coefv(double v, double h, const bool* held) {
+    return Row{T2{held[0] ? h : v, held[1] ? h : v}};
+  }
+  static __device__ __forceinline__ Row splat(double v) { return Row{T2{v, v}}; }
   static __device__ __forceinline__ Row lin3(const Row& c, const Row& x, const Row& d, double k0, double k1,
                                              double k2) {
     const T2 K0{k0, k0}, K1{k1, k1}, K2{k2, k2};
@@ -317,6 +328,25 @@ struct RowOpsN {
     return e == 0 ? c.p.x : e == 1 ? c.p.y : e == 2 ? c.q.x : c.q.y;
   }
   static __device__ __forceinline__ V vec(const Row& c) { return V{c.p.x, c.p.y, c.q.x, c.q.y}; }
+  // ---- 27-point with per-cell coefficients (box27_wxk) ----
+  // fma(k2, d, fma(k1, x, k0 * c)) with per-cell coefficient rows
+  static __device__ __forceinline__ Row lin3r(const Row& c, const Row& x, const Row& d, const Row& k0, const Row& k1,
+                                              const Row& k2) {
+    Row o;
+    o.p = __builtin_elementwise_fma(k2.p, d.p, __builtin_elementwise_fma(k1.p, x.p, k0.p * c.p));
+    o.q = __builtin_elementwise_fma(k2.q, d.q, __builtin_elementwise_fma(k1.q, x.q, k0.q * c.q));
+    return o;
+  }
+  // fma(z, a, s) for a wave-uniform z in {0, 1}: s + a (z = 1, one rounding as an add) or s (z = 0)
+  static __device__ __forceinline__ Row fmaz(float z, const Row& a, const Row& s) {
+    const T2 zz{z, z};
+    return Row{__builtin_elementwise_fma(zz, a.p, s.p), __builtin_elementwise_fma(zz, a.q, s.q)};
+  }
+  // per cell: held ? h : v
+  static __device__ __forceinline__ Row coefv(float v, float h, const bool* held) {
+    return Row{T2{held[0] ? h : v, held[1] ? h : v}, T2{held[2] ? h : v, held[3] ? h : v}};
+  }
+  static __device__ __forceinline__ Row splat(float v) { return Row{T2{v, v}, T2{v, v}}; }
   // materialise a loop-carried row where it is computed: otherwise hipcc carries the INPUTS of the
   // partial sum across the back edge and forms it in the next iteration, where the lane-shift
   // moves can no longer fold into the adds as DPP operands (DPP combining works inside a block)

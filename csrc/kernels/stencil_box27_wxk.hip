@@ -1,0 +1,302 @@
+// Deep temporal blocking for the 3D 27-point stencil with the y halo exchanged between the waves
+// of a band (box27_wxk): K = 3 fused steps per sweep, one block barrier per plane, bitwise equal to
+// K single box27_zw steps.
+//
+// The update is box27_zw's per-plane factorisation: for a plane k and an output column (x, y),
+//   H(y) = v(x-1,y) + v(x+1,y);  cross = H(y) + (v(x,y-1) + v(x,y+1));  diag = H(y-1) + H(y+1)
+//   A(k) = c3*diag + c2*cross + c1*v;  B(k) = c2*diag + c1*cross + c0*v      (sm::box27_A / _B)
+//   u'(m) = (A(m-1) + B(m)) + A(m+1)                                        (sm::box27_combine)
+// so every level keeps, per row, the running sum S(m) = A(m-1) + B(m) and the last A.
+//
+// Band organisation as heat7_wxk (stencil_heat_wxk.hip): WB waves stacked along y on one x segment
+// (overlapping segments, DPP lane shifts), the band's u0 rows streamed by LDS DMA into a
+// double-buffered window, each wave computing only its own rows at every level (the band's edge
+// waves add a one-sided trapezoid). The difference from the 7-point: A(m+1) needs the in-plane
+// neighbours (y +- 1) of plane m+1 of the level below, not just its centre column, so a level
+// cannot use a plane its neighbours finish in the same step. Each level above the first therefore
+// runs one plane later: level l finishes plane q - (2l - 1) at step q, from the plane its level
+// below finished (and published into the LDS seam table) one step earlier. Level 1 reads u0 from
+// the window, which holds whole band rows, and finishes plane q - 1.
+//
+// Held cells: per-cell coefficient rows (x): c0 -> 1 and c1 = c2 = c3 -> 0, so A = 0 and B = the
+// centre, and the cell keeps its value; rows y = 0 / ny-1 take that held coefficient set per row;
+// planes gz = 0 / gnz-1 through a 0 / 1 factor on the A terms (u' = fma(z, A, S), S = fma(z, A, B)
+// with B = the centre there). Those two run in a general copy of the march that only bands touching
+// y = 0 / ny-1 and chunks touching the first / last global plane take. (A held cell holding -0.0
+// comes back as +0.0, as in every fused kernel: 0 * t + (-0) rounds to +0.)
+//
+// Region contract (as box27_tb2): output storage planes [lz_begin, lz_end) (and optionally a second
+// region [lz2_begin, lz2_end)) need u0 valid on [lz_begin - K, lz_end + K).
+//
+// Reference parity: the generation update MDF_kernel.cu:10-22 generalised to the 27-point weighted
+// stencil of BASELINE.json config 4.
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <type_traits>
+
+#include "kcommon.hpp"
+#include "rowops.hpp"
+#include "wxk_common.hpp"
+#include "mdfx/kernels.hpp"
+#include "mdfx/stencil_math.hpp"
+
+namespace mdfx {
+namespace dev {
+
+int64_t resident_blocks(const void* kfn, int block);
+int hip_min_rounds_now();
+
+template <class T, int RY, int RE, int K, int WB, bool RES>
+__global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
+                                                     T c2, T c3, int zc, int XT, int YT, int ntasks,
+                                                     double* __restrict__ resid) {
+  using V = typename VT<T>::type;
+  using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
+  using Row = typename RO::Row;
+  constexpr int N = VT<T>::N;
+  constexpr int OV = (K + N - 1) / N;
+  constexpr int SEG = (64 - 2 * OV) * N;
+  constexpr int BR = 2 * RE + (WB - 2) * RY;
+  constexpr int RB = BR + 2 * K;
+  constexpr int NM = RY > RE + K - 1 ? RY : RE + K - 1;
+  constexpr int LAG = 2 * K - 1;  // level K finishes plane q - LAG at step q
+  static_assert(WB >= 2 && K >= 2, "box27_wxk: bands of at least two waves, at least two levels");
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
+  if (b >= ntasks) return;
+  __shared__ V win[2][RB][64];
+  __shared__ V seam[2][K - 1][WB - 1][2][64];
+  const int tiles = XT * YT;
+  const int t = b % tiles, zt = b / tiles;
+  const int P0 = (int)(g.lz_end - g.lz_begin);
+  const int zt1 = (P0 + zc - 1) / zc;
+  int zs, ze;
+  if (zt < zt1) {
+    zs = (int)g.lz_begin + zt * zc;
+    ze = min((int)g.lz_end, zs + zc);
+  } else {
+    zs = (int)g.lz2_begin + (zt - zt1) * zc;
+    ze = min((int)g.lz2_end, zs + zc);
+  }
+  const int xt = t % XT, yt = t / XT;
+  const int64_t x = (int64_t)xt * SEG - OV * N + (int64_t)lane * N;
+  const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
+  const int yb = yt * BR;
+  const int y0 = yb + (w == 0 ? 0 : RE + (w - 1) * RY);
+  const int rown = (w == 0 || w == WB - 1) ? RE : RY;
+  const int64_t pitch = g.pitch, plane = g.plane;
+  const bool xin = x >= 0 && x < pitch;
+  const bool own = lane >= OV && lane <= 63 - OV && xin;
+  bool xb[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) xb[e] = (x + e <= 0) || (x + e >= g.nx - 1);
+  // per-cell coefficients: held x cells keep their centre (A = 0, B = centre)
+  const Row k0 = RO::coefv(c0, T(1), xb), k1 = RO::coefv(c1, T(0), xb), k2 = RO::coefv(c2, T(0), xb),
+            k3 = RO::coefv(c3, T(0), xb);
+  // the fast march: no band row at y = 0 / ny-1 and no global boundary plane anywhere in the chunk
+  const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
+  const bool zint = zs - K + gzoff >= 1 && ze + K - 1 + gzoff <= gnz - 2;
+  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(rown, ny - y0)) : 0;
+  int nst = 0;
+
+  const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
+  auto issue = [&](int lz, int buf) {
+    const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
+#pragma unroll
+    for (int j = 0; j < (RB + WB - 1) / WB; ++j) {
+      const int k = w + j * WB;
+      if (k < RB) {
+        const int y = yb - K + k;
+        const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
+        const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xcb);
+        dcheck(g, in, a, N);
+        glds16(a, &win[buf][k][0]);
+      }
+    }
+  };
+
+  const int qdma = ze - 1 + K;    // last u0 plane any valid output needs
+  const int qend = ze - 1 + LAG;  // the step that finishes the chunk's last output plane
+  issue(zs - K, 0);
+  T* ob = out + (int64_t)y0 * pitch;
+  const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
+  double acc = 0.0;
+  typedef __attribute__((address_space(3))) V LV;
+  LV* const wrow = lds_vptr(&win[0][y0 - yb][lane]);
+  const int wu = w > 0 ? w - 1 : 0, wd = w < WB - 1 ? w : WB - 2;
+  LV* const s_first = lds_vptr(&seam[0][0][wu][0][lane]);
+  LV* const s_last = lds_vptr(&seam[0][0][wd][1][lane]);
+  constexpr int WIN_BUF = RB * 64;
+  constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
+  auto st = [](LV* p, const V& v) {
+    asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+  };
+  auto hs = [](const Row& v) -> Row { return RO::hsum(v, lane_up1(RO::last(v)), lane_down1(RO::first(v))); };
+
+  auto march = [&](auto role_c, auto gen_c) __attribute__((always_inline)) {
+    constexpr int ROLE = decltype(role_c)::value;
+    constexpr bool GEN = decltype(gen_c)::value;  // held rows / planes may occur
+    using SH = WxRows<ROLE, RY, RE, K>;
+    // per level l (index l-1): running sums S, the last two A (ping-pong), and for l < K the two
+    // stored output planes H (ping-pong) the level above reads
+    Row S[K][NM], Ap[K][2][NM], H[K - 1][2][NM];
+#pragma unroll
+    for (int l = 0; l < K; ++l)
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        S[l][i] = Ap[l][0][i] = Ap[l][1][i] = RO::zero();
+        if (l < K - 1) H[l][0][i] = H[l][1][i] = RO::zero();
+      }
+    auto step = [&](int q, auto par_c) __attribute__((always_inline)) {
+      constexpr int P = decltype(par_c)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      wait_vm_le(nst);
+      lds_barrier();
+      if (q < qdma) issue(q + 1, P ^ 1);
+      const int lzo = q - LAG;  // level K's output plane
+      const bool valid = lzo >= zs && lzo < ze;
+      // levels top-down: level l reads its inputs (the level below's plane from the previous step)
+      // before that level overwrites its other stored plane
+#pragma unroll
+      for (int l = K; l >= 1; --l) {
+        const int m = q - (2 * l - 1);  // output plane of level l; its inputs are plane p = m + 1
+        T zm = T(1), zp = T(1);
+        bool zhp = false;
+        if (GEN) {
+          const int gm = m + gzoff, gp = m + 1 + gzoff;
+          zm = (gm <= 0 || gm >= gnz - 1) ? T(0) : T(1);
+          zhp = gp <= 0 || gp >= gnz - 1;
+          zp = zhp ? T(0) : T(1);
+        }
+        // input rows of level l-1 at plane p: rows lo(l)-1 .. hi(l)
+        auto vin = [&](int i) -> Row {
+          if (l == 1) return RO::fromv(V(wrow[P * WIN_BUF + (i + K) * 64]));
+          const int j = l - 1;
+          if (i < SH::lo(j)) return RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
+          if (i >= SH::hi(j)) return RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
+          return H[j - 1][P ^ 1][i - SH::lo(j)];
+        };
+        Row vm = vin(SH::lo(l) - 1), vc = vin(SH::lo(l));
+        Row hm = hs(vm), hc = hs(vc);
+#pragma unroll
+        for (int i = SH::lo(l); i < SH::hi(l); ++i) {
+          const int il = i - SH::lo(l);
+          const Row vp = vin(i + 1);
+          const Row hp = hs(vp);
+          const Row cross = RO::add(hc, RO::add(vm, vp));
+          const Row diag = RO::add(hm, hp);
+          Row a, bb;
+          const bool yh = GEN && (y0 + i == 0 || y0 + i == ny - 1);
+          if (yh) {
+            a = RO::zero();
+            bb = vc;
+          } else {
+            a = RO::lin3r(vc, cross, diag, k1, k2, k3);   // sm::box27_A
+            bb = RO::lin3r(vc, cross, diag, k0, k1, k2);  // sm::box27_B
+          }
+          if (GEN && zhp) bb = vc;
+          // u_l(m) = (A(m-1) + B(m)) + A(m+1), then S(p) = A(m) + B(p)
+          const Row o = GEN ? RO::fmaz(zm, a, S[l - 1][il]) : RO::add(S[l - 1][il], a);
+          S[l - 1][il] = GEN ? RO::fmaz(zp, Ap[l - 1][P ^ 1][il], bb) : RO::add(Ap[l - 1][P ^ 1][il], bb);
+          Ap[l - 1][P][il] = a;
+          if (l == K) {
+            if (valid && i >= 0 && i < SH::R && y0 + i < ny && own) {
+              T* ad = (T*)((char*)(ob + (int64_t)lzo * plane + (int64_t)i * pitch) + xob);
+              dcheck(g, (const T*)out, ad, N);
+              store_nt((V*)ad, RO::vec(o));
+              if (RES) {
+                const Row& cen = H[K - 2][P][i - SH::lo(K - 1)];  // u_{K-1}(m): still the stored plane m
+#pragma unroll
+                for (int e = 0; e < N; ++e)
+                  if (x + e < g.nx) {
+                    const double d = (double)RO::get(o, e) - (double)RO::get(cen, e);
+                    acc += d * d;
+                  }
+              }
+            }
+          } else {
+            H[l - 1][P][il] = o;
+            if (ROLE != 0 && i == 0) st(s_first + P * SEAM_PAR + (l - 1) * SEAM_LVL, RO::vec(o));
+            if (ROLE != 2 && i == SH::R - 1) st(s_last + P * SEAM_PAR + (l - 1) * SEAM_LVL, RO::vec(o));
+          }
+          vm = vc;
+          vc = vp;
+          hm = hc;
+          hc = hp;
+        }
+      }
+      nst = valid ? nsto : 0;
+    };
+    for (int q = zs - K; q <= qend; q += 2) {
+      step(q, IC<0>{});
+      step(q + 1, IC<1>{});
+    }
+  };
+  const bool fast = yint && zint;
+  if (w == 0) {
+    if (fast) march(IC<0>{}, std::false_type{});
+    else march(IC<0>{}, std::true_type{});
+  } else if (w == WB - 1) {
+    if (fast) march(IC<2>{}, std::false_type{});
+    else march(IC<2>{}, std::true_type{});
+  } else {
+    if (fast) march(IC<1>{}, std::false_type{});
+    else march(IC<1>{}, std::true_type{});
+  }
+  wait_vm0();
+  if (RES) wave_atomic_add(resid, acc);
+}
+
+template <class T, int RY, int RE, int K, int WB>
+static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf, double* resid, hipStream_t s) {
+  constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  constexpr int BR = 2 * RE + (WB - 2) * RY;
+  const int64_t planes = g.lz_end - g.lz_begin;
+  const int64_t planes2 = g.lz2_end > g.lz2_begin ? g.lz2_end - g.lz2_begin : 0;
+  const int XT = (int)((g.nx + SEG - 1) / SEG);
+  const int YT = (int)((g.ny + BR - 1) / BR);
+  const int64_t tiles = (int64_t)XT * YT;
+  const void* kfn = (const void*)&box27_wxk<T, RY, RE, K, WB, false>;
+  const int64_t resident = resident_blocks(kfn, 64 * WB);
+  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, resident, K, 3 * K - 1, hip_min_rounds_now());
+  if (planes2 > 0) zc = (int)std::max(planes, planes2);
+  const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
+  const int64_t ntasks = tiles * ZT;
+  if (knobs().debug_zc)
+    fprintf(stderr, "[mdfx] box27_wxk K=%d RY=%d RE=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d\n", K, RY,
+            RE, WB, (long long)planes, XT, YT, (long long)resident, zc);
+  MDFX_CHECK(ntasks < (int64_t)1 << 31, "box27_wxk: too many tasks");
+  const dim3 grd((unsigned)ntasks), blk(64 * WB);
+  const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
+  if (resid)
+    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
+                       (int)ntasks, resid);
+  else
+    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
+                       (int)ntasks, resid);
+}
+
+template <class T>
+void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, int steps, double* resid,
+                      hipStream_t s) {
+  if (g.lz_end <= g.lz_begin) return;
+  MDFX_CHECK(steps == 3 && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+             format("box27_wxk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
+                    (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
+  MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
+             "box27_wxk: the second region must follow the first and have its planes + ghosts allocated");
+  MDFX_CHECK(g.pitch % VT<T>::N == 0, "box27_wxk: the row pitch must be a whole number of vectors");
+  MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
+                 g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
+             "box27_wxk: row / plane counts must fit 32-bit indices");
+  // 2-row inner waves, 1-row edge waves, bands of 8 (14 rows): the 3-row shapes need more than
+  // 256 VGPRs
+  launch_b27x<T, 2, 1, 3, 8>(g, in, out, cf, resid, s);
+}
+template void launch_box27_wxk<float>(const Geo&, const float*, float*, const StencilCoef&, int, double*, hipStream_t);
+template void launch_box27_wxk<double>(const Geo&, const double*, double*, const StencilCoef&, int, double*, hipStream_t);
+
+}  // namespace dev
+}  // namespace mdfx

@@ -43,6 +43,7 @@
 
 #include "kcommon.hpp"
 #include "rowops.hpp"
+#include "wxk_common.hpp"
 #include "mdfx/kernels.hpp"
 #include "mdfx/stencil_math.hpp"
 
@@ -51,22 +52,6 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 int hip_min_rounds_now();
-
-// rows of level l (1..K) a wave computes, relative to its first own row y0: [lo, hi)
-// ROLE 0 = the band's first wave (trapezoid above), 1 = inner waves, 2 = the band's last wave.
-// Inner waves own RY rows, the two edge waves RE: an edge wave also computes the K-l trapezoid
-// rows outside the band at level l, so RE < RY evens out the waves' work per plane (every wave
-// waits for the slowest at the plane barrier)
-template <int ROLE, int RY, int RE, int K>
-struct WxRows {
-  static constexpr int R = ROLE == 1 ? RY : RE;  // own rows
-  static constexpr int lo(int l) { return ROLE == 0 ? -(K - l) : 0; }
-  static constexpr int hi(int l) { return R + (ROLE == 2 ? K - l : 0); }
-  static constexpr int n(int l) { return hi(l) - lo(l); }
-};
-
-template <int V>
-using IC = std::integral_constant<int, V>;
 
 template <class T, int RY, int RE, int K, int WB, bool RES>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
@@ -298,27 +283,6 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   if (RES) wave_atomic_add(resid, acc);
 }
 
-struct WxkPlan {
-  int zc = 0;
-};
-// chunked schedule: z chunks minimising rounds x (zc + 2K) (as heat7_wtk's wtk_plan, chunked)
-static int wxk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int min_rounds) {
-  const int64_t fill = 2 * K;
-  const int64_t zmax = std::max<int64_t>(1, planes / (4 * K));
-  double best = 1e300;
-  int64_t bz = 1;
-  for (int64_t zt = 1; zt <= zmax; ++zt) {
-    const int64_t rounds = (tiles * zt + resident - 1) / resident;
-    if (rounds < min_rounds && zt < zmax) continue;
-    const double t = (double)rounds * (double)((planes + zt - 1) / zt + fill);
-    if (t < best * 0.999) {
-      best = t;
-      bz = zt;
-    }
-  }
-  return (int)((planes + bz - 1) / bz);
-}
-
 template <class T, int RY, int RE, int K, int WB>
 static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
@@ -330,7 +294,7 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   const int64_t tiles = (int64_t)XT * YT;
   const void* kfn = (const void*)&heat7_wxk<T, RY, RE, K, WB, false>;
   const int64_t resident = resident_blocks(kfn, 64 * WB);
-  int zc = knobs().zc > 0 ? knobs().zc : wxk_zc(planes, tiles, resident, K, hip_min_rounds_now());
+  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, resident, K, 2 * K, hip_min_rounds_now());
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = tiles * ZT;
@@ -339,8 +303,11 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
             K, RY, RE, WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
-  if constexpr (K == 5) {  // (its residual instance needs more than 256 VGPRs)
-    MDFX_CHECK(!resid, "heat7_wxk: no residual variant of the 5-step sweep (use --temporal 4 with a residual)");
+  // shapes whose residual instance would need more than 256 VGPRs have none (their callers send
+  // residual sweeps to a smaller shape)
+  constexpr bool kNoRes = K == 5 || (K == 4 && RY == 4);
+  if constexpr (kNoRes) {
+    MDFX_CHECK(!resid, "heat7_wxk: no residual variant of this shape (the 5-step sweep: use --temporal 4 with a residual)");
   } else if (resid) {
     hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
     return;
@@ -388,7 +355,8 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
       if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
       else if (ry == 31 || (ry == 0 && g.nx <= 512)) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
       else if (ry == 21) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
-      else if (ry == 32) launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 42 && !resid) launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 32 || ry == 42) launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
       else launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
     }
   } else {

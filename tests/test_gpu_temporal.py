@@ -475,7 +475,7 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
 @pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=300, ny=33, nz=9, dtype="f64")],
                          ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k,wb,ry", [(3, "8", "0"), (3, "8", "3"), (3, "4", "0"), (4, "8", "0"), (4, "8", "31"),
-                                     (4, "8", "21"), (4, "8", "32"), (4, "4", "0"), (5, "8", "0")])
+                                     (4, "8", "21"), (4, "8", "32"), (4, "8", "42"), (4, "4", "0"), (5, "8", "0")])
 @pytest.mark.parametrize("resid", [False, True])
 def test_heat7_wxk_bitwise(hip, prob, k, wb, ry, resid, knob):
     """heat7_wxk (y halo exchanged between the waves of a band through the LDS seam table, one
@@ -507,6 +507,66 @@ def test_heat7_wxk_bitwise(hip, prob, k, wb, ry, resid, knob):
     assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb, ry)
     if resid:
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
+B27X = [models.box27(n=40), models.box27(n=24, dtype="f64"), models.box27(nx=700, ny=37, nz=15),
+        models.box27(nx=1030, ny=9, nz=12), models.box27(nx=300, ny=70, nz=10, dtype="f64"),
+        models.box27(nx=8, ny=5, nz=9)]
+
+
+@pytest.mark.parametrize("prob", B27X, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("resid", [False, True])
+def test_box27_wxk_bitwise(hip, prob, resid):
+    """box27_wxk (27-point, K = 3, y halo exchanged through the LDS seam table, levels above the
+    first one plane later) == 3 naive box27 steps, bitwise, with the residual of step 3."""
+    k = 3
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res if resid else None)
+    set_kernel_variant("naive")
+    try:
+        cur = src.clone()
+        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+        for i in range(k):
+            nxt = cur.clone()
+            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx])
+    if resid:
+        assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
+def test_box27_wxk_regions_and_engine(hip, knob):
+    """box27_wxk on a middle slab (both boundary regions in one launch + the interior) == the
+    whole grid, and a 3-slab engine run at the 27-point's fused depth 3 == single steps."""
+    k = 3
+    prob = models.box27(nx=600, ny=30, nz=40)
+    full = FieldLayout.make(prob, halo=k)
+    g = alloc_field(full, "cuda")
+    init_field(prob, full, g)
+    ref = alloc_field(full, "cuda")
+    apply_stencil(prob, full, g, ref, steps=k)
+    lay = FieldLayout.make(prob, 12, 30, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    out = alloc_field(lay, "cuda")
+    h = lay.halo
+    apply_stencil(prob, lay, src, out, h, h + k, steps=k, second=(h + 18 - k, h + 18))
+    apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k)
+    torch.cuda.synchronize()
+    assert torch.equal(out[h:h + 18, :, :600], ref[12 + k:30 + k, :, :600])
+    knob("MDFX_B27_WXK", 1)
+    p3 = models.box27(nx=500, ny=33, nz=45)
+    a, _ = _sim(p3, 6, ranks=1)
+    b, _ = _sim(p3, 6, ranks=3, temporal=3)
+    assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("k", [3, 4])
