@@ -84,7 +84,7 @@ static Knobs read_knobs() {
   k.h7_wtk = env_int("MDFX_H7_WTK", 0);
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
-  k.b27_wxk = env_int("MDFX_B27_WXK", 0);
+  k.b27_wxk = env_int("MDFX_B27_WXK", -1);
   k.wxk_ry = env_int("MDFX_WXK_RY", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
@@ -277,7 +277,14 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
   switch (spec.kind) {
     case StencilKind::Jacobi5: return 8;
     case StencilKind::Life: return 12;
-    case StencilKind::Box27: return dev::knobs().b27_wxk == 1 ? 3 : 2;
+    case StencilKind::Box27:
+      // K = 3 through box27_wxk for fp64 (512^3: 663 vs 527 GCells/s for box27_tbk K = 2) and for
+      // fp32 rows of 1024 cells and more (1024^3: 1291 vs 1102); at 512-cell rows its overlapping x
+      // segments waste a third of the lanes and box27_tb2n's K = 2 stays ahead (1074 vs 1027)
+      // (profiles/r03_wxk/). MDFX_B27_WXK = 0 / 1 forces K = 2 / 3
+      if (dev::knobs().b27_wxk == 1) return 3;
+      if (dev::knobs().b27_wxk == 0) return 2;
+      return (spec.dtype == DType::F64 || nx >= 1024) ? 3 : 2;
     case StencilKind::Heat7:
       // K = 3 through heat7_wtk wherever its x segments cover at least 2/3 of the lane cells:
       // 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2 (round 2), 2048^3 fp32 1666 vs 1136,

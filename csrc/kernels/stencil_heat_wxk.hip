@@ -283,24 +283,38 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   if (RES) wave_atomic_add(resid, acc);
 }
 
+// launch geometry of one shape: tiles, z chunks, and the rounds of resident blocks they take
+struct WxGeo {
+  int XT = 0, YT = 0, zc = 0;
+  int64_t ntasks = 0, resident = 0, rounds = 0;
+};
 template <class T, int RY, int RE, int K, int WB>
-static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+static WxGeo wxk_geo(const Geo& g) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  constexpr int BR = 2 * RE + (WB - 2) * RY;
+  WxGeo w;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int64_t planes2 = g.lz2_end > g.lz2_begin ? g.lz2_end - g.lz2_begin : 0;
-  const int XT = (int)((g.nx + SEG - 1) / SEG);
-  constexpr int BR = 2 * RE + (WB - 2) * RY;
-  const int YT = (int)((g.ny + BR - 1) / BR);
-  const int64_t tiles = (int64_t)XT * YT;
-  const void* kfn = (const void*)&heat7_wxk<T, RY, RE, K, WB, false>;
-  const int64_t resident = resident_blocks(kfn, 64 * WB);
-  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, resident, K, 2 * K, hip_min_rounds_now());
-  if (planes2 > 0) zc = (int)std::max(planes, planes2);
-  const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
-  const int64_t ntasks = tiles * ZT;
+  w.XT = (int)((g.nx + SEG - 1) / SEG);
+  w.YT = (int)((g.ny + BR - 1) / BR);
+  const int64_t tiles = (int64_t)w.XT * w.YT;
+  w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false>, 64 * WB);
+  w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, hip_min_rounds_now());
+  if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
+  const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
+  w.ntasks = tiles * ZT;
+  w.rounds = (w.ntasks + w.resident - 1) / w.resident;
+  return w;
+}
+
+template <class T, int RY, int RE, int K, int WB>
+static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  const WxGeo wg = wxk_geo<T, RY, RE, K, WB>(g);
+  const int XT = wg.XT, YT = wg.YT, zc = wg.zc;
+  const int64_t ntasks = wg.ntasks;
   if (knobs().debug_zc)
     fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
-            K, RY, RE, WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
+            K, RY, RE, WB, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   // shapes whose residual instance would need more than 256 VGPRs have none (their callers send
@@ -350,14 +364,29 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
     } else if (steps == 5) {
       launch_wxk<T, 2, 1, 5, 8>(g, in, out, r, resid, s);
     } else {
-      // 2-row waves (1024^3: 2212-2262 GCells/s vs 2150-2162 for 3-row inner waves with 1-row edge
-      // waves); at rows of 512 cells and less the 3 + 1 band (512^3: 1863 vs 1746)
-      if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
-      else if (ry == 31 || (ry == 0 && g.nx <= 512)) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
-      else if (ry == 21) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
-      else if (ry == 42 && !resid) launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
-      else if (ry == 32 || ry == 42) launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
-      else launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
+      // bands of 4 + 6 x 3 + 4 rows (inner waves 3 or 4 rows, edge waves 2): 1024^3 2415-2454 /
+      // 2387-2394 GCells/s (2 + 2: 2247-2253); on thin slabs the band height decides how many
+      // tiles fill one round of resident blocks (N = 8 proxy: 1798 with 3-row, 1657 with 4-row
+      // waves). The shape is picked per launch by rounds x (chunk + fill) x the shape's measured
+      // time per block step (4-row bands 1.25x the 3-row ones, 2-row 0.77x), profiles/r03_wxk/.
+      if (wb == 4) {
+        launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
+      } else if (ry == 31) {
+        launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
+      } else if (ry == 21) {
+        launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
+      } else if (ry == 22) {
+        launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
+      } else if (ry == 32 || resid) {  // (the 4-row shape has no residual instance)
+        launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
+      } else if (ry == 42) {
+        launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
+      } else {
+        auto cost = [](const WxGeo& w, double c) { return (double)w.rounds * (double)(w.zc + 8) * c; };
+        const double c32 = cost(wxk_geo<T, 3, 2, 4, 8>(g), 1.0), c42 = cost(wxk_geo<T, 4, 2, 4, 8>(g), 1.25);
+        if (c42 < c32) launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
+        else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
+      }
     }
   } else {
     launch_wxk<T, 2, 2, 3, 8>(g, in, out, r, resid, s);
