@@ -293,7 +293,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // where heat7_wxk runs (fp32): its per-wave rows no longer grow with K, so the fourth step
       // per pass costs less than the HBM pass it saves
       if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
-        return dev::use_wxk(spec.dtype) ? 4 : 3;
+        return (dev::use_wxk(spec.dtype) && spec.dtype == DType::F32) ? 4 : 3;  // (fp64 K = 4 only in 1-row waves)
       return 2;
   }
   return 1;

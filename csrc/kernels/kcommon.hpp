@@ -220,7 +220,7 @@ struct Knobs {
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64 and rows >= 1024; 0 / 1)
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
   int wxk_ry = 0;      // MDFX_WXK_RY: heat7_wxk fp32 band (K = 3: 3 = 3-row waves; K = 4: 42 / 32 / 22 / 31 / 21 =
-                       // inner / edge rows; 0: by a cost model)
+                       // inner / edge rows; 0: 32)
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)
   int j5_nat = 2;      // MDFX_J5_NAT: jacobi5_tbk fp32 rows: 2 natural layout + 2-row unroll, 1 natural, 0 round 2's pair layout

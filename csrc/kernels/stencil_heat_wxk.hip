@@ -31,6 +31,11 @@
 // coefficient; the band-edge waves' trapezoid rows outside the grid read clamped (finite) rows and
 // never feed an unheld cell.
 //
+// The band's first, inner and last waves run different compiled copies of the march (their row
+// counts differ). Each copy executes exactly one s_barrier per plane step over the same block-
+// uniform step range, and gfx9's s_barrier counts arriving waves rather than requiring one code
+// path, so the copies meet at every barrier (tests: bands with every role, tall and short grids).
+//
 // Region contract (as heat7_wtk): output storage planes [lz_begin, lz_end) (and optionally a
 // second region [lz2_begin, lz2_end)) need u0 valid on [lz_begin - K, lz_end + K).
 //
@@ -364,29 +369,17 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
     } else if (steps == 5) {
       launch_wxk<T, 2, 1, 5, 8>(g, in, out, r, resid, s);
     } else {
-      // bands of 4 + 6 x 3 + 4 rows (inner waves 3 or 4 rows, edge waves 2): 1024^3 2415-2454 /
-      // 2387-2394 GCells/s (2 + 2: 2247-2253); on thin slabs the band height decides how many
-      // tiles fill one round of resident blocks (N = 8 proxy: 1798 with 3-row, 1657 with 4-row
-      // waves). The shape is picked per launch by rounds x (chunk + fill) x the shape's measured
-      // time per block step (4-row bands 1.25x the 3-row ones, 2-row 0.77x), profiles/r03_wxk/.
-      if (wb == 4) {
-        launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
-      } else if (ry == 31) {
-        launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
-      } else if (ry == 21) {
-        launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
-      } else if (ry == 22) {
-        launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
-      } else if (ry == 32 || resid) {  // (the 4-row shape has no residual instance)
-        launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
-      } else if (ry == 42) {
-        launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
-      } else {
-        auto cost = [](const WxGeo& w, double c) { return (double)w.rounds * (double)(w.zc + 8) * c; };
-        const double c32 = cost(wxk_geo<T, 3, 2, 4, 8>(g), 1.0), c42 = cost(wxk_geo<T, 4, 2, 4, 8>(g), 1.25);
-        if (c42 < c32) launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
-        else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
-      }
+      // bands of 2 + 6 x 3 + 2 rows (3-row inner waves, 2-row edge waves): 1024^3 2387-2394
+      // GCells/s on every box measured; 4-row inner waves ran 2415-2454 on one box and 2095-2138 on
+      // two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row
+      // band also fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
+      // (profiles/r03_wxk/). MDFX_WXK_RY picks another shape.
+      if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
+      else if (ry == 31) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 21) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 22) launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
+      else if (ry == 42 && !resid) launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
+      else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
     }
   } else {
     launch_wxk<T, 2, 2, 3, 8>(g, in, out, r, resid, s);
