@@ -43,6 +43,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   if (spec_.kind != StencilKind::Life)
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 16, "temporal blocking depth must be 1..16");
+  if (const char* v = std::getenv("MDFX_BND_FIRST")) bnd_first_ = std::atoi(v) != 0;
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
@@ -301,7 +302,10 @@ void Solver::step(bool want_resid, int k) {
     if (prof && !prof_hip && &s == &slabs_[0]) c1 = clk::now();
     // compute stream: interior, after the previous step's boundary kernels
     void* is = opt_.overlap ? s.cs : s.hs;
-    if (opt_.overlap) s.be->wait(s.cs, s.ev_bnd);
+    if (opt_.overlap) {
+      if (bnd_first_) s.be->record(s.ev_bnd, s.hs);  // this step's boundary kernels
+      s.be->wait(s.cs, s.ev_bnd);
+    }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)is));
     if (s.in_e > s.in_b) {
       a.lz_begin = s.in_b;

@@ -143,6 +143,11 @@ class Solver {
   PhaseStats phases_;
   void* pev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // timing events (slab 0)
   bool ghosts_dirty_ = false;
+  // overlapped schedule: the interior sweep of a step waits for the SAME step's boundary kernels
+  // (MDFX_BND_FIRST=1, default) instead of the previous step's, so the short boundary launch gets
+  // the whole device before the long interior sweep takes every CU; the exchange still runs under
+  // the interior (profiles/r03_wxk/)
+  bool bnd_first_ = true;
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
   // hipGraphExec_t of the 2-sweep cycle starting at buffer p (index p), and its fused depth
   void* graph_exec_[2] = {nullptr, nullptr};

@@ -474,7 +474,7 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
 
 @pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=300, ny=33, nz=9, dtype="f64")],
                          ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("k,wb,ry", [(3, "8", "0"), (3, "8", "3"), (3, "4", "0"), (4, "8", "0"), (4, "8", "31"),
+@pytest.mark.parametrize("k,wb,ry", [(3, "8", "0"), (3, "8", "3"), (3, "8", "32"), (3, "8", "31"), (3, "4", "0"), (4, "8", "0"), (4, "8", "31"),
                                      (4, "8", "21"), (4, "8", "32"), (4, "8", "42"), (4, "8", "22"), (4, "4", "0"),
                                      (5, "8", "0")])
 @pytest.mark.parametrize("resid", [False, True])
