@@ -15,17 +15,19 @@ larger than the visible GPU count is an error, never a silent 1-GPU run.
 Correctness gate (N > 1). Before timing, every rank runs a small decomposed problem of the same
 stencil (256 x 256 x 64N, 6 fused sweeps, residual included) through the SAME transport, and
 compares its owned planes bitwise against a full-grid single-slab run on its own GPU. Any mismatch
-on any rank aborts the run non-zero. With --transport auto the transports are tried in order
-(rccl, then ipc on GPUs) and the first that passes the gate is timed; the JSON names it.
+on any rank aborts the run non-zero. With --transport auto every device transport (rccl, ipc) is
+gated, the ones that pass get short timed trials and the fastest is timed; the JSON names it. If
+neither passes, the host-staged transport (faces through host memory over gloo) is gated as a
+last resort, so a node whose xGMI paths fail still yields a correct (slow, labelled) number.
 
 The grid is fixed as N grows (strong scaling, the BASELINE.json config "3D 7-pt Jacobi 1024^3 fp32
 slab-decomposed across 8xMI355X"). Data is synthetic: a uniform random initial grid generated on
 the device from a counter-based hash of the global cell index (seed 1). Every timed step is a full
 Jacobi update of every cell (boundary planes + halo exchange + interior), nothing is skipped or
-cached. By default three consecutive Jacobi steps are fused into one pass over memory (temporal
-blocking, --temporal 3 through heat7_wtk; bitwise identical to three single steps,
-tests/test_gpu_temporal.py): every step is still computed in full, the fused kernel keeps u^{t+1}
-and u^{t+2} on chip. A step count that is not a multiple of 3 ends with a shorter fused sweep.
+cached. By default four consecutive Jacobi steps are fused into one pass over memory (temporal
+blocking, --temporal 4 through heat7_wxk at 1024-cell rows; bitwise identical to four single
+steps, tests/test_gpu_temporal.py): every step is still computed in full, the fused kernel keeps
+u^{t+1}..u^{t+3} on chip. A step count that is not a multiple of 4 ends with a shorter fused sweep.
 --temporal 1 measures one sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
 torch.cuda.synchronize() on both sides; the slowest rank's time is reported. GCells/s =
 nx*ny*nz*K / t / 1e9 for the whole job. Rank 0 prints one JSON line. The DRAM fields report the
@@ -220,6 +222,10 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False):
     tag = transport + ("+graph" if graph else "")
     ok = False
     try:
+        fault = os.environ.get("MDFX_FAULT", "")
+        if fault.startswith("gate:") and transport in fault[5:].split(","):
+            # fault injection for the fallback test: this transport's gate fails on every rank
+            raise RuntimeError("injected gate failure (MDFX_FAULT=%s)" % fault)
         with Simulation(prob, distributed=True, transport=transport, graph=graph, **kw) as sim:
             trace("gate: engine up")
             sim.init()
@@ -429,6 +435,14 @@ def main(argv=None):
             recs.append(rec)
             if passed:
                 ok.append((t, g))
+        if not ok and a.transport == "auto" and hip:
+            # last resort: faces staged through host memory over the gloo group. Slow, but a
+            # correct number rather than none when neither device transport works on this node
+            trace("gate staged (fallback)")
+            passed, rec = run_gate(a, hip, "staged", temporal, world, rank, graph=False)
+            recs.append(rec)
+            if passed:
+                ok.append(("staged", False))
         gate = {"passed": bool(ok), "runs": recs}
         if not ok:
             if rank == 0:

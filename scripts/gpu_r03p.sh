@@ -4,7 +4,8 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
-scripts/gpu_session.sh "wxk=$PYT tests/test_gpu_temporal.py -k 'wxk' tests/test_gpu_engine.py tests/test_gpu_proxy.py" || exit $?
+scripts/gpu_session.sh "wxk=$PYT tests/test_gpu_temporal.py -k 'wxk' tests/test_gpu_engine.py tests/test_gpu_proxy.py" "fallback=$PYT tests/test_gpu_multiprocess.py -k 'fallback or bootstrap'" || exit $?
+grep -q ' passed' gpurun_out/fallback.log && ! grep -q 'failed' gpurun_out/fallback.log || { tail -30 gpurun_out/fallback.log; exit 1; }
 grep -q ' passed' gpurun_out/wxk.log && ! grep -q 'failed' gpurun_out/wxk.log || { tail -30 gpurun_out/wxk.log; exit 1; }
 B="python bench.py --steps 48 --warmup 12"
 P="python bench.py --steps 48 --warmup 12 --rank-proxy"

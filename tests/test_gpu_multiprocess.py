@@ -173,3 +173,20 @@ def test_bench_rccl_bootstrap_hang_exits_nonzero(hip):
     assert p.returncode != 0, p.stdout.decode()
     assert not [l for l in p.stdout.decode().splitlines() if l.startswith("{")]
     assert took < 300, took
+
+
+@pytest.mark.timeout(300)
+def test_bench_auto_falls_back_to_staged(hip):
+    """--transport auto when both device transports fail their gate (MDFX_FAULT=gate:rccl,ipc):
+    the host-staged transport is gated as a last resort and timed, and the JSON names it."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["MDFX_FAULT"] = "gate:rccl,ipc"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--n", "128",
+                        "--steps", "4", "--warmup", "2", "--graph", "off"], env=env, capture_output=True, timeout=280,
+                       cwd=ROOT)
+    out = p.stdout.decode()
+    assert p.returncode == 0, out + p.stderr.decode()
+    rec = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    assert rec["config"]["transport"] == "torch" and rec["config"]["gate"]["passed"]
+    runs = rec["config"]["gate"]["runs"]
+    assert [r["transport"] for r in runs] == ["rccl", "ipc", "staged"] and runs[-1]["passed"]
