@@ -58,14 +58,18 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
 double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
 // 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
-static bool use_wxk(DType dt);
+static bool use_wxk(DType dt, int64_t nx = 0);
 static bool use_wtk(int steps, DType dt) {
   return knobs().h7_wtk >= 0 && (heat7_wtk_supported(steps) || (steps == 5 && dt == DType::F32 && use_wxk(dt)));
 }
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
 // 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
-// 0 / 1 forces it off / on (fp64 on: K = 3 only, heat7_wtk's K = 4)
-static bool use_wxk(DType dt) { return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && dt == DType::F32); }
+// 0 / 1 forces it off / on (fp64 on: K = 3 only, heat7_wtk's K = 4). fp64 takes it from 2048-cell
+// rows on, in 3 + 1-row bands: 2048^3 fp64 + residual every 12 897 vs 796 GCells/s for heat7_wtk,
+// while at 1024-cell rows heat7_wtk's 3-row waves stay ahead (907 vs 874) (profiles/r03_session_p/)
+static bool use_wxk(DType dt, int64_t nx) {
+  return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (dt == DType::F32 || nx >= 2048));
+}
 // (K = 5: fp32 heat7_wxk only)
 
 static int env_int(const char* name, int dflt) {
@@ -293,7 +297,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // where heat7_wxk runs (fp32): its per-wave rows no longer grow with K, so the fourth step
       // per pass costs less than the HBM pass it saves
       if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
-        return (dev::use_wxk(spec.dtype) && spec.dtype == DType::F32) ? 4 : 3;  // (fp64 K = 4 only in 1-row waves)
+        return (dev::use_wxk(spec.dtype, nx) && spec.dtype == DType::F32) ? 4 : 3;  // (fp64 K = 4 only in 1-row waves)
       return 2;
   }
   return 1;
@@ -305,7 +309,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
     // slab: one fill of the device, one launch gap); every other kernel runs them one after the other
     const bool fuse = a.lz_end > a.lz_begin &&
                       ((a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps, spec.dtype) &&
-                        (dev::knobs().fuse_regions || dev::use_wxk(spec.dtype))) ||
+                        (dev::knobs().fuse_regions || dev::use_wxk(spec.dtype, a.lay.global.nx))) ||
                        (spec.kind == StencilKind::Box27 && a.steps == 3));
     if (!fuse) {
       RegionArgs r1 = a, r2 = a;
@@ -360,7 +364,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
       }
-    } else if (dev::use_wtk(a.steps, spec.dtype) && dev::use_wxk(spec.dtype)) {
+    } else if (dev::use_wtk(a.steps, spec.dtype) && dev::use_wxk(spec.dtype, a.lay.global.nx)) {
       if (spec.dtype == DType::F32)
         dev::launch_heat7_wxk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
       else

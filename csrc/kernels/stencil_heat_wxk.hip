@@ -382,9 +382,10 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
       else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
     }
   } else {
+    // fp64 K = 3: 3 + 1-row bands by default (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2)
     if (ry == 32) launch_wxk<T, 3, 2, 3, 8>(g, in, out, r, resid, s);
-    else if (ry == 31) launch_wxk<T, 3, 1, 3, 8>(g, in, out, r, resid, s);
-    else launch_wxk<T, 2, 2, 3, 8>(g, in, out, r, resid, s);
+    else if (ry == 22) launch_wxk<T, 2, 2, 3, 8>(g, in, out, r, resid, s);
+    else launch_wxk<T, 3, 1, 3, 8>(g, in, out, r, resid, s);
   }
 }
 template void launch_heat7_wxk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);

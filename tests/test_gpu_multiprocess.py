@@ -176,7 +176,7 @@ def test_bench_rccl_bootstrap_hang_exits_nonzero(hip):
 
 
 @pytest.mark.timeout(300)
-def test_bench_auto_falls_back_to_staged(hip):
+def test_bench_auto_fallback_to_staged(hip):
     """--transport auto when both device transports fail their gate (MDFX_FAULT=gate:rccl,ipc):
     the host-staged transport is gated as a last resort and timed, and the JSON names it."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}

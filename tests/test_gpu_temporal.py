@@ -6,7 +6,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-from mpi_cuda_process_amd import models  # noqa: E402
+from mpi_cuda_process_amd import models, native  # noqa: E402
 from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, init_field,  # noqa: E402
                                       set_kernel_variant)
 
@@ -474,7 +474,7 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
 
 @pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=300, ny=33, nz=9, dtype="f64")],
                          ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("k,wb,ry", [(3, "8", "0"), (3, "8", "3"), (3, "8", "32"), (3, "8", "31"), (3, "4", "0"), (4, "8", "0"), (4, "8", "31"),
+@pytest.mark.parametrize("k,wb,ry", [(3, "8", "0"), (3, "8", "3"), (3, "8", "32"), (3, "8", "31"), (3, "8", "22"), (3, "4", "0"), (4, "8", "0"), (4, "8", "31"),
                                      (4, "8", "21"), (4, "8", "32"), (4, "8", "42"), (4, "8", "22"), (4, "4", "0"),
                                      (5, "8", "0")])
 @pytest.mark.parametrize("resid", [False, True])
@@ -506,6 +506,36 @@ def test_heat7_wxk_bitwise(hip, prob, k, wb, ry, resid, knob):
     torch.cuda.synchronize()
     o = lay.owned
     assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb, ry)
+    if resid:
+        assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
+@pytest.mark.parametrize("resid", [False, True])
+def test_heat7_fp64_wide_rows_default_path(hip, resid):
+    """fp64 rows of 2048 cells and more take heat7_wxk (3 + 1-row bands) at K = 3 by default: the
+    engine's default fused depth and kernel == 3 naive single steps, bitwise."""
+    prob = models.heat3d(nx=2048, ny=23, nz=11, dtype="f64")
+    k = 3
+    assert native().hip_fused_depth(prob.kind, prob.dtype, prob.nx, False) == k
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res if resid else None)
+    set_kernel_variant("naive")
+    try:
+        cur = src.clone()
+        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+        for i in range(k):
+            nxt = cur.clone()
+            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx])
     if resid:
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
