@@ -91,7 +91,7 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
 
 // Raw waits: s_waitcnt encodings for gfx9 (vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]).
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-// vmcnt(n) for a wave-uniform n in 0..7 (an immediate per case): wait until at most the wave's n
+// vmcnt(n) for a wave-uniform n in 0..15 (an immediate per case): wait until at most the wave's n
 // youngest vector-memory operations are outstanding. The streaming kernels issue the next plane's
 // LDS DMA first and the output stores of the plane after it; waiting with n = the stores issued
 // since the DMA leaves those stores in flight across the next plane's barrier instead of
@@ -105,6 +105,14 @@ __device__ __forceinline__ void wait_vm_le(int n) {
     case 5: __builtin_amdgcn_s_waitcnt(0x0F75); break;
     case 6: __builtin_amdgcn_s_waitcnt(0x0F76); break;
     case 7: __builtin_amdgcn_s_waitcnt(0x0F77); break;
+    case 8: __builtin_amdgcn_s_waitcnt(0x0F78); break;
+    case 9: __builtin_amdgcn_s_waitcnt(0x0F79); break;
+    case 10: __builtin_amdgcn_s_waitcnt(0x0F7A); break;
+    case 11: __builtin_amdgcn_s_waitcnt(0x0F7B); break;
+    case 12: __builtin_amdgcn_s_waitcnt(0x0F7C); break;
+    case 13: __builtin_amdgcn_s_waitcnt(0x0F7D); break;
+    case 14: __builtin_amdgcn_s_waitcnt(0x0F7E); break;
+    case 15: __builtin_amdgcn_s_waitcnt(0x0F7F); break;
     default: __builtin_amdgcn_s_waitcnt(0x0F70); break;
   }
 }
@@ -219,6 +227,7 @@ struct Knobs {
   int wtk_split = -1;  // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: -1 never (default, measured slower), 0 cost model, 1 always
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64 and rows >= 1024; 0 / 1)
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
+  int wxk_nb = 0;      // MDFX_WXK_NB: heat7_wxk fp32 K = 4 window depth x seam tables (31: 3 buffers + 1 table, 21, 32: 2 + 2 rows)
   int wxk_ry = 0;      // MDFX_WXK_RY: heat7_wxk fp32 band (K = 3: 3 = 3-row waves; K = 4: 42 / 32 / 22 / 31 / 21 =
                        // inner / edge rows; 0: 32)
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)

@@ -58,7 +58,7 @@ namespace dev {
 int64_t resident_blocks(const void* kfn, int block);
 int hip_min_rounds_now();
 
-template <class T, int RY, int RE, int K, int WB, bool RES>
+template <class T, int RY, int RE, int K, int WB, bool RES, int NB = 2, int SPAR = 2>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
@@ -71,15 +71,18 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   constexpr int RB = BR + 2 * K;              // u0 window rows of a band: yb-K .. yb+BR+K-1
   constexpr int NM = RY > RE + K - 1 ? RY : RE + K - 1;  // most rows any wave computes at level 1
   static_assert(WB >= 2 && K >= 2, "heat7_wxk: bands of at least two waves, at least two levels");
+  static_assert((NB == 2 || NB == 3) && (SPAR == 1 || SPAR == 2), "heat7_wxk: 2 or 3 window buffers, 1 or 2 seam parities");
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // work: block-uniform task = one z chunk of one (x segment, y band) tile; x segments fastest, then
   // y bands, then z chunks (the first region's chunks, then the second region's)
   const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   if (b >= ntasks) return;
-  __shared__ V win[2][RB][64];
+  // NB window buffers: the u0 plane DMA runs NB - 1 planes ahead of the plane being computed
+  __shared__ V win[NB][RB][64];
   // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
-  __shared__ V seam[2][K - 1][WB - 1][2][64];
+  // (SPAR = 1: one table, the step's seam reads and writes separated by a second barrier)
+  __shared__ V seam[SPAR][K - 1][WB - 1][2][64];
   const int tiles = XT * YT;
   const int t = b % tiles, zt = b / tiles;
   const int P0 = (int)(g.lz_end - g.lz_begin);
@@ -112,6 +115,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
   const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(rown, ny - y0)) : 0;
   int nst = 0;  // output stores issued since this wave's last DMA
+  // NB = 3: vector-memory ops this wave issued after its newest (n_last) and its second newest
+  // (n_prev) window DMA; rows of the window this wave fetches per plane
+  int n_last = 0, n_prev = 0;
+  constexpr int NDW = (RB + WB - 1) / WB;
+  const int ndma = NDW - (w + (NDW - 1) * WB >= RB ? 1 : 0);
 
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
   // read the nearest valid row / vector. Wave w fetches rows w, w + WB, ... of the window.
@@ -133,6 +141,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
 
   const int qlast = ze - 1 + K;  // last u0 plane of the march
   issue(zs - K, 0);
+  if constexpr (NB == 3) {
+    issue(zs - K + 1, 1);
+    n_prev = ndma;
+  }
+  int wcur = 0;  // NB = 3: window buffer of the current step
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
   double acc = 0.0;
@@ -146,7 +159,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   LV* const s_first = lds_vptr(&seam[0][0][wu][0][lane]);  // my first row (write, w > 0)
   LV* const s_last = lds_vptr(&seam[0][0][wd][1][lane]);   // my last row (write, w < WB-1)
   constexpr int WIN_BUF = RB * 64;  // V elements per window buffer
-  constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
+  constexpr int SEAM_PAR = SPAR == 2 ? (K - 1) * (WB - 1) * 2 * 64 : 0, SEAM_LVL = (WB - 1) * 2 * 64;
   auto st = [](LV* p, const V& v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
@@ -176,9 +189,23 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // plane q's DMA has landed (the stores issued after it stay in flight); the barrier
       // publishes it and last step's seam rows, and certifies that every wave is done with the
       // other window buffer and the other seam parity
-      wait_vm_le(nst);
+      if constexpr (NB == 2) {
+        wait_vm_le(nst);
+      } else {
+        // plane q's DMA is the second newest while plane q + 1's has been issued, else the newest
+        wait_vm_le(q + 1 <= qlast ? n_prev : n_last);
+      }
       lds_barrier();
-      if (q < qlast) issue(q + 1, P ^ 1);
+      if constexpr (NB == 2) {
+        if (q < qlast) issue(q + 1, P ^ 1);
+      } else {
+        if (q + 2 <= qlast) {
+          issue(q + 2, wcur == 0 ? 2 : wcur - 1);  // the buffer plane q - 1 used
+          n_prev = n_last + ndma;
+          n_last = 0;
+        }
+      }
+      constexpr int SR = SPAR == 2 ? (P ^ 1) : 0;  // seam parity read this step
       // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact)
       Row rl[K + 1];
 #pragma unroll
@@ -191,8 +218,8 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       for (int l = 2; l <= K; ++l) {
         const int j = l - 1;  // level of the inputs
         Row up = RO::zero(), dn = RO::zero();
-        if (ROLE != 0) up = RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
-        if (ROLE != 2) dn = RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
+        if (ROLE != 0) up = RO::fromv(seam[SR][j - 1][wu][1][lane]);
+        if (ROLE != 2) dn = RO::fromv(seam[SR][j - 1][wd][0][lane]);
 #pragma unroll
         for (int i = SH::lo(l); i < SH::hi(l); ++i) {
           const int ij = i - SH::lo(j);
@@ -206,8 +233,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
           RO::pin(a);
         }
       }
+      // one seam table: every wave has read this step's seam rows before any wave overwrites them
+      if constexpr (SPAR == 1) lds_barrier();
       // (2) level 1 row by row from the u0 window, each new row cascading up through the levels
-      auto u0row = [&](int i) -> Row { return RO::fromv(V(wrow[P * WIN_BUF + (i + K) * 64])); };
+      LV* const wbuf = NB == 2 ? wrow + P * WIN_BUF : wrow + wcur * WIN_BUF;
+      auto u0row = [&](int i) -> Row { return RO::fromv(V(wbuf[(i + K) * 64])); };
       Row X[3];
       X[0] = u0row(SH::lo(1) - 1);
       X[1] = u0row(SH::lo(1));
@@ -267,6 +297,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         }
       }
       nst = valid ? nsto : 0;
+      if constexpr (NB == 3) {
+        n_last += nst;
+        n_prev += nst;
+        wcur = wcur == 2 ? 0 : wcur + 1;
+      }
     };
     // an odd plane count ends with one extra step (q = qlast + 1): no DMA, nothing stored
     for (int q = zs - K; q <= qlast; q += 2) {
@@ -293,7 +328,7 @@ struct WxGeo {
   int XT = 0, YT = 0, zc = 0;
   int64_t ntasks = 0, resident = 0, rounds = 0;
 };
-template <class T, int RY, int RE, int K, int WB>
+template <class T, int RY, int RE, int K, int WB, int NB = 2, int SPAR = 2>
 static WxGeo wxk_geo(const Geo& g) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   constexpr int BR = 2 * RE + (WB - 2) * RY;
@@ -303,7 +338,7 @@ static WxGeo wxk_geo(const Geo& g) {
   w.XT = (int)((g.nx + SEG - 1) / SEG);
   w.YT = (int)((g.ny + BR - 1) / BR);
   const int64_t tiles = (int64_t)w.XT * w.YT;
-  w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false>, 64 * WB);
+  w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false, NB, SPAR>, 64 * WB);
   w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, hip_min_rounds_now());
   if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
@@ -312,14 +347,20 @@ static WxGeo wxk_geo(const Geo& g) {
   return w;
 }
 
-template <class T, int RY, int RE, int K, int WB>
+template <class T, int RY, int RE, int K, int WB, int NB = 2, int SPAR = 2>
 static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  const WxGeo wg = wxk_geo<T, RY, RE, K, WB>(g);
+  if constexpr (NB != 2 || SPAR != 2) {
+    if (resid) {  // (the deeper-window instances have no residual copy)
+      launch_wxk<T, RY, RE, K, WB>(g, in, out, r, resid, s);
+      return;
+    }
+  }
+  const WxGeo wg = wxk_geo<T, RY, RE, K, WB, NB, SPAR>(g);
   const int XT = wg.XT, YT = wg.YT, zc = wg.zc;
   const int64_t ntasks = wg.ntasks;
   if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
-            K, RY, RE, WB, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
+    fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d NB=%d SPAR=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
+            K, RY, RE, WB, NB, SPAR, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   // shapes whose residual instance would need more than 256 VGPRs have none (their callers send
@@ -327,11 +368,14 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   constexpr bool kNoRes = K == 5 || (K == 4 && RY == 4);
   if constexpr (kNoRes) {
     MDFX_CHECK(!resid, "heat7_wxk: no residual variant of this shape (the 5-step sweep: use --temporal 4 with a residual)");
-  } else if (resid) {
-    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
-    return;
+  } else if constexpr (NB == 2 && SPAR == 2) {
+    if (resid) {
+      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+      return;
+    }
   }
-  hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, NB, SPAR>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
+                     resid);
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -374,7 +418,11 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
       // two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row
       // band also fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
       // (profiles/r03_wxk/). MDFX_WXK_RY picks another shape.
+      const int nb = knobs().wxk_nb;
       if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
+      else if (nb == 31) launch_wxk<T, 3, 2, 4, 8, 3, 1>(g, in, out, r, resid, s);  // 3 window buffers, 1 seam table
+      else if (nb == 21) launch_wxk<T, 3, 2, 4, 8, 2, 1>(g, in, out, r, resid, s);  // 1 seam table only
+      else if (nb == 32) launch_wxk<T, 2, 2, 4, 8, 3, 2>(g, in, out, r, resid, s);  // 2 + 2 rows, 3 window buffers
       else if (ry == 31) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
       else if (ry == 21) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
       else if (ry == 22) launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);

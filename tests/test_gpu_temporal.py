@@ -510,6 +510,41 @@ def test_heat7_wxk_bitwise(hip, prob, k, wb, ry, resid, knob):
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
+@pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=1024, ny=45, nz=17)],
+                         ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("nb", ["31", "21", "32"])
+@pytest.mark.parametrize("resid", [False, True])
+def test_heat7_wxk_window_depth_bitwise(hip, prob, nb, resid, knob):
+    """heat7_wxk K = 4 with the u0 DMA two planes ahead (3 window buffers) and / or one seam table
+    (its reads and writes separated by a second barrier per plane) == 4 naive single steps."""
+    if prob.dtype == "f64":
+        pytest.skip("fp32 instances")
+    k = 4
+    knob("MDFX_H7_WXK", 1)
+    knob("MDFX_WXK_NB", nb)
+    lay = FieldLayout.make(prob, halo=k)
+    src = alloc_field(lay, "cuda")
+    init_field(prob, lay, src)
+    fused = alloc_field(lay, "cuda")
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, fused, steps=k, resid=res if resid else None)
+    set_kernel_variant("naive")
+    try:
+        cur = src.clone()
+        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
+        for i in range(k):
+            nxt = cur.clone()
+            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
+            cur = nxt
+    finally:
+        set_kernel_variant("auto")
+    torch.cuda.synchronize()
+    o = lay.owned
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), nb
+    if resid:
+        assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
+
+
 @pytest.mark.parametrize("resid", [False, True])
 def test_heat7_fp64_wide_rows_default_path(hip, resid):
     """fp64 rows of 2048 cells and more take heat7_wxk (3 + 1-row bands) at K = 3 by default: the
