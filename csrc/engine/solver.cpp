@@ -527,6 +527,64 @@ bool Solver::graph_eligible() const {
          (slabs_.size() == 1 || multislab_graph_ok()) && fault().rank < 0 && !poisoned_;
 }
 
+void Solver::warm_kernels(int64_t steps) {
+  MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
+  if (slabs_.empty() || slabs_[0].be->kind() != DeviceKind::HIP) return;  // (nothing to warm on the CPU)
+  // the sweeps run(steps) would issue: (depth, residual) as its loop picks them
+  bool used[17][2] = {};
+  int64_t done = 0, at = stats_.steps;
+  while (done < steps) {
+    int64_t to_res = steps - done + 1;
+    if (opt_.residual_every > 0) to_res = ((at / opt_.residual_every) + 1) * opt_.residual_every - at;
+    int k = 1;
+    for (int kk = std::min<int64_t>({(int64_t)opt_.temporal, steps - done, to_res}); kk > 1; --kk)
+      if (depth_ok_[kk]) {
+        k = kk;
+        break;
+      }
+    used[k][to_res == k ? 1 : 0] = true;
+    done += k;
+    at += k;
+  }
+  synchronize();
+  const int nb = 1 - cur_;
+  for (int k = 1; k <= 16; ++k)
+    for (int r = 0; r < 2; ++r) {
+      if (!used[k][r]) continue;
+      for (auto& s : slabs_) {
+        s.be->activate();
+        RegionArgs a;
+        a.in = s.buf[cur_];
+        a.out = s.buf[nb];  // scratch: the next step overwrites it
+        a.lay = s.lay;
+        a.steps = k;
+        a.resid = r ? s.resid : nullptr;  // (step() clears the accumulator before it counts)
+        if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
+          a.lz_begin = s.lo_b;
+          a.lz_end = s.lo_e;
+          a.lz2_begin = s.hi_b;
+          a.lz2_end = s.hi_e;
+          s.be->stencil(spec_, a, s.hs);
+          a.lz2_begin = a.lz2_end = 0;
+        } else if (s.lo_e > s.lo_b) {
+          a.lz_begin = s.lo_b;
+          a.lz_end = s.lo_e;
+          s.be->stencil(spec_, a, s.hs);
+        } else if (s.hi_e > s.hi_b) {
+          a.lz_begin = s.hi_b;
+          a.lz_end = s.hi_e;
+          s.be->stencil(spec_, a, s.hs);
+        }
+        if (s.in_e > s.in_b) {
+          a.lz_begin = s.in_b;
+          a.lz_end = s.in_e;
+          s.be->stencil(spec_, a, s.hs);
+        }
+      }
+    }
+  synchronize();
+}
+
 int Solver::prepare_graphs() {
   MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
   if (!graph_eligible()) return 0;

@@ -74,6 +74,11 @@ class Solver {
   // cycles held (0 if graphs are off or not capturable here). init() keeps them (buffers do not
   // move); option changes that alter the captured work drop them.
   int prepare_graphs();
+  // Launch every stencil kernel instance that run(steps) would use once (each fused depth, the
+  // residual copy included), into the scratch buffer and without any exchange, then synchronize:
+  // the first launch of an instance pays one-time costs (code-object and occupancy queries) that a
+  // timed run without warm-up steps would otherwise count. The field state is unchanged.
+  void warm_kernels(int64_t steps);
   // Whether run() would replay captured cycles in this configuration.
   bool graph_eligible() const;
   void synchronize();

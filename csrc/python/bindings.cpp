@@ -446,6 +446,9 @@ PYBIND11_MODULE(_mdfx, m) {
       .def_property_readonly("graph_captures", [](PySolver& p) { return p.chk().stats().graph_captures; })
       .def("prepare_graphs", [](PySolver& p) { return p.chk().prepare_graphs(); },
            "capture both parities' 2-sweep hipGraph cycles now (0 if graphs are off / not capturable)")
+      .def("warm_kernels", [](PySolver& p, int64_t steps) { p.chk().warm_kernels(steps); }, py::arg("steps"),
+           py::call_guard<py::gil_scoped_release>(),
+           "launch every kernel instance run(steps) would use once, into the scratch buffer (state unchanged)")
       .def_property_readonly("graph_eligible", [](PySolver& p) { return p.chk().graph_eligible(); })
       .def_property_readonly("current_index", [](PySolver& p) { return p.chk().current_index(); })
       .def_property_readonly("transport_name", [](PySolver& p) { return std::string(p.chk().transport().name()); })

@@ -519,3 +519,14 @@ def test_fused_depth_policy(mdfx):
     assert auto_temporal(m.heat3d(nx=1024, ny=64, nz=64), 8, "hip") == 2   # 8-plane slabs
     assert auto_temporal(m.heat3d(nx=1024, ny=64, nz=24), 8, "hip") == 1
     assert auto_temporal(m.heat3d(n=1024), 1, "cpu") == 1
+
+
+def test_warm_kernels_is_a_noop_on_cpu():
+    import mpi_cuda_process_amd as m
+
+    prob = m.heat3d(nx=24, ny=10, nz=12)
+    with m.Simulation(prob, device="cpu", ranks=2) as sim:
+        sim.init()
+        before = sim.gather()
+        sim.warm_kernels(7)
+        assert np.array_equal(before, sim.gather())

@@ -61,6 +61,21 @@ def test_graph_replay_equals_eager(hip, prob):
     assert np.array_equal(a, e)
 
 
+@pytest.mark.parametrize("prob", PROBS + [m.heat3d(nx=1024, ny=20, nz=40)], ids=_ids)
+def test_warm_kernels_leaves_state_unchanged(hip, prob):
+    """warm_kernels(steps) launches each fused depth (and the residual copy) of a run into the
+    scratch buffer: a run after it is bitwise the run without it, on 1 and 3 slabs."""
+    for ranks in (1, 3):
+        a, ra = _run(prob, 11, ranks=ranks, residual_every=5)
+        with m.Simulation(prob, device="hip", ranks=ranks, residual_every=5) as sim:
+            sim.init()
+            sim.warm_kernels(11)
+            sim.run(11)
+            sim.synchronize()
+            b, rb = sim.gather(), sim.residual
+        assert np.array_equal(a, b) and ra == rb, ranks
+
+
 @pytest.mark.parametrize("prob", [PROBS[0], m.heat3d(nx=256, ny=20, nz=40)], ids=_ids)
 def test_prepared_graphs_replay_without_capture(hip, prob):
     """prepare_graphs() captures both parities up front; later runs (any warmup parity, across
