@@ -73,7 +73,8 @@ def test_warm_kernels_leaves_state_unchanged(hip, prob):
             sim.run(11)
             sim.synchronize()
             b, rb = sim.gather(), sim.residual
-        assert np.array_equal(a, b) and ra == rb, ranks
+        # (the residual is summed with atomics in no fixed order: equal to rounding)
+        assert np.array_equal(a, b) and abs(ra - rb) <= 1e-12 * abs(ra), ranks
 
 
 @pytest.mark.parametrize("prob", [PROBS[0], m.heat3d(nx=256, ny=20, nz=40)], ids=_ids)
