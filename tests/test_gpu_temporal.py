@@ -577,7 +577,10 @@ def test_heat7_fp64_wide_rows_default_path(hip, resid):
 
 B27X = [models.box27(n=40), models.box27(n=24, dtype="f64"), models.box27(nx=700, ny=37, nz=15),
         models.box27(nx=1030, ny=9, nz=12), models.box27(nx=300, ny=70, nz=10, dtype="f64"),
-        models.box27(nx=8, ny=5, nz=9)]
+        models.box27(nx=8, ny=5, nz=9),
+        # x-pair kernel (box27_wxp): rows of 257..512 cells, two 256-cell halves per block
+        models.box27(nx=512, ny=29, nz=14), models.box27(nx=300, ny=17, nz=11), models.box27(nx=257, ny=9, nz=8),
+        models.box27(nx=512, ny=5, nz=9), models.box27(nx=448, ny=40, nz=23)]
 
 
 @pytest.mark.parametrize("prob", B27X, ids=lambda p: p.describe().replace(" ", "_"))
@@ -609,11 +612,13 @@ def test_box27_wxk_bitwise(hip, prob, resid):
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
 
-def test_box27_wxk_regions_and_engine(hip, knob):
+@pytest.mark.parametrize("nx", [600, 480])
+def test_box27_wxk_regions_and_engine(hip, knob, nx):
     """box27_wxk on a middle slab (both boundary regions in one launch + the interior) == the
-    whole grid, and a 3-slab engine run at the 27-point's fused depth 3 == single steps."""
+    whole grid, and a 3-slab engine run at the 27-point's fused depth 3 == single steps (480-cell
+    rows: the x-pair kernel)."""
     k = 3
-    prob = models.box27(nx=600, ny=30, nz=40)
+    prob = models.box27(nx=nx, ny=30, nz=40)
     full = FieldLayout.make(prob, halo=k)
     g = alloc_field(full, "cuda")
     init_field(prob, full, g)
@@ -627,7 +632,7 @@ def test_box27_wxk_regions_and_engine(hip, knob):
     apply_stencil(prob, lay, src, out, h, h + k, steps=k, second=(h + 18 - k, h + 18))
     apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k)
     torch.cuda.synchronize()
-    assert torch.equal(out[h:h + 18, :, :600], ref[12 + k:30 + k, :, :600])
+    assert torch.equal(out[h:h + 18, :, :nx], ref[12 + k:30 + k, :, :nx])
     knob("MDFX_B27_WXK", 1)
     p3 = models.box27(nx=500, ny=33, nz=45)
     a, _ = _sim(p3, 6, ranks=1)
