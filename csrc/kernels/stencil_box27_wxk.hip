@@ -282,7 +282,10 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
   const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   if (b >= ntasks) return;
   __shared__ V win[2][RB][2][64];
-  __shared__ V seam[2][K - 1][WB - 1][2][2][64];  // [parity][level-1][boundary][first of s+1 / last of s][half][lane]
+  // [half][parity][level-1][boundary][first of s+1 / last of s][lane]: the half outermost (with it
+  // inside, hipcc loses track of which LDS array a seam read touches and drains the window's
+  // in-flight DMA with vmcnt(0) before it)
+  __shared__ V seam[2][2][K - 1][WB - 1][2][64];
   __shared__ T xs[2][K - 1][RB][2][2];            // [parity][level-1][window row][half][left / right edge cell]
   const int zt = b / YT, yt = b % YT;
   const int P0 = (int)(g.lz_end - g.lz_begin);
@@ -313,6 +316,10 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
   int nst = 0;
 
   // u0 plane lz -> window buffer `buf`: 2 RB half rows of 64 lanes, wave w fetching w, w + 2WB, ..
+  // (always half w & 1: 2WB is even). The lane's byte offset in the row stays in one VGPR for the
+  // whole march, so the DMA takes the SGPR-base form and no address register is ever recycled
+  // under an in-flight DMA (a recycled one makes hipcc drain it with vmcnt(0)).
+  const uint32_t xcb = (uint32_t)(std::min<int64_t>((int64_t)(w & 1) * HX + lane * N, pitch - N) * (int64_t)sizeof(T));
   auto issue = [&](int lz, int buf) {
     const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
 #pragma unroll
@@ -322,8 +329,11 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
         const int r = k >> 1, h = k & 1;
         const int y = yb - K + r;
         const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-        const int64_t xa = (int64_t)h * HX + lane * N;
-        const T* a = in + (int64_t)lzc * plane + (int64_t)yc * pitch + (xa < pitch ? xa : pitch - N);
+        // the row base is laundered through SGPRs so hipcc cannot hoist `in + xcb` into a 64-bit
+        // VGPR pair: the DMA keeps the SGPR-base form with xcb's own long-lived VGPR
+        const char* rb = (const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
+        asm volatile("" : "+s"(rb));
+        const T* a = (const T*)(rb + xcb);
         dcheck(g, in, a, N);
         glds16(a, &win[buf][r][h][0]);
       }
@@ -342,16 +352,17 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
   // of the left half x = 256); the outer ends (x = -1, x = 512) feed held cells only: 0
   LT* const wedge = lds_vptr(xh == 1 ? &((T*)&win[0][y0 - yb][0][63])[3] : &((T*)&win[0][y0 - yb][1][0])[0]);
   const int wu = wy > 0 ? wy - 1 : 0, wd = wy < WB - 1 ? wy : WB - 2;
-  LV* const s_first = lds_vptr(&seam[0][0][wu][0][xh][lane]);
-  LV* const s_last = lds_vptr(&seam[0][0][wd][1][xh][lane]);
+  LV* const s_first = lds_vptr(&seam[xh][0][0][wu][0][lane]);
+  LV* const s_last = lds_vptr(&seam[xh][0][0][wd][1][lane]);
   constexpr int WIN_BUF = RB * 2 * 64, WROW = 2 * 64;           // V elements
   constexpr int WIN_BUF_T = WIN_BUF * N, WROW_T = WROW * N;     // T elements
-  constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 2 * 64;
+  constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
   constexpr int XS_PAR = (K - 1) * RB * 4, XS_LVL = RB * 4;
   // this wave's edge-cell slots: lane 0 publishes its first cell, lane 63 its last
   LT* const xs_mine = lds_vptr(&xs[0][0][y0 - yb + K][xh][lane == 0 ? 0 : 1]);
-  // ... and the other half's, read by every lane (broadcast)
-  LT* const xs_other = lds_vptr(&xs[0][0][y0 - yb + K][1 - xh][xh == 1 ? 1 : 0]);
+  // (the other half's are read by indexing `xs` itself, every lane the same cell: through a laundered
+  // pointer hipcc could not tell them from the window's in-flight DMA)
+  const int xr = y0 - yb + K, xo = 1 - xh, xside = xh == 1 ? 1 : 0;
   auto st = [](LV* p, const V& v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
@@ -400,13 +411,13 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
         auto vin = [&](int i) -> Row {
           if (l == 1) return RO::fromv(V(wrow[P * WIN_BUF + (i + K) * WROW]));
           const int j = l - 1;
-          if (i < SH::lo(j)) return RO::fromv(seam[P ^ 1][j - 1][wu][1][xh][lane]);
-          if (i >= SH::hi(j)) return RO::fromv(seam[P ^ 1][j - 1][wd][0][xh][lane]);
+          if (i < SH::lo(j)) return RO::fromv(seam[xh][P ^ 1][j - 1][wu][1][lane]);
+          if (i >= SH::hi(j)) return RO::fromv(seam[xh][P ^ 1][j - 1][wd][0][lane]);
           return H[j - 1][P ^ 1][i - SH::lo(j)];
         };
         auto eo = [&](int i) -> T {
           if (l == 1) return T(wedge[P * WIN_BUF_T + (i + K) * WROW_T]);
-          return T(xs_other[(P ^ 1) * XS_PAR + (l - 2) * XS_LVL + i * 4]);
+          return xs[P ^ 1][l - 2][xr + i][xo][xside];
         };
         Row vm = vin(SH::lo(l) - 1), vc = vin(SH::lo(l));
         Row hm = hs(vm, eo(SH::lo(l) - 1)), hc = hs(vc, eo(SH::lo(l)));
