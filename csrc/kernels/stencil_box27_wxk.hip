@@ -286,7 +286,10 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
   // inside, hipcc loses track of which LDS array a seam read touches and drains the window's
   // in-flight DMA with vmcnt(0) before it)
   __shared__ V seam[2][2][K - 1][WB - 1][2][64];
-  __shared__ T xs[2][K - 1][RB][2][2];            // [parity][level-1][window row][half][left / right edge cell]
+  // x edge rows: the left half publishes the LAST cell of every lane of each row it computes, the
+  // right half the FIRST (whole rows of floats: one non-divergent ds_write_b32; the other half reads
+  // lane 63's / lane 0's entry)
+  __shared__ T xs[2][K - 1][RB][2][64];           // [parity][level-1][window row][half][lane]
   const int zt = b / YT, yt = b % YT;
   const int P0 = (int)(g.lz_end - g.lz_begin);
   const int zt1 = (P0 + zc - 1) / zc;
@@ -350,19 +353,20 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
   LV* const wrow = lds_vptr(&win[0][y0 - yb][xh][lane]);
   // the other half's edge cell of u0 window row r (lane 0 of the right half needs x = 255, lane 63
   // of the left half x = 256); the outer ends (x = -1, x = 512) feed held cells only: 0
-  LT* const wedge = lds_vptr(xh == 1 ? &((T*)&win[0][y0 - yb][0][63])[3] : &((T*)&win[0][y0 - yb][1][0])[0]);
   const int wu = wy > 0 ? wy - 1 : 0, wd = wy < WB - 1 ? wy : WB - 2;
   LV* const s_first = lds_vptr(&seam[xh][0][0][wu][0][lane]);
   LV* const s_last = lds_vptr(&seam[xh][0][0][wd][1][lane]);
   constexpr int WIN_BUF = RB * 2 * 64, WROW = 2 * 64;           // V elements
-  constexpr int WIN_BUF_T = WIN_BUF * N, WROW_T = WROW * N;     // T elements
   constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
-  constexpr int XS_PAR = (K - 1) * RB * 4, XS_LVL = RB * 4;
+  constexpr int XS_PAR = (K - 1) * RB * 2 * 64, XS_LVL = RB * 2 * 64;
   // this wave's edge-cell slots: lane 0 publishes its first cell, lane 63 its last
-  LT* const xs_mine = lds_vptr(&xs[0][0][y0 - yb + K][xh][lane == 0 ? 0 : 1]);
-  // (the other half's are read by indexing `xs` itself, every lane the same cell: through a laundered
-  // pointer hipcc could not tell them from the window's in-flight DMA)
-  const int xr = y0 - yb + K, xo = 1 - xh, xside = xh == 1 ? 1 : 0;
+  LT* const xs_mine = lds_vptr(&xs[0][0][y0 - yb + K][xh][lane]);
+  // LDS byte addresses of the other half's edge cells: of u0 window row r (buffer 0) and of edge
+  // row r (parity 0, level 1); buffers / parities / levels are fixed strides from there
+  const uint32_t a_win = (uint32_t)(uintptr_t)(LT*)(xh == 1 ? &((T*)&win[0][0][0][63])[3] : &((T*)&win[0][0][1][0])[0]);
+  const uint32_t a_xs = (uint32_t)(uintptr_t)(LT*)(xh == 1 ? &xs[0][0][0][0][63] : &xs[0][0][0][1][0]);
+  constexpr uint32_t WIN_ROW_B = 2 * 64 * sizeof(V), WIN_BUF_B = RB * WIN_ROW_B;
+  constexpr uint32_t XS_ROW_B = 2 * 64 * sizeof(T), XS_LVL_B = RB * XS_ROW_B, XS_PAR_B = (K - 1) * XS_LVL_B;
   auto st = [](LV* p, const V& v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
@@ -370,9 +374,12 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
     asm volatile("ds_write_b32 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
   // x sums of a row whose cells beyond the half's ends are `eo` (the other half's edge cell)
+  // (both shifts always take the edge operand -- the outer ends x = -1 / 512 only ever feed held
+  // cells -- so the half's choice is a select of the operand, not a branch around the shift)
+  const bool right = xh == 1;
   auto hs = [&](const Row& v, T eo) -> Row {
-    const T l = xh == 1 ? lane_up1_or(eo, RO::last(v)) : lane_up1(RO::last(v));
-    const T r = xh == 0 ? lane_down1_or(eo, RO::first(v)) : lane_down1(RO::first(v));
+    const T l = lane_up1_or(right ? eo : T(0), RO::last(v));
+    const T r = lane_down1_or(right ? T(0) : eo, RO::first(v));
     return RO::hsum(v, l, r);
   };
 
@@ -388,12 +395,42 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
         S[l][i] = Ap[l][0][i] = Ap[l][1][i] = RO::zero();
         if (l < K - 1) H[l][0][i] = H[l][1][i] = RO::zero();
       }
+    // The other half's edge cells a step uses: for level l, input rows lo(l)-1 .. hi(l) (level 1 from
+    // the u0 window of this step's plane, levels above from the edge rows of the previous step).
+    // Entry e of that list is fetched by lane e with ONE ds_read_b32 right after the plane's barrier
+    // and handed to the row code by readlane: one LDS round trip per step instead of one per row.
+    constexpr auto eidx = [](int l, int i) constexpr {  // entry of (level l, row i)
+      int e = 0;
+      for (int ll = K; ll > l; --ll) e += SH::n(ll) + 2;
+      return e + (i - (SH::lo(l) - 1));
+    };
+    static_assert(eidx(1, SH::hi(1)) < 64, "box27_wxp: one lane per edge cell");
+    uint32_t ea[2] = {a_win, a_win};  // per-lane address of entry `lane`, per parity
+#pragma unroll
+    for (int l = K; l >= 1; --l)
+#pragma unroll
+      for (int i = SH::lo(l) - 1; i <= SH::hi(l); ++i) {
+        const uint32_t r = (uint32_t)(y0 - yb + K + i);  // window / edge row
+        if (lane == eidx(l, i)) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+            ea[p] = l == 1 ? a_win + p * WIN_BUF_B + r * WIN_ROW_B
+                           : a_xs + (p ^ 1) * XS_PAR_B + (l - 2) * XS_LVL_B + r * XS_ROW_B;
+        }
+      }
     auto step = [&](int q, auto par_c) __attribute__((always_inline)) {
       constexpr int P = decltype(par_c)::value;
       __builtin_amdgcn_sched_barrier(0);
       wait_vm_le(nst);
       lds_barrier();
       if (q < qdma) issue(q + 1, P ^ 1);
+      // (outside hipcc's view, so it is not ordered against the in-flight window DMA; the u0 rows it
+      // reads landed before the barrier)
+      T ev;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(ev) : "v"(ea[P]) : "memory");
+      auto eo_at = [&](int e) -> T {
+        return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ev), e));
+      };
       const int lzo = q - LAG;
       const bool valid = lzo >= zs && lzo < ze;
 #pragma unroll
@@ -415,10 +452,7 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
           if (i >= SH::hi(j)) return RO::fromv(seam[xh][P ^ 1][j - 1][wd][0][lane]);
           return H[j - 1][P ^ 1][i - SH::lo(j)];
         };
-        auto eo = [&](int i) -> T {
-          if (l == 1) return T(wedge[P * WIN_BUF_T + (i + K) * WROW_T]);
-          return xs[P ^ 1][l - 2][xr + i][xo][xside];
-        };
+        auto eo = [&](int i) -> T { return eo_at(eidx(l, i)); };
         Row vm = vin(SH::lo(l) - 1), vc = vin(SH::lo(l));
         Row hm = hs(vm, eo(SH::lo(l) - 1)), hc = hs(vc, eo(SH::lo(l)));
 #pragma unroll
@@ -460,8 +494,7 @@ __global__ __launch_bounds__(2 * WB * 64) void box27_wxp(const T* __restrict__ i
             H[l - 1][P][il] = o;
             if (ROLE != 0 && i == 0) st(s_first + P * SEAM_PAR + (l - 1) * SEAM_LVL, RO::vec(o));
             if (ROLE != 2 && i == SH::R - 1) st(s_last + P * SEAM_PAR + (l - 1) * SEAM_LVL, RO::vec(o));
-            if (lane == 0 || lane == 63)
-              st1(xs_mine + P * XS_PAR + (l - 1) * XS_LVL + i * 4, lane == 0 ? RO::first(o) : RO::last(o));
+            st1(xs_mine + P * XS_PAR + (l - 1) * XS_LVL + i * 2 * 64, right ? RO::first(o) : RO::last(o));
           }
           vm = vc;
           vc = vp;
