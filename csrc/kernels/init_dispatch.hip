@@ -91,7 +91,7 @@ static Knobs read_knobs() {
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
   k.wxk_ry = env_int("MDFX_WXK_RY", 0);
   k.wxk_nb = env_int("MDFX_WXK_NB", 0);
-  k.b27_wxp = env_int("MDFX_B27_WXP", 1);
+  k.b27_wxp = env_int("MDFX_B27_WXP", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
@@ -290,8 +290,8 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // (profiles/r03_wxk/). MDFX_B27_WXK = 0 / 1 forces K = 2 / 3
       if (dev::knobs().b27_wxk == 1) return 3;
       if (dev::knobs().b27_wxk == 0) return 2;
-      // fp32 rows of 257..512 cells: K = 3 in box27_wxp (two 256-cell halves per block, no
-      // overlapping lanes)
+      // (fp32 rows of 257..512 cells with MDFX_B27_WXP = 1: K = 3 in box27_wxp, two 256-cell
+      // halves per block; 512^3: 909 vs 1072-1085 for box27_tb2n K = 2, profiles/r03_session_t/)
       if (spec.dtype == DType::F32 && nx > 256 && nx <= 512 && dev::knobs().b27_wxp != 0) return 3;
       return (spec.dtype == DType::F64 || nx >= 1024) ? 3 : 2;
     case StencilKind::Heat7:

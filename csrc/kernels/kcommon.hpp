@@ -227,7 +227,7 @@ struct Knobs {
   int wtk_split = -1;  // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: -1 never (default, measured slower), 0 cost model, 1 always
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64 and rows >= 1024; 0 / 1)
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
-  int b27_wxp = 1;     // MDFX_B27_WXP: box27_wxk's x-pair kernel for fp32 rows of 257..512 cells (0: overlapping segments)
+  int b27_wxp = 0;     // MDFX_B27_WXP: 1 = box27_wxk's x-pair kernel for fp32 rows of 257..512 cells (measured slower: profiles/r03_session_t/)
   int wxk_nb = 0;      // MDFX_WXK_NB: heat7_wxk fp32 K = 4 window depth x seam tables (31: 3 buffers + 1 table, 21, 32: 2 + 2 rows; all measured slower, profiles/r03_session_r/)
   int wxk_ry = 0;      // MDFX_WXK_RY: heat7_wxk fp32 band (K = 3: 3 = 3-row waves; K = 4: 42 / 32 / 22 / 31 / 21 =
                        // inner / edge rows; 0: 32)

@@ -592,8 +592,10 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
   MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
              "box27_wxk: row / plane counts must fit 32-bit indices");
-  // fp32 rows of 257..512 cells: the x-pair kernel (two 256-cell halves, no overlapping lanes),
-  // bands of 4 waves per half (MDFX_B27_WXP = 0 keeps the overlapping segments)
+  // fp32 rows of 257..512 cells with MDFX_B27_WXP = 1: the x-pair kernel (two 256-cell halves, no
+  // overlapping lanes, bands of 4 waves per half). Off by default: its 6-row bands fetch twice the
+  // window rows per output row and it ran 909 vs 1017-1026 GCells/s for the overlapping segments at
+  // 512^3 (profiles/r03_session_t/)
   if constexpr (sizeof(T) == 4) {
     if (g.pitch > 256 && g.pitch <= 512 && knobs().b27_wxp != 0) {
       launch_b27p<T, 2, 1, 3, 4>(g, in, out, cf, resid, s);

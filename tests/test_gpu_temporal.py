@@ -585,9 +585,12 @@ B27X = [models.box27(n=40), models.box27(n=24, dtype="f64"), models.box27(nx=700
 
 @pytest.mark.parametrize("prob", B27X, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("resid", [False, True])
-def test_box27_wxk_bitwise(hip, prob, resid):
+@pytest.mark.parametrize("wxp", ["0", "1"])
+def test_box27_wxk_bitwise(hip, prob, resid, wxp, knob):
     """box27_wxk (27-point, K = 3, y halo exchanged through the LDS seam table, levels above the
-    first one plane later) == 3 naive box27 steps, bitwise, with the residual of step 3."""
+    first one plane later) == 3 naive box27 steps, bitwise, with the residual of step 3; with
+    MDFX_B27_WXP = 1 the fp32 rows of 257..512 cells run the x-pair kernel box27_wxp."""
+    knob("MDFX_B27_WXP", wxp)
     k = 3
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
@@ -613,10 +616,12 @@ def test_box27_wxk_bitwise(hip, prob, resid):
 
 
 @pytest.mark.parametrize("nx", [600, 480])
-def test_box27_wxk_regions_and_engine(hip, knob, nx):
+@pytest.mark.parametrize("wxp", ["0", "1"])
+def test_box27_wxk_regions_and_engine(hip, knob, nx, wxp):
     """box27_wxk on a middle slab (both boundary regions in one launch + the interior) == the
     whole grid, and a 3-slab engine run at the 27-point's fused depth 3 == single steps (480-cell
-    rows: the x-pair kernel)."""
+    rows and MDFX_B27_WXP = 1: the x-pair kernel)."""
+    knob("MDFX_B27_WXP", wxp)
     k = 3
     prob = models.box27(nx=nx, ny=30, nz=40)
     full = FieldLayout.make(prob, halo=k)
