@@ -418,7 +418,11 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
       // two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row
       // band also fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
       // (profiles/r03_wxk/). MDFX_WXK_RY picks another shape.
-      const int nb = knobs().wxk_nb;
+      // the boundary regions of a slab (one launch for both, or a region of at most 2K planes) march
+      // K + 2K planes for K outputs: few steps, each waiting on its plane's DMA; MDFX_WXK_BNB picks
+      // their window depth separately from the interior's
+      const bool thin = g.lz2_end > g.lz2_begin || g.lz_end - g.lz_begin <= 2 * steps;
+      const int nb = thin && knobs().wxk_bnb ? knobs().wxk_bnb : knobs().wxk_nb;
       if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
       else if (nb == 31) launch_wxk<T, 3, 2, 4, 8, 3, 1>(g, in, out, r, resid, s);  // 3 window buffers, 1 seam table
       else if (nb == 21) launch_wxk<T, 3, 2, 4, 8, 2, 1>(g, in, out, r, resid, s);  // 1 seam table only
