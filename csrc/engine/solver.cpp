@@ -44,6 +44,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 16, "temporal blocking depth must be 1..16");
   if (const char* v = std::getenv("MDFX_BND_FIRST")) bnd_first_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MDFX_BND_CS")) bnd_cs_ = std::atoi(v) != 0;
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
@@ -72,6 +73,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.cs = s.be->create_stream(0);
     s.ev_bnd = s.be->create_event();
     s.ev_int = s.be->create_event();
+    s.ev_x = s.be->create_event();
     s.resid = (double*)s.be->alloc(2 * sizeof(double));
     for (int kk = 2; kk <= opt_.temporal; ++kk) {
       const bool ok = s.be->kind() != DeviceKind::HIP || hip_supports_steps(spec_, s.lay, kk);
@@ -146,6 +148,7 @@ Solver::~Solver() {
     s.be->release(s.resid);
     s.be->destroy_event(s.ev_bnd);
     s.be->destroy_event(s.ev_int);
+    s.be->destroy_event(s.ev_x);
     s.be->destroy_stream(s.hs);
     s.be->destroy_stream(s.cs);
   }
@@ -256,8 +259,20 @@ void Solver::exchange_ghosts() {
   ghosts_dirty_ = false;
 }
 
+// Boundary kernels on the compute stream: the step is then boundary -> interior on ONE stream (no
+// cross-stream event gap between them, measured 10-13 us each at the N = 8 slab shape, where a
+// 4-step sweep takes about 0.3 ms), and the exchange alone on the halo stream, after the boundary
+// kernels' event and overlapping the interior sweep. The next step's boundary kernels wait for that
+// exchange (ev_x): its ghosts are their input, and the faces it sent are what they overwrite.
+// Only for transports whose exchange is pure stream work on the halo stream (a host-side exchange
+// synchronises the halo stream alone).
+bool Solver::boundary_on_cs() const {
+  return bnd_cs_ && opt_.overlap && bnd_first_ && transport_->graph_capturable();
+}
+
 void Solver::step(bool want_resid, int k) {
   const int nb = 1 - cur_;
+  const bool bcs = boundary_on_cs();
   const bool prof = opt_.profile;
   const bool prof_hip = prof && pev_[0] != nullptr;
   using clk = std::chrono::steady_clock;
@@ -272,13 +287,16 @@ void Solver::step(bool want_resid, int k) {
     a.out = s.buf[nb];
     a.lay = s.lay;
     a.steps = k;
+    void* bs = bcs ? s.cs : s.hs;  // the boundary kernels' stream
     if (want_resid) {
-      s.be->memset(s.resid, 0, sizeof(double), s.hs);
+      s.be->memset(s.resid, 0, sizeof(double), bs);
       s.be->memset(s.resid + 1, 0, sizeof(double), opt_.overlap ? s.cs : s.hs);
     }
-    // halo stream: boundary planes of this step, after the previous interior sweep
-    s.be->wait(s.hs, s.ev_int);
-    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)s.hs));
+    // boundary planes of this step, after the previous interior sweep (same stream with bcs) and,
+    // with bcs, after the previous exchange
+    if (bcs) s.be->wait(s.cs, s.ev_x);
+    else s.be->wait(s.hs, s.ev_int);
+    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)bs));
     a.resid = want_resid ? s.resid : nullptr;
     if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
       // both boundary regions in one call (one launch where the kernel supports it)
@@ -286,23 +304,26 @@ void Solver::step(bool want_resid, int k) {
       a.lz_end = s.lo_e;
       a.lz2_begin = s.hi_b;
       a.lz2_end = s.hi_e;
-      s.be->stencil(spec_, a, s.hs);
+      s.be->stencil(spec_, a, bs);
       a.lz2_begin = a.lz2_end = 0;
     } else if (s.lo_e > s.lo_b) {
       a.lz_begin = s.lo_b;
       a.lz_end = s.lo_e;
-      s.be->stencil(spec_, a, s.hs);
+      s.be->stencil(spec_, a, bs);
     } else if (s.hi_e > s.hi_b) {
       a.lz_begin = s.hi_b;
       a.lz_end = s.hi_e;
-      s.be->stencil(spec_, a, s.hs);
+      s.be->stencil(spec_, a, bs);
     }
-    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)s.hs));
+    if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)bs));
     if (opt_.sync_debug) s.be->sync_device();
     if (prof && !prof_hip && &s == &slabs_[0]) c1 = clk::now();
     // compute stream: interior, after the previous step's boundary kernels
     void* is = opt_.overlap ? s.cs : s.hs;
-    if (opt_.overlap) {
+    if (bcs) {
+      s.be->record(s.ev_bnd, s.cs);  // this step's boundary kernels: the exchange follows them
+      s.be->wait(s.hs, s.ev_bnd);
+    } else if (opt_.overlap) {
       if (bnd_first_) s.be->record(s.ev_bnd, s.hs);  // this step's boundary kernels
       s.be->wait(s.cs, s.ev_bnd);
     }
@@ -315,7 +336,7 @@ void Solver::step(bool want_resid, int k) {
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[3], (hipStream_t)is));
     if (prof && !prof_hip && &s == &slabs_[0]) c2 = clk::now();
-    s.be->record(s.ev_bnd, s.hs);
+    if (!bcs) s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, is);
     if (opt_.sync_debug) s.be->sync_device();
     s.be->trace_pop();
@@ -323,6 +344,8 @@ void Solver::step(bool want_resid, int k) {
   if (!slabs_.empty()) slabs_[0].be->trace_push("mdfx.exchange");
   transport_->exchange(nb);
   if (!slabs_.empty()) slabs_[0].be->trace_pop();
+  if (bcs)
+    for (auto& s : slabs_) s.be->record(s.ev_x, s.hs);
   if (prof_hip) {
     Slab& s0 = slabs_[0];
     s0.be->activate();
@@ -609,6 +632,7 @@ int Solver::prepare_graphs() {
     s.be->activate();
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
+    s.be->record(s.ev_x, s.hs);
   }
   return (graph_exec_[0] ? 1 : 0) + (graph_exec_[1] ? 1 : 0);
 }
@@ -650,6 +674,7 @@ void Solver::capture_graph(int parity, int k) {
     s.be->activate();
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
+    s.be->record(s.ev_x, s.hs);
   }
   const StepStats saved = stats_;
   GDBG("capture: steps");
@@ -695,6 +720,7 @@ void Solver::run_graph(int64_t pairs, int k) {
       s.be->activate();
       s.be->record(s.ev_bnd, s.hs);
       s.be->record(s.ev_int, s.cs);
+      s.be->record(s.ev_x, s.hs);
     }
   }
   GDBG("launch");
@@ -705,6 +731,7 @@ void Solver::run_graph(int64_t pairs, int k) {
     if (&s == &o) continue;
     o.be->wait(o.hs, s.ev_bnd);
     o.be->wait(o.hs, s.ev_int);
+    o.be->wait(o.hs, s.ev_x);
   }
   o.be->wait(o.hs, o.ev_int);
   for (int64_t i = 0; i < pairs; ++i) HIPC(hipGraphLaunch((hipGraphExec_t)graph_exec_[cur_], (hipStream_t)o.hs));
@@ -720,6 +747,7 @@ void Solver::run_graph(int64_t pairs, int k) {
     s.be->activate();
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
+    s.be->record(s.ev_x, s.hs);
   }
   // a replayed cycle ends with the exchange of buffer cur_ (the parity is unchanged)
   transport_->set_last_parity(cur_);

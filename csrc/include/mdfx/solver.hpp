@@ -123,6 +123,7 @@ class Solver {
     void* cs = nullptr;  // compute stream
     void* ev_bnd = nullptr;
     void* ev_int = nullptr;
+    void* ev_x = nullptr;  // the last exchange's stream work (boundary kernels on the compute stream wait for it)
     double* resid = nullptr;  // 2 accumulators (halo-stream kernels, compute-stream kernels)
     int64_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0, in_b = 0, in_e = 0;  // storage-plane regions
   };
@@ -153,6 +154,11 @@ class Solver {
   // the whole device before the long interior sweep takes every CU; the exchange still runs under
   // the interior (profiles/r03_wxk/)
   bool bnd_first_ = true;
+  // the boundary kernels run on the compute stream, ahead of the interior sweep of the same step,
+  // and only the exchange on the halo stream (overlap + boundary-first + a pure-stream-work
+  // transport; MDFX_BND_CS=0 keeps them on the halo stream)
+  bool bnd_cs_ = true;
+  bool boundary_on_cs() const;
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
   // hipGraphExec_t of the 2-sweep cycle starting at buffer p (index p), and its fused depth
   void* graph_exec_[2] = {nullptr, nullptr};
