@@ -264,10 +264,12 @@ void Solver::exchange_ghosts() {
 // 4-step sweep takes about 0.3 ms), and the exchange alone on the halo stream, after the boundary
 // kernels' event and overlapping the interior sweep. The next step's boundary kernels wait for that
 // exchange (ev_x): its ghosts are their input, and the faces it sent are what they overwrite.
-// Only for transports whose exchange is pure stream work on the halo stream (a host-side exchange
-// synchronises the halo stream alone).
+// Only for one slab per process (the production layout; 8 slabs in one process ran 1936 vs 2023
+// GCells/s with it, rank proxies N = 8 / 4 / 2 1850 / 2073 / 2284 vs 1824 / 2069 / 2259,
+// profiles/r03_session_x/) and transports whose exchange is pure stream work on the halo stream
+// (a host-side exchange synchronises the halo stream alone).
 bool Solver::boundary_on_cs() const {
-  return bnd_cs_ && opt_.overlap && bnd_first_ && transport_->graph_capturable();
+  return bnd_cs_ && opt_.overlap && bnd_first_ && slabs_.size() == 1 && transport_->graph_capturable();
 }
 
 void Solver::step(bool want_resid, int k) {
