@@ -89,7 +89,11 @@ def _reference(prob, steps, temporal=1):
 
 
 @pytest.mark.parametrize("world,temporal,graph", [(2, 1, False), (3, 1, False), (2, 2, False), (3, 2, False),
-                                                  (3, 2, True), (2, 3, False), (3, 3, True)])
+                                                  (3, 2, True), (2, 3, False), (3, 3, True),
+                                                  # middle ranks run boundary + interior as one fused
+                                                  # launch (heat7_wxk, K = 3 / 4), the exchange
+                                                  # started by the launch's boundary-done counter
+                                                  (3, 4, False), (4, 4, True), (4, 3, False)])
 def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
     import mpi_cuda_process_amd as m
 
