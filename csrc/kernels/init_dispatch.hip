@@ -312,7 +312,8 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
 bool hip_fused_boundary_ok(const StencilSpec& spec, const FieldLayout& lay, int steps) {
   return spec.kind == StencilKind::Heat7 && spec.dtype == DType::F32 && (steps == 3 || steps == 4) &&
          dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx) && lay.halo >= steps &&
-         hip_supports_steps(spec, lay, steps) && !dev::knobs().wxk_nb && !dev::knobs().wxk_bnb;
+         hip_supports_steps(spec, lay, steps) && !dev::knobs().wxk_nb && !dev::knobs().wxk_bnb &&
+         dev::knobs().wxk_ry != 42;
 }
 
 void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {

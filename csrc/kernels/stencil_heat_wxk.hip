@@ -78,7 +78,9 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // y bands, then z chunks (the first region's chunks, then the second region's)
   // fused launch: the boundary tasks [0, nbt) come first in dispatch order, each range XCD-remapped
   // on its own
-  const bool fused = g.lz3_end > g.lz3_begin;
+  // (not compiled into the 4 + 2-row band, which is at its VGPR limit, nor the deeper-window ones)
+  constexpr bool FUSABLE = NB == 2 && SPAR == 2 && !(RY == 4 && RE == 2);
+  const bool fused = FUSABLE && g.lz3_end > g.lz3_begin;
   const int b = !fused ? (int)xcd_remap(blockIdx.x, gridDim.x)
                 : (int)blockIdx.x < g.nbt ? (int)xcd_remap(blockIdx.x, g.nbt)
                                           : g.nbt + (int)xcd_remap(blockIdx.x - g.nbt, gridDim.x - g.nbt);
@@ -398,8 +400,9 @@ static void launch_wxk(const Geo& g0, const T* in, T* out, T r, double* resid, h
   const int64_t ntasks = wg.ntasks;
   Geo g = g0;
   if (g.lz3_end > g.lz3_begin) {
-    MDFX_CHECK(g.bcnt && g.bflag && g.lz_end > g.lz_begin && g.lz2_end > g.lz2_begin && !(NB != 2 || SPAR != 2),
-               "heat7_wxk: a fused launch needs both boundary regions, its counters and the default window");
+    MDFX_CHECK(g.bcnt && g.bflag && g.lz_end > g.lz_begin && g.lz2_end > g.lz2_begin && NB == 2 && SPAR == 2 &&
+                   !(RY == 4 && RE == 2),
+               "heat7_wxk: a fused launch needs both boundary regions, its counters and a fusable band shape");
     g.zc3 = wg.zc3;
     g.nbt = 2 * XT * YT;
   }
