@@ -45,7 +45,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 16, "temporal blocking depth must be 1..16");
   if (const char* v = std::getenv("MDFX_BND_FIRST")) bnd_first_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MDFX_BND_CS")) bnd_cs_ = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MDFX_BND_FUSE")) bnd_fuse_ = std::atoi(v) != 0;
+  if (const char* v = std::getenv("MDFX_BND_FUSE")) bnd_fuse_ = std::atoi(v) != 0;  // (default off)
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)

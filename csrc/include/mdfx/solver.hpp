@@ -163,10 +163,13 @@ class Solver {
   // transport; MDFX_BND_CS=0 keeps them on the halo stream)
   bool bnd_cs_ = true;
   bool boundary_on_cs() const;
-  // ... and, where the kernel supports it (hip_fused_boundary_ok), boundary regions and interior
-  // in ONE launch, the exchange started by a device wait on the launch's boundary-done counter
-  // (MDFX_BND_FUSE=0: two launches)
-  bool bnd_fuse_ = true;
+  // ... and, with MDFX_BND_FUSE=1 where the kernel supports it (hip_fused_boundary_ok), boundary
+  // regions and interior in ONE launch, the exchange started by a device wait on the launch's
+  // boundary-done counter. Off by default: the fused launch keeps every CU busy to its end, so the
+  // exchange's copy kernels find no room beside it and run after it (rank proxy N = 8 1757-1772 vs
+  // 1846-1852 GCells/s with two launches, where the 235-block interior leaves 21 CUs free;
+  // profiles/r03_session_y/)
+  bool bnd_fuse_ = false;
   bool fused_ok_[17] = {};
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
   // hipGraphExec_t of the 2-sweep cycle starting at buffer p (index p), and its fused depth
