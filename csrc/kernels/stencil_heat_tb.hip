@@ -548,10 +548,21 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   // interior in z need no z test: one loop copy without it, one with the per-level test for chunks
   // at the z boundary.
   const bool zint = zs - K - 1 + g.gz_off >= 1 && ze + K - 1 + g.gz_off <= g.gnz - 2;
-  auto row_step = [&](int64_t q, Row(&Cin)[K], Row(&Cout)[K], auto ztest) __attribute__((always_inline)) {
+  // MODE 2 keeps TWO rows in flight (u0 rows q + 1 and q + 2 load while row q is consumed): one row
+  // of K-level work is far shorter than a loaded global-load round trip at 2-3 waves per SIMD
+  Row nx2 = MODE == 2 ? ld(zs - K + 1) : RO::zero();
+  auto row_step = [&](int64_t q, Row(&Cin)[K], Row(&Cout)[K], auto ztest, auto slot) __attribute__((always_inline)) {
     constexpr bool ZT = decltype(ztest)::value;
-    Row X = nx;
-    nx = ld(q + 1);
+    constexpr int SL = decltype(slot)::value;  // MODE 2: which of the two in-flight rows is row q
+    Row X;
+    if constexpr (MODE == 2) {
+      Row& nq = SL == 0 ? nx : nx2;
+      X = nq;
+      nq = ld(q + 2);
+    } else {
+      X = nx;
+      nx = ld(q + 1);
+    }
 #pragma unroll
     for (int l = 1; l <= K; ++l) {
       const int64_t row = q - l;
@@ -587,11 +598,11 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
     if constexpr (MODE == 2) {
       // an odd row count ends with one extra row (q = qlast + 1): loads clamp, nothing is stored
       for (int64_t q = zs - K; q <= qlast; q += 2) {
-        row_step(q, CA, CB, ztest);
-        row_step(q + 1, CB, CA, ztest);
+        row_step(q, CA, CB, ztest, std::integral_constant<int, 0>{});
+        row_step(q + 1, CB, CA, ztest, std::integral_constant<int, 1>{});
       }
     } else {
-      for (int64_t q = zs - K; q <= qlast; ++q) row_step(q, CA, CA, ztest);
+      for (int64_t q = zs - K; q <= qlast; ++q) row_step(q, CA, CA, ztest, std::integral_constant<int, 0>{});
     }
   };
   // (fp64: one loop copy with the test; the second copy costs the VGPRs of occupancy 4 at K = 8)
