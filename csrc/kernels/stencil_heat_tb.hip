@@ -507,6 +507,8 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   constexpr int N = VT<T>::N;
   constexpr int OV = (K + N - 1) / N;  // overlap lanes per side
   constexpr int SEG = (64 - 2 * OV) * N;  // owned columns per wave
+  // u0 rows in flight: MODE 2 two, MODE 3 four (the row loop unrolled by as many); modes 0 / 1 one
+  constexpr int PD = MODE == 3 ? 4 : MODE == 2 ? 2 : 1;
   const int lane = threadIdx.x & 63;
   // wave-uniform task index in an SGPR, so every row index and row test below is scalar
   const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -548,21 +550,19 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   // interior in z need no z test: one loop copy without it, one with the per-level test for chunks
   // at the z boundary.
   const bool zint = zs - K - 1 + g.gz_off >= 1 && ze + K - 1 + g.gz_off <= g.gnz - 2;
-  // MODE 2 keeps TWO rows in flight (u0 rows q + 1 and q + 2 load while row q is consumed): one row
-  // of K-level work is far shorter than a loaded global-load round trip at 2-3 waves per SIMD
-  Row nx2 = MODE == 2 ? ld(zs - K + 1) : RO::zero();
+  // MODE 2 / 3 keep PD rows in flight (u0 rows q + 1 .. q + PD load while row q is consumed): one
+  // row of K-level work is far shorter than a loaded global-load round trip at 2-3 waves per SIMD
+  // (16384^2 fp32 K = 8: 4487-4515 GCells/s with two rows in flight vs 4202-4208 with one,
+  // profiles/r03_session_aa/)
+  Row nxr[PD];
+  nxr[0] = nx;
+#pragma unroll
+  for (int i = 1; i < PD; ++i) nxr[i] = ld(zs - K + i);
   auto row_step = [&](int64_t q, Row(&Cin)[K], Row(&Cout)[K], auto ztest, auto slot) __attribute__((always_inline)) {
     constexpr bool ZT = decltype(ztest)::value;
-    constexpr int SL = decltype(slot)::value;  // MODE 2: which of the two in-flight rows is row q
-    Row X;
-    if constexpr (MODE == 2) {
-      Row& nq = SL == 0 ? nx : nx2;
-      X = nq;
-      nq = ld(q + 2);
-    } else {
-      X = nx;
-      nx = ld(q + 1);
-    }
+    constexpr int SL = decltype(slot)::value;  // which in-flight row is row q
+    Row X = nxr[SL];
+    nxr[SL] = ld(q + PD);
 #pragma unroll
     for (int l = 1; l <= K; ++l) {
       const int64_t row = q - l;
@@ -601,6 +601,14 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
         row_step(q, CA, CB, ztest, std::integral_constant<int, 0>{});
         row_step(q + 1, CB, CA, ztest, std::integral_constant<int, 1>{});
       }
+    } else if constexpr (MODE == 3) {
+      // up to three extra rows at the end: loads clamp, nothing is stored
+      for (int64_t q = zs - K; q <= qlast; q += 4) {
+        row_step(q, CA, CB, ztest, std::integral_constant<int, 0>{});
+        row_step(q + 1, CB, CA, ztest, std::integral_constant<int, 1>{});
+        row_step(q + 2, CA, CB, ztest, std::integral_constant<int, 2>{});
+        row_step(q + 3, CB, CA, ztest, std::integral_constant<int, 3>{});
+      }
     } else {
       for (int64_t q = zs - K; q <= qlast; ++q) row_step(q, CA, CA, ztest, std::integral_constant<int, 0>{});
     }
@@ -637,6 +645,10 @@ static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double*
   if constexpr (sizeof(T) == 4) {
     // the reference-precision instance keeps 4 waves per SIMD without the unroll (16384^2 K = 8:
     // 3346-3368 GCells/s vs 3131-3145 unrolled at 2 waves per SIMD; plain fp32 ties, 4147-4212)
+    if (knobs().j5_nat == 3 && !REF) {
+      launch_jacobi5_tbk_km<T, K, REF, 3>(g, in, out, r, resid, s);
+      return;
+    }
     if (knobs().j5_nat == 2 && !REF) {
       launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
       return;
