@@ -45,7 +45,6 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 16, "temporal blocking depth must be 1..16");
   if (const char* v = std::getenv("MDFX_BND_FIRST")) bnd_first_ = std::atoi(v) != 0;
   if (const char* v = std::getenv("MDFX_BND_CS")) bnd_cs_ = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MDFX_BND_FUSE")) bnd_fuse_ = std::atoi(v) != 0;  // (default off)
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
@@ -76,10 +75,6 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.ev_int = s.be->create_event();
     s.ev_x = s.be->create_event();
     s.resid = (double*)s.be->alloc(2 * sizeof(double));
-    if (s.be->kind() == DeviceKind::HIP && nranks > 1 && backends.size() == 1) {
-      s.be->activate();
-      s.bsig = (uint64_t*)hip_alloc_uncached(48 * sizeof(uint64_t));
-    }
     for (int kk = 2; kk <= opt_.temporal; ++kk) {
       const bool ok = s.be->kind() != DeviceKind::HIP || hip_supports_steps(spec_, s.lay, kk);
       depth_ok_[kk] = (i == 0 ? true : depth_ok_[kk]) && ok;
@@ -101,8 +96,6 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.hi_b = has_hi ? std::max(oe - halo, s.lo_e) : oe;
     s.in_b = s.lo_e;
     s.in_e = s.hi_b;
-    for (int kk = 2; kk <= opt_.temporal; ++kk)
-      fused_ok_[kk] = s.bsig && has_lo && has_hi && s.in_e > s.in_b && hip_fused_boundary_ok(spec_, s.lay, kk);
     slabs_.push_back(std::move(s));
   }
   for (auto& s : slabs_) s.be->sync_device();
@@ -156,10 +149,6 @@ Solver::~Solver() {
     s.be->destroy_event(s.ev_bnd);
     s.be->destroy_event(s.ev_int);
     s.be->destroy_event(s.ev_x);
-    if (s.bsig) {
-      s.be->activate();
-      hip_free_uncached(s.bsig);
-    }
     s.be->destroy_stream(s.hs);
     s.be->destroy_stream(s.cs);
   }
@@ -286,7 +275,6 @@ bool Solver::boundary_on_cs() const {
 void Solver::step(bool want_resid, int k) {
   const int nb = 1 - cur_;
   const bool bcs = boundary_on_cs();
-  const bool fuse = bcs && bnd_fuse_ && fused_ok_[k];
   const bool prof = opt_.profile;
   const bool prof_hip = prof && pev_[0] != nullptr;
   using clk = std::chrono::steady_clock;
@@ -301,34 +289,6 @@ void Solver::step(bool want_resid, int k) {
     a.out = s.buf[nb];
     a.lay = s.lay;
     a.steps = k;
-    if (fuse) {
-      // compute stream: ONE launch, both boundary regions first (their last block bumps bsig[16]),
-      // then the interior; halo stream: a device wait for that signal, then the exchange
-      a.resid = want_resid ? s.resid : nullptr;
-      if (want_resid) s.be->memset(s.resid, 0, 2 * sizeof(double), s.cs);
-      s.be->wait(s.cs, s.ev_x);
-      if (p0) {
-        HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)s.cs));
-        HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)s.cs));
-        HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)s.cs));
-      }
-      a.lz_begin = s.lo_b;
-      a.lz_end = s.lo_e;
-      a.lz2_begin = s.hi_b;
-      a.lz2_end = s.hi_e;
-      a.lz3_begin = s.in_b;
-      a.lz3_end = s.in_e;
-      a.bnd_count = (unsigned*)s.bsig;
-      a.bnd_flag = (unsigned long long*)(s.bsig + 16);
-      s.be->stencil(spec_, a, s.cs);
-      if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[3], (hipStream_t)s.cs));
-      s.be->record(s.ev_int, s.cs);
-      s.be->record(s.ev_bnd, s.cs);  // (the whole launch: for eager work that needs every plane)
-      hip_counter_wait(s.bsig + 16, s.bsig + 32, opt_.timeout_s > 0 ? opt_.timeout_s : 300.0, s.hs);
-      if (opt_.sync_debug) s.be->sync_device();
-      s.be->trace_pop();
-      continue;
-    }
     void* bs = bcs ? s.cs : s.hs;  // the boundary kernels' stream
     if (want_resid) {
       s.be->memset(s.resid, 0, sizeof(double), bs);

@@ -26,13 +26,6 @@ struct RegionArgs {
   // optional second region written by the same call (the engine passes both K-plane boundary
   // regions of a slab at once; heat7_wtk runs them as one launch, other kernels as two)
   int64_t lz2_begin = 0, lz2_end = 0;
-  // fused launch (hip_fused_boundary_ok): regions 1 / 2 are the slab's two boundary regions, this
-  // third one its interior, all in ONE launch with the boundary tasks dispatched first; when every
-  // boundary block is done the kernel bumps *bnd_flag (+1 per launch, system-scope release), which
-  // a device wait on the halo stream turns into the exchange's start (bnd_count: scratch, 0)
-  int64_t lz3_begin = 0, lz3_end = 0;
-  unsigned* bnd_count = nullptr;
-  unsigned long long* bnd_flag = nullptr;
   double* resid = nullptr;           // optional accumulator of sum((out-in)^2) over the region
   // Time steps fused into this sweep (temporal blocking). 2 needs lay.halo >= 2 and reads
   // in[lz_begin-2, lz_end+2); the residual then covers the second step only.
@@ -41,9 +34,6 @@ struct RegionArgs {
 
 // Whether a fused multi-step sweep is implemented for this stencil / grid on the device.
 bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps);
-// Whether hip_stencil can run a slab's two boundary regions and its interior as one fused launch
-// (RegionArgs::lz3_*, bnd_*) for this stencil, layout and depth (heat7_wxk, fp32, K = 3 / 4).
-bool hip_fused_boundary_ok(const StencilSpec& spec, const FieldLayout& lay, int steps);
 // The deepest fused sweep that is a measured win for this stencil at row width nx (before any
 // cap by slab depth): 8 for the 2D MDF, 12 for Life, 3 for the 3D 7-point where heat7_wtk's x
 // segments cover the row efficiently, else 2 (profiles/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt).

@@ -124,10 +124,6 @@ class Solver {
     void* ev_bnd = nullptr;
     void* ev_int = nullptr;
     void* ev_x = nullptr;  // the last exchange's stream work (boundary kernels on the compute stream wait for it)
-    // fused boundary + interior launches (HIP, one slab per process): [0] the launch's boundary
-    // blocks done (u32), [16] launches whose boundary regions are complete (u64, bumped by the
-    // kernel), [32] the halo stream's device wait's private expect counter (u64); uncached memory
-    uint64_t* bsig = nullptr;
     double* resid = nullptr;  // 2 accumulators (halo-stream kernels, compute-stream kernels)
     int64_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0, in_b = 0, in_e = 0;  // storage-plane regions
   };
@@ -163,14 +159,6 @@ class Solver {
   // transport; MDFX_BND_CS=0 keeps them on the halo stream)
   bool bnd_cs_ = true;
   bool boundary_on_cs() const;
-  // ... and, with MDFX_BND_FUSE=1 where the kernel supports it (hip_fused_boundary_ok), boundary
-  // regions and interior in ONE launch, the exchange started by a device wait on the launch's
-  // boundary-done counter. Off by default: the fused launch keeps every CU busy to its end, so the
-  // exchange's copy kernels find no room beside it and run after it (rank proxy N = 8 1757-1772 vs
-  // 1846-1852 GCells/s with two launches, where the 235-block interior leaves 21 CUs free;
-  // profiles/r03_session_y/)
-  bool bnd_fuse_ = false;
-  bool fused_ok_[17] = {};
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
   // hipGraphExec_t of the 2-sweep cycle starting at buffer p (index p), and its fused depth
   void* graph_exec_[2] = {nullptr, nullptr};

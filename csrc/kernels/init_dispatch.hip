@@ -309,32 +309,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
   return 1;
 }
 
-bool hip_fused_boundary_ok(const StencilSpec& spec, const FieldLayout& lay, int steps) {
-  return spec.kind == StencilKind::Heat7 && spec.dtype == DType::F32 && (steps == 3 || steps == 4) &&
-         dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx) && lay.halo >= steps &&
-         hip_supports_steps(spec, lay, steps) && !dev::knobs().wxk_nb && !dev::knobs().wxk_bnb &&
-         dev::knobs().wxk_ry != 42;
-}
-
 void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
-  if (a.lz3_end > a.lz3_begin) {
-    // one fused launch: both boundary regions (dispatched first, signalling bnd_flag) + the interior
-    MDFX_CHECK(hip_fused_boundary_ok(spec, a.lay, a.steps) && a.bnd_count && a.bnd_flag,
-               "fused boundary + interior launch not supported here");
-    MDFX_CHECK(a.lz_end > a.lz_begin && a.lz2_end > a.lz2_begin && a.lz_begin >= a.lay.halo &&
-                   a.lz_end <= a.lz3_begin && a.lz3_end <= a.lz2_begin && a.lz2_end <= a.lay.halo + a.lay.nzl(),
-               "fused launch: low boundary, interior, high boundary must be ordered owned regions");
-    dev::Geo g = dev::make_geo(a.lay, a.lz_begin, a.lz_end);
-    g.lz2_begin = a.lz2_begin;
-    g.lz2_end = a.lz2_end;
-    g.lz3_begin = a.lz3_begin;
-    g.lz3_end = a.lz3_end;
-    g.bcnt = a.bnd_count;
-    g.bflag = a.bnd_flag;
-    dev::launch_heat7_wxk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid,
-                                 (hipStream_t)stream);
-    return;
-  }
   if (a.lz2_end > a.lz2_begin) {
     // two regions in one call: heat7_wtk sweeps them in ONE launch (both boundary regions of a
     // slab: one fill of the device, one launch gap); every other kernel runs them one after the other

@@ -34,13 +34,6 @@ struct Geo {
   int64_t gz_off;    // global z = lz + gz_off
   int64_t lz_max;    // storage planes allocated (loads outside [0,lz_max) return 0)
   int64_t lz2_begin = 0, lz2_end = 0;  // optional second region of the same launch (heat7_wtk)
-  // fused boundary + interior launch (heat7_wxk): regions 1 and 2 are the slab's boundary regions
-  // (one z chunk each, their tasks dispatched first), region 3 the interior in chunks of zc3; the
-  // last boundary block to finish releases its writes and bumps *bflag (system scope)
-  int64_t lz3_begin = 0, lz3_end = 0;
-  int zc3 = 0, nbt = 0;                 // interior chunk height; boundary tasks of the launch
-  unsigned* bcnt = nullptr;             // boundary blocks done in this launch (uncached)
-  unsigned long long* bflag = nullptr;  // launches whose boundary regions are complete (uncached)
   int64_t alloc = 0;                 // elements allocated (planes + slack), for device checks
   unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };

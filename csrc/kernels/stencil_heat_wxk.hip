@@ -76,14 +76,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // work: block-uniform task = one z chunk of one (x segment, y band) tile; x segments fastest, then
   // y bands, then z chunks (the first region's chunks, then the second region's)
-  // fused launch: the boundary tasks [0, nbt) come first in dispatch order, each range XCD-remapped
-  // on its own
-  // (not compiled into the 4 + 2-row band, which is at its VGPR limit, nor the deeper-window ones)
-  constexpr bool FUSABLE = NB == 2 && SPAR == 2 && !(RY == 4 && RE == 2);
-  const bool fused = FUSABLE && g.lz3_end > g.lz3_begin;
-  const int b = !fused ? (int)xcd_remap(blockIdx.x, gridDim.x)
-                : (int)blockIdx.x < g.nbt ? (int)xcd_remap(blockIdx.x, g.nbt)
-                                          : g.nbt + (int)xcd_remap(blockIdx.x - g.nbt, gridDim.x - g.nbt);
+  const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   if (b >= ntasks) return;
   // NB window buffers: the u0 plane DMA runs NB - 1 planes ahead of the plane being computed
   __shared__ V win[NB][RB][64];
@@ -95,18 +88,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int P0 = (int)(g.lz_end - g.lz_begin);
   const int zt1 = (P0 + zc - 1) / zc;
   int zs, ze;
-  if (fused) {  // chunk 0: the low boundary region, 1: the high one, 2..: the interior
-    if (zt == 0) {
-      zs = (int)g.lz_begin;
-      ze = (int)g.lz_end;
-    } else if (zt == 1) {
-      zs = (int)g.lz2_begin;
-      ze = (int)g.lz2_end;
-    } else {
-      zs = (int)g.lz3_begin + (zt - 2) * g.zc3;
-      ze = min((int)g.lz3_end, zs + g.zc3);
-    }
-  } else if (zt < zt1) {
+  if (zt < zt1) {
     zs = (int)g.lz_begin + zt * zc;
     ze = min((int)g.lz_end, zs + zc);
   } else {
@@ -337,28 +319,13 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
     if (yint) march(IC<1>{}, std::false_type{});
     else march(IC<1>{}, std::true_type{});
   }
-  wait_vm0();  // no DMA may outlive the wave (and this wave's output stores are complete)
+  wait_vm0();  // no DMA may outlive the wave
   if (RES) wave_atomic_add(resid, acc);
-  if (fused && zt < 2) {
-    // a boundary block: once every wave's stores are done, release them device-wide (this XCD's
-    // L2 written back) and count the block; the launch's last boundary block resets the count and
-    // bumps the flag the halo stream's device wait is polling (vector atomics from one lane)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      const unsigned done = __hip_atomic_fetch_add(g.bcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
-      if (done == (unsigned)g.nbt) {
-        __hip_atomic_store(g.bcnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __hip_atomic_fetch_add(g.bflag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
 }
 
 // launch geometry of one shape: tiles, z chunks, and the rounds of resident blocks they take
 struct WxGeo {
-  int XT = 0, YT = 0, zc = 0, zc3 = 0;
+  int XT = 0, YT = 0, zc = 0;
   int64_t ntasks = 0, resident = 0, rounds = 0;
 };
 template <class T, int RY, int RE, int K, int WB, int NB = 2, int SPAR = 2>
@@ -374,38 +341,23 @@ static WxGeo wxk_geo(const Geo& g) {
   w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false, NB, SPAR>, 64 * WB);
   w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, hip_min_rounds_now());
   if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
-  int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
-  if (g.lz3_end > g.lz3_begin) {
-    // fused: one chunk per boundary region, then the interior chunked on the slots the boundary
-    // tasks leave over one round
-    const int64_t planes3 = g.lz3_end - g.lz3_begin;
-    w.zc3 = knobs().zc > 0 ? knobs().zc : wx_zc(planes3, tiles, w.resident, K, 2 * K, hip_min_rounds_now());
-    ZT = 2 + (int)((planes3 + w.zc3 - 1) / w.zc3);
-  }
+  const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
   w.ntasks = tiles * ZT;
   w.rounds = (w.ntasks + w.resident - 1) / w.resident;
   return w;
 }
 
 template <class T, int RY, int RE, int K, int WB, int NB = 2, int SPAR = 2>
-static void launch_wxk(const Geo& g0, const T* in, T* out, T r, double* resid, hipStream_t s) {
+static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if constexpr (NB != 2 || SPAR != 2) {
-    if (resid || g0.lz3_end > g0.lz3_begin) {  // (the deeper-window instances: no residual, no fused launch)
-      launch_wxk<T, RY, RE, K, WB>(g0, in, out, r, resid, s);
+    if (resid) {  // (the deeper-window instances have no residual copy)
+      launch_wxk<T, RY, RE, K, WB>(g, in, out, r, resid, s);
       return;
     }
   }
-  const WxGeo wg = wxk_geo<T, RY, RE, K, WB, NB, SPAR>(g0);
+  const WxGeo wg = wxk_geo<T, RY, RE, K, WB, NB, SPAR>(g);
   const int XT = wg.XT, YT = wg.YT, zc = wg.zc;
   const int64_t ntasks = wg.ntasks;
-  Geo g = g0;
-  if (g.lz3_end > g.lz3_begin) {
-    MDFX_CHECK(g.bcnt && g.bflag && g.lz_end > g.lz_begin && g.lz2_end > g.lz2_begin && NB == 2 && SPAR == 2 &&
-                   !(RY == 4 && RE == 2),
-               "heat7_wxk: a fused launch needs both boundary regions, its counters and a fusable band shape");
-    g.zc3 = wg.zc3;
-    g.nbt = 2 * XT * YT;
-  }
   if (knobs().debug_zc)
     fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d NB=%d SPAR=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
             K, RY, RE, WB, NB, SPAR, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
@@ -447,8 +399,6 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
              "heat7_wxk: the second region must follow the first and have its planes + ghosts allocated");
-  MDFX_CHECK(g.lz3_end <= g.lz3_begin || (g.lz3_begin >= g.lz_end && g.lz3_end <= g.lz2_begin),
-             "heat7_wxk: a fused launch's interior must lie between its boundary regions");
   MDFX_CHECK(g.pitch % VT<T>::N == 0, "heat7_wxk: the row pitch must be a whole number of vectors");
   MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),

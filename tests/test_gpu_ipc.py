@@ -98,13 +98,8 @@ def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
     out = str(tmp_path / "g.npy")
     steps = 13
     code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps)
-    # K >= 3 with a middle rank: also with boundary + interior as one fused launch (heat7_wxk), the
-    # exchange started by the launch's boundary-done counter (MDFX_BND_FUSE=1)
-    for fuse in (["0", "1"] if temporal >= 3 and world >= 3 else ["0"]):
-        _spawn(world, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_BND_FUSE": fuse})
-        got = np.load(out)
-        ref, rres = _reference(eval(prob_src), steps)
-        assert np.array_equal(got, ref), fuse
+    _spawn(world, lambda r: [sys.executable, "-c", code])
+    got = np.load(out)
     ref, rres = _reference(eval(prob_src), steps)
     assert np.array_equal(got, ref)
     meta = json.load(open(out + ".json"))
