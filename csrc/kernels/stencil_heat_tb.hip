@@ -662,6 +662,14 @@ static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double*
       return;
     }
   }
+  // fp64: the pair rows (RowOps<double>) with the 2-row unroll and two u0 rows in flight under
+  // MDFX_J5_F64_PD = 1
+  if constexpr (sizeof(T) == 8) {
+    if (knobs().j5_f64_pd) {
+      launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
+      return;
+    }
+  }
   launch_jacobi5_tbk_km<T, K, REF, 0>(g, in, out, r, resid, s);
 }
 
