@@ -92,7 +92,7 @@ static Knobs read_knobs() {
   k.wxk_ry = env_int("MDFX_WXK_RY", 0);
   k.wxk_nb = env_int("MDFX_WXK_NB", 0);
   k.wxk_bnb = env_int("MDFX_WXK_BNB", 0);
-  k.j5_f64_pd = env_int("MDFX_J5_F64_PD", 0);
+  k.j5_f64_pd = env_int("MDFX_J5_F64_PD", 1);
   k.b27_wxp = env_int("MDFX_B27_WXP", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);

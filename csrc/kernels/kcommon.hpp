@@ -229,7 +229,7 @@ struct Knobs {
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
   int b27_wxp = 0;     // MDFX_B27_WXP: 1 = box27_wxk's x-pair kernel for fp32 rows of 257..512 cells (measured slower: profiles/r03_session_t/)
   int wxk_nb = 0;      // MDFX_WXK_NB: heat7_wxk fp32 K = 4 window depth x seam tables (31: 3 buffers + 1 table, 21, 32: 2 + 2 rows; all measured slower, profiles/r03_session_r/)
-  int j5_f64_pd = 0;   // MDFX_J5_F64_PD: 1 = fp64 jacobi5_tbk with the 2-row unroll and two u0 rows in flight
+  int j5_f64_pd = 1;   // MDFX_J5_F64_PD: fp64 jacobi5_tbk with the 2-row unroll and two u0 rows in flight (0: mode 0)
   int wxk_bnb = 0;     // MDFX_WXK_BNB: MDFX_WXK_NB for the boundary-region launches only (fp32 K = 4)
   int wxk_ry = 0;      // MDFX_WXK_RY: heat7_wxk fp32 band (K = 3: 3 = 3-row waves; K = 4: 42 / 32 / 22 / 31 / 21 =
                        // inner / edge rows; 0: 32)

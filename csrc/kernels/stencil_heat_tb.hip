@@ -662,8 +662,9 @@ static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double*
       return;
     }
   }
-  // fp64: the pair rows (RowOps<double>) with the 2-row unroll and two u0 rows in flight under
-  // MDFX_J5_F64_PD = 1
+  // fp64: the pair rows (RowOps<double>) with the 2-row unroll and two u0 rows in flight
+  // (16384^2 K = 8: 2216-2219 vs 2005 GCells/s for mode 0, occupancy 3 vs 4;
+  // profiles/r03_session_ac/); MDFX_J5_F64_PD = 0 keeps mode 0
   if constexpr (sizeof(T) == 8) {
     if (knobs().j5_f64_pd) {
       launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
