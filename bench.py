@@ -312,13 +312,6 @@ def run_proxy(a):
         for g, rr, ov in cands:
             trials.append({"graph": g, "min_rounds": rr, "overlap": ov, "ms_per_step": round(best_t[(g, rr, ov)], 4)})
         chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
-    if len(cands) > 1:
-        # the timed run gets a fresh engine: a graph cycle replayed after init() on the engine that
-        # ran the trials measured 2.5x slower than the same cycle on a fresh one (proxy N = 8, K = 2:
-        # 410 vs 1012 GCells/s, profiles/r03_session_ai/)
-        sim.close()
-        sim = Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=chosen[0],
-                         residual_every=a.residual_every, timeout_s=a.timeout)
     sim.set_options(graph=chosen[0], min_rounds=chosen[1], overlap=chosen[2])
     sim.init()
     sim.prepare_graphs()
@@ -526,10 +519,7 @@ def main(argv=None):
             trials.append({"transport": t, "graph": g, "min_rounds": rr, "overlap": ov,
                            "ms_per_step": round(best_t[(t, g, rr, ov)], 4)})
         chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
-        if sim_t != chosen[0] or (hip and env):
-            # several processes: the timed run gets a fresh engine (a graph cycle replayed after
-            # init() on the engine that ran the trials measured 2.5x slower in the rank proxy,
-            # profiles/r03_session_ai/)
+        if sim_t != chosen[0]:
             sim.close()
             sim = None
     else:
