@@ -182,16 +182,6 @@ def make_problem(a, nx, ny, nz):
     return life2d(h=nz, w=nx)
 
 
-def trial_warmup(warmup, temporal):
-    """Warm-up steps before each timed trial: the timed run's own count, or a shorter one congruent
-    to it modulo a replayed cycle (2 sweeps of `temporal` steps), so a trial starts its graph cycles
-    on the same buffer parity as the timed run (profiles/r03_session_ak/)."""
-    cyc = 2 * max(1, temporal)
-    if warmup <= 2 * cyc:
-        return warmup
-    return cyc + warmup % cyc
-
-
 def pick_temporal(a, prob, nslab, hip):
     from mpi_cuda_process_amd import native
 
@@ -317,7 +307,7 @@ def run_proxy(a):
                 sim.set_options(graph=g, min_rounds=rr, overlap=ov)
                 sim.init()
                 sim.prepare_graphs()
-                sim.run(trial_warmup(a.warmup, temporal))
+                sim.run(max(2, min(a.warmup, 6)))
                 best_t[c] = min(best_t.get(c, 1e30), timed(n_trial) / n_trial * 1e3)
         for g, rr, ov in cands:
             trials.append({"graph": g, "min_rounds": rr, "overlap": ov, "ms_per_step": round(best_t[(g, rr, ov)], 4)})
@@ -520,7 +510,7 @@ def main(argv=None):
                     sim.init()
                 sim.set_options(graph=g, min_rounds=rr, overlap=ov)
                 sim.prepare_graphs()  # capture before timing (no-op with graphs off)
-                sim.run(trial_warmup(a.warmup, temporal))
+                sim.run(max(2, min(a.warmup, 6)))
                 dt = timed(sim, n_trial)
                 trace("trial %s graph=%s rounds=%s overlap=%s: %.3f ms/step" % (t, g, rr, ov, dt / n_trial * 1e3))
                 key = (t, g, rr, ov)
