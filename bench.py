@@ -307,7 +307,7 @@ def run_proxy(a):
                 sim.set_options(graph=g, min_rounds=rr, overlap=ov)
                 sim.init()
                 sim.prepare_graphs()
-                sim.run(max(2, min(a.warmup, 6)))
+                sim.run(a.warmup)  # the timed run's own warm-up: same buffer parity and replay state
                 best_t[c] = min(best_t.get(c, 1e30), timed(n_trial) / n_trial * 1e3)
         for g, rr, ov in cands:
             trials.append({"graph": g, "min_rounds": rr, "overlap": ov, "ms_per_step": round(best_t[(g, rr, ov)], 4)})
@@ -323,6 +323,7 @@ def run_proxy(a):
         dt = timed(a.steps)
         best = dt if best is None else min(best, dt)
     per_gpu = slab_cells * a.steps / best / 1e9
+    timed_vs_trial = (round(best / a.steps * 1e3 / min(t["ms_per_step"] for t in trials), 3) if trials else None)
     model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF", "life": "2D Game of Life"}[a.stencil]
     dram_tbps = per_gpu * prob.bytes_per_cell_per_step / temporal / 1e3
     rec = {
@@ -343,10 +344,13 @@ def run_proxy(a):
         "data": "synthetic (uniform random grid from a counter hash of the global index, seed 1)",
         "config": {"model": "%s %dx%dx%d %s" % (model, nx, ny, nz, a.dtype), "slab_planes": [lay["z0"], lay["z1"]],
                    "ghost_planes": lay["halo"], "temporal_block": temporal, "transport": sim.transport,
+                   "face_copy": native().face_copy_mode(),
+                   "ipc_protocol": "direct" if native().ipc_direct_ok(lay["bytes"]) else "mailbox",
                    "graph": (sim.graph_replays - replays0) > 0, "graph_requested": chosen[0],
                    "graph_replays_timed": sim.graph_replays - replays0,
                    "graph_captures_timed": sim.graph_captures - captures0,
-                   "min_rounds": chosen[1], "overlap": chosen[2], "trials": trials},
+                   "min_rounds": chosen[1], "overlap": chosen[2], "trials": trials,
+                   "timed_vs_trial": timed_vs_trial},
         "achieved_dram_TBps": round(dram_tbps, 3),
         "pct_of_hbm_copy_roof": round(100.0 * dram_tbps / HBM_MEASURED_TBPS, 1),
     }
@@ -507,10 +511,12 @@ def main(argv=None):
                     sim = None
                 if sim is None:
                     sim, sim_t = make_sim(t, g, rr, ov), t
-                    sim.init()
                 sim.set_options(graph=g, min_rounds=rr, overlap=ov)
+                # exactly the timed run's sequence: fresh grid, captures, its own warm-up (so the trial
+                # starts on the same buffer parity and replay history as the run it picks)
+                sim.init()
                 sim.prepare_graphs()  # capture before timing (no-op with graphs off)
-                sim.run(max(2, min(a.warmup, 6)))
+                sim.run(a.warmup)
                 dt = timed(sim, n_trial)
                 trace("trial %s graph=%s rounds=%s overlap=%s: %.3f ms/step" % (t, g, rr, ov, dt / n_trial * 1e3))
                 key = (t, g, rr, ov)
@@ -551,6 +557,12 @@ def main(argv=None):
     cells = prob.cells
     gcells = cells * a.steps / best / 1e9
     ms = best / a.steps * 1e3
+    # the timed run against the trial that chose its configuration: well above 1 means the timed
+    # run landed in a slower state than its trial measured (reported, and warned about)
+    timed_vs_trial = round(ms / min(t["ms_per_step"] for t in trials), 3) if trials else None
+    if timed_vs_trial is not None and timed_vs_trial > 1.2 and rank == 0:
+        print("bench: WARNING: the timed run took %.2fx its trial's time per step" % timed_vs_trial,
+              file=sys.stderr, flush=True)
     nproc = world if env else 1
     # per physical GPU: ranks that share a device (--share-gpu) count once
     ngpu_phys = len(set(devices)) if hip else nproc
@@ -600,6 +612,10 @@ def main(argv=None):
                 "min_rounds": chosen[2] or ("2 (auto)" if nproc > 1 or a.virtual_ranks > 1 else "1 (auto)"),
                 "trials": trials,
                 "overlap": chosen[3],
+                "timed_vs_trial": timed_vs_trial,
+                "face_copy": native().face_copy_mode() if sim_transport == "ipc" else None,
+                "ipc_protocol": (("direct" if native().ipc_direct_ok(sim.layout(0)["bytes"]) else "mailbox")
+                                 if sim_transport == "ipc" else None),
                 "temporal_block": temporal,
                 "gate": gate,
             },

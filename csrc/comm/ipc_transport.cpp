@@ -1,23 +1,28 @@
-// HIP-IPC halo transport: one process per slab; each process publishes its boundary faces in a
-// small exported "mailbox" allocation, and the neighbours pull them straight into their ghost
-// planes with the copy engines, ordered by device-side counters instead of host synchronisation.
+// HIP-IPC halo transport: one process per slab; the neighbours pull each other's boundary faces
+// straight into their ghost planes with the SDMA copy engines (hipMemcpyDeviceToDeviceNoCU, over
+// xGMI between GPUs), ordered by device-side counters instead of host synchronisation.
 //
 // Why a second device-resident transport next to RCCL: RCCL's p2p send/recv runs as kernels that
-// occupy CUs the interior sweep wants, and RCCL refuses two ranks on one GPU. A pull through the
-// copy engine (SDMA over xGMI across GPUs, or a blit on the same GPU) takes no CUs beyond a
-// one-wave counter kernel, and works for any number of processes sharing a device — which is how
-// the device-resident multi-process path is tested on a one-GPU box (tests/test_gpu_ipc.py).
+// occupy CUs the interior sweep wants, and RCCL refuses two ranks on one GPU. An SDMA pull takes no
+// CUs beyond one-wave counter kernels, and works for any number of processes sharing a device —
+// which is how the device-resident multi-process path is tested on a one-GPU box
+// (tests/test_gpu_ipc.py). (A plain hipMemcpyDeviceToDevice between buffers of one device runs as
+// __amd_rocclr_copyBuffer blit kernels on the CUs: MDFX_XCOPY=blit, the round-3 behaviour.)
 //
-// Why mailboxes instead of mapping the neighbours' whole field buffers: only the faces ever cross
-// a process boundary, and the HIP runtime PyTorch bundles (ROCm 7.0) stalls forever in
-// hipIpcOpenMemHandle on an exported hipMalloc of 2 GiB or more (scripts/ipc_probe.py on one
-// MI355X: 1900 MiB maps at once, 2048 MiB and 2 GiB + 16 MiB stall with torch's runtime loaded,
-// and the same 2 GiB + 16 MiB maps at once under /opt/rocm 7.2's) — the field buffer of a 1024^3
-// fp32 slab at N = 2 is 2 GiB + 16 MiB. A mailbox holds 2 parities x 2 sides x
-// `halo` planes (32 MiB at 1024^2 fp32, K = 2); publishing costs one local D2D copy per face.
+// Two protocols, by field-buffer size:
+//   direct  (buffers below ~1.9 GiB, e.g. 1024^3 fp32 at N >= 4): each process exports its two
+//           field buffers and pulls the neighbour's face straight out of them: one copy per face.
+//   mailbox (larger buffers): the HIP runtime PyTorch bundles (ROCm 7.0) stalls forever in
+//           hipIpcOpenMemHandle on an exported hipMalloc of 2 GiB or more (scripts/ipc_probe.py on
+//           one MI355X: 1900 MiB maps at once, 2048 MiB and 2 GiB + 16 MiB stall with torch's
+//           runtime loaded, and the same 2 GiB + 16 MiB maps at once under /opt/rocm 7.2's) — the
+//           field buffer of a 1024^3 fp32 slab at N = 2 is 2 GiB + 16 MiB. Each process then
+//           publishes its faces into a small exported mailbox (2 parities x 2 sides x `halo`
+//           planes) with one local copy per face, and the neighbours pull from there.
+// MDFX_IPC_DIRECT=0 / 1 forces one (ipc_direct_ok).
 //
-// Protocol for exchange e (every process calls exchange() the same number of times; e = 1, 2, ..)
-// on the slab's halo stream, after the boundary kernels that wrote the faces of buffer b:
+// Mailbox protocol for exchange e (every process calls exchange() the same number of times;
+// e = 1, 2, ..) on the slab's halo stream, after the boundary kernels that wrote the faces of buffer b:
 //
 //   for each neighbour n:  wait(n.pulled[mine] >= e - 2)   n is done with mailbox slot b (exchange e-2)
 //                          (>= e - 1 when exchange e-1 used the same parity b: a re-send of the
@@ -32,11 +37,25 @@
 // device memory (private `expect` counters advance inside the wait kernel), so the enqueued work is
 // identical for every exchange and a captured hipGraph replays correctly.
 //
+// Direct protocol for exchange e (same counters; `pulled` starts at 1):
+//
+//   signal(ready)                                        my faces of b are final
+//   for each neighbour n:  wait(n.ready >= e)
+//                          copy n.buf[b].face(other side) -> my ghost(b)
+//                          signal(pulled[side])
+//   for each neighbour n:  wait(n.pulled[mine] >= e - 1) n pulled exchange e-1, which sent the faces
+//                                                        of buffer 1-b that the next step's boundary
+//                                                        kernels overwrite (they follow this exchange)
+//
+// A re-sent parity (exchange_ghosts) needs no look-ahead here: the last wait is already the
+// stronger condition.
+//
 // Reference parity: the per-element host-staged MPI_Send/MPI_Recv loops of
 // MDF_kernel.cu:167-169,180-183 (D5, D12) with their rank-1 self-addressing (D3).
 #include <hip/hip_runtime_api.h>
 #include <unistd.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "mdfx/devsync.hpp"
@@ -63,11 +82,25 @@ constexpr size_t kCounterBytes = 128 * 8;
 
 struct IpcRecord {
   char magic[8];
-  int32_t rank = -1, device = -1, pid = 0, pad = 0;
+  int32_t rank = -1, device = -1, pid = 0, direct = 0;
   uint64_t face_bytes = 0;  // one face (halo planes); the mailbox holds 4
-  hipIpcMemHandle_t mbox;
+  uint64_t face_off[2] = {0, 0};  // byte offsets of the lo / hi face in each field buffer (direct)
+  char pci[32] = {0};       // PCI bus id of the device: a stable identity across HIP_VISIBLE_DEVICES
+  hipIpcMemHandle_t mbox;   // (mailbox protocol)
+  hipIpcMemHandle_t buf[2];  // the two field buffers (direct protocol)
   hipIpcMemHandle_t ctr;
 };
+
+// This process's ordinal of the device with PCI bus id `pci` (-1 if it is not visible here).
+int local_device_of(const char* pci) {
+  if (!pci[0]) return -1;
+  int d = -1;
+  if (hipDeviceGetByPCIBusId(&d, pci) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return d;
+}
 
 class IpcTransport final : public Transport {
  public:
@@ -79,6 +112,8 @@ class IpcTransport final : public Transport {
     (void)hipSetDevice(self_.be->device());
     for (auto& p : peers_) {
       if (p.mbox) (void)hipIpcCloseMemHandle(p.mbox);
+      for (void* b : p.buf)
+        if (b) (void)hipIpcCloseMemHandle(b);
       if (p.ctr) (void)hipIpcCloseMemHandle(p.ctr);
     }
     if (mbox_) (void)hipFree(mbox_);
@@ -98,27 +133,48 @@ class IpcTransport final : public Transport {
     self_.be->activate();
     ctr_ = (uint64_t*)hip_alloc_uncached(kCounterBytes);
     words_ = hip_words_alloc();  // this transport's own abort / wait-error words
-    const uint64_t two = 2;  // exchanges 1 and 2 find their mailbox slot free
-    HIPC(hipMemcpy(ctr_ + kPulled + 0, &two, 8, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(ctr_ + kPulled + 1, &two, 8, hipMemcpyHostToDevice));
     dev_ok_ = true;
     // every face has the same size (halo planes of one field layout)
     face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
-    HIPC(hipMalloc(&mbox_, 4 * face_));
-    HIPC(hipMemset(mbox_, 0, 4 * face_));
-    HIPC(hipDeviceSynchronize());
+    // the protocol is agreed below (every rank must use the same one); counters start per protocol
+    const bool want_direct = ipc_direct_ok(self_.lay.bytes());
 
     IpcRecord mine;
-    std::memcpy(mine.magic, "MDFXIPC2", 8);
+    std::memcpy(mine.magic, "MDFXIPC3", 8);
     mine.rank = self_.rank;
     mine.device = self_.be->device();
     mine.pid = (int32_t)::getpid();
+    mine.direct = want_direct ? 1 : 0;
     mine.face_bytes = face_;
-    HIPC(hipIpcGetMemHandle(&mine.mbox, mbox_));
+    for (int side = 0; side < 2; ++side)
+      mine.face_off[side] = (uint64_t)((char*)halo_span(self_, 0, side, nranks_).send - (char*)self_.buf[0]);
+    if (hipDeviceGetPCIBusId(mine.pci, (int)sizeof(mine.pci) - 1, mine.device) != hipSuccess) {
+      (void)hipGetLastError();
+      mine.pci[0] = 0;
+    }
     HIPC(hipIpcGetMemHandle(&mine.ctr, ctr_));
+    if (want_direct) {
+      for (int b = 0; b < 2; ++b) HIPC(hipIpcGetMemHandle(&mine.buf[b], self_.buf[b]));
+    }
+    // the mailbox exists in both protocols (a rank that cannot go direct makes everyone fall back)
+    HIPC(hipMalloc(&mbox_, 4 * face_));
+    HIPC(hipMemset(mbox_, 0, 4 * face_));
+    HIPC(hipIpcGetMemHandle(&mine.mbox, mbox_));
+    HIPC(hipDeviceSynchronize());
     const std::vector<std::string> all =
         f_.allgather(std::string((const char*)&mine, sizeof(mine)));  // also the setup barrier
     MDFX_CHECK((int)all.size() == nranks_, format("ipc allgather returned %zu records for %d ranks", all.size(), nranks_));
+    direct_ = true;
+    for (const std::string& rec : all) {
+      MDFX_CHECK(rec.size() == sizeof(IpcRecord), "ipc: malformed handle record");
+      IpcRecord r;
+      std::memcpy(&r, rec.data(), sizeof(r));
+      direct_ = direct_ && r.direct != 0;
+    }
+    const uint64_t pulled0 = direct_ ? 1 : 2;  // the first exchange(s) find their faces / slots free
+    HIPC(hipMemcpy(ctr_ + kPulled + 0, &pulled0, 8, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(ctr_ + kPulled + 1, &pulled0, 8, hipMemcpyHostToDevice));
+    HIPC(hipDeviceSynchronize());
 
     const SlabDecomposition dec(self_.lay.global.nz, nranks_);
     for (int side = 0; side < 2; ++side) {
@@ -126,18 +182,31 @@ class IpcTransport final : public Transport {
       p.rank = side == 0 ? dec.lo_neighbor(self_.rank) : dec.hi_neighbor(self_.rank);
       if (p.rank < 0) continue;
       IpcRecord r;
-      MDFX_CHECK(all[p.rank].size() == sizeof(IpcRecord), "ipc: malformed handle record");
       std::memcpy(&r, all[p.rank].data(), sizeof(r));
-      IpcPeerInfo me{mine.rank, mine.device, mine.pid, mine.face_bytes, true};
-      IpcPeerInfo them{r.rank, r.device, r.pid, r.face_bytes, std::memcmp(r.magic, "MDFXIPC2", 8) == 0};
+      // the neighbour's device as THIS process numbers it (PCI bus id): with per-rank
+      // HIP_VISIBLE_DEVICES both sides call their GPU "device 0"
+      const int their = local_device_of(r.pci);
+      const bool same = mine.pci[0] && r.pci[0] ? std::strcmp(mine.pci, r.pci) == 0 : r.device == mine.device;
+      IpcPeerInfo me{mine.rank, 0, mine.pid, mine.face_bytes, true};
+      IpcPeerInfo them{r.rank, same ? 0 : 1, r.pid, r.face_bytes, std::memcmp(r.magic, "MDFXIPC3", 8) == 0};
       int can = 1;
-      if (r.device != mine.device) HIPC(hipDeviceCanAccessPeer(&can, mine.device, r.device));
+      if (!same && their >= 0) HIPC(hipDeviceCanAccessPeer(&can, mine.device, their));
       const std::string why = ipc_peer_problem(me, them, p.rank, can != 0);
       MDFX_CHECK(why.empty(), why);
-      ipc_enable_peer(mine.device, r.device, p.rank);
-      HIPC(hipIpcOpenMemHandle(&p.mbox, r.mbox, hipIpcMemLazyEnablePeerAccess));
+      // explicit peer enable where the neighbour's GPU is visible here; otherwise the IPC open's
+      // lazy peer mapping is all there is
+      if (!same && their >= 0) ipc_enable_peer(mine.device, their, p.rank);
+      if (direct_) {
+        for (int b = 0; b < 2; ++b) {
+          void* q = nullptr;
+          HIPC(hipIpcOpenMemHandle(&q, r.buf[b], hipIpcMemLazyEnablePeerAccess));
+          p.buf[b] = q;
+        }
+        p.face_off = r.face_off[1 - side];  // the neighbour's face that borders me
+      } else {
+        HIPC(hipIpcOpenMemHandle(&p.mbox, r.mbox, hipIpcMemLazyEnablePeerAccess));
+      }
       HIPC(hipIpcOpenMemHandle(&p.ctr, r.ctr, hipIpcMemLazyEnablePeerAccess));
-      p.device = r.device;
     }
     f_.barrier ? f_.barrier() : (void)f_.allgather("");
   }
@@ -153,6 +222,26 @@ class IpcTransport final : public Transport {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPC(hipStreamIsCapturing(hs, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
+    if (direct_) {
+      hip_counter_signal(ctr_ + kReady, hs);
+      for (int side = 0; side < 2; ++side) {
+        const Peer& p = peers_[side];
+        if (p.rank < 0) continue;
+        const HaloSpan mine = halo_span(self_, b, side, nranks_);
+        MDFX_CHECK(mine.bytes == face_ && mine.peer == p.rank, "ipc: face geometry mismatch");
+        hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
+        hip_face_copy(mine.recv, (const char*)p.buf[b] + p.face_off, face_, hs);
+        hip_counter_signal(ctr_ + kPulled + side, hs);
+      }
+      for (int side = 0; side < 2; ++side) {
+        const Peer& p = peers_[side];
+        if (p.rank < 0) continue;
+        hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs, 0,
+                         &words_);
+      }
+      if (!capturing) last_b_ = b;
+      return;
+    }
     const uint64_t ahead = (!capturing && last_b_ == b) ? 1 : 0;
     // publish: the neighbour on `side` must be done with slot b (exchange e-2) before it is reused
     for (int side = 0; side < 2; ++side) {
@@ -162,7 +251,7 @@ class IpcTransport final : public Transport {
       MDFX_CHECK(mine.bytes == face_ && mine.peer == p.rank, "ipc: face geometry mismatch");
       hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs,
                        ahead, &words_);
-      HIPC(hipMemcpyAsync(slot(mbox_, b, side), mine.send, face_, hipMemcpyDeviceToDevice, hs));
+      hip_face_copy(slot(mbox_, b, side), mine.send, face_, hs);
     }
     hip_counter_signal(ctr_ + kReady, hs);
     // pull: the neighbour on `side` published its (1 - side) face of exchange e
@@ -171,7 +260,7 @@ class IpcTransport final : public Transport {
       if (p.rank < 0) continue;
       const HaloSpan mine = halo_span(self_, b, side, nranks_);
       hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
-      HIPC(hipMemcpyAsync(mine.recv, slot(p.mbox, b, 1 - side), face_, hipMemcpyDeviceToDevice, hs));
+      hip_face_copy(mine.recv, slot(p.mbox, b, 1 - side), face_, hs);
       hip_counter_signal(ctr_ + kPulled + side, hs);
     }
     if (!capturing) last_b_ = b;
@@ -201,8 +290,9 @@ class IpcTransport final : public Transport {
  private:
   struct Peer {
     int rank = -1;
-    int device = -1;
     void* mbox = nullptr;
+    void* buf[2] = {nullptr, nullptr};  // the neighbour's field buffers (direct protocol)
+    uint64_t face_off = 0;              // byte offset of its face that borders this slab
     void* ctr = nullptr;
   };
   CallbackFns f_;
@@ -214,6 +304,7 @@ class IpcTransport final : public Transport {
   void* mbox_ = nullptr;
   size_t face_ = 0;
   bool dev_ok_ = false;
+  bool direct_ = false;
   Peer peers_[2];
   double timeout_s_ = 300.0;
 };
@@ -249,6 +340,17 @@ void ipc_enable_peer(int mine, int peer, int peer_rank) {
   if (e != hipSuccess)
     MDFX_FAIL(format("ipc transport: enabling peer access from device %d to device %d (rank %d) failed: %s", mine,
                      peer, peer_rank, hipGetErrorString(e)));
+}
+
+// The direct protocol maps the neighbours' field buffers; torch's HIP 7.0 runtime stalls in
+// hipIpcOpenMemHandle from 2 GiB up, so only buffers of at most 1900 MiB (probed good) go direct.
+bool ipc_direct_ok(size_t field_bytes) {
+  static const int force = [] {
+    const char* v = std::getenv("MDFX_IPC_DIRECT");
+    return v && *v ? std::atoi(v) : -1;
+  }();
+  if (force >= 0) return force != 0;
+  return field_bytes <= ((size_t)1900 << 20);
 }
 
 std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns) {

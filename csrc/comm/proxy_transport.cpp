@@ -13,6 +13,9 @@
 // the copies run at local HBM speed instead of over xGMI, and the ghost values are not the
 // neighbour's. Results are therefore exact only at planes farther from a proxied boundary than the
 // steps run (tests/test_gpu_proxy.py), and every number measured this way is labelled a proxy.
+// The two ipc protocols are both modelled: the mailbox (publish copy + pull copy per face) and the
+// direct pull from the field buffer (one copy per face), chosen by the same rule as the ipc
+// transport (ipc_direct_ok: field buffers below 2 GiB) or forced with MDFX_IPC_DIRECT=0 / 1.
 //
 // Reference parity: the per-rank generation loop of MDF_kernel.cu:155-188 (C12/C13) with its
 // halo exchange MDF_kernel.cu:166-172,180-183, measured for one rank at a time.
@@ -60,11 +63,19 @@ class ProxyTransport final : public Transport {
     HIPC(hipMemcpy(ctr_ + kPulled + 0, &two, 8, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(ctr_ + kPulled + 1, &two, 8, hipMemcpyHostToDevice));
     face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
-    HIPC(hipMalloc(&mbox_, 4 * face_));
-    HIPC(hipMemset(mbox_, 0, 4 * face_));
+    direct_ = ipc_direct_ok(self_.lay.bytes());
+    if (direct_) {
+      const uint64_t one = 1;  // the direct protocol's first exchange finds the faces free
+      HIPC(hipMemcpy(ctr_ + kPulled + 0, &one, 8, hipMemcpyHostToDevice));
+      HIPC(hipMemcpy(ctr_ + kPulled + 1, &one, 8, hipMemcpyHostToDevice));
+    } else {
+      HIPC(hipMalloc(&mbox_, 4 * face_));
+      HIPC(hipMemset(mbox_, 0, 4 * face_));
+    }
     HIPC(hipDeviceSynchronize());
     ok_ = true;
   }
+  const char* protocol() const { return direct_ ? "direct" : "mailbox"; }
 
   char* slot(int b, int s) const { return (char*)mbox_ + (size_t)(2 * b + s) * face_; }
 
@@ -75,13 +86,32 @@ class ProxyTransport final : public Transport {
     HIPC(hipStreamIsCapturing(hs, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
     const uint64_t ahead = (!capturing && last_b_ == b) ? 1 : 0;
+    if (direct_) {
+      // the ipc direct sequence: ready, then per face wait + pull from the (own) field buffer +
+      // pulled, then the wait that frees the faces the next boundary kernels overwrite
+      hip_counter_signal(ctr_ + kReady, hs);
+      for (int side = 0; side < 2; ++side) {
+        const HaloSpan h = halo_span(self_, b, side, nranks_);
+        if (h.peer < 0) continue;
+        MDFX_CHECK(h.bytes == face_, "proxy: face geometry mismatch");
+        hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
+        hip_face_copy(h.recv, h.send, face_, hs);
+        hip_counter_signal(ctr_ + kPulled + side, hs);
+      }
+      for (int side = 0; side < 2; ++side) {
+        if (halo_span(self_, b, side, nranks_).peer < 0) continue;
+        hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, 0, &words_);
+      }
+      if (!capturing) last_b_ = b;
+      return;
+    }
     // publish (the ipc sequence, with this slab as its own neighbour on both sides)
     for (int side = 0; side < 2; ++side) {
       const HaloSpan h = halo_span(self_, b, side, nranks_);
       if (h.peer < 0) continue;
       MDFX_CHECK(h.bytes == face_, "proxy: face geometry mismatch");
       hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, ahead, &words_);
-      HIPC(hipMemcpyAsync(slot(b, side), h.send, face_, hipMemcpyDeviceToDevice, hs));
+      hip_face_copy(slot(b, side), h.send, face_, hs);
     }
     hip_counter_signal(ctr_ + kReady, hs);
     // pull
@@ -89,7 +119,7 @@ class ProxyTransport final : public Transport {
       const HaloSpan h = halo_span(self_, b, side, nranks_);
       if (h.peer < 0) continue;
       hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
-      HIPC(hipMemcpyAsync(h.recv, slot(b, side), face_, hipMemcpyDeviceToDevice, hs));
+      hip_face_copy(h.recv, slot(b, side), face_, hs);
       hip_counter_signal(ctr_ + kPulled + side, hs);
     }
     if (!capturing) last_b_ = b;
@@ -117,6 +147,7 @@ class ProxyTransport final : public Transport {
   void* mbox_ = nullptr;
   size_t face_ = 0;
   bool ok_ = false;
+  bool direct_ = false;
   int last_b_ = -1;
   double timeout_s_ = 300.0;
 };

@@ -184,6 +184,24 @@ int hip_device_count() {
   return n;
 }
 
+// Halo face copies of the device transports (ipc, proxy). The HIP runtime runs a same-device
+// hipMemcpyDeviceToDevice as blit kernels on the CUs, where they compete with the interior sweep
+// they are meant to hide under; hipMemcpyDeviceToDeviceNoCU hands the copy to an SDMA engine
+// instead. MDFX_XCOPY=blit / sdma picks one (default: sdma, profiles/r04_*).
+int face_copy_mode() {
+  static const int mode = [] {
+    const char* v = std::getenv("MDFX_XCOPY");
+    if (v && std::strcmp(v, "blit") == 0) return 0;
+    return 1;
+  }();
+  return mode;
+}
+
+void hip_face_copy(void* dst, const void* src, size_t n, void* stream) {
+  HIPC(hipMemcpyAsync(dst, src, n, face_copy_mode() == 1 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice,
+                      (hipStream_t)stream));
+}
+
 HaloSpan halo_span(const LocalSlab& s, int b, int side, int nranks) {
   HaloSpan h;
   const FieldLayout& l = s.lay;

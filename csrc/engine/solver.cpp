@@ -268,6 +268,11 @@ void Solver::exchange_ghosts() {
 // GCells/s with it, rank proxies N = 8 / 4 / 2 1850 / 2073 / 2284 vs 1824 / 2069 / 2259,
 // profiles/r03_session_x/) and transports whose exchange is pure stream work on the halo stream
 // (a host-side exchange synchronises the halo stream alone).
+// Rounds of resident blocks per streaming sweep: the option, else 2 with several slabs (exchange
+// kernels that need CUs find some mid-sweep) and 1 for a single slab. Passed with every launch
+// (RegionArgs::min_rounds), so eager steps, warm-up launches and captured cycles agree.
+int Solver::min_rounds() const { return opt_.min_rounds > 0 ? opt_.min_rounds : (nranks_ > 1 ? 2 : 1); }
+
 bool Solver::boundary_on_cs() const {
   return bnd_cs_ && opt_.overlap && bnd_first_ && slabs_.size() == 1 && transport_->graph_capturable();
 }
@@ -289,6 +294,7 @@ void Solver::step(bool want_resid, int k) {
     a.out = s.buf[nb];
     a.lay = s.lay;
     a.steps = k;
+    a.min_rounds = min_rounds();
     void* bs = bcs ? s.cs : s.hs;  // the boundary kernels' stream
     if (want_resid) {
       s.be->memset(s.resid, 0, sizeof(double), bs);
@@ -489,8 +495,6 @@ void Solver::run(int64_t steps) {
   MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
   if (ghosts_dirty_) exchange_ghosts();
   transport_->check();
-  const bool hip = slabs_[0].be->kind() == DeviceKind::HIP;
-  if (hip) hip_set_min_rounds(opt_.min_rounds > 0 ? opt_.min_rounds : (nranks_ > 1 ? 2 : 1));
   const int T = opt_.temporal;
   int64_t done = 0;
   while (done < steps) {
@@ -583,6 +587,7 @@ void Solver::warm_kernels(int64_t steps) {
         a.out = s.buf[nb];  // scratch: the next step overwrites it
         a.lay = s.lay;
         a.steps = k;
+        a.min_rounds = min_rounds();
         a.resid = r ? s.resid : nullptr;  // (step() clears the accumulator before it counts)
         if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
           a.lz_begin = s.lo_b;

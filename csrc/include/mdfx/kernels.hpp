@@ -30,6 +30,11 @@ struct RegionArgs {
   // Time steps fused into this sweep (temporal blocking). 2 needs lay.halo >= 2 and reads
   // in[lz_begin-2, lz_end+2); the residual then covers the second step only.
   int steps = 1;
+  // Minimum whole rounds of resident blocks per streaming fused sweep (0 = 1, at most 4). The engine
+  // asks for 2 when slabs exchange halos: the exchange's RCCL / copy kernels then find CUs freed
+  // after half the interior sweep. It is part of the launch, so a captured hipGraph replays exactly
+  // the geometry the engine asked for when it captured.
+  int min_rounds = 0;
 };
 
 // Whether a fused multi-step sweep is implemented for this stencil / grid on the device.
@@ -91,11 +96,6 @@ void hip_set_kernel_variant(const char* name);
 int hip_runtime_version();
 // Re-read the MDFX_* kernel tuning knobs from the environment (they are cached at first use).
 void hip_reload_knobs();
-// Minimum whole rounds of resident blocks per streaming fused sweep (default 1, at most 4). The
-// engine asks for 2 when slabs exchange halos: the exchange's RCCL / copy kernels then find CUs
-// freed after half the interior sweep, and blocks they displace delay it by half a round at most
-// instead of a whole one.
-void hip_set_min_rounds(int rounds);
 const char* hip_kernel_variant();
 
 // ---- CPU oracle / CPU backend ----------------------------------------------------------------

@@ -65,6 +65,10 @@ struct HaloSpan {
   size_t bytes = 0;
 };
 HaloSpan halo_span(const LocalSlab& s, int b, int side /*0 = lo, 1 = hi*/, int nranks);
+// Stream-ordered device-to-device copy of a halo face (same device or a mapped peer): SDMA copy
+// engines (hipMemcpyDeviceToDeviceNoCU, default) or the runtime's blit kernels (MDFX_XCOPY=blit).
+void hip_face_copy(void* dst, const void* src, size_t n, void* stream);
+int face_copy_mode();  // 1 = sdma, 0 = blit
 
 class Transport {
  public:
@@ -119,6 +123,10 @@ std::unique_ptr<Transport> make_callback_transport(CallbackFns fns);
 // neighbours' mapped buffers by the copy engines, ordered by device-side counters
 // (csrc/comm/ipc_transport.cpp). Needs fns.allgather; residual / barrier go through fns too.
 std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns);
+// Whether the ipc transport pulls faces straight from the neighbours' exported field buffers (one
+// copy per face) rather than through mailboxes (two): buffers of at most 1900 MiB, since torch's
+// HIP 7.0 runtime stalls mapping exported buffers of 2 GiB and more; MDFX_IPC_DIRECT=0 / 1 forces.
+bool ipc_direct_ok(size_t field_bytes);
 // Rank proxy (HIP): ONE slab of an N-way decomposition alone on a GPU, exchanging with itself
 // through the ipc transport's mailbox copies and device counters (csrc/comm/proxy_transport.cpp):
 // the per-GPU schedule of an N-GPU run, measurable on one GPU. Ghost values are the slab's own

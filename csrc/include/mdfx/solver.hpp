@@ -37,7 +37,7 @@ struct SolverOptions {
   // Per-phase hipEvent timing of slab 0 (boundary / interior / exchange / whole step); syncs the
   // host once per step, so it is a diagnostic mode, not a benchmark mode.
   bool profile = false;
-  // Minimum whole rounds of resident blocks per streaming fused sweep (hip_set_min_rounds):
+  // Minimum whole rounds of resident blocks per streaming fused sweep (RegionArgs::min_rounds):
   // 0 = automatic (2 with several slabs, so exchange kernels that need CUs find some mid-sweep; 1
   // otherwise). Fewer rounds mean longer z chunks, hence less pipeline fill per chunk.
   int min_rounds = 0;
@@ -159,6 +159,7 @@ class Solver {
   // transport; MDFX_BND_CS=0 keeps them on the halo stream)
   bool bnd_cs_ = true;
   bool boundary_on_cs() const;
+  int min_rounds() const;  // effective rounds per streaming sweep (RegionArgs::min_rounds)
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
   // hipGraphExec_t of the 2-sweep cycle starting at buffer p (index p), and its fused depth
   void* graph_exec_[2] = {nullptr, nullptr};

@@ -336,6 +336,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   dev::Geo g = dev::make_geo(a.lay, a.lz_begin, a.lz_end);
   g.lz2_begin = a.lz2_begin;
   g.lz2_end = a.lz2_end;
+  g.min_rounds = std::max(1, std::min(4, a.min_rounds));
   hipStream_t s = (hipStream_t)stream;
   if (a.steps != 1) {
     MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),

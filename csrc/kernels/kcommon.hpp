@@ -35,6 +35,7 @@ struct Geo {
   int64_t lz_max;    // storage planes allocated (loads outside [0,lz_max) return 0)
   int64_t lz2_begin = 0, lz2_end = 0;  // optional second region of the same launch (heat7_wtk)
   int64_t alloc = 0;                 // elements allocated (planes + slack), for device checks
+  int min_rounds = 1;                // whole rounds of resident blocks a streaming sweep spans at least (RegionArgs)
   unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };
 

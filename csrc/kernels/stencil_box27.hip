@@ -21,7 +21,7 @@ namespace dev {
 
 int pick_zc(int64_t planes, int64_t columns, int zc_max, int blocks_target);
 int64_t resident_blocks(const void* kfn);
-int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K);
+int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int min_rounds);
 
 template <class V, class T>
 __device__ __forceinline__ V vsplat27(T v) {
@@ -777,7 +777,7 @@ static void launch_box27_tbk_w(const Geo& g, const T* in, T* out, const StencilC
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   int zc = knobs().zc;
-  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks((const void*)&box27_tbk<T, RY, K, WXN, false>), K);
+  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks((const void*)&box27_tbk<T, RY, K, WXN, false>), K, g.min_rounds);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;

@@ -45,7 +45,6 @@ namespace mdfx {
 namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
-int hip_min_rounds_now();
 
 template <class T, int RY, int RE, int K, int WB, bool RES>
 __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
@@ -532,7 +531,7 @@ static void launch_b27p(const Geo& g, const T* in, T* out, const StencilCoef& cf
   const int YT = (int)((g.ny + BR - 1) / BR);
   const void* kfn = (const void*)&box27_wxp<T, RY, RE, K, WB, false>;
   const int64_t resident = resident_blocks(kfn, 2 * 64 * WB);
-  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, YT, resident, K, 3 * K - 1, hip_min_rounds_now());
+  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, YT, resident, K, 3 * K - 1, g.min_rounds);
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = (int64_t)YT * ZT;
@@ -561,7 +560,7 @@ static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf
   const int64_t tiles = (int64_t)XT * YT;
   const void* kfn = (const void*)&box27_wxk<T, RY, RE, K, WB, false>;
   const int64_t resident = resident_blocks(kfn, 64 * WB);
-  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, resident, K, 3 * K - 1, hip_min_rounds_now());
+  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, resident, K, 3 * K - 1, g.min_rounds);
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = tiles * ZT;

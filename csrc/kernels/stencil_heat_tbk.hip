@@ -267,16 +267,12 @@ namespace dev {
 // means on 1024^3 fp32, K = 2 (profiles/r01_tbk/zc_dispatch_stats.txt): zc 512 / 256 / 171 /
 // 128 / 86 -> 1.768 / 1.770 / 1.646 / 1.671 / 1.646 ms per sweep; the N = 8 slab (128 planes,
 // best of 3 x 20): zc 128 / 64 / 43 -> 1025 / 1358 / 1082 GCells/s.
-static std::atomic<int> g_min_rounds{1};
-
 // Every chunk also pays 2K planes of pipeline fill, so a region is never split into chunks shorter
 // than 4K planes: under the 2-round policy of multi-slab runs the K-plane boundary regions were
 // split in two (8 slabs of 1024^2 x 128 at K = 3: 1369 vs 1491 GCells/s, profiles/r02_wtk/README.txt).
-int hip_min_rounds_now() { return g_min_rounds.load(std::memory_order_relaxed); }
-
-int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K) {
+int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int min_rounds) {
   const double per_slot = (double)planes * (double)tiles / (double)resident;
-  const int64_t rounds = std::max<int64_t>(g_min_rounds.load(std::memory_order_relaxed),
+  const int64_t rounds = std::max<int64_t>(min_rounds,
                                            std::min<int64_t>(4, (int64_t)(per_slot / 128.0 + 0.5)));
   const int64_t zt = std::max<int64_t>(1, std::min<int64_t>(planes, (rounds * resident + tiles / 2) / tiles));
   const int64_t zc = (planes + zt - 1) / zt;
@@ -300,7 +296,7 @@ static void launch_tbk_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   const void* kfn = (const void*)&heat7_tbk<T, RY, K, WXN, false>;
   int zc = knobs().zc;
-  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks(kfn), K);
+  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks(kfn), K, g.min_rounds);
   if (knobs().debug_zc) fprintf(stderr, "[mdfx] tbk K=%d RY=%d: %lld planes x %d tiles -> zc %d\n", K, RY, (long long)planes, YT, zc);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
@@ -357,11 +353,6 @@ void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double*
   }
 }
 template void launch_heat7_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
-}  // namespace dev
-
-void hip_set_min_rounds(int rounds) { dev::g_min_rounds.store(std::max(1, std::min(4, rounds))); }
-
-namespace dev {
 template void launch_heat7_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
 
 }  // namespace dev

@@ -39,7 +39,6 @@ namespace mdfx {
 namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
-int hip_min_rounds_now();
 
 // Schedule of one streaming sweep over `planes` planes of `tiles` tiles on `resident` block slots,
 // every block paying 2K planes of pipeline fill per segment it marches:
@@ -332,7 +331,7 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
   const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, NAT, false>;
   const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
   const int64_t resident = resident_blocks(kfn, 64 * WB);
-  WtkPlan plan = wtk_plan(planes, tiles, resident, K, WB, hip_min_rounds_now(), knobs().wtk_split);
+  WtkPlan plan = wtk_plan(planes, tiles, resident, K, WB, g.min_rounds, knobs().wtk_split);
   if (knobs().zc > 0 || (sizeof(T) == 8 && RY == 3 && WB == 8)) {  // (no split instance of that shape)
     if (knobs().zc > 0) plan.zc = knobs().zc;
     plan.split = false;

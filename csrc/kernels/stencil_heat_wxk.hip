@@ -56,7 +56,6 @@ namespace mdfx {
 namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
-int hip_min_rounds_now();
 
 template <class T, int RY, int RE, int K, int WB, bool RES, int NB = 2, int SPAR = 2>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
@@ -339,7 +338,7 @@ static WxGeo wxk_geo(const Geo& g) {
   w.YT = (int)((g.ny + BR - 1) / BR);
   const int64_t tiles = (int64_t)w.XT * w.YT;
   w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false, NB, SPAR>, 64 * WB);
-  w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, hip_min_rounds_now());
+  w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds);
   if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
   w.ntasks = tiles * ZT;

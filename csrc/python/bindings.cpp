@@ -282,6 +282,10 @@ PYBIND11_MODULE(_mdfx, m) {
   m.def("hip_runtime_version", &hip_runtime_version,
         "version of the HIP runtime the process loaded (PyTorch's bundled one under torch), 0 if none");
   m.def("kernel_variant", []() { return std::string(hip_kernel_variant()); });
+  m.def("face_copy_mode", []() { return std::string(face_copy_mode() == 1 ? "sdma" : "blit"); },
+        "engine of the ipc / proxy halo face copies (MDFX_XCOPY)");
+  m.def("ipc_direct_ok", [](size_t bytes) { return ipc_direct_ok(bytes); },
+        "whether the ipc transport pulls straight from field buffers of this size (MDFX_IPC_DIRECT)");
   m.def("layout", [](int64_t nx, int64_t ny, int64_t nz, int64_t z0, int64_t z1, int halo,
                      const std::string& dtype) {
     return layout_dict(FieldLayout::make(Extent3{nx, ny, nz}, z0, z1, halo, dtype_from_name(dtype)));
