@@ -66,7 +66,8 @@ def parse(argv=None):
     p.add_argument("--stencil", default="heat7", choices=["heat7", "box27", "jacobi5", "life"])
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "u8"])
     p.add_argument("--transport", default="auto",
-                   help="auto|rccl|ipc|torch|staged (distributed), loopback (1 process)")
+                   help="auto|rccl|ipc|ipc_sdma|torch|staged (distributed), loopback (1 process); with "
+                        "--rank-proxy: ipc_sdma models the SDMA pulls (proxy_sdma)")
     p.add_argument("--virtual-ranks", type=int, default=0,
                    help="split the grid into P slabs inside ONE process (loopback transport)")
     p.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -78,9 +79,10 @@ def parse(argv=None):
                    help="steps of each short timed trial that picks transport / graph mode / rounds / "
                         "overlap (auto); every candidate is timed twice, interleaved, and its faster run counts")
     p.add_argument("--temporal", type=int, default=0,
-                   help="time steps fused per memory sweep (temporal blocking); 0 = auto: 3 for the 3D "
-                        "7-point at 1024-cell rows, else 2 for the 3D stencils, 8 (2D MDF) / 12 (Life) "
-                        "for the 2D ones, where a fused kernel exists")
+                   help="time steps fused per memory sweep (temporal blocking); 0 = auto (native "
+                        "hip_fused_depth): 4 for the 3D 7-point fp32 where heat7_wxk's x segments cover the "
+                        "row (3 in fp64), 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 (2D "
+                        "MDF) / 12 (Life)")
     p.add_argument("--ref-precision", action="store_true",
                    help="jacobi5: the reference program's mixed fp32/fp64 update (MDF_kernel.cu:20)")
     p.add_argument("--no-overlap", action="store_true")
@@ -187,10 +189,10 @@ def pick_temporal(a, prob, nslab, hip):
 
     if a.temporal > 0:
         return a.temporal
-    # the deepest measured-win fused depth (native hip_fused_depth: 3 for the 3D 7-point at
-    # 1024-cell rows through heat7_wtk, else 2 for the 3D stencils; 8 (MDF) / 12 (Life) for the 2D
-    # ones; profiles/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt), made shallower until every slab is at
-    # least 4 sweeps deep
+    # the deepest measured-win fused depth (native hip_fused_depth: 4 for the 3D 7-point fp32 through
+    # heat7_wxk where its x segments cover the row, 3 in fp64; 3 for the 27-point at 1024-cell rows
+    # and in fp64, else 2; 8 (MDF) / 12 (Life) for the 2D ones; profiles/r03_wxk/, r02_mdf2d/,
+    # r02_life.txt), made shallower until every slab is at least 4 sweeps deep
     want = native().hip_fused_depth(prob.kind, prob.dtype, prob.nx, prob.ref_precision) if hip else \
         {"jacobi5": 8, "life": 12}.get(a.stencil, 2)
     while want > 1 and prob.nz < 4 * want * nslab:
@@ -281,8 +283,10 @@ def run_proxy(a):
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True])
     overlaps = [True, False] if (n > 1 and not a.no_overlap) else [not a.no_overlap]
     rounds = [int(a.rounds)] if a.rounds != "auto" else ([2, 1] if n > 1 else [0])
+    sdma = a.transport in ("ipc_sdma", "proxy_sdma")
     sim = Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graphs[0],
-                     residual_every=a.residual_every, timeout_s=a.timeout)
+                     residual_every=a.residual_every, timeout_s=a.timeout,
+                     transport="proxy_sdma" if sdma else "proxy")
     lay = sim.layout(0)
     slab_cells = (lay["z1"] - lay["z0"]) * prob.nx * prob.ny
 
@@ -344,7 +348,7 @@ def run_proxy(a):
         "data": "synthetic (uniform random grid from a counter hash of the global index, seed 1)",
         "config": {"model": "%s %dx%dx%d %s" % (model, nx, ny, nz, a.dtype), "slab_planes": [lay["z0"], lay["z1"]],
                    "ghost_planes": lay["halo"], "temporal_block": temporal, "transport": sim.transport,
-                   "face_copy": native().face_copy_mode(),
+                   "face_copy": "sdma" if sdma else native().face_copy_mode(),
                    "ipc_protocol": "direct" if native().ipc_direct_ok(lay["bytes"]) else "mailbox",
                    "graph": (sim.graph_replays - replays0) > 0, "graph_requested": chosen[0],
                    "graph_replays_timed": sim.graph_replays - replays0,
@@ -412,7 +416,9 @@ def main(argv=None):
     # the full problem; the fastest is timed for real. With one candidate there is no trial.
     transports = [a.transport]
     if env and a.transport == "auto":
-        transports = ["rccl", "ipc"] if hip else ["torch"]
+        # rccl (p2p kernels), ipc (pulls by the runtime's blit kernels), ipc_sdma (pulls by the
+        # SDMA engines: no CUs taken from the interior sweep, lower bandwidth on one device)
+        transports = ["rccl", "ipc", "ipc_sdma"] if hip else ["torch"]
     elif not env:
         transports = [a.transport if a.transport in ("loopback", "host") else "auto"]
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True] if hip else [False])
@@ -613,9 +619,10 @@ def main(argv=None):
                 "trials": trials,
                 "overlap": chosen[3],
                 "timed_vs_trial": timed_vs_trial,
-                "face_copy": native().face_copy_mode() if sim_transport == "ipc" else None,
+                "face_copy": ("sdma" if sim_transport == "ipc_sdma" else native().face_copy_mode())
+                if sim_transport in ("ipc", "ipc_sdma") else None,
                 "ipc_protocol": (("direct" if native().ipc_direct_ok(sim.layout(0)["bytes"]) else "mailbox")
-                                 if sim_transport == "ipc" else None),
+                                 if sim_transport in ("ipc", "ipc_sdma") else None),
                 "temporal_block": temporal,
                 "gate": gate,
             },

@@ -271,7 +271,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     } else if (tname == "tcp") {
       MDFX_CHECK(rv != nullptr, "tcp transport needs a multi-process launch (mpirun / torchrun)");
       tr = make_tcp_transport(*rv);
-    } else if (tname == "ipc") {
+    } else if (tname == "ipc" || tname == "ipc_sdma") {
       MDFX_CHECK(rv != nullptr && hip, "ipc transport needs a multi-process launch on HIP devices");
       Rendezvous* r = rv.get();
       CallbackFns f;
@@ -279,7 +279,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
       f.allreduce_sum = [r](double v) { return r->allreduce_sum(v); };
       f.allreduce_max = [r](double v) { return r->allreduce_max(v); };
       f.barrier = [r]() { r->barrier(); };
-      tr = make_ipc_transport(std::move(f));
+      tr = make_ipc_transport(std::move(f), tname == "ipc_sdma" ? 1 : -1);
     } else {
       MDFX_FAIL("unknown transport " + tname);
     }

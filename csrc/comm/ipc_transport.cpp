@@ -104,12 +104,15 @@ int local_device_of(const char* pci) {
 
 class IpcTransport final : public Transport {
  public:
-  explicit IpcTransport(CallbackFns f) : f_(std::move(f)) {
+  IpcTransport(CallbackFns f, int copy_mode) : f_(std::move(f)), copy_(copy_mode) {
     MDFX_CHECK((bool)f_.allgather, "ipc transport needs an allgather control plane");
   }
   ~IpcTransport() override {
     if (!dev_ok_) return;
     (void)hipSetDevice(self_.be->device());
+    if (aux_) (void)hipStreamDestroy(aux_);
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
     for (auto& p : peers_) {
       if (p.mbox) (void)hipIpcCloseMemHandle(p.mbox);
       for (void* b : p.buf)
@@ -120,7 +123,7 @@ class IpcTransport final : public Transport {
     hip_free_uncached(ctr_);
     hip_words_free(words_);
   }
-  const char* name() const override { return "ipc"; }
+  const char* name() const override { return copy_ == 1 ? "ipc_sdma" : "ipc"; }
   bool in_process_only() const override { return false; }
   bool graph_capturable() const override { return true; }
   void set_timeout(double s) override { timeout_s_ = s > 0 ? s : 300.0; }
@@ -134,6 +137,13 @@ class IpcTransport final : public Transport {
     ctr_ = (uint64_t*)hip_alloc_uncached(kCounterBytes);
     words_ = hip_words_alloc();  // this transport's own abort / wait-error words
     dev_ok_ = true;
+    // the hi-side pull runs on a second stream, concurrently with the lo-side pull on the halo
+    // stream: two neighbours are two different xGMI links (or two blits on one device)
+    int lo = 0, hi = 0;
+    HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, hi));
+    HIPC(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     // every face has the same size (halo planes of one field layout)
     face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
     // the protocol is agreed below (every rank must use the same one); counters start per protocol
@@ -187,8 +197,9 @@ class IpcTransport final : public Transport {
       // HIP_VISIBLE_DEVICES both sides call their GPU "device 0"
       const int their = local_device_of(r.pci);
       const bool same = mine.pci[0] && r.pci[0] ? std::strcmp(mine.pci, r.pci) == 0 : r.device == mine.device;
-      IpcPeerInfo me{mine.rank, 0, mine.pid, mine.face_bytes, true};
-      IpcPeerInfo them{r.rank, same ? 0 : 1, r.pid, r.face_bytes, std::memcmp(r.magic, "MDFXIPC3", 8) == 0};
+      IpcPeerInfo me{mine.rank, mine.device, mine.pid, mine.face_bytes, true};
+      IpcPeerInfo them{r.rank, same ? mine.device : (their >= 0 ? their : -1), r.pid, r.face_bytes,
+                       std::memcmp(r.magic, "MDFXIPC3", 8) == 0};
       int can = 1;
       if (!same && their >= 0) HIPC(hipDeviceCanAccessPeer(&can, mine.device, their));
       const std::string why = ipc_peer_problem(me, them, p.rank, can != 0);
@@ -222,17 +233,34 @@ class IpcTransport final : public Transport {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPC(hipStreamIsCapturing(hs, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
+    // the two pulls: lo side on the halo stream, hi side on the aux stream (forked after the
+    // publish / ready signal, joined back before the exchange ends)
+    const bool both = peers_[0].rank >= 0 && peers_[1].rank >= 0;
+    auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
+    auto fork = [&]() {
+      if (!both) return;
+      HIPC(hipEventRecord(ev_fork_, hs));
+      HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
+    };
+    auto join = [&]() {
+      if (!both) return;
+      HIPC(hipEventRecord(ev_join_, aux_));
+      HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
+    };
     if (direct_) {
       hip_counter_signal(ctr_ + kReady, hs);
+      fork();
       for (int side = 0; side < 2; ++side) {
         const Peer& p = peers_[side];
         if (p.rank < 0) continue;
         const HaloSpan mine = halo_span(self_, b, side, nranks_);
         MDFX_CHECK(mine.bytes == face_ && mine.peer == p.rank, "ipc: face geometry mismatch");
-        hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
-        hip_face_copy(mine.recv, (const char*)p.buf[b] + p.face_off, face_, hs);
-        hip_counter_signal(ctr_ + kPulled + side, hs);
+        hipStream_t ps = pull_stream(side);
+        hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
+        hip_face_copy(mine.recv, (const char*)p.buf[b] + p.face_off, face_, ps, copy_);
+        hip_counter_signal(ctr_ + kPulled + side, ps);
       }
+      join();
       for (int side = 0; side < 2; ++side) {
         const Peer& p = peers_[side];
         if (p.rank < 0) continue;
@@ -251,18 +279,21 @@ class IpcTransport final : public Transport {
       MDFX_CHECK(mine.bytes == face_ && mine.peer == p.rank, "ipc: face geometry mismatch");
       hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs,
                        ahead, &words_);
-      hip_face_copy(slot(mbox_, b, side), mine.send, face_, hs);
+      hip_face_copy(slot(mbox_, b, side), mine.send, face_, hs, copy_);
     }
     hip_counter_signal(ctr_ + kReady, hs);
     // pull: the neighbour on `side` published its (1 - side) face of exchange e
+    fork();
     for (int side = 0; side < 2; ++side) {
       const Peer& p = peers_[side];
       if (p.rank < 0) continue;
       const HaloSpan mine = halo_span(self_, b, side, nranks_);
-      hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
-      hip_face_copy(mine.recv, slot(p.mbox, b, 1 - side), face_, hs);
-      hip_counter_signal(ctr_ + kPulled + side, hs);
+      hipStream_t ps = pull_stream(side);
+      hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
+      hip_face_copy(mine.recv, slot(p.mbox, b, 1 - side), face_, ps, copy_);
+      hip_counter_signal(ctr_ + kPulled + side, ps);
     }
+    join();
     if (!capturing) last_b_ = b;
   }
   void set_last_parity(int b) override { last_b_ = b; }
@@ -296,6 +327,9 @@ class IpcTransport final : public Transport {
     void* ctr = nullptr;
   };
   CallbackFns f_;
+  int copy_ = 0;  // face copy engine: 0 blit kernels, 1 SDMA (hip_face_copy)
+  hipStream_t aux_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   LocalSlab self_;
   int nranks_ = 1;
   uint64_t* ctr_ = nullptr;
@@ -345,16 +379,14 @@ void ipc_enable_peer(int mine, int peer, int peer_rank) {
 // The direct protocol maps the neighbours' field buffers; torch's HIP 7.0 runtime stalls in
 // hipIpcOpenMemHandle from 2 GiB up, so only buffers of at most 1900 MiB (probed good) go direct.
 bool ipc_direct_ok(size_t field_bytes) {
-  static const int force = [] {
-    const char* v = std::getenv("MDFX_IPC_DIRECT");
-    return v && *v ? std::atoi(v) : -1;
-  }();
+  const char* v = std::getenv("MDFX_IPC_DIRECT");  // (read per call: tests switch it within a process)
+  const int force = v && *v ? std::atoi(v) : -1;
   if (force >= 0) return force != 0;
   return field_bytes <= ((size_t)1900 << 20);
 }
 
-std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns) {
-  return std::unique_ptr<Transport>(new IpcTransport(std::move(fns)));
+std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode) {
+  return std::unique_ptr<Transport>(new IpcTransport(std::move(fns), copy_mode < 0 ? face_copy_mode() : copy_mode));
 }
 
 }  // namespace mdfx

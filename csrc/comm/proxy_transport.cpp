@@ -40,9 +40,13 @@ constexpr size_t kCounterBytes = 128 * 8;
 
 class ProxyTransport final : public Transport {
  public:
+  explicit ProxyTransport(int copy_mode) : copy_(copy_mode) {}
   ~ProxyTransport() override {
     if (!ok_) return;
     (void)hipSetDevice(self_.be->device());
+    if (aux_) (void)hipStreamDestroy(aux_);
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (mbox_) (void)hipFree(mbox_);
     hip_free_uncached(ctr_);
     hip_words_free(words_);
@@ -59,23 +63,24 @@ class ProxyTransport final : public Transport {
     self_.be->activate();
     ctr_ = (uint64_t*)hip_alloc_uncached(kCounterBytes);
     words_ = hip_words_alloc();
-    const uint64_t two = 2;
-    HIPC(hipMemcpy(ctr_ + kPulled + 0, &two, 8, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(ctr_ + kPulled + 1, &two, 8, hipMemcpyHostToDevice));
     face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
     direct_ = ipc_direct_ok(self_.lay.bytes());
-    if (direct_) {
-      const uint64_t one = 1;  // the direct protocol's first exchange finds the faces free
-      HIPC(hipMemcpy(ctr_ + kPulled + 0, &one, 8, hipMemcpyHostToDevice));
-      HIPC(hipMemcpy(ctr_ + kPulled + 1, &one, 8, hipMemcpyHostToDevice));
-    } else {
+    // the first exchange(s) find their faces (direct) / mailbox slots free
+    const uint64_t pulled0 = direct_ ? 1 : 2;
+    HIPC(hipMemcpy(ctr_ + kPulled + 0, &pulled0, 8, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(ctr_ + kPulled + 1, &pulled0, 8, hipMemcpyHostToDevice));
+    if (!direct_) {
       HIPC(hipMalloc(&mbox_, 4 * face_));
       HIPC(hipMemset(mbox_, 0, 4 * face_));
     }
+    int lo = 0, hi = 0;
+    HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, hi));
+    HIPC(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIPC(hipDeviceSynchronize());
     ok_ = true;
   }
-  const char* protocol() const { return direct_ ? "direct" : "mailbox"; }
 
   char* slot(int b, int s) const { return (char*)mbox_ + (size_t)(2 * b + s) * face_; }
 
@@ -86,18 +91,35 @@ class ProxyTransport final : public Transport {
     HIPC(hipStreamIsCapturing(hs, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
     const uint64_t ahead = (!capturing && last_b_ == b) ? 1 : 0;
+    // the ipc transport's stream layout: the hi-side pull on a second stream, concurrent with the
+    // lo-side pull on the halo stream
+    const bool both = halo_span(self_, b, 0, nranks_).peer >= 0 && halo_span(self_, b, 1, nranks_).peer >= 0;
+    auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
+    auto fork = [&]() {
+      if (!both) return;
+      HIPC(hipEventRecord(ev_fork_, hs));
+      HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
+    };
+    auto join = [&]() {
+      if (!both) return;
+      HIPC(hipEventRecord(ev_join_, aux_));
+      HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
+    };
     if (direct_) {
       // the ipc direct sequence: ready, then per face wait + pull from the (own) field buffer +
       // pulled, then the wait that frees the faces the next boundary kernels overwrite
       hip_counter_signal(ctr_ + kReady, hs);
+      fork();
       for (int side = 0; side < 2; ++side) {
         const HaloSpan h = halo_span(self_, b, side, nranks_);
         if (h.peer < 0) continue;
         MDFX_CHECK(h.bytes == face_, "proxy: face geometry mismatch");
-        hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
-        hip_face_copy(h.recv, h.send, face_, hs);
-        hip_counter_signal(ctr_ + kPulled + side, hs);
+        hipStream_t ps = pull_stream(side);
+        hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
+        hip_face_copy(h.recv, h.send, face_, ps, copy_);
+        hip_counter_signal(ctr_ + kPulled + side, ps);
       }
+      join();
       for (int side = 0; side < 2; ++side) {
         if (halo_span(self_, b, side, nranks_).peer < 0) continue;
         hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, 0, &words_);
@@ -111,17 +133,20 @@ class ProxyTransport final : public Transport {
       if (h.peer < 0) continue;
       MDFX_CHECK(h.bytes == face_, "proxy: face geometry mismatch");
       hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, ahead, &words_);
-      hip_face_copy(slot(b, side), h.send, face_, hs);
+      hip_face_copy(slot(b, side), h.send, face_, hs, copy_);
     }
     hip_counter_signal(ctr_ + kReady, hs);
     // pull
+    fork();
     for (int side = 0; side < 2; ++side) {
       const HaloSpan h = halo_span(self_, b, side, nranks_);
       if (h.peer < 0) continue;
-      hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
-      hip_face_copy(h.recv, slot(b, side), face_, hs);
-      hip_counter_signal(ctr_ + kPulled + side, hs);
+      hipStream_t ps = pull_stream(side);
+      hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
+      hip_face_copy(h.recv, slot(b, side), face_, ps, copy_);
+      hip_counter_signal(ctr_ + kPulled + side, ps);
     }
+    join();
     if (!capturing) last_b_ = b;
   }
   int last_parity() const override { return last_b_; }
@@ -140,6 +165,9 @@ class ProxyTransport final : public Transport {
   }
 
  private:
+  int copy_ = -1;  // face copy engine (hip_face_copy)
+  hipStream_t aux_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   LocalSlab self_;
   int nranks_ = 1;
   uint64_t* ctr_ = nullptr;
@@ -154,6 +182,8 @@ class ProxyTransport final : public Transport {
 
 }  // namespace
 
-std::unique_ptr<Transport> make_proxy_transport() { return std::unique_ptr<Transport>(new ProxyTransport()); }
+std::unique_ptr<Transport> make_proxy_transport(int copy_mode) {
+  return std::unique_ptr<Transport>(new ProxyTransport(copy_mode));
+}
 
 }  // namespace mdfx

@@ -184,21 +184,21 @@ int hip_device_count() {
   return n;
 }
 
-// Halo face copies of the device transports (ipc, proxy). The HIP runtime runs a same-device
+// Halo face copies of the device transports (ipc, proxy). The HIP runtime runs a
 // hipMemcpyDeviceToDevice as blit kernels on the CUs, where they compete with the interior sweep
 // they are meant to hide under; hipMemcpyDeviceToDeviceNoCU hands the copy to an SDMA engine
-// instead. MDFX_XCOPY=blit / sdma picks one (default: sdma, profiles/r04_*).
+// instead. On one device the SDMA copies are the slower choice (N = 8 rank proxy: 1,499 vs 1,923
+// GCells/s per GPU with the mailbox protocol's four 16 MiB copies per sweep, 1,906 vs 1,872 with
+// the direct protocol's two; profiles/r04_session_a/), so blit is the default; between GPUs the
+// bench's trials time both (transport "ipc" vs "ipc_sdma"). MDFX_XCOPY=sdma changes the default.
 int face_copy_mode() {
-  static const int mode = [] {
-    const char* v = std::getenv("MDFX_XCOPY");
-    if (v && std::strcmp(v, "blit") == 0) return 0;
-    return 1;
-  }();
-  return mode;
+  const char* v = std::getenv("MDFX_XCOPY");  // (read per call: tests switch it within a process)
+  return v && std::strcmp(v, "sdma") == 0 ? 1 : 0;
 }
 
-void hip_face_copy(void* dst, const void* src, size_t n, void* stream) {
-  HIPC(hipMemcpyAsync(dst, src, n, face_copy_mode() == 1 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice,
+void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode) {
+  if (mode < 0) mode = face_copy_mode();
+  HIPC(hipMemcpyAsync(dst, src, n, mode == 1 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice,
                       (hipStream_t)stream));
 }
 

@@ -65,10 +65,12 @@ struct HaloSpan {
   size_t bytes = 0;
 };
 HaloSpan halo_span(const LocalSlab& s, int b, int side /*0 = lo, 1 = hi*/, int nranks);
-// Stream-ordered device-to-device copy of a halo face (same device or a mapped peer): SDMA copy
-// engines (hipMemcpyDeviceToDeviceNoCU, default) or the runtime's blit kernels (MDFX_XCOPY=blit).
-void hip_face_copy(void* dst, const void* src, size_t n, void* stream);
-int face_copy_mode();  // 1 = sdma, 0 = blit
+// Stream-ordered device-to-device copy of a halo face (same device or a mapped peer): mode 0 the
+// runtime's blit kernels (hipMemcpyDeviceToDevice: copy shaders on the CUs), 1 the SDMA copy
+// engines (hipMemcpyDeviceToDeviceNoCU: no CUs, lower bandwidth on one device), -1 the process
+// default (face_copy_mode(): MDFX_XCOPY=blit / sdma, blit unless set).
+void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode = -1);
+int face_copy_mode();
 
 class Transport {
  public:
@@ -122,7 +124,9 @@ std::unique_ptr<Transport> make_callback_transport(CallbackFns fns);
 // HIP IPC, one slab per process (any number of processes per GPU): faces pulled from the
 // neighbours' mapped buffers by the copy engines, ordered by device-side counters
 // (csrc/comm/ipc_transport.cpp). Needs fns.allgather; residual / barrier go through fns too.
-std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns);
+// copy_mode: the face copy engine (hip_face_copy; -1 = process default). Named "ipc" (blit) or
+// "ipc_sdma".
+std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode = -1);
 // Whether the ipc transport pulls faces straight from the neighbours' exported field buffers (one
 // copy per face) rather than through mailboxes (two): buffers of at most 1900 MiB, since torch's
 // HIP 7.0 runtime stalls mapping exported buffers of 2 GiB and more; MDFX_IPC_DIRECT=0 / 1 forces.
@@ -131,7 +135,7 @@ bool ipc_direct_ok(size_t field_bytes);
 // through the ipc transport's mailbox copies and device counters (csrc/comm/proxy_transport.cpp):
 // the per-GPU schedule of an N-GPU run, measurable on one GPU. Ghost values are the slab's own
 // faces, so results are exact only away from the proxied boundaries.
-std::unique_ptr<Transport> make_proxy_transport();
+std::unique_ptr<Transport> make_proxy_transport(int copy_mode = -1);
 // What the ipc transport knows about one process's slab when it maps a neighbour (the host-side
 // part of its handle record).
 struct IpcPeerInfo {

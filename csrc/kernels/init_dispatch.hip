@@ -60,7 +60,8 @@ double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
 static bool use_wxk(DType dt, int64_t nx = 0);
 static bool use_wtk(int steps, DType dt) {
-  return knobs().h7_wtk >= 0 && (heat7_wtk_supported(steps) || (steps == 5 && dt == DType::F32 && use_wxk(dt)));
+  (void)dt;
+  return knobs().h7_wtk >= 0 && heat7_wtk_supported(steps);
 }
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
 // 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
@@ -70,7 +71,6 @@ static bool use_wtk(int steps, DType dt) {
 static bool use_wxk(DType dt, int64_t nx) {
   return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (dt == DType::F32 || nx >= 2048));
 }
-// (K = 5: fp32 heat7_wxk only)
 
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -89,9 +89,8 @@ static Knobs read_knobs() {
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
-  k.wxk_ry = env_int("MDFX_WXK_RY", 0);
-  k.wxk_nb = env_int("MDFX_WXK_NB", 0);
-  k.wxk_bnb = env_int("MDFX_WXK_BNB", 0);
+  k.wxk_pf = env_int("MDFX_WXK_PF", 0);
+  if (k.wxk_pf != 0 && k.wxk_pf != 64 && k.wxk_pf != 128 && k.wxk_pf != 256) k.wxk_pf = 0;
   k.j5_f64_pd = env_int("MDFX_J5_F64_PD", 1);
   k.b27_wxp = env_int("MDFX_B27_WXP", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);

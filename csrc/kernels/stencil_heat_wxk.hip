@@ -57,9 +57,10 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 
-template <class T, int RY, int RE, int K, int WB, bool RES, int NB = 2, int SPAR = 2>
+template <class T, int RY, int RE, int K, int WB, bool RES>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
+                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
+                                                     int pf) {
   using V = typename VT<T>::type;
   using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
@@ -70,18 +71,22 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   constexpr int RB = BR + 2 * K;              // u0 window rows of a band: yb-K .. yb+BR+K-1
   constexpr int NM = RY > RE + K - 1 ? RY : RE + K - 1;  // most rows any wave computes at level 1
   static_assert(WB >= 2 && K >= 2, "heat7_wxk: bands of at least two waves, at least two levels");
-  static_assert((NB == 2 || NB == 3) && (SPAR == 1 || SPAR == 2), "heat7_wxk: 2 or 3 window buffers, 1 or 2 seam parities");
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // work: block-uniform task = one z chunk of one (x segment, y band) tile; x segments fastest, then
   // y bands, then z chunks (the first region's chunks, then the second region's)
   const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   if (b >= ntasks) return;
-  // NB window buffers: the u0 plane DMA runs NB - 1 planes ahead of the plane being computed
-  __shared__ V win[NB][RB][64];
+  // two window buffers: the u0 plane DMA runs one plane ahead of the plane being computed
+  __shared__ V win[2][RB][64];
   // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
-  // (SPAR = 1: one table, the step's seam reads and writes separated by a second barrier)
-  __shared__ V seam[SPAR][K - 1][WB - 1][2][64];
+  __shared__ V seam[2][K - 1][WB - 1][2][64];
+  // L2 prefetch (pf = byte stride 64 / 128 / 256, 0 = off): at step q every wave touches one dword
+  // per pf bytes of its window rows of plane q + 2 with a 4-byte LDS DMA into this scratch, so the
+  // window DMA of plane q + 2, issued one step later, hits L2 instead of waiting a full HBM round
+  // trip: a second plane in flight without a third window buffer (which would not fit next to the
+  // seam tables: round 3 measured it with one seam table and a second barrier, and lost)
+  __shared__ uint32_t pfdump[WB][64];
   const int tiles = XT * YT;
   const int t = b % tiles, zt = b / tiles;
   const int P0 = (int)(g.lz_end - g.lz_begin);
@@ -114,11 +119,6 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
   const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(rown, ny - y0)) : 0;
   int nst = 0;  // output stores issued since this wave's last DMA
-  // NB = 3: vector-memory ops this wave issued after its newest (n_last) and its second newest
-  // (n_prev) window DMA; rows of the window this wave fetches per plane
-  int n_last = 0, n_prev = 0;
-  constexpr int NDW = (RB + WB - 1) / WB;
-  const int ndma = NDW - (w + (NDW - 1) * WB >= RB ? 1 : 0);
 
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
   // read the nearest valid row / vector. Wave w fetches rows w, w + WB, ... of the window.
@@ -138,13 +138,32 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
     }
   };
 
+  // prefetch geometry: `lpr` lanes per window row, `rpi` rows per instruction; wave w touches rows
+  // w * rpi .. w * rpi + rpi - 1 of the window (one instruction per wave and plane; with the shipped
+  // bands WB * rpi covers the window's rows, taller windows leave their last rows to the DMA)
+  const int lpr = pf > 0 ? (int)(64 * sizeof(V) / (unsigned)pf) : 64, rpi = 64 / lpr;
+  const bool pfw = pf > 0 && w * rpi < RB;  // wave-uniform: this wave prefetches
+  uint32_t pfo = 0;                         // the lane's byte offset inside a plane
+  if (pfw) {
+    int k = w * rpi + lane / lpr;
+    k = k < RB ? k : RB - 1;
+    const int y = yb - K + k;
+    const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
+    const int64_t xo = std::min<int64_t>(std::max<int64_t>(xs, 0) * (int64_t)sizeof(T) + (int64_t)(lane % lpr) * pf,
+                                         pitch * (int64_t)sizeof(T) - 4);
+    pfo = (uint32_t)((int64_t)yc * pitch * (int64_t)sizeof(T) + xo);
+  }
+  auto prefetch = [&](int lz) {
+    const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
+    const char* a = (const char*)(in + (int64_t)lzc * plane) + pfo;
+    dcheck(g, (const char*)in, a, 4);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)a,
+                                     (__attribute__((address_space(3))) void*)&pfdump[w][0], 4, 0, 0);
+  };
+  int npf_last = 0;  // prefetches this wave issued after its newest window DMA (0 / 1)
+
   const int qlast = ze - 1 + K;  // last u0 plane of the march
   issue(zs - K, 0);
-  if constexpr (NB == 3) {
-    issue(zs - K + 1, 1);
-    n_prev = ndma;
-  }
-  int wcur = 0;  // NB = 3: window buffer of the current step
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
   double acc = 0.0;
@@ -158,7 +177,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   LV* const s_first = lds_vptr(&seam[0][0][wu][0][lane]);  // my first row (write, w > 0)
   LV* const s_last = lds_vptr(&seam[0][0][wd][1][lane]);   // my last row (write, w < WB-1)
   constexpr int WIN_BUF = RB * 64;  // V elements per window buffer
-  constexpr int SEAM_PAR = SPAR == 2 ? (K - 1) * (WB - 1) * 2 * 64 : 0, SEAM_LVL = (WB - 1) * 2 * 64;
+  constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
   auto st = [](LV* p, const V& v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
@@ -185,26 +204,18 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // no instruction moves across a plane boundary (the two planes of an unrolled trip would
       // otherwise interleave, with both planes' rows live at once)
       __builtin_amdgcn_sched_barrier(0);
-      // plane q's DMA has landed (the stores issued after it stay in flight); the barrier
-      // publishes it and last step's seam rows, and certifies that every wave is done with the
-      // other window buffer and the other seam parity
-      if constexpr (NB == 2) {
-        wait_vm_le(nst);
-      } else {
-        // plane q's DMA is the second newest while plane q + 1's has been issued, else the newest
-        wait_vm_le(q + 1 <= qlast ? n_prev : n_last);
-      }
+      // plane q's DMA has landed (the prefetches and stores issued after it stay in flight); the
+      // barrier publishes it and last step's seam rows, and certifies that every wave is done with
+      // the other window buffer and the other seam parity
+      wait_vm_le(nst + npf_last);
       lds_barrier();
-      if constexpr (NB == 2) {
-        if (q < qlast) issue(q + 1, P ^ 1);
-      } else {
-        if (q + 2 <= qlast) {
-          issue(q + 2, wcur == 0 ? 2 : wcur - 1);  // the buffer plane q - 1 used
-          n_prev = n_last + ndma;
-          n_last = 0;
-        }
+      if (q < qlast) issue(q + 1, P ^ 1);
+      npf_last = 0;
+      if (pfw && q + 2 <= qlast) {
+        prefetch(q + 2);
+        npf_last = 1;
       }
-      constexpr int SR = SPAR == 2 ? (P ^ 1) : 0;  // seam parity read this step
+      constexpr int SR = P ^ 1;  // seam parity read this step
       // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact)
       Row rl[K + 1];
 #pragma unroll
@@ -232,10 +243,8 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
           RO::pin(a);
         }
       }
-      // one seam table: every wave has read this step's seam rows before any wave overwrites them
-      if constexpr (SPAR == 1) lds_barrier();
       // (2) level 1 row by row from the u0 window, each new row cascading up through the levels
-      LV* const wbuf = NB == 2 ? wrow + P * WIN_BUF : wrow + wcur * WIN_BUF;
+      LV* const wbuf = wrow + P * WIN_BUF;
       auto u0row = [&](int i) -> Row { return RO::fromv(V(wbuf[(i + K) * 64])); };
       Row X[3];
       X[0] = u0row(SH::lo(1) - 1);
@@ -296,11 +305,6 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         }
       }
       nst = valid ? nsto : 0;
-      if constexpr (NB == 3) {
-        n_last += nst;
-        n_prev += nst;
-        wcur = wcur == 2 ? 0 : wcur + 1;
-      }
     };
     // an odd plane count ends with one extra step (q = qlast + 1): no DMA, nothing stored
     for (int q = zs - K; q <= qlast; q += 2) {
@@ -327,7 +331,7 @@ struct WxGeo {
   int XT = 0, YT = 0, zc = 0;
   int64_t ntasks = 0, resident = 0, rounds = 0;
 };
-template <class T, int RY, int RE, int K, int WB, int NB = 2, int SPAR = 2>
+template <class T, int RY, int RE, int K, int WB>
 static WxGeo wxk_geo(const Geo& g) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   constexpr int BR = 2 * RE + (WB - 2) * RY;
@@ -337,7 +341,7 @@ static WxGeo wxk_geo(const Geo& g) {
   w.XT = (int)((g.nx + SEG - 1) / SEG);
   w.YT = (int)((g.ny + BR - 1) / BR);
   const int64_t tiles = (int64_t)w.XT * w.YT;
-  w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false, NB, SPAR>, 64 * WB);
+  w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false>, 64 * WB);
   w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds);
   if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
@@ -346,35 +350,23 @@ static WxGeo wxk_geo(const Geo& g) {
   return w;
 }
 
-template <class T, int RY, int RE, int K, int WB, int NB = 2, int SPAR = 2>
+template <class T, int RY, int RE, int K, int WB>
 static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  if constexpr (NB != 2 || SPAR != 2) {
-    if (resid) {  // (the deeper-window instances have no residual copy)
-      launch_wxk<T, RY, RE, K, WB>(g, in, out, r, resid, s);
-      return;
-    }
-  }
-  const WxGeo wg = wxk_geo<T, RY, RE, K, WB, NB, SPAR>(g);
+  const WxGeo wg = wxk_geo<T, RY, RE, K, WB>(g);
   const int XT = wg.XT, YT = wg.YT, zc = wg.zc;
   const int64_t ntasks = wg.ntasks;
   if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d NB=%d SPAR=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
-            K, RY, RE, WB, NB, SPAR, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
+    fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
+            K, RY, RE, WB, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
-  // shapes whose residual instance would need more than 256 VGPRs have none (their callers send
-  // residual sweeps to a smaller shape)
-  constexpr bool kNoRes = K == 5 || (K == 4 && RY == 4);
-  if constexpr (kNoRes) {
-    MDFX_CHECK(!resid, "heat7_wxk: no residual variant of this shape (the 5-step sweep: use --temporal 4 with a residual)");
-  } else if constexpr (NB == 2 && SPAR == 2) {
-    if (resid) {
-      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
-      return;
-    }
+  if (resid) {
+    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid,
+                       knobs().wxk_pf);
+    return;
   }
-  hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, NB, SPAR>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
-                     resid);
+  hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
+                     resid, knobs().wxk_pf);
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -382,10 +374,16 @@ bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
 template <class T>
 void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
 
-// fp32: K = 3 in 4-row waves (MDFX_WXK_RY = 3: 3 rows), K = 4 in 2-row waves, bands of 8 waves
-// (MDFX_WTK_WB = 4: bands of 4 with 4 / 3 rows); fp64: K = 3 in 2-row waves, K = 4 stays on
-// heat7_wtk. The shapes that would spill (fp32 K = 4 3-row waves in 8-wave bands, fp64 K = 4 and
-// 3-row waves) are not built (tests/test_kernel_resources.py).
+// Shipped bands of 8 waves: fp32 K = 4 in 2 + 6 x 3 + 2 rows (3-row inner waves, 2-row edge
+// waves): 1024^3 2387-2394 GCells/s on every box measured; 4-row inner waves ran 2415-2454 on one
+// box and 2095-2138 on two others (near the LDS limit, 156 KB, and spilling once the prefetch
+// came in), 2-row waves 2247-2253; on thin slabs the 3-row band also
+// fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
+// (profiles/r03_wxk/). fp32 K = 3 (step-count remainders): 4-row waves. fp64 K = 3: 3 + 1-row bands
+// (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2); fp64 K = 4 stays on heat7_wtk. Round 3's
+// other shapes (4-wave bands, 2-row and 3 + 1-row fp32 bands, the 5-step sweep, 3 window buffers /
+// one seam table) measured slower and were removed in round 4; their numbers stay in
+// profiles/r03_wxk/ and profiles/r03_session_r/.
 template <class T>
 void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
@@ -393,7 +391,7 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
     launch_heat7_wtk<T>(g, in, out, r, steps, resid, s);
     return;
   }
-  MDFX_CHECK((steps == 3 || steps == 4 || (steps == 5 && sizeof(T) == 4)) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+  MDFX_CHECK((steps == 3 || steps == 4) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_wxk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
@@ -402,41 +400,11 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
              "heat7_wxk: row / plane counts must fit 32-bit indices");
-  const int wb = knobs().wtk_wb == 4 ? 4 : 8;
-  const int ry = knobs().wxk_ry;
   if constexpr (sizeof(T) == 4) {
-    if (steps == 3) {
-      if (wb == 4) launch_wxk<T, 4, 4, 3, 4>(g, in, out, r, resid, s);
-      else if (ry == 3) launch_wxk<T, 3, 3, 3, 8>(g, in, out, r, resid, s);
-      else launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
-    } else if (steps == 5) {
-      launch_wxk<T, 2, 1, 5, 8>(g, in, out, r, resid, s);
-    } else {
-      // bands of 2 + 6 x 3 + 2 rows (3-row inner waves, 2-row edge waves): 1024^3 2387-2394
-      // GCells/s on every box measured; 4-row inner waves ran 2415-2454 on one box and 2095-2138 on
-      // two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row
-      // band also fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
-      // (profiles/r03_wxk/). MDFX_WXK_RY picks another shape.
-      // the boundary regions of a slab (one launch for both, or a region of at most 2K planes) march
-      // K + 2K planes for K outputs: few steps, each waiting on its plane's DMA; MDFX_WXK_BNB picks
-      // their window depth separately from the interior's
-      const bool thin = g.lz2_end > g.lz2_begin || g.lz_end - g.lz_begin <= 2 * steps;
-      const int nb = thin && knobs().wxk_bnb ? knobs().wxk_bnb : knobs().wxk_nb;
-      if (wb == 4) launch_wxk<T, 3, 3, 4, 4>(g, in, out, r, resid, s);
-      else if (nb == 31) launch_wxk<T, 3, 2, 4, 8, 3, 1>(g, in, out, r, resid, s);  // 3 window buffers, 1 seam table
-      else if (nb == 21) launch_wxk<T, 3, 2, 4, 8, 2, 1>(g, in, out, r, resid, s);  // 1 seam table only
-      else if (nb == 32) launch_wxk<T, 2, 2, 4, 8, 3, 2>(g, in, out, r, resid, s);  // 2 + 2 rows, 3 window buffers
-      else if (ry == 31) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);
-      else if (ry == 21) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
-      else if (ry == 22) launch_wxk<T, 2, 2, 4, 8>(g, in, out, r, resid, s);
-      else if (ry == 42 && !resid) launch_wxk<T, 4, 2, 4, 8>(g, in, out, r, resid, s);
-      else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
-    }
+    if (steps == 3) launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
+    else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
   } else {
-    // fp64 K = 3: 3 + 1-row bands by default (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2)
-    if (ry == 32) launch_wxk<T, 3, 2, 3, 8>(g, in, out, r, resid, s);
-    else if (ry == 22) launch_wxk<T, 2, 2, 3, 8>(g, in, out, r, resid, s);
-    else launch_wxk<T, 3, 1, 3, 8>(g, in, out, r, resid, s);
+    launch_wxk<T, 3, 1, 3, 8>(g, in, out, r, resid, s);
   }
 }
 template void launch_heat7_wxk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);

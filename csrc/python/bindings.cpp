@@ -218,14 +218,14 @@ class PySolver {
       CallbackFns f = callback_fns(callbacks);
       if (!f.exchange) throw Error("callback transport needs an exchange callback");
       tr = make_callback_transport(std::move(f));
-    } else if (transport == "ipc") {
+    } else if (transport == "ipc" || transport == "ipc_sdma") {
       CallbackFns f = callback_fns(callbacks);
       if (!f.allgather) throw Error("ipc transport needs an allgather callback");
-      tr = make_ipc_transport(std::move(f));
-    } else if (transport == "proxy") {
-      tr = make_proxy_transport();
+      tr = make_ipc_transport(std::move(f), transport == "ipc_sdma" ? 1 : -1);
+    } else if (transport == "proxy" || transport == "proxy_sdma") {
+      tr = make_proxy_transport(transport == "proxy_sdma" ? 1 : -1);
     } else {
-      throw Error("unknown transport '" + transport + "' (host|loopback|rccl|ipc|callback|proxy)");
+      throw Error("unknown transport '" + transport + "' (host|loopback|rccl|ipc|ipc_sdma|callback|proxy|proxy_sdma)");
     }
     SolverOptions o;
     o.overlap = overlap;

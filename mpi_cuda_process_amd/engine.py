@@ -32,7 +32,7 @@ from ._native import hip_available, native
 from .models import InitCondition, Problem
 from .ops import TORCH_DTYPE
 from .parallel.decomp import slab_bounds
-from .parallel.dist import ControlPlane, TorchP2PTransport, broadcast_bytes, is_distributed
+from .parallel.dist import ControlPlane, TorchP2PTransport, broadcast_bytes, group_for, is_distributed
 
 
 def auto_temporal(problem: Problem, nranks: int, device: str) -> int:
@@ -82,7 +82,7 @@ class Simulation:
         self.group = group
 
         if self.distributed:
-            if transport in ("rccl", "ipc") and device != "hip":
+            if transport in ("rccl", "ipc", "ipc_sdma") and device != "hip":
                 raise ValueError("%s transport needs HIP devices" % transport)
             world = dist.get_world_size(group)
             rank = dist.get_rank(group)
@@ -102,23 +102,24 @@ class Simulation:
                 uid = native().rccl_unique_id() if rank == 0 else None
                 uid = broadcast_bytes(uid, src=0, group=group)
                 args = dict(transport="rccl", unique_id=uid)
-            elif transport == "ipc":
+            elif transport in ("ipc", "ipc_sdma"):
+                # ipc: faces pulled by the runtime's blit kernels; ipc_sdma: by the SDMA engines
                 if device != "hip":
                     raise ValueError("ipc transport needs HIP devices")
                 torch.cuda.set_device(dev_list[0])
                 self._control = ControlPlane(group, timeout_s=max(60.0, 2 * timeout_s))
-                args = dict(transport="ipc", callbacks=self._control.callbacks())
+                args = dict(transport=transport, callbacks=self._control.callbacks())
             elif transport in ("torch", "staged"):
                 p2p_group = group
                 staged = transport == "staged" and device == "hip"
                 if device == "hip":
                     torch.cuda.set_device(dev_list[0])
                     if not staged:
-                        p2p_group = dist.new_group(backend="nccl") if group is None else group
+                        p2p_group = group_for("nccl", group, max(60.0, 2 * timeout_s)) if group is None else group
                 self._torch_transport = TorchP2PTransport(p2p_group, staged=staged)
                 args = dict(transport="callback", callbacks=self._torch_transport.callbacks())
             else:
-                raise ValueError("distributed transport must be rccl|ipc|torch|staged|auto")
+                raise ValueError("distributed transport must be rccl|ipc|ipc_sdma|torch|staged|auto")
         elif proxy_rank is not None:
             # rank proxy: only slab `proxy_rank` of a `ranks`-way split, on one GPU, its halo
             # exchange looped back through the ipc mailbox machinery (proxy_transport.cpp)
@@ -129,7 +130,10 @@ class Simulation:
                 raise ValueError("proxy_rank must be in [0, ranks)")
             local_ranks = [int(proxy_rank)]
             dev_list = [devices[0] if devices else torch.cuda.current_device()]
-            args = dict(transport="proxy")
+            # proxy_sdma: the face copies on the SDMA engines (the ipc_sdma transport's exchange)
+            if transport not in ("auto", "proxy", "proxy_sdma"):
+                raise ValueError("the rank proxy's transport is proxy or proxy_sdma")
+            args = dict(transport="proxy_sdma" if transport == "proxy_sdma" else "proxy")
         else:
             nranks = ranks or 1
             local_ranks = list(range(nranks))

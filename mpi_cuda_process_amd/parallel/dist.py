@@ -67,6 +67,31 @@ def broadcast_bytes(data: Optional[bytes], src: int = 0, group=None) -> bytes:
     return obj[0]
 
 
+# groups made for engines on a default group of another backend, one per (backend, rank set) and
+# process: dist.new_group is a collective every default-group rank must join in the same order, so
+# building one per engine would leak groups and hang any rank that builds an engine its peers do not
+_GROUPS: dict = {}
+
+
+def group_for(backend: str, group=None, timeout_s: float = 300.0):
+    """A ``backend`` group over the ranks of ``group`` (the default group if None): ``group`` itself
+    if it already uses that backend, else one created once per process and rank set (with the given
+    timeout) and reused by every later engine."""
+    if dist.get_backend(group) == backend:
+        return group
+    ranks = tuple(range(dist.get_world_size())) if group is None else tuple(dist.get_process_group_ranks(group))
+    g = _GROUPS.get((backend, ranks))
+    if g is None:
+        g = dist.new_group(ranks=list(ranks), backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        _GROUPS[(backend, ranks)] = g
+    return g
+
+
+def gloo_group_for(group=None, timeout_s: float = 300.0):
+    """The CPU (gloo) group a control plane over ``group``'s ranks uses (see :func:`group_for`)."""
+    return group_for("gloo", group, timeout_s)
+
+
 class ControlPlane:
     """Host-side collectives for the native transports that move data on the device themselves
     (``ipc``): the handle swap (allgather of byte strings), the residual all-reduce and barriers,
@@ -74,11 +99,8 @@ class ControlPlane:
 
     def __init__(self, group=None, timeout_s: float = 300.0):
         # the control plane moves CPU tensors: on a non-gloo group (e.g. a torchrun default NCCL
-        # group) it makes its own gloo group over the same ranks instead of failing on CPU tensors
-        if dist.get_backend(group) != "gloo":
-            group = dist.new_group(backend="gloo") if group is None else \
-                dist.new_group(ranks=dist.get_process_group_ranks(group), backend="gloo")
-        self.group = group
+        # group) it uses a gloo group over the same ranks (made once per process, gloo_group_for)
+        self.group = gloo_group_for(group, timeout_s)
         self.timeout_s = timeout_s
 
     def callbacks(self) -> dict:

@@ -112,7 +112,7 @@ def test_bench_multiprocess_cpu_json(mdfx, tmp_path):
 
 def _bench(args, env_extra=None, timeout=300):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MDFX_FORCE_DIST")}
-    env.update(OMP_NUM_THREADS="2", **(env_extra or {}))
+    env.update({"OMP_NUM_THREADS": "2", **(env_extra or {})})
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
                        timeout=timeout)
     return p.returncode, p.stdout.decode(), p.stderr.decode()
@@ -132,6 +132,26 @@ def test_bench_self_launches_ranks_cpu(mdfx):
     gate = rec["config"]["gate"]
     run = gate["runs"][0]
     assert gate["passed"] and run["transport"] == "torch" and run["grid"][2] % 3 == 0
+
+
+def test_bench_self_launches_8_ranks_cpu(mdfx):
+    """The driver's N = 8 path rehearsed on the CPU: 8 self-launched gloo ranks, every rank gated
+    bitwise against a full-grid run through the same transport, one JSON line with n_gpus = 8 that
+    names the transport, the gate records and the timed-vs-trial ratio (the reference
+    only ever meant 2 ranks, MDF_kernel.cu:29,37,155,189)."""
+    import json
+
+    rc, out, err = _bench(["--device", "cpu", "--gpus", "8", "--n", "64", "--steps", "4", "--warmup", "1"],
+                          env_extra={"OMP_NUM_THREADS": "1"}, timeout=600)
+    assert rc == 0, err
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    rec = json.loads(lines[0])
+    cfg = rec["config"]
+    assert rec["n_gpus"] == 8 and cfg["ranks"] == 8 and cfg["transport"] == "torch"
+    assert cfg["gate"]["passed"] and all(r["passed"] for r in cfg["gate"]["runs"])
+    assert cfg["gate"]["runs"][0]["grid"][2] % 8 == 0
+    assert "timed_vs_trial" in cfg and rec["steps"] == 4 and rec["value"] > 0
 
 
 def test_bench_json_reports_effective_graph_mode(mdfx):
@@ -174,8 +194,9 @@ cp = ControlPlane()
 _real = dist.get_backend
 dist.get_backend = lambda g=None: "nccl" if g is None else _real(g)
 cp2 = ControlPlane()
+cp3 = ControlPlane()  # a second engine's control plane reuses the group (no new collective)
 dist.get_backend = _real
-own_gloo = cp2.group is not None and _real(cp2.group) == "gloo"
+own_gloo = cp2.group is not None and _real(cp2.group) == "gloo" and cp3.group is cp2.group
 cb2 = cp2.callbacks()
 s2 = cb2["allreduce_sum"](1.0)
 cb = cp.callbacks()

@@ -31,9 +31,9 @@ from mpi_cuda_process_amd.parallel.dist import init_distributed
 env = init_distributed("gloo")
 torch.cuda.set_device(0)
 prob = %(prob)s
-with m.Simulation(prob, device="hip", distributed=True, transport="ipc", residual_every=4,
+with m.Simulation(prob, device="hip", distributed=True, transport=%(transport)r, residual_every=4,
                   temporal=%(temporal)d, devices=[0], graph=%(graph)s, timeout_s=60.0) as sim:
-    assert sim.transport == "ipc", sim.transport
+    assert sim.transport == %(transport)r, sim.transport
     sim.init()
     sim.run(%(steps)d)
     sim.synchronize()
@@ -97,7 +97,8 @@ def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
     prob_src = "m.heat3d(nx=256, ny=40, nz=47)"
     out = str(tmp_path / "g.npy")
     steps = 13
-    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps)
+    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
+                         transport="ipc")
     _spawn(world, lambda r: [sys.executable, "-c", code])
     got = np.load(out)
     ref, rres = _reference(eval(prob_src), steps)
@@ -106,13 +107,35 @@ def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
     assert meta["nranks"] == world and abs(meta["residual"] - rres) <= 1e-9 * rres
 
 
+@pytest.mark.parametrize("transport,direct,world,temporal,graph", [
+    ("ipc", "0", 3, 2, True), ("ipc", "0", 4, 4, False),          # mailbox protocol (blit copies)
+    ("ipc_sdma", "1", 3, 2, True), ("ipc_sdma", "1", 4, 4, False),  # direct pulls on the SDMA engines
+    ("ipc_sdma", "0", 3, 3, True)])                                # mailbox on the SDMA engines
+def test_ipc_protocols_and_copy_engines(hip, tmp_path, transport, direct, world, temporal, graph):
+    """Both ipc protocols (direct pulls from the neighbours' exported field buffers / mailboxes) on
+    both copy engines (blit kernels / SDMA), the two pulls of a middle rank on two streams:
+    bitwise equal to one process, residual included, eager and replayed."""
+    prob_src = "m.heat3d(nx=256, ny=40, nz=47)"
+    out = str(tmp_path / "g.npy")
+    steps = 13
+    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
+                         transport=transport)
+    _spawn(world, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_IPC_DIRECT": direct})
+    import mpi_cuda_process_amd as m  # noqa: F401 (eval below)
+
+    ref, rres = _reference(eval(prob_src), steps)
+    assert np.array_equal(np.load(out), ref)
+    meta = json.load(open(out + ".json"))
+    assert abs(meta["residual"] - rres) <= 1e-9 * rres
+
+
 @pytest.mark.parametrize("prob_src", ["m.mdf2d(h=203, w=300)", "m.life2d(h=150, w=257)",
                                       "m.box27(nx=130, ny=33, nz=40, dtype='f64')"])
 def test_ipc_other_stencils(hip, tmp_path, prob_src):
     import mpi_cuda_process_amd as m
 
     out = str(tmp_path / "g.npy")
-    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=9)
+    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=9, transport="ipc")
     _spawn(3, lambda r: [sys.executable, "-c", code])
     ref, _ = _reference(eval(prob_src), 9)
     assert np.array_equal(np.load(out), ref)
@@ -160,7 +183,7 @@ def test_ipc_dead_peer_is_an_error_not_a_hang(hip, tmp_path):
     reports a transport failure and exits non-zero instead of hanging."""
     out = str(tmp_path / "g.npy")
     code = WORKER.replace("timeout_s=60.0", "timeout_s=5.0") % dict(
-        root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=40)
+        root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=40, transport="ipc")
     t0 = time.time()
     procs, outs = _spawn(2, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_FAULT": "exit@1:3"},
                          timeout=150, expect_ok=False)
@@ -180,3 +203,18 @@ def test_ipc_slabs_larger_than_2gib(hip):
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     rec = json.loads([l for l in p.stdout.decode().splitlines() if l.startswith("{")][0])
     assert rec["n_gpus"] == 2 and rec["config"]["gate"]["passed"] and rec["config"]["transport"] == "ipc"
+    assert rec["config"]["ipc_protocol"] == "mailbox"
+
+
+def test_ipc_direct_protocol_at_the_headline_size(hip):
+    """1024^3 fp32 over 4 processes: field buffers of 1.1 GB map through HIP IPC, so the ranks pull
+    each other's faces straight out of them (the direct protocol of the N >= 4 runs)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--share-gpu", "--transport",
+                        "ipc", "--n", "1024", "--steps", "8", "--warmup", "4", "--timeout", "30"],
+                       env=env, capture_output=True, timeout=110, cwd=ROOT)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    rec = json.loads([l for l in p.stdout.decode().splitlines() if l.startswith("{")][0])
+    cfg = rec["config"]
+    assert rec["n_gpus"] == 4 and cfg["gate"]["passed"] and cfg["transport"] == "ipc"
+    assert cfg["ipc_protocol"] == "direct" and cfg["face_copy"] == "blit"

@@ -26,13 +26,19 @@ def _full(prob, steps, temporal):
         return sim.gather()
 
 
-@pytest.mark.parametrize("n,r,temporal,graph", [(2, 0, 1, False), (2, 1, 3, True), (4, 1, 3, False),
-                                                (4, 2, 2, True), (8, 3, 3, True), (8, 7, 3, False)])
-def test_proxy_slab_matches_full_grid_away_from_boundaries(hip, n, r, temporal, graph):
-    prob = m.heat3d(nx=1024 if temporal == 3 else 256, ny=24, nz=36 * n)
+@pytest.mark.parametrize("n,r,temporal,graph,transport,direct", [
+    (2, 0, 1, False, "proxy", "1"), (2, 1, 3, True, "proxy", "1"), (4, 1, 3, False, "proxy", "1"),
+    (4, 2, 2, True, "proxy", "1"), (8, 3, 3, True, "proxy", "1"), (8, 7, 3, False, "proxy", "1"),
+    (8, 3, 4, True, "proxy", "0"), (4, 2, 4, True, "proxy_sdma", "1"), (4, 1, 2, False, "proxy_sdma", "0")])
+def test_proxy_slab_matches_full_grid_away_from_boundaries(hip, monkeypatch, n, r, temporal, graph, transport,
+                                                           direct):
+    """(both ipc protocols: direct pulls / mailboxes; both copy engines: blit / SDMA)"""
+    monkeypatch.setenv("MDFX_IPC_DIRECT", direct)
+    prob = m.heat3d(nx=1024 if temporal >= 3 else 256, ny=24, nz=36 * n)
     steps = 6
     full = _full(prob, steps, temporal)
-    with m.Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graph) as sim:
+    with m.Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graph,
+                      transport=transport) as sim:
         assert sim.transport == "proxy"
         sim.init()
         sim.prepare_graphs()

@@ -474,19 +474,16 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
 
 @pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=300, ny=33, nz=9, dtype="f64")],
                          ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("k,wb,ry", [(3, "8", "0"), (3, "8", "3"), (3, "8", "32"), (3, "8", "31"), (3, "8", "22"), (3, "4", "0"), (4, "8", "0"), (4, "8", "31"),
-                                     (4, "8", "21"), (4, "8", "32"), (4, "8", "42"), (4, "8", "22"), (4, "4", "0"),
-                                     (5, "8", "0")])
+@pytest.mark.parametrize("k", [3, 4])
+@pytest.mark.parametrize("pf", ["0", "64", "128", "256"])
 @pytest.mark.parametrize("resid", [False, True])
-def test_heat7_wxk_bitwise(hip, prob, k, wb, ry, resid, knob):
+def test_heat7_wxk_bitwise(hip, prob, k, pf, resid, knob):
     """heat7_wxk (y halo exchanged between the waves of a band through the LDS seam table, one
     barrier per plane) == K naive single steps, bitwise, with the residual of step K, for every
-    band shape and row count, including bands taller than the grid and waves wholly outside it."""
-    if k == 5 and (resid or prob.dtype == "f64"):
-        pytest.skip("the 5-step sweep is fp32 without a residual")
+    shipped band and row count, including bands taller than the grid and waves wholly outside it,
+    with and without the L2 prefetch of plane q + 2 (MDFX_WXK_PF byte strides)."""
     knob("MDFX_H7_WXK", 1)
-    knob("MDFX_WTK_WB", wb)
-    knob("MDFX_WXK_RY", ry)
+    knob("MDFX_WXK_PF", pf)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -505,42 +502,7 @@ def test_heat7_wxk_bitwise(hip, prob, k, wb, ry, resid, knob):
         set_kernel_variant("auto")
     torch.cuda.synchronize()
     o = lay.owned
-    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb, ry)
-    if resid:
-        assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
-
-
-@pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=1024, ny=45, nz=17)],
-                         ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("nb", ["31", "21", "32"])
-@pytest.mark.parametrize("resid", [False, True])
-def test_heat7_wxk_window_depth_bitwise(hip, prob, nb, resid, knob):
-    """heat7_wxk K = 4 with the u0 DMA two planes ahead (3 window buffers) and / or one seam table
-    (its reads and writes separated by a second barrier per plane) == 4 naive single steps."""
-    if prob.dtype == "f64":
-        pytest.skip("fp32 instances")
-    k = 4
-    knob("MDFX_H7_WXK", 1)
-    knob("MDFX_WXK_NB", nb)
-    lay = FieldLayout.make(prob, halo=k)
-    src = alloc_field(lay, "cuda")
-    init_field(prob, lay, src)
-    fused = alloc_field(lay, "cuda")
-    res = torch.zeros((), dtype=torch.float64, device="cuda")
-    apply_stencil(prob, lay, src, fused, steps=k, resid=res if resid else None)
-    set_kernel_variant("naive")
-    try:
-        cur = src.clone()
-        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
-        for i in range(k):
-            nxt = cur.clone()
-            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
-            cur = nxt
-    finally:
-        set_kernel_variant("auto")
-    torch.cuda.synchronize()
-    o = lay.owned
-    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), nb
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, pf)
     if resid:
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
@@ -634,10 +596,18 @@ def test_box27_wxk_regions_and_engine(hip, knob, nx, wxp):
     init_field(prob, lay, src)
     out = alloc_field(lay, "cuda")
     h = lay.halo
-    apply_stencil(prob, lay, src, out, h, h + k, steps=k, second=(h + 18 - k, h + 18))
-    apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k)
+    res = torch.zeros((), dtype=torch.float64, device="cuda")
+    apply_stencil(prob, lay, src, out, h, h + k, steps=k, second=(h + 18 - k, h + 18), resid=res)
+    apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k, resid=res)
     torch.cuda.synchronize()
     assert torch.equal(out[h:h + 18, :, :nx], ref[12 + k:30 + k, :, :nx])
+    # the two-region launch's residual == three single-region launches'
+    res3 = torch.zeros((), dtype=torch.float64, device="cuda")
+    out3 = alloc_field(lay, "cuda")
+    for lo, hi in ((h, h + k), (h + 18 - k, h + 18), (h + k, h + 18 - k)):
+        apply_stencil(prob, lay, src, out3, lo, hi, steps=k, resid=res3)
+    torch.cuda.synchronize()
+    assert res.item() > 0 and abs(res.item() - res3.item()) <= 1e-9 * res3.item()
     knob("MDFX_B27_WXK", 1)
     p3 = models.box27(nx=500, ny=33, nz=45)
     a, _ = _sim(p3, 6, ranks=1)
@@ -666,7 +636,14 @@ def test_heat7_wxk_regions_and_engine(hip, k, knob):
     apply_stencil(prob, lay, src, out, h + k, h + 18 - k, steps=k, resid=res)
     torch.cuda.synchronize()
     assert torch.equal(out[h:h + 18, :, :1024], ref[12 + k:30 + k, :, :1024])
-    assert res.item() > 0
+    # the fused two-region launch's residual == three single-region launches' (a wrong residual from
+    # the second region's tasks would show here)
+    res3 = torch.zeros((), dtype=torch.float64, device="cuda")
+    out3 = alloc_field(lay, "cuda")
+    for lo, hi in ((h, h + k), (h + 18 - k, h + 18), (h + k, h + 18 - k)):
+        apply_stencil(prob, lay, src, out3, lo, hi, steps=k, resid=res3)
+    torch.cuda.synchronize()
+    assert res.item() > 0 and abs(res.item() - res3.item()) <= 1e-9 * res3.item()
     p3 = models.heat3d(nx=600, ny=37, nz=45)
     a, _ = _sim(p3, 2 * k, ranks=1)
     b, _ = _sim(p3, 2 * k, ranks=3, temporal=k)

@@ -49,16 +49,22 @@ def test_lds_never_limits_occupancy(recs):
 
 
 @pytest.mark.parametrize("name,min_waves", [
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 2, false>", 2),       # headline K = 3 sweep (8-wave bands)
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 2, false>", 2),       # thin slabs (4-wave bands)
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 1, false>", 2),       # natural layout, no unroll
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 1, true>", 2),        # balanced one-round schedule
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 1, true>", 2),
+    # the shipped headline sweep: 1024^3 fp32, 4 fused steps, 3 + 2-row bands of 8 waves (one 512-thread
+    # block per CU: 2 waves per SIMD is all a block of 8 waves can have)
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true>", 2),         # its residual sweeps
+    ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false>", 2),        # K = 3 (step-count remainders)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false>", 2),       # fp64 K = 3 (2048^3 + residual)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true>", 2),
+    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false>", 2),              # 27-point K = 3 (1024-cell rows, fp64)
+    ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false>", 2),
+    ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true>", 2),
+    ("mdfx::dev::box27_tb2n<1, 1, false>", 3),                          # 27-point K = 2 fp32 (512^3)
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 2, false>", 2),       # K = 3 where heat7_wxk does not run
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 2, false>", 2),       # (thin slabs: 4-wave bands)
     ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0, false>", 2),
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, true, 1, false>", 2),        # residual sweeps
     ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 2>", 3),           # 2D MDF, 8 steps per sweep
     ("mdfx::dev::jacobi5_tbk<float, 8, false, true, 2>", 2),            # reference precision
-    ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 1>", 4),
     ("mdfx::dev::heat7_tbk<float, 4, 2, 4, false>", 2),                 # K = 2 fused sweep
     ("mdfx::dev::heat7_tbk<double, 4, 2, 4, false>", 2),
     ("mdfx::dev::heat7_tb2<float, 2, 4, false, 1, true>", 3),           # x-tiled rows
