@@ -89,8 +89,6 @@ static Knobs read_knobs() {
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
-  k.wxk_pf = env_int("MDFX_WXK_PF", 0);
-  if (k.wxk_pf != 0 && k.wxk_pf != 64 && k.wxk_pf != 128 && k.wxk_pf != 256) k.wxk_pf = 0;
   k.j5_f64_pd = env_int("MDFX_J5_F64_PD", 1);
   k.b27_wxp = env_int("MDFX_B27_WXP", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);

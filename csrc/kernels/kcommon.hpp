@@ -230,7 +230,6 @@ struct Knobs {
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
   int b27_wxp = 0;     // MDFX_B27_WXP: 1 = box27_wxk's x-pair kernel for fp32 rows of 257..512 cells (measured slower: profiles/r03_session_t/)
   int j5_f64_pd = 1;   // MDFX_J5_F64_PD: fp64 jacobi5_tbk with the 2-row unroll and two u0 rows in flight (0: mode 0)
-  int wxk_pf = 0;      // MDFX_WXK_PF: heat7_wxk L2 prefetch of plane q + 2 (byte stride 64 / 128; 0 = off)
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)
   int j5_nat = 2;      // MDFX_J5_NAT: jacobi5_tbk fp32 rows: 2 natural layout + 2-row unroll, 1 natural, 0 round 2's pair layout

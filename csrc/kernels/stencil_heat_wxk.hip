@@ -59,8 +59,7 @@ int64_t resident_blocks(const void* kfn, int block);
 
 template <class T, int RY, int RE, int K, int WB, bool RES>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
-                                                     int pf) {
+                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
@@ -81,12 +80,9 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   __shared__ V win[2][RB][64];
   // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
   __shared__ V seam[2][K - 1][WB - 1][2][64];
-  // L2 prefetch (pf = byte stride 64 / 128 / 256, 0 = off): at step q every wave touches one dword
-  // per pf bytes of its window rows of plane q + 2 with a 4-byte LDS DMA into this scratch, so the
-  // window DMA of plane q + 2, issued one step later, hits L2 instead of waiting a full HBM round
-  // trip: a second plane in flight without a third window buffer (which would not fit next to the
-  // seam tables: round 3 measured it with one seam table and a second barrier, and lost)
-  __shared__ uint32_t pfdump[WB][64];
+  // (A second plane in flight does not help this sweep: a third window buffer with one seam table
+  // and a second barrier lost in round 3 (profiles/r03_session_r/), and an L2 prefetch of plane
+  // q + 2 by 4-byte LDS DMAs lost 15-24 % in round 4 (profiles/r04_session_b/).)
   const int tiles = XT * YT;
   const int t = b % tiles, zt = b / tiles;
   const int P0 = (int)(g.lz_end - g.lz_begin);
@@ -138,30 +134,6 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
     }
   };
 
-  // prefetch geometry: `lpr` lanes per window row, `rpi` rows per instruction; wave w touches rows
-  // w * rpi .. w * rpi + rpi - 1 of the window (one instruction per wave and plane; with the shipped
-  // bands WB * rpi covers the window's rows, taller windows leave their last rows to the DMA)
-  const int lpr = pf > 0 ? (int)(64 * sizeof(V) / (unsigned)pf) : 64, rpi = 64 / lpr;
-  const bool pfw = pf > 0 && w * rpi < RB;  // wave-uniform: this wave prefetches
-  uint32_t pfo = 0;                         // the lane's byte offset inside a plane
-  if (pfw) {
-    int k = w * rpi + lane / lpr;
-    k = k < RB ? k : RB - 1;
-    const int y = yb - K + k;
-    const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-    const int64_t xo = std::min<int64_t>(std::max<int64_t>(xs, 0) * (int64_t)sizeof(T) + (int64_t)(lane % lpr) * pf,
-                                         pitch * (int64_t)sizeof(T) - 4);
-    pfo = (uint32_t)((int64_t)yc * pitch * (int64_t)sizeof(T) + xo);
-  }
-  auto prefetch = [&](int lz) {
-    const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
-    const char* a = (const char*)(in + (int64_t)lzc * plane) + pfo;
-    dcheck(g, (const char*)in, a, 4);
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)a,
-                                     (__attribute__((address_space(3))) void*)&pfdump[w][0], 4, 0, 0);
-  };
-  int npf_last = 0;  // prefetches this wave issued after its newest window DMA (0 / 1)
-
   const int qlast = ze - 1 + K;  // last u0 plane of the march
   issue(zs - K, 0);
   T* ob = out + (int64_t)y0 * pitch;
@@ -204,17 +176,12 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // no instruction moves across a plane boundary (the two planes of an unrolled trip would
       // otherwise interleave, with both planes' rows live at once)
       __builtin_amdgcn_sched_barrier(0);
-      // plane q's DMA has landed (the prefetches and stores issued after it stay in flight); the
-      // barrier publishes it and last step's seam rows, and certifies that every wave is done with
-      // the other window buffer and the other seam parity
-      wait_vm_le(nst + npf_last);
+      // plane q's DMA has landed (the stores issued after it stay in flight); the barrier
+      // publishes it and last step's seam rows, and certifies that every wave is done with the
+      // other window buffer and the other seam parity
+      wait_vm_le(nst);
       lds_barrier();
       if (q < qlast) issue(q + 1, P ^ 1);
-      npf_last = 0;
-      if (pfw && q + 2 <= qlast) {
-        prefetch(q + 2);
-        npf_last = 1;
-      }
       constexpr int SR = P ^ 1;  // seam parity read this step
       // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact)
       Row rl[K + 1];
@@ -361,12 +328,11 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   if (resid) {
-    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid,
-                       knobs().wxk_pf);
+    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
     return;
   }
   hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
-                     resid, knobs().wxk_pf);
+                     resid);
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -376,8 +342,7 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 
 // Shipped bands of 8 waves: fp32 K = 4 in 2 + 6 x 3 + 2 rows (3-row inner waves, 2-row edge
 // waves): 1024^3 2387-2394 GCells/s on every box measured; 4-row inner waves ran 2415-2454 on one
-// box and 2095-2138 on two others (near the LDS limit, 156 KB, and spilling once the prefetch
-// came in), 2-row waves 2247-2253; on thin slabs the 3-row band also
+// box and 2095-2138 on two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row band also
 // fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
 // (profiles/r03_wxk/). fp32 K = 3 (step-count remainders): 4-row waves. fp64 K = 3: 3 + 1-row bands
 // (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2); fp64 K = 4 stays on heat7_wtk. Round 3's

@@ -475,15 +475,12 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
 @pytest.mark.parametrize("prob", WTK3D + [models.heat3d(nx=700, ny=70, nz=12), models.heat3d(nx=300, ny=33, nz=9, dtype="f64")],
                          ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k", [3, 4])
-@pytest.mark.parametrize("pf", ["0", "64", "128", "256"])
 @pytest.mark.parametrize("resid", [False, True])
-def test_heat7_wxk_bitwise(hip, prob, k, pf, resid, knob):
+def test_heat7_wxk_bitwise(hip, prob, k, resid, knob):
     """heat7_wxk (y halo exchanged between the waves of a band through the LDS seam table, one
     barrier per plane) == K naive single steps, bitwise, with the residual of step K, for every
-    shipped band and row count, including bands taller than the grid and waves wholly outside it,
-    with and without the L2 prefetch of plane q + 2 (MDFX_WXK_PF byte strides)."""
+    shipped band and row count, including bands taller than the grid and waves wholly outside it."""
     knob("MDFX_H7_WXK", 1)
-    knob("MDFX_WXK_PF", pf)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -502,7 +499,7 @@ def test_heat7_wxk_bitwise(hip, prob, k, pf, resid, knob):
         set_kernel_variant("auto")
     torch.cuda.synchronize()
     o = lay.owned
-    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, pf)
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), k
     if resid:
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
