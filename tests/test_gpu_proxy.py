@@ -62,3 +62,47 @@ def test_bench_rank_proxy_json(hip):
     assert rec["proxy_rank"] == 2 and rec["config"]["slab_planes"] == [128, 192]
     assert rec["implied_node_gcells"] == pytest.approx(4 * rec["value"], rel=1e-3)
     assert rec["config"]["graph_captures_timed"] == 0
+
+
+def test_replayed_cycles_run_as_fast_as_eager_steps_after_reinit(hip):
+    """Round 3's slow graph replay (N = 8 proxy, K = 2, 2 rounds: 2.5x the eager time per step
+    after init() on a used engine and three replayed warm-up cycles). Its cause: the block-round
+    count was a process-wide setting that only run() updated, so cycles captured by
+    prepare_graphs() after set_options(min_rounds=...) replayed the previous configuration's
+    launch geometry (1-round sweeps under the overlapped schedule). The round count now travels
+    with every launch (RegionArgs::min_rounds): the replay must stay within 1.2x the eager steps."""
+    import time
+
+    import torch
+
+    prob = m.heat3d(n=1024)
+    steps = 48
+
+    def ms_per_step(sim):
+        sim.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sim.run(steps)
+        sim.synchronize()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    with m.Simulation(prob, device="hip", ranks=8, proxy_rank=4, temporal=2, graph=True) as sim:
+        # a used engine: other round counts captured and run first (the trial loop's history)
+        for rr in (1, 2, 1):
+            sim.set_options(graph=True, min_rounds=rr, overlap=True)
+            sim.init()
+            sim.prepare_graphs()
+            sim.run(12)
+        sim.set_options(graph=False, min_rounds=2, overlap=True)
+        sim.init()
+        sim.run(12)
+        eager = min(ms_per_step(sim) for _ in range(2))
+        sim.set_options(graph=True, min_rounds=2, overlap=True)
+        sim.init()
+        sim.prepare_graphs()
+        sim.run(12)  # three replayed warm-up cycles (2 sweeps of 2 steps each)
+        r0 = sim.graph_replays
+        replay = min(ms_per_step(sim) for _ in range(2))
+        assert sim.graph_replays > r0
+    assert replay <= 1.2 * eager, (replay, eager)
