@@ -43,8 +43,6 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   if (spec_.kind != StencilKind::Life)
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 16, "temporal blocking depth must be 1..16");
-  if (const char* v = std::getenv("MDFX_BND_FIRST")) bnd_first_ = std::atoi(v) != 0;
-  if (const char* v = std::getenv("MDFX_BND_CS")) bnd_cs_ = std::atoi(v) != 0;
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
@@ -274,7 +272,7 @@ void Solver::exchange_ghosts() {
 int Solver::min_rounds() const { return opt_.min_rounds > 0 ? opt_.min_rounds : (nranks_ > 1 ? 2 : 1); }
 
 bool Solver::boundary_on_cs() const {
-  return bnd_cs_ && opt_.overlap && bnd_first_ && slabs_.size() == 1 && transport_->graph_capturable();
+  return opt_.overlap && slabs_.size() == 1 && transport_->graph_capturable();
 }
 
 void Solver::step(bool want_resid, int k) {
@@ -332,7 +330,7 @@ void Solver::step(bool want_resid, int k) {
       s.be->record(s.ev_bnd, s.cs);  // this step's boundary kernels: the exchange follows them
       s.be->wait(s.hs, s.ev_bnd);
     } else if (opt_.overlap) {
-      if (bnd_first_) s.be->record(s.ev_bnd, s.hs);  // this step's boundary kernels
+      s.be->record(s.ev_bnd, s.hs);  // this step's boundary kernels (the interior waits for them)
       s.be->wait(s.cs, s.ev_bnd);
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)is));

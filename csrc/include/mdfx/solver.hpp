@@ -150,14 +150,12 @@ class Solver {
   void* pev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // timing events (slab 0)
   bool ghosts_dirty_ = false;
   // overlapped schedule: the interior sweep of a step waits for the SAME step's boundary kernels
-  // (MDFX_BND_FIRST=1, default) instead of the previous step's, so the short boundary launch gets
-  // the whole device before the long interior sweep takes every CU; the exchange still runs under
-  // the interior (profiles/r03_wxk/)
-  bool bnd_first_ = true;
-  // the boundary kernels run on the compute stream, ahead of the interior sweep of the same step,
-  // and only the exchange on the halo stream (overlap + boundary-first + a pure-stream-work
-  // transport; MDFX_BND_CS=0 keeps them on the halo stream)
-  bool bnd_cs_ = true;
+  // instead of the previous step's, so the short boundary launch gets the whole device before the
+  // long interior sweep takes every CU; the exchange still runs under the interior (rank proxy
+  // N = 8 1,833 vs 1,759 GCells/s per GPU, N = 4 2,058 vs 1,816: profiles/r03_session_p/; the
+  // other order was removed in round 4). With one slab per process and a transport whose exchange
+  // is pure stream work, the boundary kernels run on the compute stream ahead of the interior and
+  // only the exchange on the halo stream (boundary_on_cs).
   bool boundary_on_cs() const;
   int min_rounds() const;  // effective rounds per streaming sweep (RegionArgs::min_rounds)
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown

@@ -89,20 +89,11 @@ static Knobs read_knobs() {
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
-  k.j5_f64_pd = env_int("MDFX_J5_F64_PD", 1);
-  k.b27_wxp = env_int("MDFX_B27_WXP", 0);
   k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
   k.j5_tbk = env_int("MDFX_J5_TBK", 0);
   k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
   k.b27_tbk = env_int("MDFX_B27_TBK", 0);
   k.life_bits = env_int("MDFX_LIFE_BITS", 1);
-  k.vm_lag = env_int("MDFX_VM_LAG", 1);
-  k.wtk_nat = env_int("MDFX_WTK_NAT", 2);
-  k.j5_nat = env_int("MDFX_J5_NAT", 2);
-  k.wtk_res_shape = env_int("MDFX_WTK_RES_SHAPE", 0);
-  k.b27_nat = env_int("MDFX_B27_NAT", 1);
-  k.wtk_split = env_int("MDFX_WTK_SPLIT", -1);
-  k.fuse_regions = env_int("MDFX_FUSE_REGIONS", 0);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
@@ -289,9 +280,6 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // (profiles/r03_wxk/). MDFX_B27_WXK = 0 / 1 forces K = 2 / 3
       if (dev::knobs().b27_wxk == 1) return 3;
       if (dev::knobs().b27_wxk == 0) return 2;
-      // (fp32 rows of 257..512 cells with MDFX_B27_WXP = 1: K = 3 in box27_wxp, two 256-cell
-      // halves per block; 512^3: 909 vs 1072-1085 for box27_tb2n K = 2, profiles/r03_session_t/)
-      if (spec.dtype == DType::F32 && nx > 256 && nx <= 512 && dev::knobs().b27_wxp != 0) return 3;
       return (spec.dtype == DType::F64 || nx >= 1024) ? 3 : 2;
     case StencilKind::Heat7:
       // K = 3 through heat7_wtk wherever its x segments cover at least 2/3 of the lane cells:
@@ -313,7 +301,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
     // slab: one fill of the device, one launch gap); every other kernel runs them one after the other
     const bool fuse = a.lz_end > a.lz_begin &&
                       ((a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps, spec.dtype) &&
-                        (dev::knobs().fuse_regions || dev::use_wxk(spec.dtype, a.lay.global.nx))) ||
+                        dev::use_wxk(spec.dtype, a.lay.global.nx)) ||
                        (spec.kind == StencilKind::Box27 && a.steps == 3));
     if (!fuse) {
       RegionArgs r1 = a, r2 = a;

@@ -222,24 +222,14 @@ struct Knobs {
   int tb_ry = 0;       // MDFX_TB_RY: rows per tile of heat7_tb2 (x-tiled rows) / box27_tb2 (0: 2)
   int tbk_ry = 0;      // MDFX_TBK_RY: rows per tile of heat7_tbk (0: 4 at K = 2, 2 deeper)
   int wtk_ry8 = 0;     // MDFX_WTK_RY8: fp64 rows per wave in 8-wave bands (2 / 3; 0: 3 up to 1024-cell rows, else 2)
-  int wtk_nat = 2;     // MDFX_WTK_NAT: heat7_wtk fp32 rows: 2 natural pair layout + 2-plane unroll, 1 natural, 0 round 2's
-  int wtk_res_shape = 0;  // MDFX_WTK_RES_SHAPE: 1 = residual sweeps in round 2's 2-row 4-wave bands
-  int fuse_regions = 0;  // MDFX_FUSE_REGIONS: 1 = both boundary regions of a slab in one heat7_wtk launch (measured slower)
-  int wtk_split = -1;  // MDFX_WTK_SPLIT: heat7_wtk balanced one-round schedule: -1 never (default, measured slower), 0 cost model, 1 always
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64 and rows >= 1024; 0 / 1)
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: fp32, 0: never, 1: always)
-  int b27_wxp = 0;     // MDFX_B27_WXP: 1 = box27_wxk's x-pair kernel for fp32 rows of 257..512 cells (measured slower: profiles/r03_session_t/)
-  int j5_f64_pd = 1;   // MDFX_J5_F64_PD: fp64 jacobi5_tbk with the 2-row unroll and two u0 rows in flight (0: mode 0)
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wtk = 0;      // MDFX_H7_WTK: 3D 7-point sweeps of K >= 3 steps through heat7_wtk (0), or heat7_tbk (-1)
-  int j5_nat = 2;      // MDFX_J5_NAT: jacobi5_tbk fp32 rows: 2 natural layout + 2-row unroll, 1 natural, 0 round 2's pair layout
   int j5_tbk = 0;      // MDFX_J5_TBK: 2D MDF two-step sweeps through the K-step kernel
   int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
   int life_bits = 1;   // MDFX_LIFE_BITS: Life sweeps of K > 2 generations bit-sliced (0: SWAR life_tbk)
-  int b27_nat = 1;     // MDFX_B27_NAT: fp32 box27_tb2 in the natural layout with the 2-plane unroll (0: round 2's)
   int b27_tbk = 0;     // MDFX_B27_TBK: 27-point fused kernel (0: per dtype, -1: box27_tb2, 1/2/4: box27_tbk rows)
-  int vm_lag = 1;      // MDFX_VM_LAG: streaming kernels leave the last plane's stores in flight across the
-                       // next plane's DMA wait (0: wait for every vector-memory operation, round 2)
   int debug_zc = 0;    // MDFX_DEBUG_ZC: print the z chunking of the streaming kernels
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
 };

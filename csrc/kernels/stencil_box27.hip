@@ -580,8 +580,7 @@ __global__ __launch_bounds__(256) void box27_tb2n(const float* __restrict__ in, 
 // one barrier per level and plane. Region contract as heat7_tbk: u0 valid on [lz_begin - K, lz_end + K).
 template <class T, int RY, int K, int WXN, bool RES>
 __global__ __launch_bounds__(256) void box27_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
-                                                 T c2, T c3, int zc, int YT, double* __restrict__ resid,
-                                                 int lag) {
+                                                 T c2, T c3, int zc, int YT, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
   using Row = typename RO::Row;
@@ -657,7 +656,7 @@ __global__ __launch_bounds__(256) void box27_tbk(const T* __restrict__ in, T* __
     C[i] = RO::zero();
   }
   // output stores per stored plane (wave-uniform; a wave with no lane in the row issues none)
-  const int nsto = (lag && __builtin_amdgcn_ballot_w64(xin) != 0) ? (int)max((int64_t)0, min((int64_t)RY, g.ny - y0)) : 0;
+  const int nsto = __builtin_amdgcn_ballot_w64(xin) != 0 ? (int)max((int64_t)0, min((int64_t)RY, g.ny - y0)) : 0;
   int nst = 0;  // stores issued since this wave's last DMA
   double acc = 0.0;
   const int64_t cend = ze + K;
@@ -782,9 +781,9 @@ static void launch_box27_tbk_w(const Geo& g, const T* in, T* out, const StencilC
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
   if (resid)
-    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
   else
-    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((box27_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
 }
 
 template <class T, int RY, int K>
@@ -825,22 +824,21 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
-  // fp32: the natural-layout unrolled kernel unless MDFX_B27_NAT=0
+  // fp32: the natural-layout kernel with the 2-plane unroll (box27_tb2n; round 2's pair-layout
+  // fp32 box27_tb2, 937-944 vs 1005-1013 GCells/s at 512^3, was removed in round 4,
+  // profiles/r03_wtk/b27f32_*); fp64 (MDFX_B27_TBK = -1 only: box27_tbk is its default): box27_tb2
+  // with the next-plane prefetch (491.8 vs 479.8 without, profiles/r01_box27_tb2.txt)
   if constexpr (std::is_same<T, float>::value) {
-    if (knobs().b27_nat) {
-      if (resid)
-        hipLaunchKernelGGL((box27_tb2n<RY, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-      else
-        hipLaunchKernelGGL((box27_tb2n<RY, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-      return;
-    }
+    if (resid)
+      hipLaunchKernelGGL((box27_tb2n<RY, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+    else
+      hipLaunchKernelGGL((box27_tb2n<RY, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+  } else {
+    if (resid)
+      hipLaunchKernelGGL((box27_tb2<T, RY, WXN, true, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+    else
+      hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
   }
-  // next-plane prefetch always: fp32 985.7 vs 773.3 GCells/s without, fp64 491.8 vs 479.8 (512^3,
-  // profiles/r01_box27_tb2.txt)
-  if (resid)
-    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, true, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-  else
-    hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
 }
 
 template <class T, int RY>

@@ -601,14 +601,6 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
         row_step(q, CA, CB, ztest, std::integral_constant<int, 0>{});
         row_step(q + 1, CB, CA, ztest, std::integral_constant<int, 1>{});
       }
-    } else if constexpr (MODE == 3) {
-      // up to three extra rows at the end: loads clamp, nothing is stored
-      for (int64_t q = zs - K; q <= qlast; q += 4) {
-        row_step(q, CA, CB, ztest, std::integral_constant<int, 0>{});
-        row_step(q + 1, CB, CA, ztest, std::integral_constant<int, 1>{});
-        row_step(q + 2, CA, CB, ztest, std::integral_constant<int, 2>{});
-        row_step(q + 3, CB, CA, ztest, std::integral_constant<int, 3>{});
-      }
     } else {
       for (int64_t q = zs - K; q <= qlast; ++q) row_step(q, CA, CA, ztest, std::integral_constant<int, 0>{});
     }
@@ -638,40 +630,18 @@ static void launch_jacobi5_tbk_km(const Geo& g, const T* in, T* out, T r, double
     hipLaunchKernelGGL((jacobi5_tbk<T, K, false, REF, MODE>), grd, blk, 0, s, in, out, g, r, zc, XT, ntasks, resid);
 }
 
-// fp32: MDFX_J5_NAT = 2 (default) natural layout + 2-row unroll, 1 natural layout, 0 round 2's
-// pair layout; fp64: mode 0
+// fp32: the natural layout with the 2-row unroll (mode 2); the reference-precision instance keeps
+// 4 waves per SIMD without the unroll (mode 1; 16384^2 K = 8: 3346-3368 GCells/s vs 3131-3145
+// unrolled at 2 waves per SIMD). fp64: the pair rows (RowOps<double>) with the 2-row unroll and two
+// u0 rows in flight (mode 2; 16384^2 K = 8: 2216-2219 vs 2005 GCells/s for mode 0,
+// profiles/r03_session_ac/). Round 2's fp32 pair layout and fp64 mode 0, and a 4-row unroll
+// (mode 3), measured slower and were removed in round 4 (profiles/r03_mdf2d/, r03_session_ac/).
 template <class T, int K, bool REF>
 static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  if constexpr (sizeof(T) == 4) {
-    // the reference-precision instance keeps 4 waves per SIMD without the unroll (16384^2 K = 8:
-    // 3346-3368 GCells/s vs 3131-3145 unrolled at 2 waves per SIMD; plain fp32 ties, 4147-4212)
-    if (knobs().j5_nat == 3 && !REF) {
-      launch_jacobi5_tbk_km<T, K, REF, 3>(g, in, out, r, resid, s);
-      return;
-    }
-    if (knobs().j5_nat == 2 && !REF) {
-      launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
-      return;
-    }
-    if (knobs().j5_nat == 2 && REF) {
-      launch_jacobi5_tbk_km<T, K, REF, 1>(g, in, out, r, resid, s);
-      return;
-    }
-    if (knobs().j5_nat == 1) {
-      launch_jacobi5_tbk_km<T, K, REF, 1>(g, in, out, r, resid, s);
-      return;
-    }
-  }
-  // fp64: the pair rows (RowOps<double>) with the 2-row unroll and two u0 rows in flight
-  // (16384^2 K = 8: 2216-2219 vs 2005 GCells/s for mode 0, occupancy 3 vs 4;
-  // profiles/r03_session_ac/); MDFX_J5_F64_PD = 0 keeps mode 0
-  if constexpr (sizeof(T) == 8) {
-    if (knobs().j5_f64_pd) {
-      launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
-      return;
-    }
-  }
-  launch_jacobi5_tbk_km<T, K, REF, 0>(g, in, out, r, resid, s);
+  if constexpr (sizeof(T) == 4 && REF)
+    launch_jacobi5_tbk_km<T, K, REF, 1>(g, in, out, r, resid, s);
+  else
+    launch_jacobi5_tbk_km<T, K, REF, 2>(g, in, out, r, resid, s);
 }
 
 template <class T, bool REF>

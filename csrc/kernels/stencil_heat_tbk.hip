@@ -50,7 +50,7 @@ int64_t resident_blocks(const void* kfn);
 
 template <class T, int RY, int K, int WXN, bool RES>
 __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                 int zc, int YT, double* __restrict__ resid, int lag) {
+                                                 int zc, int YT, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = RowOps<T>;
   using Row = typename RO::Row;
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
     C[i] = RO::zero();
   }
   // output stores per stored plane (wave-uniform; a wave with no lane in the row issues none)
-  const int nsto = (lag && __builtin_amdgcn_ballot_w64(xin) != 0) ? max(0, min(RY, ny - y0)) : 0;
+  const int nsto = __builtin_amdgcn_ballot_w64(xin) != 0 ? max(0, min(RY, ny - y0)) : 0;
   int nst = 0;  // stores issued since this wave's last DMA
   double acc = 0.0;
   const int cend = ze + K;
@@ -301,9 +301,9 @@ static void launch_tbk_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
-    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, true>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
   else
-    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid, knobs().vm_lag);
+    hipLaunchKernelGGL((heat7_tbk<T, RY, K, WXN, false>), grd, blk, 0, s, in, out, g, r, zc, YT, resid);
 }
 
 template <class T, int RY, int K>

@@ -40,25 +40,16 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 
-// Schedule of one streaming sweep over `planes` planes of `tiles` tiles on `resident` block slots,
-// every block paying 2K planes of pipeline fill per segment it marches:
-//  chunked: z chunks of zc planes, tiles x chunks blocks, dealt in rounds of `resident`; the chunk
-//           count minimises rounds x (zc + 2K) (chunks of at least 4K planes; at least `min_rounds`
-//           rounds when several slabs leave CUs for exchange kernels). 1024^3 fp32 in 8-wave bands:
-//           7 chunks of 147 planes (5.9 rounds), the measured optimum of round 2's zc sweep, where 6
-//           or 4 chunks (171, 256 planes) end on a nearly empty round.
-//  split:   one round of blocks, block b marching the b-th equal share of the tile-major
-//           (tile, plane) work: no ragged last round, at most two segments (two fills) per block,
-//           but neighbouring y bands no longer march in lockstep, so bands of 8 waves lose their
-//           L2 sharing of the y-halo rows (priced at +6%). Thin slabs: the interior of a 1024^2 x
-//           128 slab at K = 3 (430 tiles, 512 slots) is 128 plane-times chunked (one 84%-full
-//           round), 115 split.
-struct WtkPlan {
-  int zc = 0;
-  bool split = false;
-};
-static WtkPlan wtk_plan(int64_t planes, int64_t tiles, int64_t resident, int K, int WB, int min_rounds, int knob) {
-  WtkPlan p;
+// Schedule of one streaming sweep over `planes` planes of `tiles` tiles on `resident` block slots:
+// z chunks of zc planes, tiles x chunks blocks, dealt in rounds of `resident`; every chunk pays 2K
+// planes of pipeline fill, so the chunk count minimises rounds x (zc + 2K) (chunks of at least 4K
+// planes; at least `min_rounds` rounds when several slabs leave CUs for exchange kernels). 1024^3
+// fp32 in 8-wave bands: 7 chunks of 147 planes (5.9 rounds), the measured optimum of round 2's zc
+// sweep, where 6 or 4 chunks (171, 256 planes) end on a nearly empty round. (A balanced one-round
+// "split" schedule, block b marching the b-th equal share of the tile-major work, measured slower:
+// neighbouring y bands stop marching in lockstep and lose their L2 sharing of the y-halo rows, 1.59
+// instead of 1.20 fields fetched; removed in round 4, numbers in profiles/r03_wtk/.)
+static int wtk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int min_rounds) {
   const int64_t fill = 2 * K;
   const int64_t zmax = std::max<int64_t>(1, planes / (4 * K));
   double best = 1e300;
@@ -72,16 +63,7 @@ static WtkPlan wtk_plan(int64_t planes, int64_t tiles, int64_t resident, int K, 
       bz = zt;
     }
   }
-  p.zc = (int)((planes + bz - 1) / bz);
-  const double share = (double)planes * (double)tiles / (double)resident;
-  if (knob == 1) {
-    p.split = true;  // forced (tests: any size, blocks with an empty share included)
-  } else if (knob == 0 && min_rounds <= 1 && tiles * planes > resident) {
-    const double segs = std::ceil(share / (double)planes) + 1.0;
-    const double ts = (share + (double)fill * segs) * (WB == 8 ? 1.06 : 1.0);
-    p.split = ts < best;
-  }
-  return p;
+  return (int)((planes + bz - 1) / bz);
 }
 
 // A block is one task: WB = 4 or 8 waves stacked along y on one x segment (a y band of WB * RY
@@ -90,10 +72,9 @@ static WtkPlan wtk_plan(int64_t planes, int64_t tiles, int64_t resident, int K, 
 // -> 18 per 12 / 30 per 24), at one block barrier per plane. (The first version ran every wave as
 // an independent task with a private LDS slot and no barrier: 1.565 fields fetched per sweep
 // against 1.444 / 1.108 for bands of 4 / 8, and slower on every shape, profiles/r02_wtk/README.txt.)
-template <class T, int RY, int K, int WB, bool RES, int MODE, bool SPLIT>
+template <class T, int RY, int K, int WB, bool RES, int MODE>
 __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                 int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
-                                                 int lag, int64_t split_w) {
+                                                 int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = typename std::conditional<sizeof(T) == 4 && MODE >= 1, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
@@ -105,23 +86,12 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   constexpr int RB = WB * RY + 2 * K;         // shared window rows of a band
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // Work: tile t = (x segment, y band) x planes of the region, flattened tile-major (index
-  // t * P + plane). Chunked schedule (split_w == 0): block-uniform task = one z chunk of one tile;
-  // order x segments fastest, then y bands, then z chunks. Balanced schedule (split_w = tiles * P):
-  // the grid is one round of resident blocks and block b takes the equal share
-  // [b * W / B, (b+1) * W / B) of the flattened work, i.e. the tail of one tile's planes and the
-  // head of the next (each segment pays its own 2K-plane pipeline fill), so no round ends ragged.
-  // A second region (g.lz2_*: the other boundary region of a slab) adds its own z chunks after the
-  // first region's, chunked schedule only.
+  // Work: block-uniform task = one z chunk of one tile (x segment, y band); order x segments
+  // fastest, then y bands, then z chunks. A second region (g.lz2_*: the other boundary region of a
+  // slab) adds its own z chunks after the first region's.
   const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   const int P = (int)(g.lz_end - g.lz_begin);
-  int64_t wlo = 0, whi = 0;
-  if constexpr (SPLIT) {
-    wlo = split_w * b / gridDim.x;
-    whi = split_w * (b + 1) / gridDim.x;
-  } else {
-    if (b >= ntasks) return;  // block-uniform (the grid has exactly ntasks blocks)
-  }
+  if (b >= ntasks) return;  // block-uniform (the grid has exactly ntasks blocks)
   __shared__ V slot[2][RB][64];
   double acc = 0.0;
   // one segment: storage planes [zs, ze) for tile `tile`
@@ -150,7 +120,7 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
   const bool yint = yb - (K - 1) >= 1 && yb + WB * RY + K - 2 <= ny - 2;
   // output stores this wave issues per stored plane (wave-uniform; a store whose lanes are all
   // masked may be skipped by the compiler, so a wave without owned lanes counts none)
-  const int nsto = (lag && __builtin_amdgcn_ballot_w64(own) != 0) ? max(0, min(RY, ny - y0)) : 0;
+  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(RY, ny - y0)) : 0;
   int nst = 0;  // stores issued since this wave's last DMA
 
   // u0 plane lz -> LDS by LDS DMA (global_load_lds, no VGPR destination): rows outside [0, ny) and
@@ -284,106 +254,63 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
     march(std::integral_constant<bool, true>{});
   wait_vm0();  // no DMA may outlive the wave (or the segment)
   };
-  if constexpr (SPLIT) {
-    for (int64_t cur = wlo; cur < whi;) {  // block-uniform segment loop
-      const int tile = (int)(cur / P), z0 = (int)(cur - (int64_t)tile * P);
-      const int z1 = (int)min((int64_t)P, (int64_t)z0 + (whi - cur));
-      if (cur > wlo) lds_barrier();  // a block's next segment reuses the LDS window
-      cur += z1 - z0;
-      segment(tile, (int)g.lz_begin + z0, (int)g.lz_begin + z1);
-    }
+  const int t = b % (XT * YT), zt = b / (XT * YT);
+  const int zt1 = (P + zc - 1) / zc;  // chunks of the first region
+  if (zt < zt1) {
+    const int zs = (int)g.lz_begin + zt * zc;
+    segment(t, zs, min((int)g.lz_end, zs + zc));
   } else {
-    const int t = b % (XT * YT), zt = b / (XT * YT);
-    const int zt1 = (P + zc - 1) / zc;  // chunks of the first region
-    if (zt < zt1) {
-      const int zs = (int)g.lz_begin + zt * zc;
-      segment(t, zs, min((int)g.lz_end, zs + zc));
-    } else {
-      const int zs = (int)g.lz2_begin + (zt - zt1) * zc;
-      segment(t, zs, min((int)g.lz2_end, zs + zc));
-    }
+    const int zs = (int)g.lz2_begin + (zt - zt1) * zc;
+    segment(t, zs, min((int)g.lz2_end, zs + zc));
   }
   if (RES) wave_atomic_add(resid, acc);
 }
 
-template <class T, int RY, int K, int WB, bool RES, int NAT>
-static void launch_split(bool split, dim3 grd, dim3 blk, hipStream_t s, const T* in, T* out, const Geo& g, T r, int zc,
-                         int XT, int YT, int ntasks, double* resid, int64_t split_w) {
-  // the segment loop's scalar state does not fit beside the 2-plane unroll (SGPR spills, scratch):
-  // split sweeps run the natural layout without the unroll (mode 1)
-  // (fp32 always mode 1; fp64 3-row 8-wave bands have no split instance: they need scratch for it)
-  constexpr int NS = sizeof(T) == 4 ? 1 : NAT;
-  constexpr bool kSplit = !(sizeof(T) == 8 && RY == 3 && WB == 8);
-  if (kSplit && split)
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, RES, NS, kSplit>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, ntasks,
-                       resid, knobs().vm_lag, split_w);
-  else
-    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, RES, NAT, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, ntasks, resid,
-                       knobs().vm_lag, split_w);
-}
-
-template <class T, int RY, int K, int WB, int NAT>
+template <class T, int RY, int K, int WB, int MODE>
 static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
   const int YT = (int)((g.ny + RY * WB - 1) / (RY * WB));  // y bands
-  const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, NAT, false>;
+  const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, MODE>;
   const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
   const int64_t resident = resident_blocks(kfn, 64 * WB);
-  WtkPlan plan = wtk_plan(planes, tiles, resident, K, WB, g.min_rounds, knobs().wtk_split);
-  if (knobs().zc > 0 || (sizeof(T) == 8 && RY == 3 && WB == 8)) {  // (no split instance of that shape)
-    if (knobs().zc > 0) plan.zc = knobs().zc;
-    plan.split = false;
-  }
-  const int64_t planes2 = g.lz2_end - g.lz2_begin;  // a second region (boundary pair): chunked
-  if (planes2 > 0) {
-    plan.split = false;
-    plan.zc = (int)std::max(planes, planes2);
-  }
-  const int zc = plan.zc;
+  int zc = knobs().zc > 0 ? knobs().zc : wtk_zc(planes, tiles, resident, K, g.min_rounds);
+  const int64_t planes2 = g.lz2_end - g.lz2_begin;  // a second region (boundary pair): one chunk each
+  if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
-  const int64_t ntasks = plan.split ? resident : (int64_t)XT * YT * ZT;
-  const int64_t split_w = plan.split ? tiles * planes : 0;
+  const int64_t ntasks = (int64_t)XT * YT * ZT;
   if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] wtk K=%d RY=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> %s\n", K, RY, WB,
-            (long long)planes, XT, YT, (long long)resident,
-            plan.split ? "split" : format("zc %d (%lld blocks)", zc, (long long)ntasks).c_str());
+    fprintf(stderr, "[mdfx] wtk K=%d RY=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n", K, RY,
+            WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wtk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   // residual instances exist where they fit 256 VGPRs without spills: every fp64 shape, fp32 in
-  // mode 1 (the fp32 mode-0 / mode-2 3-row residual instances spill), and 2-row waves
-  constexpr bool kRes = sizeof(T) == 8 || NAT == 1 || RY <= 2;
+  // mode 1 (the fp32 mode-2 3-row residual instance spills), and 2-row waves
+  constexpr bool kRes = sizeof(T) == 8 || MODE == 1 || RY <= 2;
   if constexpr (!kRes) {
     MDFX_CHECK(!resid, "heat7_wtk: no residual variant of this shape");
-    launch_split<T, RY, K, WB, false, NAT>(plan.split, grd, blk, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, split_w);
   } else if (resid) {
-    launch_split<T, RY, K, WB, true, NAT>(plan.split, grd, blk, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, split_w);
-  } else {
-    launch_split<T, RY, K, WB, false, NAT>(plan.split, grd, blk, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, split_w);
+    hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, true, MODE>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
+                       resid);
+    return;
   }
+  hipLaunchKernelGGL((heat7_wtk<T, RY, K, WB, false, MODE>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
+                     resid);
 }
 
-// fp32 rows: MDFX_WTK_NAT = 2 (default) natural pair layout (RowOpsN) with the plane loop unrolled
-// by two; 1 the same without the unroll; 0 round 2's regrouped layout (RowOps<float>). fp64 has one
-// layout (mode 0)
+// fp32 rows: the natural pair layout (RowOpsN) with the plane loop unrolled by two (mode 2); the
+// 3-row residual sweeps without the unroll (mode 1: the unrolled residual instance spills). fp64:
+// one layout (mode 0). (Round 2's regrouped fp32 layout, mode 0, measured slower and was removed
+// in round 4: 1.985 vs 1.736 ms per 3-step sweep, profiles/r03_pmc/.)
 template <class T, int RY, int K, int WB>
 static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if constexpr (sizeof(T) == 4) {
-    if (resid && RY == 3 && knobs().wtk_nat != 0) {  // the spill-free 3-row residual instance
-      launch_wtk_kn<T, RY, K, WB, 1>(g, in, out, r, resid, s);
-      return;
-    }
-    if (knobs().wtk_nat == 2) {
-      launch_wtk_kn<T, RY, K, WB, 2>(g, in, out, r, resid, s);
-      return;
-    }
-    if (knobs().wtk_nat == 1) {
-      launch_wtk_kn<T, RY, K, WB, 1>(g, in, out, r, resid, s);
-      return;
-    }
+    if (resid && RY == 3) launch_wtk_kn<T, RY, K, WB, 1>(g, in, out, r, resid, s);
+    else launch_wtk_kn<T, RY, K, WB, 2>(g, in, out, r, resid, s);
+  } else {
+    launch_wtk_kn<T, RY, K, WB, 0>(g, in, out, r, resid, s);
   }
-  launch_wtk_kn<T, RY, K, WB, 0>(g, in, out, r, resid, s);
 }
 
 bool heat7_wtk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -411,18 +338,13 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
              "heat7_wtk: row / plane counts must fit 32-bit indices");
   // bands of 8 waves (one 512-thread block per CU) only for deep regions: 1024^3 1632-1674 vs
   // 1593-1612 GCells/s for bands of 4, but on 128..512-plane slabs the few large blocks leave CUs
-  // idle (8 slabs of 128 planes: 1188-1223 vs 1347-1385). Residual sweeps run the same band shape
-  // as plain ones (round 2 forced 2-row bands of 4 waves on them: MDFX_WTK_RES_SHAPE=1)
-  const bool old_res = resid && knobs().wtk_res_shape == 1;
+  // idle (8 slabs of 128 planes: 1188-1223 vs 1347-1385); MDFX_WTK_WB = 4 / 8 forces one
   int wb = knobs().wtk_wb;
-  if (wb != 4 && wb != 8) wb = (g.lz_end - g.lz_begin >= 768 && !old_res) ? 8 : 4;
-  if (old_res) wb = 4;
+  if (wb != 4 && wb != 8) wb = g.lz_end - g.lz_begin >= 768 ? 8 : 4;
   // rows per wave at K = 3: fp32 3 (1024^3: 1679 vs 1447 GCells/s for 2 rows); fp64 2 in bands of
   // 4 (3 rows need more than 256 VGPRs there), see below for bands of 8
   constexpr int RY3 = sizeof(T) == 4 ? 3 : 2;
-  if (steps == 3 && old_res) {
-    launch_wtk_k<T, 2, 3, 4>(g, in, out, r, resid, s);
-  } else if (steps == 3) {
+  if (steps == 3) {
     if (wb == 8) {
       // fp64 8-wave bands: 3 rows per wave at rows up to 1024 cells (1024^3 923-925 vs 849-852
       // GCells/s), 2 rows on wider rows (2048^3 835 vs 802); MDFX_WTK_RY8 = 2 / 3 forces

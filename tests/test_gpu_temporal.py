@@ -77,13 +77,12 @@ BOX27 = [models.box27(nx=1024, ny=11, nz=9), models.box27(nx=512, ny=21, nz=15),
 
 
 @pytest.mark.parametrize("prob", BOX27, ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("kernel", ["-1", "-1n", "1", "2", "4"])
+@pytest.mark.parametrize("kernel", ["-1", "1", "2", "4"])
 def test_box27_fused_kernels_bitwise(hip, prob, kernel, knob):
     """Both fused 27-point kernels (MDFX_B27_TBK=-1: box27_tb2, fp32 in the natural layout with
-    the 2-plane unroll (box27_tb2n) or, -1n here, round 2's pair layout; 1 / 2 / 4: box27_tbk with
-    that many rows per tile) == two naive single steps, bitwise, with the residual of step 2."""
-    knob("MDFX_B27_TBK", kernel.rstrip("n"))
-    knob("MDFX_B27_NAT", "0" if kernel.endswith("n") else "1")
+    the 2-plane unroll (box27_tb2n); 1 / 2 / 4: box27_tbk with that many rows per tile) == two
+    naive single steps, bitwise, with the residual of step 2."""
+    knob("MDFX_B27_TBK", kernel)
     lay = FieldLayout.make(prob, halo=2)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -439,14 +438,14 @@ WTK3D = DEEP3D + [models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, n
 
 
 @pytest.mark.parametrize("prob", WTK3D, ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("k,wb,split", [(3, "4", "-1"), (3, "8", "-1"), (4, "4", "-1"), (3, "4", "1"), (3, "8", "1")])
+@pytest.mark.parametrize("k,wb", [(3, "4"), (3, "8"), (4, "4")])
 @pytest.mark.parametrize("resid", [False, True])
-def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
-    """heat7_wtk's K fused steps (the default 3D 7-point kernel for K >= 3) == K naive single
-    steps, bitwise, with or without the residual of step K, in bands of 4 or 8 waves, under the
-    chunked and the balanced one-round (MDFX_WTK_SPLIT=1) schedules."""
+def test_heat7_wtk_bitwise(hip, prob, k, wb, resid, knob):
+    """heat7_wtk's K fused steps (the 3D 7-point kernel for K >= 3 where heat7_wxk does not run:
+    fp64 rows below 2048 cells, MDFX_H7_WXK=0) == K naive single steps, bitwise, with or without the
+    residual of step K, in bands of 4 or 8 waves."""
+    knob("MDFX_H7_WXK", 0)
     knob("MDFX_WTK_WB", wb)
-    knob("MDFX_WTK_SPLIT", split)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -467,7 +466,7 @@ def test_heat7_wtk_bitwise(hip, prob, k, wb, split, resid, knob):
         set_kernel_variant("auto")
     torch.cuda.synchronize()
     o = lay.owned
-    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb, split)
+    assert torch.equal(fused[o, :, :lay.nx], cur[o, :, :lay.nx]), (k, wb)
     if resid:
         assert res.item() > 0 and abs(res.item() - ref_res.item()) <= 1e-9 * ref_res.item()
 
@@ -544,12 +543,9 @@ B27X = [models.box27(n=40), models.box27(n=24, dtype="f64"), models.box27(nx=700
 
 @pytest.mark.parametrize("prob", B27X, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("resid", [False, True])
-@pytest.mark.parametrize("wxp", ["0", "1"])
-def test_box27_wxk_bitwise(hip, prob, resid, wxp, knob):
+def test_box27_wxk_bitwise(hip, prob, resid):
     """box27_wxk (27-point, K = 3, y halo exchanged through the LDS seam table, levels above the
-    first one plane later) == 3 naive box27 steps, bitwise, with the residual of step 3; with
-    MDFX_B27_WXP = 1 the fp32 rows of 257..512 cells run the x-pair kernel box27_wxp."""
-    knob("MDFX_B27_WXP", wxp)
+    first one plane later) == 3 naive box27 steps, bitwise, with the residual of step 3."""
     k = 3
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
@@ -575,12 +571,9 @@ def test_box27_wxk_bitwise(hip, prob, resid, wxp, knob):
 
 
 @pytest.mark.parametrize("nx", [600, 480])
-@pytest.mark.parametrize("wxp", ["0", "1"])
-def test_box27_wxk_regions_and_engine(hip, knob, nx, wxp):
+def test_box27_wxk_regions_and_engine(hip, knob, nx):
     """box27_wxk on a middle slab (both boundary regions in one launch + the interior) == the
-    whole grid, and a 3-slab engine run at the 27-point's fused depth 3 == single steps (480-cell
-    rows and MDFX_B27_WXP = 1: the x-pair kernel)."""
-    knob("MDFX_B27_WXP", wxp)
+    whole grid, and a 3-slab engine run at the 27-point's fused depth 3 == single steps."""
     k = 3
     prob = models.box27(nx=nx, ny=30, nz=40)
     full = FieldLayout.make(prob, halo=k)
@@ -680,9 +673,11 @@ def test_heat7_wtk_regions_on_a_slab(hip, k):
     assert res2.item() > 0 and abs(res2.item() - res1.item()) <= 1e-9 * res1.item()
 
 
-@pytest.mark.parametrize("k,ranks,split", [(3, 1, "0"), (3, 3, "0"), (4, 2, "0"), (3, 1, "1"), (3, 3, "1")])
-def test_engine_wtk_temporal_3d(hip, k, ranks, split, knob):
-    knob("MDFX_WTK_SPLIT", split)
+@pytest.mark.parametrize("k,ranks,wxk", [(3, 1, "-1"), (3, 3, "-1"), (4, 2, "-1"), (3, 3, "0"), (4, 2, "0")])
+def test_engine_wtk_temporal_3d(hip, k, ranks, wxk, knob):
+    """The engine's K-step sweeps (heat7_wxk by default, heat7_wtk with MDFX_H7_WXK=0) over 1-3
+    slabs with a residual every 10 steps == single steps."""
+    knob("MDFX_H7_WXK", wxk)
     prob = mm.heat3d(nx=1024, ny=24, nz=60)
     ref, rr = _sim(prob, 23, ranks=1, temporal=1, residual_every=10)
     got, rg = _sim(prob, 23, ranks=ranks, temporal=k, residual_every=10)

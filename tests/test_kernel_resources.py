@@ -60,11 +60,11 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false>", 2),
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true>", 2),
     ("mdfx::dev::box27_tb2n<1, 1, false>", 3),                          # 27-point K = 2 fp32 (512^3)
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 2, false>", 2),       # K = 3 where heat7_wxk does not run
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 2, false>", 2),       # (thin slabs: 4-wave bands)
-    ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0, false>", 2),
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 2>", 2),       # K = 3 where heat7_wxk does not run
+    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 2>", 2),       # (thin slabs: 4-wave bands)
+    ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0>", 2),
     ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 2>", 3),           # 2D MDF, 8 steps per sweep
-    ("mdfx::dev::jacobi5_tbk<float, 8, false, true, 2>", 2),            # reference precision
+    ("mdfx::dev::jacobi5_tbk<float, 8, false, true, 1>", 4),            # reference precision (no unroll)
     ("mdfx::dev::heat7_tbk<float, 4, 2, 4, false>", 2),                 # K = 2 fused sweep
     ("mdfx::dev::heat7_tbk<double, 4, 2, 4, false>", 2),
     ("mdfx::dev::heat7_tb2<float, 2, 4, false, 1, true>", 3),           # x-tiled rows
