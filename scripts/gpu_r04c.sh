@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round 4 session C: the round-3 tree (ab_alt/, commit 791b0ce) against this tree on one box
+# Round 4 session C: the whole GPU test tier on the pruned tree; the round-3 tree (ab_alt/, commit 791b0ce) against this tree on one box
 # (headline bench and N = 8 / 4 proxies, interleaved); the graph-replay regression test; the
 # driver's N = 8 path rehearsed with 8 processes sharing the GPU (full gate / trial flow).
 set -o pipefail
 cd "$(dirname "$0")/.."
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-scripts/gpu_session.sh "graph_t=$PYT tests/test_gpu_proxy.py -k replayed" || exit $?
+LIMIT=700 scripts/gpu_session.sh "gputests=python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests" || exit $?
+grep -q " passed" gpurun_out/gputests.log && ! grep -q "failed" gpurun_out/gputests.log || { tail -40 gpurun_out/gputests.log; exit 1; }
 B="--steps 20 --warmup 5"
 P8="--rank-proxy 8 --steps 48 --warmup 5"
 P4="--rank-proxy 4 --steps 48 --warmup 5"
