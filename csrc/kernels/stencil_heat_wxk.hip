@@ -57,9 +57,14 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 
-template <class T, int RY, int RE, int K, int WB, bool RES>
+// DG: a diagnostic copy (MDFX_WXK_DIAG, timing only, results are garbage) whose `diag` bits drop
+// parts of the sweep to see where its time goes: 1 the window DMAs after the first plane, 2 the
+// output stores, 4 the per-plane barrier
+template <class T, int RY, int RE, int K, int WB, bool RES, bool DG = false>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
+                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
+                                                     int diag = 0) {
+  const int dg = DG ? diag : 0;
   using V = typename VT<T>::type;
   using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
@@ -113,7 +118,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // block-uniform: every row the band computes at any level is y-interior, so no wave needs the
   // per-row held test (bands at y = 0 / ny-1 run the tested copy, all their waves together)
   const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
-  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(rown, ny - y0)) : 0;
+  const int nsto = (__builtin_amdgcn_ballot_w64(own) != 0 && !(dg & 2)) ? max(0, min(rown, ny - y0)) : 0;
   int nst = 0;  // output stores issued since this wave's last DMA
 
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
@@ -180,8 +185,9 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // publishes it and last step's seam rows, and certifies that every wave is done with the
       // other window buffer and the other seam parity
       wait_vm_le(nst);
-      lds_barrier();
-      if (q < qlast) issue(q + 1, P ^ 1);
+      if (!(dg & 4)) lds_barrier();
+      else wait_lgkm0();
+      if (q < qlast && !(dg & 1)) issue(q + 1, P ^ 1);
       constexpr int SR = P ^ 1;  // seam parity read this step
       // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact)
       Row rl[K + 1];
@@ -239,7 +245,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
 #pragma unroll
         for (int j = 1; j <= K; ++j) {
           if (j == K) {  // the sweep's output row
-            if (valid && i >= 0 && i < SH::R && y0 + i < ny && own) {
+            if (valid && i >= 0 && i < SH::R && y0 + i < ny && own && !(dg & 2)) {
               T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
               dcheck(g, (const T*)out, a, N);
               store_nt((V*)a, RO::vec(cur));
@@ -328,11 +334,18 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   if (resid) {
-    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, 0);
     return;
   }
+  if constexpr (sizeof(T) == 4 && RY == 3 && RE == 2 && K == 4 && WB == 8) {  // the headline shape only
+    if (knobs().wxk_diag) {
+      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT,
+                         (int)ntasks, resid, knobs().wxk_diag);
+      return;
+    }
+  }
   hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
-                     resid);
+                     resid, 0);
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }

@@ -51,11 +51,11 @@ def test_lds_never_limits_occupancy(recs):
 @pytest.mark.parametrize("name,min_waves", [
     # the shipped headline sweep: 1024^3 fp32, 4 fused steps, 3 + 2-row bands of 8 waves (one 512-thread
     # block per CU: 2 waves per SIMD is all a block of 8 waves can have)
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false>", 2),
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true>", 2),         # its residual sweeps
-    ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false>", 2),        # K = 3 (step-count remainders)
-    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false>", 2),       # fp64 K = 3 (2048^3 + residual)
-    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false>", 2),         # its residual sweeps
+    ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false, false>", 2),        # K = 3 (step-count remainders)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false, false>", 2),       # fp64 K = 3 (2048^3 + residual)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true, false>", 2),
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false>", 2),              # 27-point K = 3 (1024-cell rows, fp64)
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false>", 2),
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true>", 2),
