@@ -85,7 +85,9 @@ def parse(argv=None):
                         "MDF) / 12 (Life)")
     p.add_argument("--ref-precision", action="store_true",
                    help="jacobi5: the reference program's mixed fp32/fp64 update (MDF_kernel.cu:20)")
-    p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--no-overlap", action="store_true", help="one full sweep after the exchange (no trial)")
+    p.add_argument("--overlap", action="store_true",
+                   help="only the overlapped schedule (interior || boundary + exchange; no trial)")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
     p.add_argument("--device", default="auto", choices=["auto", "hip", "cpu"])
@@ -281,7 +283,7 @@ def run_proxy(a):
     prob = make_problem(a, nx, ny, nz)
     temporal = pick_temporal(a, prob, max(1, n), True)
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True])
-    overlaps = [True, False] if (n > 1 and not a.no_overlap) else [not a.no_overlap]
+    overlaps = [True, False] if (n > 1 and not a.no_overlap and not a.overlap) else [not a.no_overlap]
     rounds = [int(a.rounds)] if a.rounds != "auto" else ([2, 1] if n > 1 else [0])
     sdma = a.transport in ("ipc_sdma", "proxy_sdma")
     sim = Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graphs[0],
@@ -466,7 +468,7 @@ def main(argv=None):
     # the round count and the overlap mode need no gate of their own (scheduling only; the
     # overlapped == serialised equality is a test). Several processes: interior || boundary +
     # exchange (overlap) against one full sweep after the exchange, whichever the trial finds faster.
-    overlaps = [True, False] if (hip and env and world > 1 and not a.no_overlap) else [not a.no_overlap]
+    overlaps = [True, False] if (hip and env and world > 1 and not a.no_overlap and not a.overlap) else [not a.no_overlap]
     cands = [(t, g, r, ov) for t, g in cands for r in rounds for ov in overlaps]
     kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap,
               residual_every=a.residual_every, timeout_s=timeout, temporal=temporal)
