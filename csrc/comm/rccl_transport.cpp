@@ -86,6 +86,7 @@ class RcclTransport final : public Transport {
   // other rank abort its half-built communicator and fail with a message instead of blocking in
   // ncclCommInitRank forever (the reference's D4 hang class starts at its MPI_Init / first send).
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
+    require_slabs(locals, "rccl");
     locals_ = locals;
     nranks_ = nranks;
     comms_.assign(locals_.size(), nullptr);

@@ -233,6 +233,7 @@ class TcpTransport final : public Transport {
   const char* name() const override { return "tcp"; }
   bool in_process_only() const override { return false; }
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
+    require_slabs(locals, "tcp");
     MDFX_CHECK(locals.size() == 1, "tcp transport: one slab per process");
     MDFX_CHECK(locals[0].be->kind() == DeviceKind::CPU, "tcp transport carries host memory (CPU backend)");
     MDFX_CHECK(nranks == rv_.world() && locals[0].rank == rv_.rank(), "tcp transport: slab index = process rank");

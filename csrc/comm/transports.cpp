@@ -30,13 +30,15 @@ class InProcessBase : public Transport {
     by_rank_.clear();
     for (size_t i = 0; i < locals_.size(); ++i) by_rank_[locals_[i].rank] = (int)i;
     for (auto& s : locals_)
-      for (int side = 0; side < 2; ++side) {
+      for (int side = 0; side < 4; ++side) {
         const HaloSpan h = halo_span(s, 0, side, nranks_);
         MDFX_CHECK(h.peer < 0 || by_rank_.count(h.peer),
                    format("%s transport needs every rank in this process (rank %d has remote neighbour %d)",
                           name(), s.rank, h.peer));
       }
   }
+  // the face across `side` seen from the neighbour (0 <-> 1, 2 <-> 3)
+  static int opposite(int side) { return side ^ 1; }
   double allreduce_sum(double v) override { return v; }
   double allreduce_max(double v) override { return v; }
   void barrier() override {}
@@ -57,13 +59,16 @@ class HostTransport final : public InProcessBase {
     for (auto& s : locals_) MDFX_CHECK(s.be->kind() == DeviceKind::CPU, "host transport needs CPU backends");
   }
   void exchange(int b) override {
-    for (auto& q : locals_)
-      for (int side = 0; side < 2; ++side) {
-        const HaloSpan hq = halo_span(q, b, side, nranks_);
-        if (hq.peer < 0) continue;
-        const HaloSpan hp = halo_span(peer_slab(hq.peer), b, 1 - side, nranks_);
-        std::memcpy(hq.recv, hp.send, hq.bytes);
-      }
+    // y faces first (pencils), then the z faces, which then carry the fresh y ghosts (corners)
+    for (int phase = 0; phase < 2; ++phase)
+      for (auto& q : locals_)
+        for (int side = phase == 0 ? 2 : 0; side < (phase == 0 ? 4 : 2); ++side) {
+          const HaloSpan hq = halo_span(q, b, side, nranks_);
+          if (hq.peer < 0) continue;
+          const HaloSpan hp = halo_span(peer_slab(hq.peer), b, opposite(side), nranks_);
+          for (size_t i = 0; i < hq.height; ++i)
+            std::memcpy((char*)hq.recv + i * hq.stride, (const char*)hp.send + i * hp.stride, hq.width);
+        }
   }
 };
 
@@ -71,6 +76,7 @@ class LoopbackTransport final : public InProcessBase {
  public:
   ~LoopbackTransport() override {
     for (size_t i = 0; i < ev_.size(); ++i) locals_[i].be->destroy_event(ev_[i]);
+    for (size_t i = 0; i < ev_y_.size(); ++i) locals_[i].be->destroy_event(ev_y_[i]);
   }
   const char* name() const override { return "loopback"; }
   bool graph_capturable() const override { return true; }
@@ -79,10 +85,11 @@ class LoopbackTransport final : public InProcessBase {
     for (auto& s : locals_) {
       MDFX_CHECK(s.be->kind() == DeviceKind::HIP, "loopback transport needs HIP backends");
       ev_.push_back(s.be->create_event());
+      ev_y_.push_back(s.be->create_event());
     }
     // enable peer access between distinct devices that neighbour each other
     for (auto& s : locals_)
-      for (int side = 0; side < 2; ++side) {
+      for (int side = 0; side < 4; ++side) {
         const HaloSpan h = halo_span(s, 0, side, nranks_);
         if (h.peer < 0) continue;
         const int pd = peer_slab(h.peer).be->device();
@@ -99,28 +106,52 @@ class LoopbackTransport final : public InProcessBase {
       }
   }
   void exchange(int b) override {
-    // pull: each receiver waits for its neighbour's boundary kernel, then copies the face
+    // pull: each receiver waits for its neighbour's boundary kernels, then copies the face. A
+    // pencil pulls its y faces first; its z pulls then wait for the z neighbour's y pulls (ev_y_),
+    // so the z faces carry fresh y ghosts into the corners
+    bool pencil = false;
+    for (auto& s : locals_) pencil = pencil || (s.py > 1 && s.lay.hy > 0);
+    auto pull = [&](const LocalSlab& q, const HaloSpan& hq, const LocalSlab& p, const HaloSpan& hp) {
+      q.be->activate();
+      hipStream_t hs = (hipStream_t)q.halo_stream;
+      if (hq.height <= 1) {
+        if (p.be->device() == q.be->device())
+          HIPC(hipMemcpyAsync(hq.recv, hp.send, hq.bytes, hipMemcpyDeviceToDevice, hs));
+        else
+          HIPC(hipMemcpyPeerAsync(hq.recv, q.be->device(), hp.send, p.be->device(), hq.bytes, hs));
+      } else {
+        HIPC(hipMemcpy2DAsync(hq.recv, hq.stride, hp.send, hp.stride, hq.width, hq.height, hipMemcpyDeviceToDevice, hs));
+      }
+    };
+    if (pencil) {
+      for (size_t i = 0; i < locals_.size(); ++i) {
+        const LocalSlab& q = locals_[i];
+        for (int side = 2; side < 4; ++side) {
+          const HaloSpan hq = halo_span(q, b, side, nranks_);
+          if (hq.peer < 0) continue;
+          const LocalSlab& p = peer_slab(hq.peer);
+          q.be->wait(q.halo_stream, p.bnd_event);
+          pull(q, hq, p, halo_span(p, b, opposite(side), nranks_));
+        }
+        q.be->record(ev_y_[i], q.halo_stream);
+      }
+    }
     for (size_t i = 0; i < locals_.size(); ++i) {
       const LocalSlab& q = locals_[i];
       for (int side = 0; side < 2; ++side) {
         const HaloSpan hq = halo_span(q, b, side, nranks_);
         if (hq.peer < 0) continue;
         const LocalSlab& p = peer_slab(hq.peer);
-        const HaloSpan hp = halo_span(p, b, 1 - side, nranks_);
-        q.be->wait(q.halo_stream, p.bnd_event);
-        q.be->activate();
-        if (p.be->device() == q.be->device())
-          HIPC(hipMemcpyAsync(hq.recv, hp.send, hq.bytes, hipMemcpyDeviceToDevice, (hipStream_t)q.halo_stream));
-        else
-          HIPC(hipMemcpyPeerAsync(hq.recv, q.be->device(), hp.send, p.be->device(), hq.bytes,
-                                  (hipStream_t)q.halo_stream));
+        q.be->wait(q.halo_stream, pencil ? ev_y_[by_rank_.at(hq.peer)] : p.bnd_event);
+        pull(q, hq, p, halo_span(p, b, opposite(side), nranks_));
       }
       q.be->record(ev_[i], q.halo_stream);
     }
-    // a sender may not overwrite its faces until its neighbours have pulled them
+    // a sender may not overwrite its faces (or, a pencil, its y ghosts its z faces carry) until its
+    // neighbours have pulled them
     for (size_t i = 0; i < locals_.size(); ++i) {
       const LocalSlab& p = locals_[i];
-      for (int side = 0; side < 2; ++side) {
+      for (int side = 0; side < 4; ++side) {
         const HaloSpan hp = halo_span(p, b, side, nranks_);
         if (hp.peer < 0) continue;
         p.be->wait(p.halo_stream, ev_[by_rank_.at(hp.peer)]);
@@ -129,14 +160,15 @@ class LoopbackTransport final : public InProcessBase {
   }
 
  private:
-  std::vector<void*> ev_;
+  std::vector<void*> ev_;    // a receiver's pulls of this exchange are done
+  std::vector<void*> ev_y_;  // a receiver's y pulls are done (pencils)
 };
 
 class CallbackTransport final : public Transport {
  public:
   explicit CallbackTransport(CallbackFns f) : f_(std::move(f)) {}
   const char* name() const override { return "callback"; }
-  void setup(const std::vector<LocalSlab>&, int) override {}
+  void setup(const std::vector<LocalSlab>& locals, int) override { require_slabs(locals, "callback / torch"); }
   void exchange(int b) override {
     if (f_.exchange) f_.exchange(b);
   }

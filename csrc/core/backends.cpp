@@ -6,6 +6,7 @@
 // the missing cudaSetDevice (D13): a HIP backend is bound to one device ordinal.
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <dlfcn.h>
@@ -207,17 +208,47 @@ HaloSpan halo_span(const LocalSlab& s, int b, int side, int nranks) {
   const FieldLayout& l = s.lay;
   const size_t pb = l.plane_bytes();
   char* base = (char*)s.buf[b];
-  h.bytes = (size_t)l.halo * pb;
-  if (side == 0) {
-    h.peer = s.rank > 0 ? s.rank - 1 : -1;
-    h.send = base + (size_t)l.halo * pb;  // first owned planes
-    h.recv = base;                          // lower ghosts
+  const int py = std::max(1, s.py);
+  if (side < 2) {
+    h.bytes = h.width = (size_t)l.halo * pb;
+    h.stride = h.width;
+    if (side == 0) {
+      h.peer = s.rank - py >= 0 ? s.rank - py : -1;
+      h.send = base + (size_t)l.halo * pb;  // first owned planes
+      h.recv = base;                          // lower ghosts
+    } else {
+      h.peer = s.rank + py < nranks ? s.rank + py : -1;
+      h.send = base + (size_t)l.nzl() * pb;                // last `halo` owned planes
+      h.recv = base + (size_t)(l.halo + l.nzl()) * pb;     // upper ghosts
+    }
+    return h;
+  }
+  // y faces: hy rows of every owned plane
+  if (py <= 1 || l.hy == 0) return h;
+  const int ry = s.rank % py;
+  const size_t es = l.esize(), rowb = (size_t)l.pitch * es;
+  h.width = (size_t)l.hy * rowb;
+  h.height = (size_t)l.nzl();
+  h.stride = pb;
+  h.bytes = h.width * h.height;
+  char* p0 = base + (size_t)l.halo * pb;  // first owned plane
+  if (side == 2) {
+    h.peer = ry > 0 ? s.rank - 1 : -1;
+    h.send = p0 + (size_t)l.hy * rowb;  // first owned rows
+    h.recv = p0;                          // lower ghost rows
   } else {
-    h.peer = s.rank + 1 < nranks ? s.rank + 1 : -1;
-    h.send = base + (size_t)l.nzl() * pb;                // last `halo` owned planes
-    h.recv = base + (size_t)(l.halo + l.nzl()) * pb;     // upper ghosts
+    h.peer = ry + 1 < py ? s.rank + 1 : -1;
+    h.send = p0 + (size_t)l.nyl() * rowb;              // last `hy` owned rows
+    h.recv = p0 + (size_t)(l.hy + l.nyl()) * rowb;     // upper ghost rows
   }
   return h;
+}
+
+void require_slabs(const std::vector<LocalSlab>& locals, const char* transport) {
+  for (const LocalSlab& s : locals)
+    MDFX_CHECK(s.py <= 1 && s.lay.hy == 0,
+               format("the %s transport exchanges z faces only; a pencil decomposition (y split) needs the "
+                      "loopback, host, proxy or ipc transport", transport));
 }
 
 }  // namespace mdfx

@@ -90,19 +90,25 @@ StencilKind stencil_from_name(const std::string& s) {
   MDFX_FAIL("unknown stencil '" + s + "' (5|7|27|life)");
 }
 
-FieldLayout FieldLayout::make(Extent3 g, int64_t z0, int64_t z1, int halo, DType dt) {
+FieldLayout FieldLayout::make(Extent3 g, int64_t z0, int64_t z1, int halo, DType dt, int64_t y0, int64_t y1, int hy) {
   MDFX_CHECK(g.nx >= 1 && g.ny >= 1 && g.nz >= 1, "grid extents must be positive");
   MDFX_CHECK(0 <= z0 && z0 <= z1 && z1 <= g.nz, "owned plane range out of the grid");
   MDFX_CHECK(halo >= 1, "halo must be >= 1");
+  if (y1 < 0) y1 = g.ny;
+  MDFX_CHECK(0 <= y0 && y0 < y1 && y1 <= g.ny, "owned row range out of the grid");
+  MDFX_CHECK(hy >= 0 && (hy == 0 || g.ny > 1), "ghost rows need a 3D grid");
   FieldLayout l;
   l.global = g;
   l.z0 = z0;
   l.z1 = z1;
   l.halo = halo;
+  l.y0 = y0;
+  l.y1 = y1;
+  l.hy = hy;
   l.dtype = dt;
   const int64_t align = kRowAlignBytes / (int64_t)dtype_size(dt);
   l.pitch = (g.nx + align - 1) / align * align;
-  l.plane = l.pitch * g.ny;
+  l.plane = l.pitch * l.rows();
   return l;
 }
 

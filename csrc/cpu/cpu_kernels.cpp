@@ -4,6 +4,7 @@
 // Reference parity: MDF_kernel.cu:10-22 / kernel.cu:10-68 (point updates), create_universe
 // MDF_kernel.cu:88-99 / kernel.cu:131-146 (initial grids). This is also the CPU reference path
 // of BASELINE.json config 1 (2D 5-pt Laplace 256x256 fp32, single rank).
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +41,8 @@ void cpu_stencil(const StencilSpec& spec, const RegionArgs& a) {
   if (a.lz_end <= a.lz_begin) return;
   MDFX_CHECK(a.lz_begin >= a.lay.halo && a.lz_end <= a.lay.halo + a.lay.nzl(),
              "region must lie inside the owned planes");
+  MDFX_CHECK(a.ly_end <= a.ly_begin || (a.ly_begin >= a.lay.hy && a.ly_end <= a.lay.hy + a.lay.nyl()),
+             "row range must lie inside the owned rows");
   if (a.steps == 1) {
     cpu_region(spec, a);
     return;
@@ -52,12 +55,17 @@ void cpu_stencil(const StencilSpec& spec, const RegionArgs& a) {
   tmp[0].assign(a.lay.bytes(), 0);
   tmp[1].assign(a.lay.bytes(), 0);
   std::memcpy(tmp[0].data(), a.in, a.lay.bytes());
+  const int64_t yb = a.ly_end > a.ly_begin ? a.ly_begin : a.lay.hy, ye = a.ly_end > a.ly_begin ? a.ly_end : a.lay.hy + a.lay.nyl();
   for (int s = 1; s <= k; ++s) {
     RegionArgs b = a;
     b.in = tmp[(s - 1) & 1].data();
     b.out = s == k ? a.out : (void*)tmp[s & 1].data();
     b.lz_begin = a.lz_begin - (k - s);
     b.lz_end = a.lz_end + (k - s);
+    // the rows the later steps read, as far as the layout holds them (a pencil's ghost rows;
+    // global boundary rows are held, so a slab needs no widening)
+    b.ly_begin = std::max<int64_t>(yb - (k - s), a.lay.hy > 0 ? 1 : 0);
+    b.ly_end = std::min<int64_t>(ye + (k - s), a.lay.hy > 0 ? a.lay.rows() - 1 : a.lay.rows());
     b.resid = s == k ? a.resid : nullptr;
     if (s < k) std::memcpy(tmp[s & 1].data(), tmp[(s - 1) & 1].data(), a.lay.bytes());
     cpu_region(spec, b);
@@ -86,11 +94,12 @@ static void init_cpu_t(const InitSpec& s, const FieldLayout& l, T* buf) {
     for (int64_t y = 0; y < g.ny; ++y)
       for (int64_t x = 0; x < g.pitch; ++x) {
         double v = 0.0;
-        if (x < g.nx && gz >= 0 && gz < g.gnz) {
+        const int64_t gy = y + g.gy_off;  // (ghost rows beyond the grid stay 0, as ghost planes)
+        if (x < g.nx && gz >= 0 && gz < g.gnz && gy >= 0 && gy < g.gny) {
           const bool bnd = x == 0 || x == g.nx - 1 || gz == 0 || gz == g.gnz - 1 ||
-                           (dims == 3 && (y == 0 || y == g.ny - 1));
+                           (dims == 3 && (gy == 0 || gy == g.gny - 1));
           const uint64_t gidx =
-              (uint64_t)x + (uint64_t)g.nx * ((uint64_t)y + (uint64_t)g.ny * (uint64_t)gz);
+              (uint64_t)x + (uint64_t)g.nx * ((uint64_t)gy + (uint64_t)g.gny * (uint64_t)gz);
           switch (s.kind) {
             case InitKind::Constant: v = s.value; break;
             case InitKind::Dirichlet: v = bnd ? s.edge : s.interior; break;

@@ -30,8 +30,7 @@ namespace mdfx {
 Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<int> local_ranks,
                std::vector<std::unique_ptr<Backend>> backends, std::unique_ptr<Transport> transport,
                SolverOptions opt)
-    : spec_(spec), global_(global), nranks_(nranks), decomp_(global.nz, nranks),
-      transport_(std::move(transport)), opt_(opt) {
+    : spec_(spec), global_(global), nranks_(nranks), transport_(std::move(transport)), opt_(opt) {
   MDFX_CHECK(!local_ranks.empty(), "a process must own at least one slab");
   MDFX_CHECK(local_ranks.size() == backends.size(), "one backend per local slab");
   MDFX_CHECK(transport_ != nullptr, "transport required");
@@ -43,6 +42,10 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   if (spec_.kind != StencilKind::Life)
     MDFX_CHECK(spec_.dtype == DType::F32 || spec_.dtype == DType::F64, "stencil dtype must be f32 or f64");
   MDFX_CHECK(opt_.temporal >= 1 && opt_.temporal <= 16, "temporal blocking depth must be 1..16");
+  MDFX_CHECK(opt_.py >= 1 && nranks % opt_.py == 0,
+             format("%d ranks do not form a grid of pencils with %d along y", nranks, opt_.py));
+  MDFX_CHECK(opt_.py == 1 || !stencil_is_2d(spec_.kind), "pencil decompositions split 3D grids (y); 2D grids split rows");
+  decomp_ = PencilDecomposition(global_, nranks / opt_.py, opt_.py);
   // several slabs: leave room in each interior sweep for the halo exchange's kernels
   if (!backends.empty() && backends[0]->kind() == DeviceKind::HIP) {
     // a fresh engine starts with the device waits armed (a poisoned predecessor may have raised them)
@@ -56,9 +59,14 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     Slab s;
     s.rank = r;
     s.be = std::move(backends[i]);
-    s.lay = FieldLayout::make(global_, decomp_.z0(r), decomp_.z1(r), halo, spec_.dtype);
+    const int rz = decomp_.rz(r), ry = decomp_.ry(r);
+    s.lay = FieldLayout::make(global_, decomp_.z.z0(rz), decomp_.z.z1(rz), halo, spec_.dtype, decomp_.y.z0(ry),
+                              decomp_.y.z1(ry), opt_.py > 1 ? halo : 0);
     MDFX_CHECK(s.lay.nzl() >= 1, "every slab needs at least one plane");
-    MDFX_CHECK(nranks == 1 || s.lay.nzl() >= halo,
+    MDFX_CHECK(opt_.py == 1 || s.lay.nyl() >= halo,
+               format("pencil %d has %lld rows, fewer than the %d ghost rows temporal blocking exchanges", r,
+                      (long long)s.lay.nyl(), halo));
+    MDFX_CHECK(decomp_.pz() == 1 || s.lay.nzl() >= halo,
                format("slab %d has %lld planes, fewer than the %d ghost planes temporal blocking exchanges "
                       "(use a smaller --temporal or fewer ranks)",
                       r, (long long)s.lay.nzl(), halo));
@@ -87,13 +95,24 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     // planes at each end that the exchange sends: they are computed on the halo stream so the
     // exchange can follow them in stream order; everything else is interior.
     const int64_t ob = halo, oe = halo + s.lay.nzl();
-    const bool has_lo = r > 0, has_hi = r + 1 < nranks;
+    const bool has_lo = decomp_.neighbor(r, 0) >= 0, has_hi = decomp_.neighbor(r, 1) >= 0;
     s.lo_b = ob;
     s.lo_e = has_lo ? std::min(ob + halo, oe) : ob;
     s.hi_e = oe;
     s.hi_b = has_hi ? std::max(oe - halo, s.lo_e) : oe;
     s.in_b = s.lo_e;
     s.in_e = s.hi_b;
+    if (opt_.py > 1) {
+      // the interior planes' rows next to a y neighbour are boundary strips too (the exchange
+      // sends them); the rest is interior
+      const int64_t yb = s.lay.hy, ye = s.lay.hy + s.lay.nyl();
+      s.ylo_b = yb;
+      s.ylo_e = decomp_.neighbor(r, 2) >= 0 ? std::min(yb + halo, ye) : yb;
+      s.yhi_e = ye;
+      s.yhi_b = decomp_.neighbor(r, 3) >= 0 ? std::max(ye - halo, s.ylo_e) : ye;
+      s.yin_b = s.ylo_e;
+      s.yin_e = s.yhi_b;
+    }
     slabs_.push_back(std::move(s));
   }
   for (auto& s : slabs_) s.be->sync_device();
@@ -105,6 +124,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
   for (auto& s : slabs_) {
     LocalSlab l;
     l.rank = s.rank;
+    l.py = opt_.py;
     l.be = s.be.get();
     l.halo_stream = s.hs;
     l.bnd_event = s.ev_bnd;
@@ -275,6 +295,53 @@ bool Solver::boundary_on_cs() const {
   return opt_.overlap && slabs_.size() == 1 && transport_->graph_capturable();
 }
 
+// The boundary regions of a step: the `halo` planes at each z face with a neighbour (all owned
+// rows), and for a pencil the `halo` rows at each y face with a neighbour (interior planes).
+// Everything the exchange sends is written here.
+void Solver::boundary_kernels(Slab& s, RegionArgs a, void* stream) {
+  if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
+    // both z boundary regions in one call (one launch where the kernel supports it)
+    a.lz_begin = s.lo_b;
+    a.lz_end = s.lo_e;
+    a.lz2_begin = s.hi_b;
+    a.lz2_end = s.hi_e;
+    s.be->stencil(spec_, a, stream);
+    a.lz2_begin = a.lz2_end = 0;
+  } else if (s.lo_e > s.lo_b) {
+    a.lz_begin = s.lo_b;
+    a.lz_end = s.lo_e;
+    s.be->stencil(spec_, a, stream);
+  } else if (s.hi_e > s.hi_b) {
+    a.lz_begin = s.hi_b;
+    a.lz_end = s.hi_e;
+    s.be->stencil(spec_, a, stream);
+  }
+  if (s.in_e > s.in_b) {
+    a.lz_begin = s.in_b;
+    a.lz_end = s.in_e;
+    for (const auto& yr : {std::make_pair(s.ylo_b, s.ylo_e), std::make_pair(s.yhi_b, s.yhi_e)}) {
+      if (yr.second <= yr.first) continue;
+      a.ly_begin = yr.first;
+      a.ly_end = yr.second;
+      s.be->stencil(spec_, a, stream);
+    }
+  }
+}
+
+// The interior region: interior planes, and for a pencil its interior rows.
+void Solver::interior_kernel(Slab& s, RegionArgs a, void* stream) {
+  if (s.in_e <= s.in_b) return;
+  a.lz_begin = s.in_b;
+  a.lz_end = s.in_e;
+  a.lz2_begin = a.lz2_end = 0;
+  if (opt_.py > 1) {
+    if (s.yin_e <= s.yin_b) return;
+    a.ly_begin = s.yin_b;
+    a.ly_end = s.yin_e;
+  }
+  s.be->stencil(spec_, a, stream);
+}
+
 void Solver::step(bool want_resid, int k) {
   const int nb = 1 - cur_;
   const bool bcs = boundary_on_cs();
@@ -304,23 +371,7 @@ void Solver::step(bool want_resid, int k) {
     else s.be->wait(s.hs, s.ev_int);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)bs));
     a.resid = want_resid ? s.resid : nullptr;
-    if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
-      // both boundary regions in one call (one launch where the kernel supports it)
-      a.lz_begin = s.lo_b;
-      a.lz_end = s.lo_e;
-      a.lz2_begin = s.hi_b;
-      a.lz2_end = s.hi_e;
-      s.be->stencil(spec_, a, bs);
-      a.lz2_begin = a.lz2_end = 0;
-    } else if (s.lo_e > s.lo_b) {
-      a.lz_begin = s.lo_b;
-      a.lz_end = s.lo_e;
-      s.be->stencil(spec_, a, bs);
-    } else if (s.hi_e > s.hi_b) {
-      a.lz_begin = s.hi_b;
-      a.lz_end = s.hi_e;
-      s.be->stencil(spec_, a, bs);
-    }
+    boundary_kernels(s, a, bs);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)bs));
     if (opt_.sync_debug) s.be->sync_device();
     if (prof && !prof_hip && &s == &slabs_[0]) c1 = clk::now();
@@ -334,12 +385,8 @@ void Solver::step(bool want_resid, int k) {
       s.be->wait(s.cs, s.ev_bnd);
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)is));
-    if (s.in_e > s.in_b) {
-      a.lz_begin = s.in_b;
-      a.lz_end = s.in_e;
-      a.resid = want_resid ? s.resid + 1 : nullptr;
-      s.be->stencil(spec_, a, is);
-    }
+    a.resid = want_resid ? s.resid + 1 : nullptr;
+    interior_kernel(s, a, is);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[3], (hipStream_t)is));
     if (prof && !prof_hip && &s == &slabs_[0]) c2 = clk::now();
     if (!bcs) s.be->record(s.ev_bnd, s.hs);
@@ -471,7 +518,7 @@ void Solver::maybe_inject_fault() {
         std::memcpy(v.data(), &q, es);
       }
       // an interior cell of the first owned plane (not on the Dirichlet frame)
-      const size_t off = ((size_t)s.lay.halo * s.lay.plane + (size_t)std::min<int64_t>(1, s.lay.global.ny - 1) * s.lay.pitch +
+      const size_t off = ((size_t)s.lay.halo * s.lay.plane + (size_t)(s.lay.hy + std::min<int64_t>(1, s.lay.nyl() - 1)) * s.lay.pitch +
                           (size_t)std::min<int64_t>(1, s.lay.global.nx - 1)) * es;
       s.be->copy((char*)s.buf[cur_] + off, v.data(), es, CopyKind::H2D, s.hs);
       s.be->sync_stream(s.hs);
@@ -587,27 +634,8 @@ void Solver::warm_kernels(int64_t steps) {
         a.steps = k;
         a.min_rounds = min_rounds();
         a.resid = r ? s.resid : nullptr;  // (step() clears the accumulator before it counts)
-        if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
-          a.lz_begin = s.lo_b;
-          a.lz_end = s.lo_e;
-          a.lz2_begin = s.hi_b;
-          a.lz2_end = s.hi_e;
-          s.be->stencil(spec_, a, s.hs);
-          a.lz2_begin = a.lz2_end = 0;
-        } else if (s.lo_e > s.lo_b) {
-          a.lz_begin = s.lo_b;
-          a.lz_end = s.lo_e;
-          s.be->stencil(spec_, a, s.hs);
-        } else if (s.hi_e > s.hi_b) {
-          a.lz_begin = s.hi_b;
-          a.lz_end = s.hi_e;
-          s.be->stencil(spec_, a, s.hs);
-        }
-        if (s.in_e > s.in_b) {
-          a.lz_begin = s.in_b;
-          a.lz_end = s.in_e;
-          s.be->stencil(spec_, a, s.hs);
-        }
+        boundary_kernels(s, a, s.hs);
+        interior_kernel(s, a, s.hs);
       }
     }
   synchronize();
@@ -774,8 +802,8 @@ void Solver::read_owned(int i, void* host) {
   s.be->sync_stream(s.hs);
   char* dst = (char*)host;
   for (int64_t z = 0; z < l.nzl(); ++z)
-    for (int64_t y = 0; y < l.global.ny; ++y) {
-      std::memcpy(dst, stage.data() + ((size_t)z * l.plane + (size_t)y * l.pitch) * es,
+    for (int64_t y = 0; y < l.nyl(); ++y) {
+      std::memcpy(dst, stage.data() + ((size_t)z * l.plane + (size_t)(l.hy + y) * l.pitch) * es,
                   (size_t)l.global.nx * es);
       dst += (size_t)l.global.nx * es;
     }
@@ -789,8 +817,8 @@ void Solver::write_owned(int i, const void* host) {
   std::vector<char> stage((size_t)l.nzl() * l.plane_bytes(), 0);
   const char* src = (const char*)host;
   for (int64_t z = 0; z < l.nzl(); ++z)
-    for (int64_t y = 0; y < l.global.ny; ++y) {
-      std::memcpy(stage.data() + ((size_t)z * l.plane + (size_t)y * l.pitch) * es, src,
+    for (int64_t y = 0; y < l.nyl(); ++y) {
+      std::memcpy(stage.data() + ((size_t)z * l.plane + (size_t)(l.hy + y) * l.pitch) * es, src,
                   (size_t)l.global.nx * es);
       src += (size_t)l.global.nx * es;
     }
@@ -823,7 +851,8 @@ void Solver::save_checkpoint(const std::string& dir) {
     std::ofstream j(base + ".json");
     j << "{\"format\": \"mdfx-slab-v1\", \"stencil\": \"" << stencil_name(spec_.kind) << "\", \"dtype\": \""
       << dtype_name(spec_.dtype) << "\", \"nx\": " << global_.nx << ", \"ny\": " << global_.ny
-      << ", \"nz\": " << global_.nz << ", \"z0\": " << l.z0 << ", \"z1\": " << l.z1
+      << ", \"nz\": " << global_.nz << ", \"z0\": " << l.z0 << ", \"z1\": " << l.z1 << ", \"y0\": " << l.y0
+      << ", \"y1\": " << l.y1
       << ", \"rank\": " << slabs_[i].rank << ", \"nranks\": " << nranks_
       << ", \"step\": " << stats_.steps << "}\n";
   }
@@ -860,7 +889,7 @@ void Solver::load_checkpoint(const std::string& dir) {
   // slabs written by any decomposition: slab_0 names the writer's rank count, and every one of
   // slab_0 .. slab_<nranks-1> must carry that count and the same step
   struct F {
-    long long z0, z1, step;
+    long long z0, z1, y0, y1, step;
     std::string bin;
   };
   std::vector<F> files;
@@ -881,6 +910,11 @@ void Solver::load_checkpoint(const std::string& dir) {
     MDFX_CHECK(json_int(js, "z0", f.z0) && json_int(js, "z1", f.z1) && json_int(js, "step", f.step) &&
                    json_int(js, "nx", nx) && json_int(js, "ny", ny) && json_int(js, "nz", nz),
                "malformed checkpoint header " + base + ".json");
+    // (y0 / y1: a pencil's rows; slab checkpoints hold every row)
+    if (!json_int(js, "y0", f.y0) || !json_int(js, "y1", f.y1)) {
+      f.y0 = 0;
+      f.y1 = ny;
+    }
     MDFX_CHECK(nx == global_.nx && ny == global_.ny && nz == global_.nz,
                "checkpoint grid does not match the solver grid");
     MDFX_CHECK(js.find(std::string("\"dtype\": \"") + dtype_name(spec_.dtype) + "\"") != std::string::npos,
@@ -900,20 +934,26 @@ void Solver::load_checkpoint(const std::string& dir) {
   MDFX_CHECK(!files.empty(), "no checkpoint slabs in " + dir);
   for (int i = 0; i < num_local(); ++i) {
     const FieldLayout& l = slabs_[i].lay;
-    const size_t pb = (size_t)global_.nx * global_.ny * l.esize();  // dense plane bytes
-    std::vector<char> data((size_t)l.nzl() * pb);
+    const size_t rb = (size_t)global_.nx * l.esize();  // dense row bytes
+    std::vector<char> data((size_t)l.nzl() * l.nyl() * rb);
+    std::vector<std::ifstream> ins(files.size());
     for (int64_t z = l.z0; z < l.z1; ++z) {
-      bool found = false;
-      for (auto& f : files)
-        if (z >= f.z0 && z < f.z1) {
-          std::ifstream in(f.bin, std::ios::binary);
-          in.seekg((std::streamoff)((z - f.z0) * pb));
-          in.read(data.data() + (size_t)(z - l.z0) * pb, (std::streamsize)pb);
-          MDFX_CHECK(in.good(), "short read in " + f.bin);
-          found = true;
-          break;
-        }
-      MDFX_CHECK(found, format("checkpoint is missing plane %lld", (long long)z));
+      // the rows of plane z this slab owns, gathered from every file that holds some of them (any
+      // slab or pencil decomposition wrote them)
+      int64_t got = 0;
+      for (size_t fi = 0; fi < files.size(); ++fi) {
+        const F& f = files[fi];
+        if (z < f.z0 || z >= f.z1) continue;
+        const int64_t ya = std::max<int64_t>(l.y0, f.y0), yb = std::min<int64_t>(l.y1, f.y1);
+        if (ya >= yb) continue;
+        if (!ins[fi].is_open()) ins[fi].open(f.bin, std::ios::binary);
+        ins[fi].seekg((std::streamoff)((((z - f.z0) * (f.y1 - f.y0)) + (ya - f.y0)) * (int64_t)rb));
+        ins[fi].read(data.data() + ((size_t)(z - l.z0) * l.nyl() + (size_t)(ya - l.y0)) * rb,
+                     (std::streamsize)((yb - ya) * (int64_t)rb));
+        MDFX_CHECK(ins[fi].good(), "short read in " + f.bin);
+        got += yb - ya;
+      }
+      MDFX_CHECK(got == l.nyl(), format("checkpoint is missing rows of plane %lld", (long long)z));
     }
     write_owned(i, data.data());
     stats_.steps = files[0].step;

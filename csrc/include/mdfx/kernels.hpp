@@ -26,6 +26,8 @@ struct RegionArgs {
   // optional second region written by the same call (the engine passes both K-plane boundary
   // regions of a slab at once; heat7_wtk runs them as one launch, other kernels as two)
   int64_t lz2_begin = 0, lz2_end = 0;
+  // storage rows to write (pencil layouts: the y-boundary strips); empty = every owned row
+  int64_t ly_begin = 0, ly_end = 0;
   double* resid = nullptr;           // optional accumulator of sum((out-in)^2) over the region
   // Time steps fused into this sweep (temporal blocking). 2 needs lay.halo >= 2 and reads
   // in[lz_begin-2, lz_end+2); the residual then covers the second step only.

@@ -50,6 +50,7 @@ int hip_device_count();
 // What a transport needs to know about one subdomain owned by this process.
 struct LocalSlab {
   int rank = 0;               // global subdomain index (0..nranks-1)
+  int py = 1;                 // pencil decomposition: subdomains per slab along y (1 = slabs)
   Backend* be = nullptr;
   void* halo_stream = nullptr;
   void* bnd_event = nullptr;  // recorded right after this step's boundary kernel(s)
@@ -57,14 +58,24 @@ struct LocalSlab {
   void* buf[2] = {nullptr, nullptr};
 };
 
-// Byte ranges of one side of a halo exchange for buffer b.
+// Byte ranges of one side of a halo exchange for buffer b. Sides 0 / 1 are the z faces (the first /
+// last `halo` owned planes, whole planes with any ghost rows: one contiguous span), sides 2 / 3
+// the y faces of a pencil (the first / last `hy` owned rows of every owned plane: `height` pieces
+// of `width` bytes, `stride` bytes apart, on both ends). A pencil exchanges y first, then z, so the
+// z faces carry the y ghosts just received and fill the corner ghosts (the fused K-step sweeps
+// read them).
 struct HaloSpan {
   int peer = -1;            // neighbouring subdomain, -1 if none (global boundary)
-  void* send = nullptr;     // first/last `halo` owned planes
-  void* recv = nullptr;     // ghost planes
-  size_t bytes = 0;
+  void* send = nullptr;     // first piece of the owned cells sent
+  void* recv = nullptr;     // first piece of the ghost cells received
+  size_t bytes = 0;         // width * height
+  size_t width = 0;         // contiguous bytes per piece
+  size_t height = 1;        // pieces (1: contiguous)
+  size_t stride = 0;        // bytes from one piece to the next
 };
-HaloSpan halo_span(const LocalSlab& s, int b, int side /*0 = lo, 1 = hi*/, int nranks);
+HaloSpan halo_span(const LocalSlab& s, int b, int side /*0 z-lo, 1 z-hi, 2 y-lo, 3 y-hi*/, int nranks);
+// Throws unless every slab is a slab of a 1-D decomposition (transports without y faces).
+void require_slabs(const std::vector<LocalSlab>& locals, const char* transport);
 // Stream-ordered device-to-device copy of a halo face (same device or a mapped peer): mode 0 the
 // runtime's blit kernels (hipMemcpyDeviceToDevice: copy shaders on the CUs), 1 the SDMA copy
 // engines (hipMemcpyDeviceToDeviceNoCU: no CUs, lower bandwidth on one device), -1 the process

@@ -41,6 +41,10 @@ struct SolverOptions {
   // 0 = automatic (2 with several slabs, so exchange kernels that need CUs find some mid-sweep; 1
   // otherwise). Fewer rounds mean longer z chunks, hence less pipeline fill per chunk.
   int min_rounds = 0;
+  // Pencil decomposition: subdomains per slab along y (1 = slabs along z only). The nranks
+  // subdomains form a (nranks / py) x py grid of (z, y) pencils, each with `temporal` ghost rows
+  // per split y side as well as ghost planes. 3D grids only; fixed at construction.
+  int py = 1;
 };
 
 struct PhaseStats {
@@ -126,8 +130,13 @@ class Solver {
     void* ev_x = nullptr;  // the last exchange's stream work (boundary kernels on the compute stream wait for it)
     double* resid = nullptr;  // 2 accumulators (halo-stream kernels, compute-stream kernels)
     int64_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0, in_b = 0, in_e = 0;  // storage-plane regions
+    // pencils: storage-row regions of the interior planes (y-boundary strips and interior rows;
+    // all 0 for slabs: every owned row)
+    int64_t ylo_b = 0, ylo_e = 0, yhi_b = 0, yhi_e = 0, yin_b = 0, yin_e = 0;
   };
   void step(bool want_resid, int k);
+  void boundary_kernels(Slab& s, RegionArgs a, void* stream);
+  void interior_kernel(Slab& s, RegionArgs a, void* stream);
   void maybe_inject_fault();
   void sync_all();
   bool drain(double limit_s);                  // bounded stream drain (teardown after an abort)
@@ -140,7 +149,7 @@ class Solver {
   StencilSpec spec_;
   Extent3 global_;
   int nranks_;
-  SlabDecomposition decomp_;
+  PencilDecomposition decomp_;  // pz x py subdomains (py = 1: slabs)
   std::vector<Slab> slabs_;
   std::unique_ptr<Transport> transport_;
   SolverOptions opt_;

@@ -50,6 +50,7 @@ bool heat7_tbk_supported(const Geo& g, int steps);
 template <class T>
 void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
 bool heat7_wtk_supported(int steps);
+bool heat7_wxk_supported(int steps);
 template <class T>
 void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
 template <class T>
@@ -126,12 +127,12 @@ __global__ __launch_bounds__(256) void init_kernel(T* __restrict__ buf, Geo g, I
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t x = i % g.pitch, t = i / g.pitch, y = t % g.ny, lz = t / g.ny;
-    const int64_t gz = lz + g.gz_off;
+    const int64_t gz = lz + g.gz_off, gy = y + g.gy_off;  // (a pencil's ghost rows beyond the grid stay 0)
     double v = 0.0;
-    if (x < g.nx && gz >= 0 && gz < g.gnz) {
+    if (x < g.nx && gz >= 0 && gz < g.gnz && gy >= 0 && gy < g.gny) {
       const bool bnd = x == 0 || x == g.nx - 1 || gz == 0 || gz == g.gnz - 1 ||
-                       (a.dims == 3 && (y == 0 || y == g.ny - 1));
-      const uint64_t gidx = (uint64_t)x + (uint64_t)g.nx * ((uint64_t)y + (uint64_t)g.ny * (uint64_t)gz);
+                       (a.dims == 3 && (gy == 0 || gy == g.gny - 1));
+      const uint64_t gidx = (uint64_t)x + (uint64_t)g.nx * ((uint64_t)gy + (uint64_t)g.gny * (uint64_t)gz);
       switch (a.kind) {
         case 0: v = a.value; break;
         case 1: v = bnd ? a.edge : a.interior; break;
@@ -172,7 +173,11 @@ static Geo make_geo(const FieldLayout& lay, int64_t lz_begin, int64_t lz_end) {
   g.pitch = lay.pitch;
   g.plane = lay.plane;
   g.nx = lay.global.nx;
-  g.ny = lay.global.ny;
+  g.ny = lay.rows();
+  g.gny = lay.global.ny;
+  g.gy_off = lay.y0 - lay.hy;
+  g.ly_begin = lay.hy;
+  g.ly_end = lay.hy + lay.nyl();
   g.gnz = lay.global.nz;
   g.lz_begin = lz_begin;
   g.lz_end = lz_end;
@@ -228,7 +233,7 @@ void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* str
   const dev::Geo g = dev::make_geo(lay, 0, lay.planes());
   dev::InitArgs a{(int)init.kind, init.seed, init.lo,       init.hi,  init.value,
                   init.edge,      init.interior, init.density, lay.global.ny == 1 ? 2 : 3};
-  const int64_t n = lay.pitch * lay.global.ny * lay.planes();
+  const int64_t n = lay.pitch * lay.rows() * lay.planes();
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 256 * 64);
   hipStream_t s = (hipStream_t)stream;
   switch (lay.dtype) {
@@ -249,6 +254,10 @@ void hip_init(const InitSpec& init, const FieldLayout& lay, void* buf, void* str
 bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps) {
   if (steps == 1) return true;
   if (steps < 2 || lay.halo < steps) return false;
+  if (lay.pencil())  // pencils (y ghost rows): the fused 7-point sweep of heat7_wxk only
+    return spec.kind == StencilKind::Heat7 && dev::heat7_wxk_supported(steps) && lay.hy >= steps &&
+           dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx) &&
+           !(spec.dtype == DType::F64 && steps == 4);
   const bool k2d = steps == 2 || steps == 3 || steps == 4 || steps == 6 || steps == 8;
   if (spec.kind == StencilKind::Jacobi5)  // deep temporal blocking of the 2D problems
     return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d;  // ref precision too (jacobi5_tbk REF)
@@ -323,7 +332,31 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   g.lz2_begin = a.lz2_begin;
   g.lz2_end = a.lz2_end;
   g.min_rounds = std::max(1, std::min(4, a.min_rounds));
+  if (a.ly_end > a.ly_begin) {
+    MDFX_CHECK(a.ly_begin >= a.lay.hy && a.ly_end <= a.lay.hy + a.lay.nyl(), "row range must lie inside the owned rows");
+    g.ly_begin = a.ly_begin;
+    g.ly_end = a.ly_end;
+  }
   hipStream_t s = (hipStream_t)stream;
+  if (a.lay.pencil()) {
+    // pencil layouts: the fused 7-point sweeps through heat7_wxk, single steps through the
+    // one-cell-per-lane kernels (every stencil); the other tuned kernels assume slab geometry
+    if (a.steps != 1) {
+      MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),
+                 format("no fused %d-step kernel for %s %s on a pencil layout (heat7_wxk: the 3D 7-point, K = 3 / 4)",
+                        a.steps, stencil_name(spec.kind), dtype_name(spec.dtype)));
+      if (spec.dtype == DType::F32)
+        dev::launch_heat7_wxk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
+      else
+        dev::launch_heat7_wxk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
+    } else {
+      MDFX_CHECK(a.lz2_end <= a.lz2_begin, "single pencil steps take one region per call");
+      dev::naive_launch(spec, g, a.in, a.out, a.resid, s);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) MDFX_FAIL(std::string("stencil launch failed: ") + hipGetErrorString(e));
+    return;
+  }
   if (a.steps != 1) {
     MDFX_CHECK(hip_supports_steps(spec, a.lay, a.steps),
                format("no fused %d-step kernel for %s %s at nx=%lld (halo %d)", a.steps, stencil_name(spec.kind),

@@ -27,7 +27,7 @@ struct VT<double> {
 struct Geo {
   int64_t pitch;     // elements per row
   int64_t plane;     // elements per plane
-  int64_t nx, ny;    // global x / y extents
+  int64_t nx, ny;    // global x extent; y: storage rows per plane (the global extent for slabs)
   int64_t gnz;       // global z extent
   int64_t lz_begin;  // first storage plane to write
   int64_t lz_end;    // one past the last storage plane to write
@@ -36,6 +36,10 @@ struct Geo {
   int64_t lz2_begin = 0, lz2_end = 0;  // optional second region of the same launch (heat7_wtk)
   int64_t alloc = 0;                 // elements allocated (planes + slack), for device checks
   int min_rounds = 1;                // whole rounds of resident blocks a streaming sweep spans at least (RegionArgs)
+  // pencil layouts (a y split with ghost rows): global rows, global y = storage row + gy_off, and the
+  // storage rows [ly_begin, ly_end) to write (slabs: gny = ny, gy_off = 0, every row). Kernels
+  // without pencil support only ever see slab geometry (hip_stencil routes pencils to naive / wxk)
+  int64_t gny = 0, gy_off = 0, ly_begin = 0, ly_end = 0;
   unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };
 

@@ -104,7 +104,10 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
   const int64_t x = xs + (int64_t)lane * N;
   const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
-  const int yb = yt * BR;                              // first row of the band
+  // rows: storage rows [0, ny) (a pencil's include ghost rows), output rows [ly0, ly1), global row =
+  // storage row + gyoff of gny (slabs: ly0 = 0, ly1 = ny = gny, gyoff = 0)
+  const int ly0 = (int)g.ly_begin, ly1 = (int)g.ly_end, gyoff = (int)g.gy_off, gny = (int)g.gny;
+  const int yb = ly0 + yt * BR;                        // first row of the band
   const int y0 = yb + (w == 0 ? 0 : RE + (w - 1) * RY);  // first own row of this wave
   const int rown = (w == 0 || w == WB - 1) ? RE : RY;    // own rows of this wave
   const int64_t pitch = g.pitch, plane = g.plane;
@@ -115,10 +118,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
   const Row rx = RO::coef(r, xb);
   const Row r0 = RO::zero();
-  // block-uniform: every row the band computes at any level is y-interior, so no wave needs the
-  // per-row held test (bands at y = 0 / ny-1 run the tested copy, all their waves together)
-  const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
-  const int nsto = (__builtin_amdgcn_ballot_w64(own) != 0 && !(dg & 2)) ? max(0, min(rown, ny - y0)) : 0;
+  // block-uniform: every row the band computes at any level is y-interior (globally), so no wave
+  // needs the per-row held test (bands at global y = 0 / gny-1 run the tested copy, all their waves
+  // together)
+  const bool yint = yb - (K - 1) + gyoff >= 1 && yb + BR + K - 2 + gyoff <= gny - 2;
+  const int nsto = (__builtin_amdgcn_ballot_w64(own) != 0 && !(dg & 2)) ? max(0, min(rown, ly1 - y0)) : 0;
   int nst = 0;  // output stores issued since this wave's last DMA
 
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         const Row& xm = X[i1 % 3];
         const Row& cen = X[(i1 + 1) % 3];
         const Row& xp = X[(i1 + 2) % 3];
-        const bool yh = EDGE && (y0 + i == 0 || y0 + i == ny - 1);
+        const bool yh = EDGE && (y0 + i + gyoff == 0 || y0 + i + gyoff == gny - 1);
         Row ri = rl[1];
         if (yh) ri = r0;
         const Row cold = Cin[i1];
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
 #pragma unroll
         for (int j = 1; j <= K; ++j) {
           if (j == K) {  // the sweep's output row
-            if (valid && i >= 0 && i < SH::R && y0 + i < ny && own && !(dg & 2)) {
+            if (valid && i >= 0 && i < SH::R && y0 + i < ly1 && own && !(dg & 2)) {
               T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
               dcheck(g, (const T*)out, a, N);
               store_nt((V*)a, RO::vec(cur));
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
             if (yh) rj = r0;
             const Row& bc = H[j - 1][P ^ 1][ij];  // u_j(q - j - 1): the centre of u_{j+1}(q - j - 1)
             nxt = RO::fin(H[j - 1][P][ij], cur, bc, rj);
-            if (RES && j + 1 == K && valid && i >= 0 && i < SH::R && y0 + i < ny && own) {
+            if (RES && j + 1 == K && valid && i >= 0 && i < SH::R && y0 + i < ly1 && own) {
 #pragma unroll
               for (int e = 0; e < N; ++e)
                 if (x + e < g.nx) {
@@ -312,7 +316,7 @@ static WxGeo wxk_geo(const Geo& g) {
   const int64_t planes = g.lz_end - g.lz_begin;
   const int64_t planes2 = g.lz2_end > g.lz2_begin ? g.lz2_end - g.lz2_begin : 0;
   w.XT = (int)((g.nx + SEG - 1) / SEG);
-  w.YT = (int)((g.ny + BR - 1) / BR);
+  w.YT = (int)((g.ly_end - g.ly_begin + BR - 1) / BR);
   const int64_t tiles = (int64_t)w.XT * w.YT;
   w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false>, 64 * WB);
   w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds);
@@ -375,7 +379,8 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
              "heat7_wxk: the second region must follow the first and have its planes + ghosts allocated");
   MDFX_CHECK(g.pitch % VT<T>::N == 0, "heat7_wxk: the row pitch must be a whole number of vectors");
-  MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
+  MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.gny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) &&
+                 g.gnz < ((int64_t)1 << 30) && g.gy_off > -((int64_t)1 << 30) && g.gy_off < ((int64_t)1 << 30) &&
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
              "heat7_wxk: row / plane counts must fit 32-bit indices");
   if constexpr (sizeof(T) == 4) {

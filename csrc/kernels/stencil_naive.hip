@@ -12,19 +12,21 @@
 namespace mdfx {
 namespace dev {
 
+// (3D kernels: rows [ly_begin, ly_end) of a pencil's storage, held at the GLOBAL y boundary)
 template <class T, bool RES>
 __global__ __launch_bounds__(256) void naive_heat7(const T* __restrict__ in, T* __restrict__ out,
                                                    Geo g, T r, double* __restrict__ resid) {
-  const int64_t n = g.nx * g.ny * (g.lz_end - g.lz_begin);
+  const int64_t nr = g.ly_end - g.ly_begin;
+  const int64_t n = g.nx * nr * (g.lz_end - g.lz_begin);
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t x = i % g.nx, t = i / g.nx, y = t % g.ny, lz = g.lz_begin + t / g.ny;
-    const int64_t gz = lz + g.gz_off;
+    const int64_t x = i % g.nx, t = i / g.nx, y = g.ly_begin + t % nr, lz = g.lz_begin + t / nr;
+    const int64_t gz = lz + g.gz_off, gy = y + g.gy_off;
     const int64_t idx = lz * g.plane + y * g.pitch + x;
     const T c = in[idx];
     T o = c;
-    if (x > 0 && x < g.nx - 1 && y > 0 && y < g.ny - 1 && gz > 0 && gz < g.gnz - 1)
+    if (x > 0 && x < g.nx - 1 && gy > 0 && gy < g.gny - 1 && gz > 0 && gz < g.gnz - 1)
       o = sm::heat7<T>(c, in[idx - 1], in[idx + 1], in[idx - g.pitch], in[idx + g.pitch],
                        in[idx - g.plane], in[idx + g.plane], r);
     out[idx] = o;
@@ -76,16 +78,17 @@ template <class T, bool RES>
 __global__ __launch_bounds__(256) void naive_box27(const T* __restrict__ in, T* __restrict__ out,
                                                    Geo g, T c0, T c1, T c2, T c3,
                                                    double* __restrict__ resid) {
-  const int64_t n = g.nx * g.ny * (g.lz_end - g.lz_begin);
+  const int64_t nr = g.ly_end - g.ly_begin;
+  const int64_t n = g.nx * nr * (g.lz_end - g.lz_begin);
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t x = i % g.nx, t = i / g.nx, y = t % g.ny, lz = g.lz_begin + t / g.ny;
-    const int64_t gz = lz + g.gz_off;
+    const int64_t x = i % g.nx, t = i / g.nx, y = g.ly_begin + t % nr, lz = g.lz_begin + t / nr;
+    const int64_t gz = lz + g.gz_off, gy = y + g.gy_off;
     const int64_t idx = lz * g.plane + y * g.pitch + x;
     const T c = in[idx];
     T o = c;
-    if (x > 0 && x < g.nx - 1 && y > 0 && y < g.ny - 1 && gz > 0 && gz < g.gnz - 1) {
+    if (x > 0 && x < g.nx - 1 && gy > 0 && gy < g.gny - 1 && gz > 0 && gz < g.gnz - 1) {
       T ce, cr, dg;
       box27_plane_partials(in + idx - g.plane, g.pitch, ce, cr, dg);
       const T am = sm::box27_A(ce, cr, dg, c1, c2, c3);
@@ -138,7 +141,7 @@ static int naive_grid(int64_t n) {
 
 void naive_launch(const StencilSpec& spec, const Geo& g, const void* in, void* out, double* resid,
                   hipStream_t s) {
-  const int64_t n = g.nx * g.ny * (g.lz_end - g.lz_begin);
+  const int64_t n = g.nx * (g.ly_end - g.ly_begin) * (g.lz_end - g.lz_begin);
   if (n <= 0) return;
   const dim3 grd(naive_grid(n)), blk(256);
   const bool res = resid != nullptr;
