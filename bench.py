@@ -89,6 +89,9 @@ def parse(argv=None):
     p.add_argument("--overlap", action="store_true",
                    help="only the overlapped schedule (interior || boundary + exchange; no trial)")
     p.add_argument("--residual-every", type=int, default=0)
+    p.add_argument("--py", type=int, default=0,
+                   help="ranks along y of a (z, y) pencil decomposition (1 = z slabs; 0 = auto: at 4+ GPUs the "
+                        "3D 7-point tries slabs and 2-along-y pencils on the ipc transports and times the faster)")
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
     p.add_argument("--device", default="auto", choices=["auto", "hip", "cpu"])
     p.add_argument("--repeats", type=int, default=1, help="timed repetitions; the best is reported")
@@ -205,7 +208,7 @@ def pick_temporal(a, prob, nslab, hip):
     return 1
 
 
-def run_gate(a, hip, transport, temporal, world, rank, graph=False):
+def run_gate(a, hip, transport, temporal, world, rank, graph=False, py=1):
     """Bitwise check of the decomposed engine (same transport, same fused depth, same graph mode)
     against a full-grid single-slab run on this rank's own device. Returns (passed, record)."""
     import numpy as np
@@ -223,14 +226,14 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False):
     kw = dict(device="hip" if hip else "cpu", temporal=temporal, residual_every=steps,
               timeout_s=a.timeout if hip else 0.0)
     err = ""
-    tag = transport + ("+graph" if graph else "")
+    tag = transport + ("+graph" if graph else "") + ("+py%d" % py if py > 1 else "")
     ok = False
     try:
         fault = os.environ.get("MDFX_FAULT", "")
         if fault.startswith("gate:") and transport in fault[5:].split(","):
             # fault injection for the fallback test: this transport's gate fails on every rank
             raise RuntimeError("injected gate failure (MDFX_FAULT=%s)" % fault)
-        with Simulation(prob, distributed=True, transport=transport, graph=graph, **kw) as sim:
+        with Simulation(prob, distributed=True, transport=transport, graph=graph, py=py, **kw) as sim:
             trace("gate: engine up")
             sim.init()
             sim.prepare_graphs()  # the timed run's path: cycles captured before any step
@@ -247,7 +250,8 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False):
             ref.synchronize()
             full = ref.read_local(0)
             rres = ref.residual
-        ok = bool(np.array_equal(mine, full[lay["z0"]:lay["z1"]])) and abs(res - rres) <= 1e-9 * max(1.0, abs(rres))
+        own = full[lay["z0"]:lay["z1"], lay["y0"]:lay["y1"]]
+        ok = bool(np.array_equal(mine, own)) and abs(res - rres) <= 1e-9 * max(1.0, abs(rres))
         if not ok:
             err = "rank %d: owned planes or residual differ from the full-grid run (residual %r vs %r)" % (
                 rank, res, rres)
@@ -258,7 +262,7 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False):
     bad = int(t.item())
     if err:
         print("bench gate [%s]: %s" % (tag, err), file=sys.stderr, flush=True)
-    rec = {"grid": [prob.nx, prob.ny, prob.nz], "steps": steps, "transport": transport, "graph": graph,
+    rec = {"grid": [prob.nx, prob.ny, prob.nz], "steps": steps, "transport": transport, "graph": graph, "py": py,
            "ranks_failed": bad, "passed": bad == 0}
     return bad == 0, rec
 
@@ -281,16 +285,17 @@ def run_proxy(a):
     if a.stencil in ("jacobi5", "life"):
         ny = 1
     prob = make_problem(a, nx, ny, nz)
-    temporal = pick_temporal(a, prob, max(1, n), True)
+    py = max(1, a.py)
+    temporal = pick_temporal(a, prob, max(1, n // py), True)
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True])
     overlaps = [True, False] if (n > 1 and not a.no_overlap and not a.overlap) else [not a.no_overlap]
     rounds = [int(a.rounds)] if a.rounds != "auto" else ([2, 1] if n > 1 else [0])
     sdma = a.transport in ("ipc_sdma", "proxy_sdma")
     sim = Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graphs[0],
                      residual_every=a.residual_every, timeout_s=a.timeout,
-                     transport="proxy_sdma" if sdma else "proxy")
+                     transport="proxy_sdma" if sdma else "proxy", py=py)
     lay = sim.layout(0)
-    slab_cells = (lay["z1"] - lay["z0"]) * prob.nx * prob.ny
+    slab_cells = (lay["z1"] - lay["z0"]) * (lay["y1"] - lay["y0"]) * prob.nx
 
     def timed(steps):
         sim.synchronize()
@@ -333,8 +338,9 @@ def run_proxy(a):
     model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF", "life": "2D Game of Life"}[a.stencil]
     dram_tbps = per_gpu * prob.bytes_per_cell_per_step / temporal / 1e3
     rec = {
-        "metric": "PROXY per-GPU GCells/s, rank %d of a %d-GPU slab split, %s %dx%dx%d %s (one GPU; not a "
-                  "whole-node measurement)" % (r, n, model, nx, ny, nz, a.dtype),
+        "metric": "PROXY per-GPU GCells/s, rank %d of a %d-GPU %s split, %s %dx%dx%d %s (one GPU; not a "
+                  "whole-node measurement)" % (r, n, "slab" if py == 1 else "%dx%d (z, y) pencil" % (n // py, py),
+                                               model, nx, ny, nz, a.dtype),
         "value": round(per_gpu, 3),
         "unit": "GCells/s per GPU",
         "proxy": True,
@@ -349,6 +355,7 @@ def run_proxy(a):
         "dtype": {"f32": "fp32", "f64": "fp64", "u8": "u8"}[a.dtype],
         "data": "synthetic (uniform random grid from a counter hash of the global index, seed 1)",
         "config": {"model": "%s %dx%dx%d %s" % (model, nx, ny, nz, a.dtype), "slab_planes": [lay["z0"], lay["z1"]],
+                   "rows": [lay["y0"], lay["y1"]], "py": py,
                    "ghost_planes": lay["halo"], "temporal_block": temporal, "transport": sim.transport,
                    "face_copy": "sdma" if sdma else native().face_copy_mode(),
                    "ipc_protocol": "direct" if native().ipc_direct_ok(lay["bytes"]) else "mailbox",
@@ -410,7 +417,13 @@ def main(argv=None):
     if a.stencil in ("jacobi5", "life"):
         ny = 1  # 2D grids: nx = width, nz = height
     prob = make_problem(a, nx, ny, nz)
-    temporal = pick_temporal(a, prob, max(1, world, a.virtual_ranks), hip)
+    # (z, y) pencils: py ranks along y. Auto: at 4+ processes the 3D 7-point (whose fused sweep
+    # takes y ghost rows) tries 2 along y next to the z slabs, on every transport but rccl
+    if a.py > 0:
+        pys = [a.py]
+    else:
+        pys = [1, 2] if (env and world >= 4 and world % 2 == 0 and a.stencil == "heat7") else [1]
+    temporal = pick_temporal(a, prob, max(1, world, a.virtual_ranks) // max(pys), hip)
     timeout = a.timeout if hip else 0.0
 
     # ---- transport / graph mode: correctness gate (N > 1), then short timed trials ---------
@@ -424,13 +437,14 @@ def main(argv=None):
     elif not env:
         transports = [a.transport if a.transport in ("loopback", "host") else "auto"]
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True] if hip else [False])
-    cands = [(t, g) for t in transports for g in graphs]
+    # rccl exchanges z faces only: no pencils there
+    cands = [(t, g, q) for t in transports for q in pys for g in graphs if q == 1 or t != "rccl"]
     if hip and a.graph == "auto" and len(graphs) > 1:
         # rccl steps are captured only under HIP >= 7.2 (RcclTransport::graph_capturable); under the
         # runtime PyTorch bundles a graph candidate would just repeat the eager one
         from mpi_cuda_process_amd import native as _nat
         if not _nat().hip_runtime_version() >= 70200000:
-            cands = [(t, g) for t, g in cands if not (t == "rccl" and g)]
+            cands = [(t, g, q) for t, g, q in cands if not (t == "rccl" and g)]
     if a.rounds != "auto":
         rounds = [int(a.rounds)]
     else:
@@ -438,15 +452,15 @@ def main(argv=None):
     gate = None
     if env and world > 1 and not a.no_gate:
         recs, ok = [], []
-        for t, g in cands:
-            if g and (t, False) in cands and (t, False) not in ok:
+        for t, g, q in cands:
+            if g and (t, False, q) in cands and (t, False, q) not in ok:
                 continue  # a transport whose eager run failed is not tried with graphs
-            trace("gate %s graph=%s" % (t, g))
-            passed, rec = run_gate(a, hip, t, temporal, world, rank, graph=g)
-            trace("gate %s graph=%s passed=%s" % (t, g, passed))
+            trace("gate %s graph=%s py=%d" % (t, g, q))
+            passed, rec = run_gate(a, hip, t, temporal, world, rank, graph=g, py=q)
+            trace("gate %s graph=%s py=%d passed=%s" % (t, g, q, passed))
             recs.append(rec)
             if passed:
-                ok.append((t, g))
+                ok.append((t, g, q))
         if not ok and a.transport == "auto" and hip:
             # last resort: faces staged through host memory over the gloo group. Slow, but a
             # correct number rather than none when neither device transport works on this node
@@ -454,12 +468,12 @@ def main(argv=None):
             passed, rec = run_gate(a, hip, "staged", temporal, world, rank, graph=False)
             recs.append(rec)
             if passed:
-                ok.append(("staged", False))
+                ok.append(("staged", False, 1))
         gate = {"passed": bool(ok), "runs": recs}
         if not ok:
             if rank == 0:
                 print("bench: correctness gate FAILED for every transport tried (%s); not timing"
-                      % ", ".join(sorted(set(t for t, _ in cands))), file=sys.stderr)
+                      % ", ".join(sorted(set(t for t, _, _ in cands))), file=sys.stderr)
             dist.barrier()
             dist.destroy_process_group()
             return 3
@@ -469,16 +483,16 @@ def main(argv=None):
     # overlapped == serialised equality is a test). Several processes: interior || boundary +
     # exchange (overlap) against one full sweep after the exchange, whichever the trial finds faster.
     overlaps = [True, False] if (hip and env and world > 1 and not a.no_overlap and not a.overlap) else [not a.no_overlap]
-    cands = [(t, g, r, ov) for t, g in cands for r in rounds for ov in overlaps]
+    cands = [(t, g, r, ov, q) for t, g, q in cands for r in rounds for ov in overlaps]
     kw = dict(device="hip" if hip else "cpu", overlap=not a.no_overlap,
               residual_every=a.residual_every, timeout_s=timeout, temporal=temporal)
 
-    def make_sim(transport, graph, rounds=0, overlap=True):
+    def make_sim(transport, graph, rounds=0, overlap=True, py=1):
         if env:
-            sim = Simulation(prob, distributed=True, transport=transport, graph=graph, **kw)
+            sim = Simulation(prob, distributed=True, transport=transport, graph=graph, py=py, **kw)
         else:
             sim = Simulation(prob, ranks=a.virtual_ranks or 1, distributed=False, transport=transport, graph=graph,
-                             **kw)
+                             py=py, **kw)
         sim.set_options(min_rounds=rounds, overlap=overlap)
         return sim
 
@@ -513,12 +527,12 @@ def main(argv=None):
         n_trial = max(2, a.trial_steps)
         best_t = {}
         for _pass in range(2):
-            for t, g, rr, ov in cands:
-                if sim is not None and sim_t != t:
+            for t, g, rr, ov, q in cands:
+                if sim is not None and sim_t != (t, q):
                     sim.close()
                     sim = None
                 if sim is None:
-                    sim, sim_t = make_sim(t, g, rr, ov), t
+                    sim, sim_t = make_sim(t, g, rr, ov, q), (t, q)
                 sim.set_options(graph=g, min_rounds=rr, overlap=ov)
                 # exactly the timed run's sequence: fresh grid, captures, its own warm-up (so the trial
                 # starts on the same buffer parity and replay history as the run it picks)
@@ -526,14 +540,15 @@ def main(argv=None):
                 sim.prepare_graphs()  # capture before timing (no-op with graphs off)
                 sim.run(a.warmup)
                 dt = timed(sim, n_trial)
-                trace("trial %s graph=%s rounds=%s overlap=%s: %.3f ms/step" % (t, g, rr, ov, dt / n_trial * 1e3))
-                key = (t, g, rr, ov)
+                trace("trial %s graph=%s rounds=%s overlap=%s py=%d: %.3f ms/step" % (t, g, rr, ov, q,
+                                                                                    dt / n_trial * 1e3))
+                key = (t, g, rr, ov, q)
                 best_t[key] = min(best_t.get(key, 1e30), dt / n_trial * 1e3)
-        for t, g, rr, ov in cands:
-            trials.append({"transport": t, "graph": g, "min_rounds": rr, "overlap": ov,
-                           "ms_per_step": round(best_t[(t, g, rr, ov)], 4)})
+        for t, g, rr, ov, q in cands:
+            trials.append({"transport": t, "graph": g, "min_rounds": rr, "overlap": ov, "py": q,
+                           "ms_per_step": round(best_t[(t, g, rr, ov, q)], 4)})
         chosen = cands[min(range(len(trials)), key=lambda i: trials[i]["ms_per_step"])]
-        if sim_t != chosen[0]:
+        if sim_t != (chosen[0], chosen[4]):
             sim.close()
             sim = None
     else:
@@ -580,8 +595,9 @@ def main(argv=None):
     dram_tbps = per_gpu * prob.bytes_per_cell_per_step / temporal / 1e3
     if rank == 0:
         sim_transport = sim.transport
-        par = ("slab-z%d (1 process/GPU, %s halo, %s)" % (
-            world, sim_transport, "interior||boundary streams" if chosen[3] else "exchange then one sweep")
+        decomp = "slab-z%d" % world if chosen[4] == 1 else "pencil-z%dy%d" % (world // chosen[4], chosen[4])
+        par = ("%s (1 process/GPU, %s halo, %s)" % (
+            decomp, sim_transport, "interior||boundary streams" if chosen[3] else "exchange then one sweep")
                if env else ("slab-z%d virtual in 1 process (%s)" % (a.virtual_ranks, sim_transport)
                             if a.virtual_ranks > 1 else "single GPU" if hip else "cpu"))
         model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF",
@@ -626,6 +642,7 @@ def main(argv=None):
                 "ipc_protocol": (("direct" if native().ipc_direct_ok(sim.layout(0)["bytes"]) else "mailbox")
                                  if sim_transport in ("ipc", "ipc_sdma") else None),
                 "temporal_block": temporal,
+                "py": chosen[4],
                 "gate": gate,
             },
             "per_gpu_gcells": round(per_gpu, 3),

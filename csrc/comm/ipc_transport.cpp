@@ -50,6 +50,15 @@
 // A re-sent parity (exchange_ghosts) needs no look-ahead here: the last wait is already the
 // stronger condition.
 //
+// (z, y) pencils (direct protocol only) have four neighbours and exchange in two phases, because a
+// z face spans the y ghost rows too (they carry the edge and corner cells of the 27-point stencil):
+//
+//   signal(ready)
+//   for each y neighbour n:  wait(n.ready >= e); 2-D copy n's y face -> my ghost rows; signal(pulled[side])
+//   signal(readyZ)                                        my y ghost rows of b landed
+//   for each z neighbour n:  wait(n.readyZ >= e); copy n's z face -> my ghost planes; signal(pulled[side])
+//   for each neighbour n:    wait(n.pulled[mine] >= e - 1)
+//
 // Reference parity: the per-element host-staged MPI_Send/MPI_Recv loops of
 // MDF_kernel.cu:167-169,180-183 (D5, D12) with their rank-1 self-addressing (D3).
 #include <hip/hip_runtime_api.h>
@@ -78,13 +87,15 @@ constexpr int kReady = 0;                 // public: exchanges whose faces I pub
 constexpr int kPulled = 16;               // public: [kPulled + side] pulls I completed from side
 constexpr int kExpReady = 48;             // private: [kExpReady + side]
 constexpr int kExpPulled = 64;            // private: [kExpPulled + side]
+constexpr int kReadyZ = 96;               // public: exchanges whose y ghost rows landed (pencils)
 constexpr size_t kCounterBytes = 128 * 8;
 
 struct IpcRecord {
   char magic[8];
-  int32_t rank = -1, device = -1, pid = 0, direct = 0;
-  uint64_t face_bytes = 0;  // one face (halo planes); the mailbox holds 4
-  uint64_t face_off[2] = {0, 0};  // byte offsets of the lo / hi face in each field buffer (direct)
+  int32_t rank = -1, device = -1, pid = 0, direct = 0, pencil = 0, pad = 0;
+  uint64_t face_bytes[4] = {0, 0, 0, 0};    // per side (z lo, z hi, y lo, y hi); the mailbox holds 4 z faces
+  uint64_t face_off[4] = {0, 0, 0, 0};      // byte offsets of each face in the field buffers (direct)
+  uint64_t face_stride[4] = {0, 0, 0, 0};   // bytes between a face's pieces (a y face: one per plane)
   char pci[32] = {0};       // PCI bus id of the device: a stable identity across HIP_VISIBLE_DEVICES
   hipIpcMemHandle_t mbox;   // (mailbox protocol)
   hipIpcMemHandle_t buf[2];  // the two field buffers (direct protocol)
@@ -132,6 +143,7 @@ class IpcTransport final : public Transport {
     MDFX_CHECK(locals.size() == 1, "ipc transport: one slab per process");
     self_ = locals[0];
     nranks_ = nranks;
+    pencil_ = self_.py > 1 && self_.lay.hy > 0;
     MDFX_CHECK(self_.be->kind() == DeviceKind::HIP, "ipc transport needs a HIP backend");
     self_.be->activate();
     ctr_ = (uint64_t*)hip_alloc_uncached(kCounterBytes);
@@ -150,14 +162,19 @@ class IpcTransport final : public Transport {
     const bool want_direct = ipc_direct_ok(self_.lay.bytes());
 
     IpcRecord mine;
-    std::memcpy(mine.magic, "MDFXIPC3", 8);
+    std::memcpy(mine.magic, "MDFXIPC4", 8);
     mine.rank = self_.rank;
     mine.device = self_.be->device();
     mine.pid = (int32_t)::getpid();
     mine.direct = want_direct ? 1 : 0;
-    mine.face_bytes = face_;
-    for (int side = 0; side < 2; ++side)
-      mine.face_off[side] = (uint64_t)((char*)halo_span(self_, 0, side, nranks_).send - (char*)self_.buf[0]);
+    mine.pencil = pencil_ ? 1 : 0;
+    for (int side = 0; side < 4; ++side) {
+      const HaloSpan h = halo_span(self_, 0, side, nranks_);
+      if (h.peer < 0) continue;
+      mine.face_bytes[side] = h.bytes;
+      mine.face_off[side] = (uint64_t)((char*)h.send - (char*)self_.buf[0]);
+      mine.face_stride[side] = h.stride;
+    }
     if (hipDeviceGetPCIBusId(mine.pci, (int)sizeof(mine.pci) - 1, mine.device) != hipSuccess) {
       (void)hipGetLastError();
       mine.pci[0] = 0;
@@ -175,21 +192,24 @@ class IpcTransport final : public Transport {
         f_.allgather(std::string((const char*)&mine, sizeof(mine)));  // also the setup barrier
     MDFX_CHECK((int)all.size() == nranks_, format("ipc allgather returned %zu records for %d ranks", all.size(), nranks_));
     direct_ = true;
+    bool any_pencil = false;
     for (const std::string& rec : all) {
       MDFX_CHECK(rec.size() == sizeof(IpcRecord), "ipc: malformed handle record");
       IpcRecord r;
       std::memcpy(&r, rec.data(), sizeof(r));
       direct_ = direct_ && r.direct != 0;
+      any_pencil = any_pencil || r.pencil != 0;
     }
+    // (every rank reaches the same verdict from the same records: all fail together)
+    MDFX_CHECK(direct_ || !any_pencil, "ipc transport: a pencil decomposition needs the direct protocol (field buffers "
+                                       "up to 1900 MiB on every rank, or MDFX_IPC_DIRECT=1)");
     const uint64_t pulled0 = direct_ ? 1 : 2;  // the first exchange(s) find their faces / slots free
-    HIPC(hipMemcpy(ctr_ + kPulled + 0, &pulled0, 8, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(ctr_ + kPulled + 1, &pulled0, 8, hipMemcpyHostToDevice));
+    for (int side = 0; side < 4; ++side) HIPC(hipMemcpy(ctr_ + kPulled + side, &pulled0, 8, hipMemcpyHostToDevice));
     HIPC(hipDeviceSynchronize());
 
-    const SlabDecomposition dec(self_.lay.global.nz, nranks_);
-    for (int side = 0; side < 2; ++side) {
+    for (int side = 0; side < 4; ++side) {
       Peer& p = peers_[side];
-      p.rank = side == 0 ? dec.lo_neighbor(self_.rank) : dec.hi_neighbor(self_.rank);
+      p.rank = halo_span(self_, 0, side, nranks_).peer;
       if (p.rank < 0) continue;
       IpcRecord r;
       std::memcpy(&r, all[p.rank].data(), sizeof(r));
@@ -197,9 +217,10 @@ class IpcTransport final : public Transport {
       // HIP_VISIBLE_DEVICES both sides call their GPU "device 0"
       const int their = local_device_of(r.pci);
       const bool same = mine.pci[0] && r.pci[0] ? std::strcmp(mine.pci, r.pci) == 0 : r.device == mine.device;
-      IpcPeerInfo me{mine.rank, mine.device, mine.pid, mine.face_bytes, true};
-      IpcPeerInfo them{r.rank, same ? mine.device : (their >= 0 ? their : -1), r.pid, r.face_bytes,
-                       std::memcmp(r.magic, "MDFXIPC3", 8) == 0};
+      // the neighbour's face that borders me is its opposite side's
+      IpcPeerInfo me{mine.rank, mine.device, mine.pid, mine.face_bytes[side], true};
+      IpcPeerInfo them{r.rank, same ? mine.device : (their >= 0 ? their : -1), r.pid, r.face_bytes[side ^ 1],
+                       std::memcmp(r.magic, "MDFXIPC4", 8) == 0};
       int can = 1;
       if (!same && their >= 0) HIPC(hipDeviceCanAccessPeer(&can, mine.device, their));
       const std::string why = ipc_peer_problem(me, them, p.rank, can != 0);
@@ -213,7 +234,9 @@ class IpcTransport final : public Transport {
           HIPC(hipIpcOpenMemHandle(&q, r.buf[b], hipIpcMemLazyEnablePeerAccess));
           p.buf[b] = q;
         }
-        p.face_off = r.face_off[1 - side];  // the neighbour's face that borders me
+        p.face = halo_span(self_, 0, side, nranks_);  // its geometry as my ghost receives it ...
+        p.face.stride = r.face_stride[side ^ 1];      // ... read at the neighbour's pitch
+        p.face_off = r.face_off[side ^ 1];
       } else {
         HIPC(hipIpcOpenMemHandle(&p.mbox, r.mbox, hipIpcMemLazyEnablePeerAccess));
       }
@@ -248,23 +271,41 @@ class IpcTransport final : public Transport {
       HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
     };
     if (direct_) {
+      // one pair of faces: the lo side's pull on the halo stream, the hi side's on the aux stream
+      auto phase = [&](int s0, int ready) {
+        const bool two = peers_[s0].rank >= 0 && peers_[s0 + 1].rank >= 0;
+        if (two) {
+          HIPC(hipEventRecord(ev_fork_, hs));
+          HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
+        }
+        for (int side = s0; side < s0 + 2; ++side) {
+          const Peer& p = peers_[side];
+          if (p.rank < 0) continue;
+          const HaloSpan mine = halo_span(self_, b, side, nranks_);
+          MDFX_CHECK(mine.peer == p.rank, "ipc: neighbour mismatch");
+          hipStream_t ps = two && side == s0 + 1 ? aux_ : hs;
+          hip_counter_wait((const uint64_t*)p.ctr + ready, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
+          hip_face_copy(mine.recv, mine, (const char*)p.buf[b] + p.face_off, p.face, ps, copy_);
+          hip_counter_signal(ctr_ + kPulled + side, ps);
+        }
+        if (two) {
+          HIPC(hipEventRecord(ev_join_, aux_));
+          HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
+        }
+      };
       hip_counter_signal(ctr_ + kReady, hs);
-      fork();
-      for (int side = 0; side < 2; ++side) {
-        const Peer& p = peers_[side];
-        if (p.rank < 0) continue;
-        const HaloSpan mine = halo_span(self_, b, side, nranks_);
-        MDFX_CHECK(mine.bytes == face_ && mine.peer == p.rank, "ipc: face geometry mismatch");
-        hipStream_t ps = pull_stream(side);
-        hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
-        hip_face_copy(mine.recv, (const char*)p.buf[b] + p.face_off, face_, ps, copy_);
-        hip_counter_signal(ctr_ + kPulled + side, ps);
+      if (pencil_) {
+        // y faces first; readyZ tells the z neighbours my y ghost rows (inside my z faces) landed
+        phase(2, kReady);
+        hip_counter_signal(ctr_ + kReadyZ, hs);
+        phase(0, kReadyZ);
+      } else {
+        phase(0, kReady);
       }
-      join();
-      for (int side = 0; side < 2; ++side) {
+      for (int side = 0; side < 4; ++side) {
         const Peer& p = peers_[side];
         if (p.rank < 0) continue;
-        hip_counter_wait((const uint64_t*)p.ctr + kPulled + (1 - side), ctr_ + kExpPulled + side, timeout_s_, hs, 0,
+        hip_counter_wait((const uint64_t*)p.ctr + kPulled + (side ^ 1), ctr_ + kExpPulled + side, timeout_s_, hs, 0,
                          &words_);
       }
       if (!capturing) last_b_ = b;
@@ -324,6 +365,7 @@ class IpcTransport final : public Transport {
     void* mbox = nullptr;
     void* buf[2] = {nullptr, nullptr};  // the neighbour's field buffers (direct protocol)
     uint64_t face_off = 0;              // byte offset of its face that borders this slab
+    HaloSpan face;                      // that face's geometry (width, height, the neighbour's stride)
     void* ctr = nullptr;
   };
   CallbackFns f_;
@@ -339,7 +381,8 @@ class IpcTransport final : public Transport {
   size_t face_ = 0;
   bool dev_ok_ = false;
   bool direct_ = false;
-  Peer peers_[2];
+  bool pencil_ = false;  // (z, y) pencil: y faces first, then the z faces (which carry the y ghosts)
+  Peer peers_[4];
   double timeout_s_ = 300.0;
 };
 

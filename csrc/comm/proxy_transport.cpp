@@ -1,5 +1,5 @@
-// Rank-proxy halo transport: ONE slab of an N-way slab decomposition, alone on one GPU, exchanging
-// with itself through the ipc transport's machinery.
+// Rank-proxy halo transport: ONE slab (or pencil) of an N-way decomposition, alone on one GPU,
+// exchanging with itself through the ipc transport's machinery.
 //
 // Purpose: measure on a single MI355X what each GPU of an N-GPU run does per step, which the
 // one-GPU pool cannot otherwise show (the whole-node bench is the driver's). The slab is exactly
@@ -35,7 +35,7 @@ namespace mdfx {
 namespace {
 
 // counter block layout as the ipc transport's (64-bit words on separate 128-B lines)
-constexpr int kReady = 0, kPulled = 16, kExpReady = 48, kExpPulled = 64;
+constexpr int kReady = 0, kPulled = 16, kExpReady = 48, kExpPulled = 64, kReadyZ = 96;
 constexpr size_t kCounterBytes = 128 * 8;
 
 class ProxyTransport final : public Transport {
@@ -65,10 +65,12 @@ class ProxyTransport final : public Transport {
     words_ = hip_words_alloc();
     face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
     direct_ = ipc_direct_ok(self_.lay.bytes());
+    pencil_ = self_.py > 1 && self_.lay.hy > 0;
+    MDFX_CHECK(direct_ || !pencil_, "proxy transport: a pencil needs the direct protocol (field buffers up to 1900 MiB "
+                                    "or MDFX_IPC_DIRECT=1)");
     // the first exchange(s) find their faces (direct) / mailbox slots free
     const uint64_t pulled0 = direct_ ? 1 : 2;
-    HIPC(hipMemcpy(ctr_ + kPulled + 0, &pulled0, 8, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(ctr_ + kPulled + 1, &pulled0, 8, hipMemcpyHostToDevice));
+    for (int side = 0; side < 4; ++side) HIPC(hipMemcpy(ctr_ + kPulled + side, &pulled0, 8, hipMemcpyHostToDevice));
     if (!direct_) {
       HIPC(hipMalloc(&mbox_, 4 * face_));
       HIPC(hipMemset(mbox_, 0, 4 * face_));
@@ -91,8 +93,27 @@ class ProxyTransport final : public Transport {
     HIPC(hipStreamIsCapturing(hs, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
     const uint64_t ahead = (!capturing && last_b_ == b) ? 1 : 0;
-    // the ipc transport's stream layout: the hi-side pull on a second stream, concurrent with the
-    // lo-side pull on the halo stream
+    // the ipc transport's stream layout: per pair of faces the hi-side pull on a second stream,
+    // concurrent with the lo-side pull on the halo stream
+    auto phase = [&](int s0, int ready) {
+      const bool both = halo_span(self_, b, s0, nranks_).peer >= 0 && halo_span(self_, b, s0 + 1, nranks_).peer >= 0;
+      if (both) {
+        HIPC(hipEventRecord(ev_fork_, hs));
+        HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
+      }
+      for (int side = s0; side < s0 + 2; ++side) {
+        const HaloSpan h = halo_span(self_, b, side, nranks_);
+        if (h.peer < 0) continue;
+        hipStream_t ps = both && side == s0 + 1 ? aux_ : hs;
+        hip_counter_wait(ctr_ + ready, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
+        hip_face_copy(h.recv, h, h.send, h, ps, copy_);
+        hip_counter_signal(ctr_ + kPulled + side, ps);
+      }
+      if (both) {
+        HIPC(hipEventRecord(ev_join_, aux_));
+        HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
+      }
+    };
     const bool both = halo_span(self_, b, 0, nranks_).peer >= 0 && halo_span(self_, b, 1, nranks_).peer >= 0;
     auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
     auto fork = [&]() {
@@ -107,20 +128,17 @@ class ProxyTransport final : public Transport {
     };
     if (direct_) {
       // the ipc direct sequence: ready, then per face wait + pull from the (own) field buffer +
-      // pulled, then the wait that frees the faces the next boundary kernels overwrite
+      // pulled, then the wait that frees the faces the next boundary kernels overwrite. A pencil
+      // pulls its y faces first and signals readyZ once they landed: its z faces carry those ghost rows
       hip_counter_signal(ctr_ + kReady, hs);
-      fork();
-      for (int side = 0; side < 2; ++side) {
-        const HaloSpan h = halo_span(self_, b, side, nranks_);
-        if (h.peer < 0) continue;
-        MDFX_CHECK(h.bytes == face_, "proxy: face geometry mismatch");
-        hipStream_t ps = pull_stream(side);
-        hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
-        hip_face_copy(h.recv, h.send, face_, ps, copy_);
-        hip_counter_signal(ctr_ + kPulled + side, ps);
+      if (pencil_) {
+        phase(2, kReady);
+        hip_counter_signal(ctr_ + kReadyZ, hs);
+        phase(0, kReadyZ);
+      } else {
+        phase(0, kReady);
       }
-      join();
-      for (int side = 0; side < 2; ++side) {
+      for (int side = 0; side < 4; ++side) {
         if (halo_span(self_, b, side, nranks_).peer < 0) continue;
         hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, 0, &words_);
       }
@@ -176,6 +194,7 @@ class ProxyTransport final : public Transport {
   size_t face_ = 0;
   bool ok_ = false;
   bool direct_ = false;
+  bool pencil_ = false;  // (z, y) pencil: y faces first, then the z faces
   int last_b_ = -1;
   double timeout_s_ = 300.0;
 };

@@ -168,7 +168,8 @@ class CallbackTransport final : public Transport {
  public:
   explicit CallbackTransport(CallbackFns f) : f_(std::move(f)) {}
   const char* name() const override { return "callback"; }
-  void setup(const std::vector<LocalSlab>& locals, int) override { require_slabs(locals, "callback / torch"); }
+  // pencils are fine: the callback reads halo_spans(), which lists the y faces first
+  void setup(const std::vector<LocalSlab>&, int) override {}
   void exchange(int b) override {
     if (f_.exchange) f_.exchange(b);
   }

@@ -203,6 +203,21 @@ void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode)
                       (hipStream_t)stream));
 }
 
+void hip_face_copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height, void* stream,
+                     int mode) {
+  if (mode < 0) mode = face_copy_mode();
+  HIPC(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height,
+                        mode == 1 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice, (hipStream_t)stream));
+}
+
+void hip_face_copy(void* dst, const HaloSpan& d, const void* src, const HaloSpan& s, void* stream, int mode) {
+  MDFX_CHECK(d.width == s.width && d.height == s.height, "halo face geometry mismatch between neighbours");
+  if (d.height <= 1)
+    hip_face_copy(dst, src, d.width, stream, mode);
+  else
+    hip_face_copy2d(dst, d.stride, src, s.stride, d.width, d.height, stream, mode);
+}
+
 HaloSpan halo_span(const LocalSlab& s, int b, int side, int nranks) {
   HaloSpan h;
   const FieldLayout& l = s.lay;

@@ -89,7 +89,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
       MDFX_CHECK(hip_supports_steps(spec_, s.lay, opt_.temporal),
                  format("no fused %d-step kernel for %s %s with nx=%lld (fused depths: 2 for every stencil "
                         "(box27 rows up to 1024 fp32 / 512 fp64); 3, 4 for the 3D 7-point; 3, 4, 6, 8 for the 2D stencils, "
-                        "also 12, 16 for Life)",
+                        "also 12, 16 for Life; pencils: 3, 4 fp32 / 3 fp64 for the 3D 7-point only)",
                         opt_.temporal, stencil_name(spec_.kind), dtype_name(spec_.dtype), (long long)global_.nx));
     // regions (storage planes); owned = [halo, halo + nzl). The boundary regions are the `halo`
     // planes at each end that the exchange sends: they are computed on the halo stream so the

@@ -81,6 +81,13 @@ void require_slabs(const std::vector<LocalSlab>& locals, const char* transport);
 // engines (hipMemcpyDeviceToDeviceNoCU: no CUs, lower bandwidth on one device), -1 the process
 // default (face_copy_mode(): MDFX_XCOPY=blit / sdma, blit unless set).
 void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode = -1);
+// The same for a 2-D face (a pencil's y face: `height` pieces of `width` bytes, each side at its own
+// pitch) ...
+void hip_face_copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height, void* stream,
+                     int mode = -1);
+// ... and the copy of span `s` (the sender's, data at `src`) into span `d` (the receiver's, at `dst`),
+// 1-D or 2-D by the spans' geometry.
+void hip_face_copy(void* dst, const HaloSpan& d, const void* src, const HaloSpan& s, void* stream, int mode = -1);
 int face_copy_mode();
 
 class Transport {

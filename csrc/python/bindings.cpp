@@ -126,6 +126,11 @@ py::dict layout_dict(const FieldLayout& l) {
   d["plane"] = l.plane;
   d["planes"] = l.planes();
   d["nzl"] = l.nzl();
+  d["y0"] = l.y0;
+  d["y1"] = l.y1;
+  d["hy"] = l.hy;
+  d["nyl"] = l.nyl();
+  d["rows"] = l.rows();
   d["bytes"] = l.bytes();
   d["esize"] = l.esize();
   d["dtype"] = dtype_name(l.dtype);
@@ -200,7 +205,7 @@ class PySolver {
            int nranks, std::vector<int> local_ranks, std::vector<int> devices,
            const std::string& transport, py::bytes unique_id, py::object callbacks, bool overlap,
            bool sync_debug, int residual_every, bool graph, double timeout_s, double r, double c0,
-           double c1, double c2, double c3, int temporal, bool ref_precision) {
+           double c1, double c2, double c3, int temporal, bool ref_precision, int pencil_py) {
     const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3, ref_precision);
     if (devices.size() == 1 && local_ranks.size() > 1) devices.assign(local_ranks.size(), devices[0]);
     if (devices.size() != local_ranks.size())
@@ -234,6 +239,7 @@ class PySolver {
     o.graph = graph;
     o.timeout_s = timeout_s;
     o.temporal = temporal;
+    o.py = pencil_py;
     py::gil_scoped_release nogil;  // RCCL comm init may block on peers
     s_.reset(new Solver(spec, Extent3{nx, ny, nz}, nranks, std::move(local_ranks), std::move(bes),
                         std::move(tr), o));
@@ -287,10 +293,10 @@ PYBIND11_MODULE(_mdfx, m) {
   m.def("ipc_direct_ok", [](size_t bytes) { return ipc_direct_ok(bytes); },
         "whether the ipc transport pulls straight from field buffers of this size (MDFX_IPC_DIRECT)");
   m.def("layout", [](int64_t nx, int64_t ny, int64_t nz, int64_t z0, int64_t z1, int halo,
-                     const std::string& dtype) {
-    return layout_dict(FieldLayout::make(Extent3{nx, ny, nz}, z0, z1, halo, dtype_from_name(dtype)));
+                     const std::string& dtype, int64_t y0, int64_t y1, int hy) {
+    return layout_dict(FieldLayout::make(Extent3{nx, ny, nz}, z0, z1, halo, dtype_from_name(dtype), y0, y1, hy));
   }, py::arg("nx"), py::arg("ny"), py::arg("nz"), py::arg("z0"), py::arg("z1"), py::arg("halo") = 1,
-        py::arg("dtype") = "f32");
+        py::arg("dtype") = "f32", py::arg("y0") = 0, py::arg("y1") = -1, py::arg("hy") = 0);
   m.def("slab_bounds", [](int64_t nz, int parts) {
     SlabDecomposition d(nz, parts);
     std::vector<std::pair<int64_t, int64_t>> out;
@@ -363,14 +369,14 @@ PYBIND11_MODULE(_mdfx, m) {
   py::class_<PySolver>(m, "Solver")
       .def(py::init<const std::string&, const std::string&, int64_t, int64_t, int64_t, int,
                     std::vector<int>, std::vector<int>, const std::string&, py::bytes, py::object,
-                    bool, bool, int, bool, double, double, double, double, double, double, int, bool>(),
+                    bool, bool, int, bool, double, double, double, double, double, double, int, bool, int>(),
            py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ny"), py::arg("nz"),
            py::arg("nranks"), py::arg("local_ranks"), py::arg("devices"), py::arg("transport"),
            py::arg("unique_id") = py::bytes(""), py::arg("callbacks") = py::none(),
            py::arg("overlap") = true, py::arg("sync_debug") = false, py::arg("residual_every") = 0,
            py::arg("graph") = false, py::arg("timeout_s") = 0.0, py::arg("r") = -1.0,
            py::arg("c0") = 0.25, py::arg("c1") = 0.05, py::arg("c2") = 0.025,
-           py::arg("c3") = 3.0 / 160.0, py::arg("temporal") = 1, py::arg("ref_precision") = false)
+           py::arg("c3") = 3.0 / 160.0, py::arg("temporal") = 1, py::arg("ref_precision") = false, py::arg("py") = 1)
       .def("close", &PySolver::close)
       .def("phase_times",
            [](PySolver& p) {
@@ -438,6 +444,7 @@ PYBIND11_MODULE(_mdfx, m) {
              d["profile"] = o.profile;
              d["temporal"] = o.temporal;
              d["min_rounds"] = o.min_rounds;
+             d["py"] = o.py;
              return d;
            })
       .def_property_readonly("num_local", [](PySolver& p) { return p.chk().num_local(); })
@@ -470,8 +477,12 @@ PYBIND11_MODULE(_mdfx, m) {
              ls.lay = s.layout(i);
              ls.buf[0] = s.buffer(i, 0);
              ls.buf[1] = s.buffer(i, 1);
+             ls.py = s.options().py;
              py::list out;
-             for (int side = 0; side < 2; ++side) {
+             // pencils: the y faces (sides 2, 3: height pieces of width bytes, stride apart) come
+             // first; the z faces (0, 1) carry the y ghost rows, so they go once those have landed
+             const std::vector<int> sides = ls.py > 1 ? std::vector<int>{2, 3, 0, 1} : std::vector<int>{0, 1};
+             for (int side : sides) {
                const HaloSpan h = halo_span(ls, b, side, s.nranks());
                py::dict d;
                d["side"] = side;
@@ -479,6 +490,9 @@ PYBIND11_MODULE(_mdfx, m) {
                d["send"] = (uintptr_t)h.send;
                d["recv"] = (uintptr_t)h.recv;
                d["bytes"] = h.bytes;
+               d["width"] = h.width;
+               d["height"] = h.height;
+               d["stride"] = h.stride;
                out.append(d);
              }
              return out;
@@ -488,7 +502,7 @@ PYBIND11_MODULE(_mdfx, m) {
              Solver& s = p.chk();
              const FieldLayout& l = s.layout(i);
              return make_dlpack(s.buffer(i, b), s.backend(i).device(), l.dtype,
-                                {l.planes(), l.global.ny, l.pitch}, {l.plane, l.pitch, 1});
+                                {l.planes(), l.rows(), l.pitch}, {l.plane, l.pitch, 1});
            })
       .def("bytes_view",
            [](PySolver& p, int i, uintptr_t ptr, int64_t nbytes) {
@@ -499,7 +513,7 @@ PYBIND11_MODULE(_mdfx, m) {
            [](PySolver& p, int i) {
              Solver& s = p.chk();
              const FieldLayout& l = s.layout(i);
-             py::array a(np_dtype(l.dtype), std::vector<int64_t>{l.nzl(), l.global.ny, l.global.nx});
+             py::array a(np_dtype(l.dtype), std::vector<int64_t>{l.nzl(), l.nyl(), l.global.nx});
              void* dst = a.mutable_data();
              {
                py::gil_scoped_release nogil;

@@ -35,13 +35,21 @@ from .parallel.decomp import slab_bounds
 from .parallel.dist import ControlPlane, TorchP2PTransport, broadcast_bytes, group_for, is_distributed
 
 
-def auto_temporal(problem: Problem, nranks: int, device: str) -> int:
+def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1) -> int:
     """Fused steps per sweep chosen like the CLIs' auto mode: the deepest fused kernel that exists on
     this device (``hip_fused_depth``: 3 for the 3D 7-point at 1024-cell rows, else 2 for the 3D
     stencils, 8 for the 2D MDF, 12 for Life), made shallower until every slab is at least 4 sweeps
     deep; 1 on the CPU, where fused sweeps bring nothing."""
     if device != "hip":
         return 1
+    if py > 1:
+        # pencils: the fused 7-point sweep (heat7_wxk, K = 4 fp32 / 3 fp64) is the one that takes
+        # y ghost rows; the other stencils step singly
+        if problem.kind != "heat7":
+            return 1
+        want = 4 if problem.dtype == "f32" else 3
+        pz = nranks // py
+        return want if problem.nz >= 4 * want * pz and problem.ny >= 4 * want * py else 1
     want = native().hip_fused_depth(problem.kind, problem.dtype, problem.nx, problem.ref_precision)
     while want > 1 and problem.nz < 4 * want * nranks:
         want = 2 if want == 3 else want // 2
@@ -67,7 +75,7 @@ class Simulation:
                  devices: Optional[Sequence[int]] = None, transport: str = "auto",
                  distributed: Optional[bool] = None, overlap: bool = True, sync_debug: bool = False,
                  residual_every: int = 0, graph: bool = False, timeout_s: float = 0.0,
-                 temporal: int = 1, group=None, proxy_rank: Optional[int] = None):
+                 temporal: int = 1, group=None, proxy_rank: Optional[int] = None, py: int = 1):
         self.problem = problem
         if device == "auto":
             device = "hip" if hip_available() else "cpu"
@@ -154,16 +162,18 @@ class Simulation:
                 args["unique_id"] = native().rccl_unique_id()
 
         self.nranks = nranks
+        self.py = int(py)
         if temporal <= 0:
-            temporal = auto_temporal(problem, nranks, device)
+            temporal = auto_temporal(problem, nranks, device, int(py))
         self._s = native().Solver(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                   nranks, local_ranks, dev_list, overlap=overlap,
                                   sync_debug=sync_debug, residual_every=residual_every, graph=graph,
-                                  timeout_s=timeout_s, temporal=temporal, **problem.coef_kwargs(), **args)
+                                  timeout_s=timeout_s, temporal=temporal, py=int(py),
+                                  **problem.coef_kwargs(), **args)
         if self._torch_transport is not None:
             self._torch_transport.solver = self._s
         self.transport = self._s.transport_name if self._torch_transport is None else "torch"
-        self.bounds = slab_bounds(problem.nz, nranks)
+        self.bounds = slab_bounds(problem.nz, nranks // max(1, self.py))
 
     # ---- lifecycle -------------------------------------------------------------------------
     def close(self):
@@ -270,14 +280,15 @@ class Simulation:
         return self._s.layout(i)
 
     def read_local(self, i: int = 0) -> np.ndarray:
-        """Owned planes of local slab i as a dense (nzl, ny, nx) numpy array."""
+        """Owned cells of local part i as a dense (nzl, nyl, nx) numpy array (nyl = ny for slabs)."""
         return self._s.read_owned(i)
 
     def write_local(self, i: int, a: np.ndarray):
         self._s.write_owned(i, np.ascontiguousarray(a))
 
     def view(self, i: int = 0, current: bool = True) -> torch.Tensor:
-        """Zero-copy torch view (planes, ny, pitch) of a slab buffer (ghosts included)."""
+        """Zero-copy torch view (planes, rows, pitch) of a part's buffer (ghost planes and, for
+        pencils, ghost rows included)."""
         b = self._s.current_index if current else 1 - self._s.current_index
         t = torch.from_dlpack(self._s.view(i, b))
         t._mdfx_owner = self  # keep the engine alive while the view is
@@ -286,15 +297,23 @@ class Simulation:
     def gather(self) -> np.ndarray:
         """The whole global grid (nz, ny, nx) as numpy, on every caller.
 
-        In-process: concatenation of the local slabs. Distributed: all_gather_object over the
-        control group (debug / test sized grids only).
+        Each part lands at its (z0:z1, y0:y1) block, so slabs and pencils gather alike. In-process:
+        the local parts; distributed: all_gather_object over the control group (debug / test sized
+        grids only).
         """
-        parts = [self.read_local(i) for i in range(self.num_local)]
+        parts = []
+        for i in range(self.num_local):
+            lay = self._s.layout(i)
+            parts.append((lay["z0"], lay["z1"], lay["y0"], lay["y1"], self.read_local(i)))
         if self.distributed:
             allp: List = [None] * dist.get_world_size(self.group)
             dist.all_gather_object(allp, parts[0], group=self.group)
             parts = allp
-        return np.concatenate(parts, axis=0)
+        p = self.problem
+        out = np.empty((p.nz, p.ny, p.nx), dtype=parts[0][4].dtype)
+        for z0, z1, y0, y1, a in parts:
+            out[z0:z1, y0:y1] = a
+        return out
 
     def save_checkpoint(self, path: str):
         self._s.save_checkpoint(path)

@@ -36,3 +36,18 @@ def owner(gz: int, nz: int, parts: int) -> int:
 def neighbors(rank: int, parts: int) -> Tuple[int, int]:
     """(lower, upper) neighbour slab of ``rank``; -1 at the global boundary."""
     return (rank - 1 if rank > 0 else -1, rank + 1 if rank + 1 < parts else -1)
+
+
+def pencil_bounds(nz: int, ny: int, pz: int, py: int) -> List[Tuple[Tuple[int, int], Tuple[int, int]]]:
+    """((z0, z1), (y0, y1)) of every rank of a pz x py (z, y) pencil decomposition (mirrors
+    ``mdfx::PencilDecomposition``): rank r = rz * py + ry; its z neighbours are r -/+ py, its y
+    neighbours r -/+ 1."""
+    zs, ys = slab_bounds(nz, pz), slab_bounds(ny, py)
+    return [(zs[r // py], ys[r % py]) for r in range(pz * py)]
+
+
+def pencil_neighbors(rank: int, pz: int, py: int) -> Tuple[int, int, int, int]:
+    """(z-lower, z-upper, y-lower, y-upper) neighbour of ``rank``; -1 at the global boundary."""
+    rz, ry = divmod(rank, py)
+    return (rank - py if rz > 0 else -1, rank + py if rz + 1 < pz else -1,
+            rank - 1 if ry > 0 else -1, rank + 1 if ry + 1 < py else -1)

@@ -154,23 +154,41 @@ class TorchP2PTransport:
     def _bytes(self, ptr: int, n: int) -> torch.Tensor:
         return torch.from_dlpack(self.solver.bytes_view(0, ptr, n))
 
+    def _face(self, sp: dict, key: str) -> torch.Tensor:
+        """The span's send or recv cells as a (height, width) byte view: z faces are one
+        contiguous piece, pencil y faces `height` rows of planes `stride` bytes apart."""
+        h, w, st = sp.get("height", 1), sp.get("width", sp["bytes"]), sp.get("stride", sp["bytes"])
+        flat = self._bytes(sp[key], (h - 1) * st + w)
+        return flat.as_strided((h, w), (st, 1))
+
     def exchange(self, b: int) -> None:
         s = self.solver
         spans = [sp for sp in s.halo_spans(0, b) if sp["peer"] >= 0]
         if not spans:
             return
+        # pencils: the y faces first, then the z faces, which carry the y ghost rows just received
+        # (the edge / corner cells of the 27-point stencil)
+        for ph in ([sp for sp in spans if sp["side"] >= 2], [sp for sp in spans if sp["side"] < 2]):
+            if ph:
+                self._exchange_phase(ph)
+
+    def _exchange_phase(self, spans) -> None:
+        s = self.solver
         dev = s.device(0)
         if dev >= 0 and self.staged:
             self._exchange_staged(spans)
             return
         ctx = torch.cuda.stream(torch.cuda.ExternalStream(s.halo_stream(0))) if dev >= 0 else _null()
         with ctx:
-            ops = []
+            ops, unpack = [], []
             for sp in spans:
-                recv = self._bytes(sp["recv"], sp["bytes"])
-                send = self._bytes(sp["send"], sp["bytes"])
+                send, recv = self._face(sp, "send"), self._face(sp, "recv")
+                if not recv.is_contiguous():
+                    tmp = torch.empty(recv.shape, dtype=recv.dtype, device=recv.device)
+                    unpack.append((recv, tmp))
+                    recv = tmp
                 ops.append(dist.P2POp(dist.irecv, recv, sp["peer"], self.group))
-                ops.append(dist.P2POp(dist.isend, send, sp["peer"], self.group))
+                ops.append(dist.P2POp(dist.isend, send.contiguous(), sp["peer"], self.group))
             if dev >= 0:
                 # one NCCL (= RCCL) group for all faces: no pairwise ordering hazards
                 reqs = dist.batch_isend_irecv(ops)
@@ -178,6 +196,8 @@ class TorchP2PTransport:
                 reqs = [op.op(op.tensor, op.peer, op.group) for op in ops]
             for r in reqs:
                 r.wait()
+            for dst, tmp in unpack:
+                dst.copy_(tmp)
 
     def _exchange_staged(self, spans) -> None:
         s = self.solver
@@ -185,8 +205,8 @@ class TorchP2PTransport:
         hs.synchronize()  # the boundary kernels that produced the faces are done
         sends, recvs, reqs = [], [], []
         for sp in spans:
-            sends.append(self._bytes(sp["send"], sp["bytes"]).cpu())
-            recvs.append(torch.empty(sp["bytes"], dtype=torch.uint8))
+            sends.append(self._face(sp, "send").cpu().contiguous())
+            recvs.append(torch.empty((sp.get("height", 1), sp.get("width", sp["bytes"])), dtype=torch.uint8))
         for sp, snd, rcv in zip(spans, sends, recvs):
             reqs.append(dist.irecv(rcv, src=sp["peer"], group=self.group))
             reqs.append(dist.isend(snd, dst=sp["peer"], group=self.group))
@@ -194,7 +214,7 @@ class TorchP2PTransport:
             r.wait()
         with torch.cuda.stream(hs):
             for sp, rcv in zip(spans, recvs):
-                self._bytes(sp["recv"], sp["bytes"]).copy_(rcv, non_blocking=False)
+                self._face(sp, "recv").copy_(rcv, non_blocking=False)
         hs.synchronize()
 
     def allreduce_sum(self, v: float) -> float:

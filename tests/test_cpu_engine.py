@@ -530,3 +530,83 @@ def test_warm_kernels_is_a_noop_on_cpu():
         before = sim.gather()
         sim.warm_kernels(7)
         assert np.array_equal(before, sim.gather())
+
+
+# ---- (z, y) pencil decomposition on the CPU backend ------------------------------------------
+@pytest.mark.parametrize("kind", ["heat7", "box27"])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("ranks,py", [(4, 2), (8, 2), (8, 4), (6, 3), (2, 2)])
+@pytest.mark.parametrize("temporal", [1, 2, 3])
+def test_pencil_bitwise_equals_single_rank(mdfx, kind, dtype, ranks, py, temporal):
+    # pz x py pencils (2x2, 4x2, 2x4, 2x3, 1x2): two-phase exchange (y faces, then z faces with the
+    # y ghost rows, which carries the edge / corner cells box27 reads) must reproduce P = 1 bitwise
+    prob = (m.heat3d if kind == "heat7" else m.box27)(nx=20, ny=18, nz=16, dtype=dtype)
+    with m.Simulation(prob, device="cpu") as sim:
+        ref = sim.init().run(7).gather()
+    with m.Simulation(prob, device="cpu", ranks=ranks, py=py, temporal=temporal) as sim:
+        sim.init().run(7)
+        assert sim.options["py"] == py
+        assert np.array_equal(sim.gather(), ref)
+
+
+def test_pencil_layouts_and_neighbours(mdfx):
+    from mpi_cuda_process_amd.parallel.decomp import pencil_bounds, pencil_neighbors
+    prob = m.heat3d(nx=12, ny=11, nz=9)
+    with m.Simulation(prob, device="cpu", ranks=6, py=3, temporal=2) as sim:
+        want = pencil_bounds(9, 11, 2, 3)
+        for r in range(6):
+            lay = sim.layout(r)
+            (z0, z1), (y0, y1) = want[r]
+            assert (lay["z0"], lay["z1"], lay["y0"], lay["y1"]) == (z0, z1, y0, y1)
+            assert lay["hy"] == lay["halo"] == 2 and lay["nyl"] == y1 - y0
+            assert lay["rows"] == lay["nyl"] + 2 * lay["hy"]
+            assert lay["plane"] == lay["pitch"] * lay["rows"]
+            assert sim.read_local(r).shape == (z1 - z0, y1 - y0, 12)
+            assert tuple(sim.view(r).shape) == (lay["planes"], lay["rows"], lay["pitch"])
+    assert pencil_neighbors(0, 2, 3) == (-1, 3, -1, 1)
+    assert pencil_neighbors(4, 2, 3) == (1, -1, 3, 5)
+    assert pencil_neighbors(5, 2, 3) == (2, -1, 4, -1)
+
+
+def test_pencil_overlap_residual_and_sync_debug(mdfx):
+    prob = m.box27(nx=18, ny=16, nz=14)
+    outs, res = [], []
+    for kw in (dict(overlap=True), dict(overlap=False), dict(sync_debug=True)):
+        with m.Simulation(prob, device="cpu", ranks=4, py=2, residual_every=3, **kw) as sim:
+            sim.init().run(6)
+            outs.append(sim.gather())
+            res.append(sim.residual)
+    with m.Simulation(prob, device="cpu", residual_every=3) as sim:
+        sim.init().run(6)
+        want = sim.residual
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
+    assert all(abs(r - want) <= 1e-12 * max(1.0, want) for r in res)
+
+
+def test_pencil_checkpoint_redecomposes(mdfx, tmp_path):
+    # pencils -> slabs -> other pencils: every load gathers the row blocks it owns from any layout
+    prob = m.heat3d(nx=14, ny=12, nz=10)
+    with m.Simulation(prob, device="cpu") as sim:
+        ref = sim.init().run(9).gather()
+    with m.Simulation(prob, device="cpu", ranks=4, py=2) as sim:
+        sim.init().run(3)
+        sim.save_checkpoint(str(tmp_path / "a"))
+    hdr = json.load(open(os.path.join(tmp_path, "a", "slab_3.json")))
+    assert (hdr["y0"], hdr["y1"]) == (6, 12)
+    with m.Simulation(prob, device="cpu", ranks=3) as sim:
+        sim.load_checkpoint(str(tmp_path / "a"))
+        sim.run(3)
+        sim.save_checkpoint(str(tmp_path / "b"))
+    with m.Simulation(prob, device="cpu", ranks=6, py=3, temporal=2) as sim:
+        sim.load_checkpoint(str(tmp_path / "b"))
+        sim.run(3)
+        assert np.array_equal(sim.gather(), ref)
+
+
+def test_pencil_bad_configs_rejected(mdfx):
+    with pytest.raises(RuntimeError):
+        m.Simulation(m.heat3d(n=8), device="cpu", ranks=6, py=4)  # py must divide the rank count
+    with pytest.raises(RuntimeError):
+        m.Simulation(m.heat3d(nx=8, ny=3, nz=8), device="cpu", ranks=4, py=4)  # too few rows
+    with pytest.raises(RuntimeError):
+        m.Simulation(m.mdf2d(h=16, w=16), device="cpu", ranks=2, py=2)  # 2D grids have one row

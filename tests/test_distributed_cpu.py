@@ -22,7 +22,7 @@ import mpi_cuda_process_amd as m
 from mpi_cuda_process_amd.parallel.dist import init_distributed
 env = init_distributed("gloo")
 prob = %(prob)s
-with m.Simulation(prob, device="cpu", distributed=True, transport="torch", residual_every=3) as sim:
+with m.Simulation(prob, device="cpu", distributed=True, transport="torch", residual_every=3%(kw)s) as sim:
     sim.init()
     sim.run(7)
     g = sim.gather()
@@ -43,13 +43,13 @@ def _free_port():
     return p
 
 
-def _launch(world, prob_src, out):
+def _launch(world, prob_src, out, kw=""):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2")
-        procs.append(subprocess.Popen([sys.executable, "-c", WORKER % dict(root=ROOT, prob=prob_src, out=out)],
+        procs.append(subprocess.Popen([sys.executable, "-c", WORKER % dict(root=ROOT, prob=prob_src, out=out, kw=kw)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = []
     for p in procs:
@@ -83,6 +83,26 @@ def test_gloo_multiprocess_matches_single(mdfx, tmp_path, world, prob_src):
 
     meta = json.load(open(out + ".json"))
     assert meta["transport"] == "torch" and meta["nranks"] == world
+    assert abs(meta["residual"] - ref_res) < 1e-9 * max(1.0, ref_res)
+
+
+@pytest.mark.parametrize("world,py,prob_src", [(4, 2, "m.box27(nx=14, ny=12, nz=10)"),
+                                               (4, 4, "m.heat3d(nx=16, ny=13, nz=9)"),
+                                               (2, 2, "m.heat3d(nx=10, ny=12, nz=7, dtype='f64')")])
+def test_gloo_multiprocess_pencils_match_single(mdfx, tmp_path, world, py, prob_src):
+    # one process per pencil: y faces as strided (height, width) byte views over gloo, then z faces
+    import json
+
+    import mpi_cuda_process_amd as m
+
+    out = str(tmp_path / "g.npy")
+    _launch(world, prob_src, out, kw=", py=%d, temporal=2" % py)
+    prob = eval(prob_src)
+    with m.Simulation(prob, device="cpu", residual_every=3) as sim:
+        ref = sim.init().run(7).gather()
+        ref_res = sim.residual
+    assert np.array_equal(np.load(out), ref)
+    meta = json.load(open(out + ".json"))
     assert abs(meta["residual"] - ref_res) < 1e-9 * max(1.0, ref_res)
 
 
@@ -152,6 +172,10 @@ def test_bench_self_launches_8_ranks_cpu(mdfx):
     assert cfg["gate"]["passed"] and all(r["passed"] for r in cfg["gate"]["runs"])
     assert cfg["gate"]["runs"][0]["grid"][2] % 8 == 0
     assert "timed_vs_trial" in cfg and rec["steps"] == 4 and rec["value"] > 0
+    # slabs (z8) and 4 x 2 pencils are both gated and timed; the faster one is reported
+    assert sorted({r["py"] for r in cfg["gate"]["runs"]}) == [1, 2]
+    assert sorted({t["py"] for t in cfg["trials"]}) == [1, 2]
+    assert cfg["py"] in (1, 2) and cfg["parallelism"].startswith("slab-z8" if cfg["py"] == 1 else "pencil-z4y2")
 
 
 def test_bench_json_reports_effective_graph_mode(mdfx):

@@ -286,3 +286,48 @@ def test_mdf_ref_precision_gpu_equals_cpu(hip, ranks):
             out[dev] = (sim.gather(), sim.residual)
     assert np.array_equal(out["cpu"][0], out["hip"][0])
     assert abs(out["cpu"][1] - out["hip"][1]) <= 1e-9 * out["cpu"][1]
+
+
+# ---- (z, y) pencils, virtual ranks on one GPU (loopback transport) ----------------------------
+@pytest.mark.parametrize("ranks,py", [(4, 2), (8, 2), (8, 4)])
+@pytest.mark.parametrize("temporal", [1, 3, 4])
+@pytest.mark.parametrize("graph", [False, True])
+def test_pencil_loopback_bitwise_equals_single_rank(hip, ranks, py, temporal, graph):
+    # 2x2 / 4x2 / 2x4 pencils: the y faces as 2-D copies, the z faces after the y pulls of the z
+    # neighbour; the fused heat7_wxk sweep over the pencil's row range (K = 3, 4)
+    prob = m.heat3d(nx=1024, ny=88, nz=72)
+    with m.Simulation(prob, device="hip") as sim:
+        ref = sim.init().run(9).gather()
+    with m.Simulation(prob, device="hip", ranks=ranks, py=py, temporal=temporal, graph=graph) as sim:
+        sim.init()
+        sim.prepare_graphs()
+        sim.run(9)
+        assert np.array_equal(sim.gather(), ref)
+
+
+@pytest.mark.parametrize("prob,temporal", [(m.box27(nx=130, ny=44, nz=36), 1),
+                                           (m.box27(nx=130, ny=44, nz=36, dtype="f64"), 1),
+                                           (m.heat3d(nx=200, ny=51, nz=40, dtype="f64"), 1),
+                                           (m.heat3d(nx=200, ny=51, nz=40, dtype="f64"), 3),
+                                           (m.heat3d(nx=200, ny=51, nz=40), 3)],
+                         ids=["box27-f32", "box27-f64", "heat7-f64", "heat7-f64-k3", "heat7-f32-k3"])
+def test_pencil_loopback_other_stencils(hip, prob, temporal):
+    with m.Simulation(prob, device="hip", residual_every=3) as sim:
+        ref = sim.init().run(7).gather()
+        rres = sim.residual
+    with m.Simulation(prob, device="hip", ranks=6, py=3, temporal=temporal, residual_every=3) as sim:
+        sim.init().run(7)
+        assert np.array_equal(sim.gather(), ref)
+        assert abs(sim.residual - rres) <= 1e-9 * rres
+
+
+def test_pencil_headline_shape_matches_slabs(hip):
+    # the 1024^3 fp32 grid as 4 x 2 pencils (520-row pencils: the fused sweep's band / z-chunk
+    # geometry at the N = 8 shape) against the slab split of the same ranks
+    prob = m.heat3d(n=1024)
+    outs = []
+    for py in (1, 2):
+        with m.Simulation(prob, device="hip", ranks=8, py=py, temporal=4) as sim:
+            sim.init().run(8)
+            outs.append(sim.gather())
+    assert np.array_equal(outs[0], outs[1])

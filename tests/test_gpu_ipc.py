@@ -32,7 +32,7 @@ env = init_distributed("gloo")
 torch.cuda.set_device(0)
 prob = %(prob)s
 with m.Simulation(prob, device="hip", distributed=True, transport=%(transport)r, residual_every=4,
-                  temporal=%(temporal)d, devices=[0], graph=%(graph)s, timeout_s=60.0) as sim:
+                  temporal=%(temporal)d, devices=[0], graph=%(graph)s, timeout_s=60.0, py=%(py)d) as sim:
     assert sim.transport == %(transport)r, sim.transport
     sim.init()
     sim.run(%(steps)d)
@@ -97,7 +97,7 @@ def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
     prob_src = "m.heat3d(nx=256, ny=40, nz=47)"
     out = str(tmp_path / "g.npy")
     steps = 13
-    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
+    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
                          transport="ipc")
     _spawn(world, lambda r: [sys.executable, "-c", code])
     got = np.load(out)
@@ -118,11 +118,35 @@ def test_ipc_protocols_and_copy_engines(hip, tmp_path, transport, direct, world,
     prob_src = "m.heat3d(nx=256, ny=40, nz=47)"
     out = str(tmp_path / "g.npy")
     steps = 13
-    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
+    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
                          transport=transport)
     _spawn(world, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_IPC_DIRECT": direct})
     import mpi_cuda_process_amd as m  # noqa: F401 (eval below)
 
+    ref, rres = _reference(eval(prob_src), steps)
+    assert np.array_equal(np.load(out), ref)
+    meta = json.load(open(out + ".json"))
+    assert abs(meta["residual"] - rres) <= 1e-9 * rres
+
+
+@pytest.mark.parametrize("world,py,temporal,graph,transport,prob_src", [
+    (4, 2, 4, False, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),   # 2 x 2 pencils, the fused K = 4 sweep
+    (4, 2, 3, True, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),    # ... K = 3, replayed
+    (4, 4, 4, True, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),    # 1 x 4 (y neighbours only)
+    (6, 2, 2, False, "ipc_sdma", "m.heat3d(nx=130, ny=41, nz=44)"),  # 3 x 2, 2-D pulls on the SDMA engines
+    (4, 2, 1, False, "ipc", "m.box27(nx=130, ny=41, nz=40, dtype='f64')"),  # edge / corner ghosts
+])
+def test_ipc_pencils_match_single(hip, tmp_path, world, py, temporal, graph, transport, prob_src):
+    """(z, y) pencils, one process each, sharing the GPU: the y faces pulled as 2-D copies out of
+    the neighbours' field buffers, then the z faces (carrying the fresh y ghost rows) once the z
+    neighbours signal readyZ. Bitwise equal to one process, residual included."""
+    import mpi_cuda_process_amd as m
+
+    out = str(tmp_path / "g.npy")
+    steps = 11
+    code = WORKER % dict(py=py, root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
+                         transport=transport)
+    _spawn(world, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_IPC_DIRECT": "1"})
     ref, rres = _reference(eval(prob_src), steps)
     assert np.array_equal(np.load(out), ref)
     meta = json.load(open(out + ".json"))
@@ -135,7 +159,7 @@ def test_ipc_other_stencils(hip, tmp_path, prob_src):
     import mpi_cuda_process_amd as m
 
     out = str(tmp_path / "g.npy")
-    code = WORKER % dict(root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=9, transport="ipc")
+    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=9, transport="ipc")
     _spawn(3, lambda r: [sys.executable, "-c", code])
     ref, _ = _reference(eval(prob_src), 9)
     assert np.array_equal(np.load(out), ref)

@@ -53,6 +53,30 @@ def test_proxy_slab_matches_full_grid_away_from_boundaries(hip, monkeypatch, n, 
     assert np.array_equal(got[lo:(z1 - z0) - hi], full[z0 + lo:z1 - hi])
 
 
+@pytest.mark.parametrize("n,py,r,temporal,graph", [(8, 2, 3, 4, True), (8, 2, 4, 3, False), (8, 4, 5, 4, True),
+                                                    (4, 2, 0, 2, False)])
+def test_proxy_pencil_matches_full_grid_away_from_boundaries(hip, n, py, r, temporal, graph):
+    """A (z, y) pencil of a pz x py split (4 x 2, 2 x 4, 2 x 2) looped back: the y faces as 2-D
+    copies, then the z faces after the readyZ signal; exact wherever no proxied ghost can reach."""
+    from mpi_cuda_process_amd.parallel.decomp import pencil_neighbors
+
+    prob = m.heat3d(nx=1024 if temporal >= 3 else 256, ny=40 * py, nz=36 * (n // py))
+    steps = 6
+    full = _full(prob, steps, temporal)
+    with m.Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graph, py=py) as sim:
+        sim.init()
+        sim.prepare_graphs()
+        sim.run(steps)
+        got = sim.read_local(0)
+        lay = sim.layout(0)
+        if graph:
+            assert sim.graph_replays >= 1
+    zl, zh, yl, yh = (steps if q >= 0 else 0 for q in pencil_neighbors(r, n // py, py))
+    z0, z1, y0, y1 = lay["z0"], lay["z1"], lay["y0"], lay["y1"]
+    assert got.shape == (z1 - z0, y1 - y0, prob.nx)
+    assert np.array_equal(got[zl:(z1 - z0) - zh, yl:(y1 - y0) - yh], full[z0 + zl:z1 - zh, y0 + yl:y1 - yh])
+
+
 def test_bench_rank_proxy_json(hip):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--rank-proxy", "4", "--n", "256",
                         "--steps", "6", "--warmup", "3"], capture_output=True, timeout=300, cwd=ROOT)
