@@ -47,6 +47,10 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# hipGraph replay on one hardware queue (set before anything starts the HIP runtime; see
+# mpi_cuda_process_amd/__init__.py)
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1")
+
 import torch  # noqa: E402  (importing torch does not initialise the GPU)
 
 METRIC = "GCells/s (whole node), 3D 7-pt Jacobi 1024^3 fp32 at 1/2/4/8 MI355X"

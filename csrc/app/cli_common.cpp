@@ -166,6 +166,10 @@ void print_grid(const std::vector<char>& g, int64_t nx, int64_t ny, int64_t nz) 
 }  // namespace
 
 int run_cli(int argc, char** argv, const char* default_stencil, const char* prog) {
+  // one hardware queue for hipGraph execution (before the HIP runtime starts): see
+  // docs/DESIGN.md "hipGraph replay" - the multi-queue graph executor runs a captured cycle's
+  // branches 1.4-2x slower than eager launches, one queue matches them
+  setenv("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1", 0);
   try {
     Opts o = parse(argc, argv, prog);
     const ProcEnv env = detect_proc_env();

@@ -258,7 +258,7 @@ class IpcTransport final : public Transport {
     const bool capturing = cap != hipStreamCaptureStatusNone;
     // the two pulls: lo side on the halo stream, hi side on the aux stream (forked after the
     // publish / ready signal, joined back before the exchange ends)
-    const bool both = peers_[0].rank >= 0 && peers_[1].rank >= 0;
+    const bool both = concurrent_pulls() && peers_[0].rank >= 0 && peers_[1].rank >= 0;
     auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
     auto fork = [&]() {
       if (!both) return;
@@ -273,7 +273,7 @@ class IpcTransport final : public Transport {
     if (direct_) {
       // one pair of faces: the lo side's pull on the halo stream, the hi side's on the aux stream
       auto phase = [&](int s0, int ready) {
-        const bool two = peers_[s0].rank >= 0 && peers_[s0 + 1].rank >= 0;
+        const bool two = concurrent_pulls() && peers_[s0].rank >= 0 && peers_[s0 + 1].rank >= 0;
         if (two) {
           HIPC(hipEventRecord(ev_fork_, hs));
           HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
@@ -421,6 +421,13 @@ void ipc_enable_peer(int mine, int peer, int peer_rank) {
 
 // The direct protocol maps the neighbours' field buffers; torch's HIP 7.0 runtime stalls in
 // hipIpcOpenMemHandle from 2 GiB up, so only buffers of at most 1900 MiB (probed good) go direct.
+// Whether the two pulls of a pair of faces run on two streams (default) or one after the other on
+// the halo stream (MDFX_XPULL=serial; read per call).
+bool concurrent_pulls() {
+  const char* v = std::getenv("MDFX_XPULL");
+  return !(v && std::string(v) == "serial");
+}
+
 bool ipc_direct_ok(size_t field_bytes) {
   const char* v = std::getenv("MDFX_IPC_DIRECT");  // (read per call: tests switch it within a process)
   const int force = v && *v ? std::atoi(v) : -1;

@@ -149,6 +149,7 @@ std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode = -
 // copy per face) rather than through mailboxes (two): buffers of at most 1900 MiB, since torch's
 // HIP 7.0 runtime stalls mapping exported buffers of 2 GiB and more; MDFX_IPC_DIRECT=0 / 1 forces.
 bool ipc_direct_ok(size_t field_bytes);
+bool concurrent_pulls();
 // Rank proxy (HIP): ONE slab of an N-way decomposition alone on a GPU, exchanging with itself
 // through the ipc transport's mailbox copies and device counters (csrc/comm/proxy_transport.cpp):
 // the per-GPU schedule of an N-GPU run, measurable on one GPU. Ghost values are the slab's own

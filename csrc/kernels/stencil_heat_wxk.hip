@@ -60,7 +60,10 @@ int64_t resident_blocks(const void* kfn, int block);
 // DG: a diagnostic copy (MDFX_WXK_DIAG, timing only, results are garbage) whose `diag` bits drop
 // parts of the sweep to see where its time goes: 1 the window DMAs after the first plane, 2 the
 // output stores, 4 the per-plane barrier
-template <class T, int RY, int RE, int K, int WB, bool RES, bool DG = false>
+// PEN: the pencil copy (output rows [ly_begin, ly_end) of storage rows holding ghost rows, global
+// row = storage row + gy_off). Slabs run the copy without it: the four extra row bounds held in
+// scalars cost the slab sweep ~4 % (six more vmcnt(0) waits in front of window reads, round 4).
+template <class T, int RY, int RE, int K, int WB, bool RES, bool DG = false, bool PEN = false>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
                                                      int diag = 0) {
@@ -106,7 +109,8 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
   // rows: storage rows [0, ny) (a pencil's include ghost rows), output rows [ly0, ly1), global row =
   // storage row + gyoff of gny (slabs: ly0 = 0, ly1 = ny = gny, gyoff = 0)
-  const int ly0 = (int)g.ly_begin, ly1 = (int)g.ly_end, gyoff = (int)g.gy_off, gny = (int)g.gny;
+  const int ly0 = PEN ? (int)g.ly_begin : 0, ly1 = PEN ? (int)g.ly_end : ny, gyoff = PEN ? (int)g.gy_off : 0,
+            gny = PEN ? (int)g.gny : ny;
   const int yb = ly0 + yt * BR;                        // first row of the band
   const int y0 = yb + (w == 0 ? 0 : RE + (w - 1) * RY);  // first own row of this wave
   const int rown = (w == 0 || w == WB - 1) ? RE : RY;    // own rows of this wave
@@ -337,8 +341,19 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
             K, RY, RE, WB, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
+  const bool pen = g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny;
   if (resid) {
-    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid, 0);
+    if (pen)
+      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT,
+                         (int)ntasks, resid, 0);
+    else
+      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
+                         resid, 0);
+    return;
+  }
+  if (pen) {
+    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT,
+                       (int)ntasks, resid, 0);
     return;
   }
   if constexpr (sizeof(T) == 4 && RY == 3 && RE == 2 && K == 4 && WB == 8) {  // the headline shape only

@@ -21,7 +21,16 @@ Layout::
     lib/       libmdfx.so (native core: kernels, runtime, transports, engine)
 """
 
-from ._native import hip_available, native, require_hip  # noqa: F401  (imports torch first)
+import os as _os
+
+# hipGraph replay on ONE hardware queue. The HIP runtime's graph executor spreads a captured
+# cycle's parallel branches (interior sweep || boundary sweep + halo exchange) over several internal
+# queues, and the cross-queue dependencies made replayed cycles 1.4-2x slower than the same work
+# launched eagerly (bench/graph_probe.py, profiles/r04_session_c/); on one queue replay matches
+# eager. Read when the runtime starts, so it must be set before the first HIP call of the process.
+_os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "1")
+
+from ._native import hip_available, native, require_hip  # noqa: F401,E402  (imports torch first)
 from .engine import Simulation  # noqa: F401
 from .models import InitCondition, Problem, box27, from_name, heat3d, life2d, mdf2d  # noqa: F401
 from .ops import advance  # noqa: F401

@@ -133,7 +133,7 @@ def test_ipc_protocols_and_copy_engines(hip, tmp_path, transport, direct, world,
     (4, 2, 4, False, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),   # 2 x 2 pencils, the fused K = 4 sweep
     (4, 2, 3, True, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),    # ... K = 3, replayed
     (4, 4, 4, True, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),    # 1 x 4 (y neighbours only)
-    (6, 2, 2, False, "ipc_sdma", "m.heat3d(nx=130, ny=41, nz=44)"),  # 3 x 2, 2-D pulls on the SDMA engines
+    (6, 2, 3, False, "ipc_sdma", "m.heat3d(nx=130, ny=41, nz=44)"),  # 3 x 2, 2-D pulls on the SDMA engines
     (4, 2, 1, False, "ipc", "m.box27(nx=130, ny=41, nz=40, dtype='f64')"),  # edge / corner ghosts
 ])
 def test_ipc_pencils_match_single(hip, tmp_path, world, py, temporal, graph, transport, prob_src):
@@ -207,7 +207,7 @@ def test_ipc_dead_peer_is_an_error_not_a_hang(hip, tmp_path):
     reports a transport failure and exits non-zero instead of hanging."""
     out = str(tmp_path / "g.npy")
     code = WORKER.replace("timeout_s=60.0", "timeout_s=5.0") % dict(
-        root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=40, transport="ipc")
+        py=1, root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=40, transport="ipc")
     t0 = time.time()
     procs, outs = _spawn(2, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_FAULT": "exit@1:3"},
                          timeout=150, expect_ok=False)

@@ -177,10 +177,10 @@ def test_bench_rccl_bootstrap_hang_exits_nonzero(hip):
 
 @pytest.mark.timeout(300)
 def test_bench_auto_fallback_to_staged(hip):
-    """--transport auto when both device transports fail their gate (MDFX_FAULT=gate:rccl,ipc):
+    """--transport auto when every device transport fails its gate (MDFX_FAULT=gate:rccl,ipc,ipc_sdma):
     the host-staged transport is gated as a last resort and timed, and the JSON names it."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
-    env["MDFX_FAULT"] = "gate:rccl,ipc"
+    env["MDFX_FAULT"] = "gate:rccl,ipc,ipc_sdma"
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--n", "128",
                         "--steps", "4", "--warmup", "2", "--graph", "off"], env=env, capture_output=True, timeout=280,
                        cwd=ROOT)
@@ -189,4 +189,4 @@ def test_bench_auto_fallback_to_staged(hip):
     rec = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
     assert rec["config"]["transport"] == "torch" and rec["config"]["gate"]["passed"]
     runs = rec["config"]["gate"]["runs"]
-    assert [r["transport"] for r in runs] == ["rccl", "ipc", "staged"] and runs[-1]["passed"]
+    assert [r["transport"] for r in runs] == ["rccl", "ipc", "ipc_sdma", "staged"] and runs[-1]["passed"]

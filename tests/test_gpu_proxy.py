@@ -35,7 +35,7 @@ def test_proxy_slab_matches_full_grid_away_from_boundaries(hip, monkeypatch, n, 
     """(both ipc protocols: direct pulls / mailboxes; both copy engines: blit / SDMA)"""
     monkeypatch.setenv("MDFX_IPC_DIRECT", direct)
     prob = m.heat3d(nx=1024 if temporal >= 3 else 256, ny=24, nz=36 * n)
-    steps = 6
+    steps = 2 * temporal  # at least one replayed 2-sweep cycle at the full depth
     full = _full(prob, steps, temporal)
     with m.Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graph,
                       transport=transport) as sim:
@@ -54,7 +54,7 @@ def test_proxy_slab_matches_full_grid_away_from_boundaries(hip, monkeypatch, n, 
 
 
 @pytest.mark.parametrize("n,py,r,temporal,graph", [(8, 2, 3, 4, True), (8, 2, 4, 3, False), (8, 4, 5, 4, True),
-                                                    (4, 2, 0, 2, False)])
+                                                    (4, 2, 0, 3, False)])
 def test_proxy_pencil_matches_full_grid_away_from_boundaries(hip, n, py, r, temporal, graph):
     """A (z, y) pencil of a pz x py split (4 x 2, 2 x 4, 2 x 2) looped back: the y faces as 2-D
     copies, then the z faces after the readyZ signal; exact wherever no proxied ghost can reach."""
