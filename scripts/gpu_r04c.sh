@@ -16,6 +16,13 @@ if [[ $part == 1 ]]; then
   LIMIT=360 scripts/gpu_session.sh "pencil=python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu -k pencil tests/test_gpu_engine.py tests/test_gpu_proxy.py tests/test_gpu_ipc.py" || exit $?
   LIMIT=780 scripts/gpu_session.sh "gputests=python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu -k 'not pencil' tests" || exit $?
   grep -E "passed|failed" gpurun_out/pencil.log gpurun_out/gputests.log | tail -4
+  N1="--graph off --steps 50 --warmup 10"
+  Q4="--rank-proxy 4 --graph off --rounds 1 --steps 48 --warmup 5"
+  scripts/gpu_session.sh "n3_a=python ab_alt/bench.py $N1" "n4_a=python bench.py $N1" "n3_b=python ab_alt/bench.py $N1" "n4_b=python bench.py $N1" \
+    "q3=python ab_alt/bench.py $Q4" "q4=python bench.py $Q4" "q3b=python ab_alt/bench.py $Q4" "q4b=python bench.py $Q4" \
+    "b4=python bench.py $B" "p8=python bench.py $P8" "p8pen=python bench.py $P8 --py 2" "p4=python bench.py $P4" || exit $?
+  for f in n3_a n4_a n3_b n4_b q3 q4 q3b q4b b4 p8 p8pen p4; do
+    echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/$f.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$f.log | head -1)"; done
 elif [[ $part == 2 ]]; then
   scripts/gpu_session.sh "r4_p8pen=python bench.py $P8 --py 2" "r4_p8pen4=python bench.py $P8 --py 4" "r4_p4pen=python bench.py $P4 --py 2" \
     "r3_a=python ab_alt/bench.py $B" "r4_a=python bench.py $B" "r3_b=python ab_alt/bench.py $B" "r4_b=python bench.py $B" \

@@ -74,6 +74,41 @@ def kernel_resources(lib=None):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def kernel_isa(lib, mangled_prefix):
+    """Disassembly lines (instructions only) of the kernels whose mangled name starts with
+    `mangled_prefix`, keyed by mangled name."""
+    tmp = tempfile.mkdtemp(prefix="mdfx_isa_")
+    try:
+        local = os.path.join(tmp, os.path.basename(lib))
+        shutil.copy(lib, local)
+        subprocess.run([os.path.join(LLVM, "llvm-objdump"), "--offloading", local], cwd=tmp, check=True,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        out = {}
+        for f in sorted(os.listdir(tmp)):
+            if "gfx950" not in f:
+                continue
+            path = os.path.join(tmp, f)
+            syms = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "-s", path], stdout=subprocess.PIPE,
+                                  text=True, check=True).stdout
+            if mangled_prefix not in syms:
+                continue
+            dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", path], stdout=subprocess.PIPE,
+                                 text=True, check=True).stdout
+            cur = None
+            for line in dis.splitlines():
+                m = re.match(r"^[0-9a-f]+ <(.*)>:", line)
+                if m:
+                    cur = m.group(1) if m.group(1).startswith(mangled_prefix) else None
+                    if cur:
+                        out[cur] = []
+                    continue
+                if cur and line.strip():
+                    out[cur].append(line.split("//")[0].strip())
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--lib", default=None)

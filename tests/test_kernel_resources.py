@@ -9,7 +9,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
-from kernel_resources import kernel_resources  # noqa: E402
+from kernel_resources import kernel_isa, kernel_resources  # noqa: E402
 
 LIB = os.path.join(ROOT, "mpi_cuda_process_amd", "lib", "libmdfx.so")
 
@@ -51,11 +51,12 @@ def test_lds_never_limits_occupancy(recs):
 @pytest.mark.parametrize("name,min_waves", [
     # the shipped headline sweep: 1024^3 fp32, 4 fused steps, 3 + 2-row bands of 8 waves (one 512-thread
     # block per CU: 2 waves per SIMD is all a block of 8 waves can have)
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false>", 2),
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false>", 2),         # its residual sweeps
-    ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false, false>", 2),        # K = 3 (step-count remainders)
-    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false, false>", 2),       # fp64 K = 3 (2048^3 + residual)
-    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true, false>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, false>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, true>", 2),   # its pencil copy
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, false>", 2),         # its residual sweeps
+    ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false, false, false>", 2),        # K = 3 (step-count remainders)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false, false, false>", 2),       # fp64 K = 3 (2048^3 + residual)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true, false, false>", 2),
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false>", 2),              # 27-point K = 3 (1024-cell rows, fp64)
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false>", 2),
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true>", 2),
@@ -75,3 +76,16 @@ def test_lds_never_limits_occupancy(recs):
 def test_default_kernels_keep_their_occupancy(recs, name, min_waves):
     assert name in recs, sorted(k for k in recs if name.split("<")[0] in k)[:8]
     assert recs[name]["waves_per_simd"] >= min_waves, recs[name]
+
+
+def test_headline_sweep_keeps_its_memory_waits():
+    # the 1024^3 slab sweep (heat7_wxk fp32 K = 4) waits for ALL outstanding vector-memory ops in
+    # 13 places; round 4's pencil row bounds, compiled into the same kernel, made it 19 (six waits in
+    # front of window LDS reads: the sweep lost 3-4 %, profiles/r04_session_c/summary.txt). The
+    # slab and pencil copies are separate instances now: pin the slab one's count.
+    isa = kernel_isa(LIB, "_ZN4mdfx3dev9heat7_wxkIfLi3ELi2ELi4ELi8ELb0ELb0ELb0E")
+    assert len(isa) == 1, sorted(isa)
+    body = next(iter(isa.values()))
+    assert len(body) > 5000
+    n0 = sum(1 for l in body if l.startswith("s_waitcnt") and "vmcnt(0)" in l)
+    assert n0 <= 13, n0
