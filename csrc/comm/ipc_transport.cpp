@@ -124,11 +124,26 @@ class IpcTransport final : public Transport {
     if (aux_) (void)hipStreamDestroy(aux_);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
+    bool mapped = false;
     for (auto& p : peers_) {
+      mapped = mapped || p.mbox || p.buf[0] || p.ctr;
       if (p.mbox) (void)hipIpcCloseMemHandle(p.mbox);
       for (void* b : p.buf)
         if (b) (void)hipIpcCloseMemHandle(b);
       if (p.ctr) (void)hipIpcCloseMemHandle(p.ctr);
+    }
+    // Every rank unmaps its neighbours' exports before any rank frees its own (the engine frees the
+    // field buffers right after this destructor). Without this meeting a rank could free and
+    // re-allocate memory a neighbour still had mapped, and the next engine's hipIpcGetMemHandle on
+    // the new buffer failed with "invalid argument" (round-4 8-process rehearsal of bench.py's
+    // trial loop, which builds and closes engines in turn; scripts/ipc_churn.py). Skipped once the
+    // transport was aborted (a peer may be gone) and with MDFX_IPC_CLOSE_BARRIER=0.
+    const char* cb = std::getenv("MDFX_IPC_CLOSE_BARRIER");
+    if (mapped && setup_done_ && !aborted_ && f_.barrier && !(cb && std::string(cb) == "0")) {
+      try {
+        f_.barrier();
+      } catch (...) {
+      }
     }
     if (mbox_) (void)hipFree(mbox_);
     hip_free_uncached(ctr_);
@@ -243,6 +258,7 @@ class IpcTransport final : public Transport {
       HIPC(hipIpcOpenMemHandle(&p.ctr, r.ctr, hipIpcMemLazyEnablePeerAccess));
     }
     f_.barrier ? f_.barrier() : (void)f_.allgather("");
+    setup_done_ = true;
   }
 
   // mailbox slot of buffer parity b, side s (0 = lo, 1 = hi), in a process's mailbox
@@ -356,6 +372,7 @@ class IpcTransport final : public Transport {
       MDFX_FAIL(format("ipc transport: rank %d was aborted; its halo copies are no longer ordered", self_.rank));
   }
   void abort() override {
+    aborted_ = true;
     if (words_.host) words_.set_abort(1);
   }
 
@@ -382,6 +399,7 @@ class IpcTransport final : public Transport {
   bool dev_ok_ = false;
   bool direct_ = false;
   bool pencil_ = false;  // (z, y) pencil: y faces first, then the z faces (which carry the y ghosts)
+  bool setup_done_ = false, aborted_ = false;
   Peer peers_[4];
   double timeout_s_ = 300.0;
 };

@@ -48,6 +48,9 @@ elif [[ $part == 3 ]]; then
   PROF_TAG=p8g1 BENCH_ARGS="--rank-proxy 8 --steps 24 --warmup 4 --graph on --rounds 1 --overlap" scripts/gpu_session.sh prof || exit $?
   PROF_TAG=p8e1 BENCH_ARGS="--rank-proxy 8 --steps 24 --warmup 4 --graph off --rounds 1 --overlap" scripts/gpu_session.sh prof || exit $?
 elif [[ $part == 4 ]]; then
+  LIMIT=300 scripts/gpu_session.sh "churn_nobar=MDFX_IPC_CLOSE_BARRIER=0 python scripts/ipc_churn.py --world 8" \
+    "churn=python scripts/ipc_churn.py --world 8" || exit $?
+  tail -3 gpurun_out/churn_nobar.log gpurun_out/churn.log
   LIMIT=1000 scripts/gpu_session.sh "share8=python bench.py --gpus 8 --share-gpu --steps 20 --warmup 5 --verbose" || exit $?
   echo "share8 $(grep -o '"value": [0-9.]*' gpurun_out/share8.log) $(grep -o '"parallelism": "[^"]*"' gpurun_out/share8.log)"
 fi
