@@ -242,3 +242,15 @@ def test_ipc_direct_protocol_at_the_headline_size(hip):
     cfg = rec["config"]
     assert rec["n_gpus"] == 4 and cfg["gate"]["passed"] and cfg["transport"] == "ipc"
     assert cfg["ipc_protocol"] == "direct" and cfg["face_copy"] == "blit"
+
+
+def test_ipc_engines_rebuilt_in_turn_by_eight_processes(hip):
+    """bench.py's trial loop builds and closes ipc engines in turn (slabs / pencils, blit / SDMA).
+    With 8 processes on one GPU the 4th engine's hipIpcGetMemHandle failed ("invalid argument")
+    until the transport's teardown made every rank unmap its neighbours' exports before any rank
+    freed its own buffers (profiles/r04_session_e/)."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_churn.py"), "--world", "8"],
+                       capture_output=True, timeout=240, cwd=ROOT)
+    out = p.stdout.decode()
+    assert p.returncode == 0, out + p.stderr.decode()[-3000:]
+    assert "engine 7 ipc_sdma py=2 ok" in out
