@@ -169,8 +169,8 @@ class IpcTransport final : public Transport {
     int lo = 0, hi = 0;
     HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, hi));
-    HIPC(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    HIPC(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&ev_fork_, sync_event_flags()));
+    HIPC(hipEventCreateWithFlags(&ev_join_, sync_event_flags()));
     // every face has the same size (halo planes of one field layout)
     face_ = (size_t)self_.lay.halo * self_.lay.plane_bytes();
     // the protocol is agreed below (every rank must use the same one); counters start per protocol

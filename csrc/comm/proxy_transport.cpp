@@ -78,8 +78,8 @@ class ProxyTransport final : public Transport {
     int lo = 0, hi = 0;
     HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, hi));
-    HIPC(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    HIPC(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&ev_fork_, sync_event_flags()));
+    HIPC(hipEventCreateWithFlags(&ev_join_, sync_event_flags()));
     HIPC(hipDeviceSynchronize());
     ok_ = true;
   }

@@ -91,7 +91,7 @@ class HipBackend final : public Backend {
   void* create_event() override {
     activate();
     hipEvent_t e;
-    HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPC(hipEventCreateWithFlags(&e, sync_event_flags()));
     return e;
   }
   void destroy_event(void* e) override {
@@ -201,6 +201,17 @@ void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode)
   if (mode < 0) mode = face_copy_mode();
   HIPC(hipMemcpyAsync(dst, src, n, mode == 1 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice,
                       (hipStream_t)stream));
+}
+
+// Flags of the engine's stream-ordering events (boundary -> exchange, interior -> next boundary,
+// exchange -> next boundary, the transports' fork / join). MDFX_EVENT_FENCE: "system" (the HIP
+// default: a system-scope release, i.e. an L2 writeback, when the event is recorded) or "device"
+// (hipEventDisableSystemFence: these events only order work on one device; data that another GPU
+// reads is published by the counter signal kernels' own system-scope release).
+unsigned sync_event_flags() {
+  const char* v = std::getenv("MDFX_EVENT_FENCE");
+  const bool device = v && std::string(v) == "device";
+  return hipEventDisableTiming | (device ? hipEventDisableSystemFence : 0u);
 }
 
 void hip_face_copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height, void* stream,

@@ -81,6 +81,10 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.ev_int = s.be->create_event();
     s.ev_x = s.be->create_event();
     s.resid = (double*)s.be->alloc(2 * sizeof(double));
+    if (s.be->kind() == DeviceKind::HIP && opt_.py == 1 && local_ranks.size() == 1) {
+      s.be->activate();
+      s.sig = (unsigned long long*)hip_alloc_uncached(128 * 8);
+    }
     for (int kk = 2; kk <= opt_.temporal; ++kk) {
       const bool ok = s.be->kind() != DeviceKind::HIP || hip_supports_steps(spec_, s.lay, kk);
       depth_ok_[kk] = (i == 0 ? true : depth_ok_[kk]) && ok;
@@ -164,6 +168,10 @@ Solver::~Solver() {
     s.be->release(s.buf[0]);
     s.be->release(s.buf[1]);
     s.be->release(s.resid);
+    if (s.sig) {
+      s.be->activate();
+      hip_free_uncached(s.sig);
+    }
     s.be->destroy_event(s.ev_bnd);
     s.be->destroy_event(s.ev_int);
     s.be->destroy_event(s.ev_x);
@@ -269,6 +277,7 @@ void Solver::synchronize() {
 void Solver::exchange_ghosts() {
   // make the current buffer's owned planes visible to the exchange (ordered on the halo stream)
   for (auto& s : slabs_) {
+    s.be->record(s.ev_int, opt_.overlap ? s.cs : s.hs);
     s.be->wait(s.hs, s.ev_int);
     s.be->record(s.ev_bnd, s.hs);
   }
@@ -289,6 +298,20 @@ void Solver::exchange_ghosts() {
 // Rounds of resident blocks per streaming sweep: the option, else 2 with several slabs (exchange
 // kernels that need CUs find some mid-sweep) and 1 for a single slab. Passed with every launch
 // (RegionArgs::min_rounds), so eager steps, warm-up launches and captured cycles agree.
+// Fold the lower boundary region into the interior sweep (one slab per process with the boundary
+// kernels on the compute stream, a lower neighbour, fused sweeps through heat7_wxk): instead of a
+// separate launch over both K-plane boundary regions (each needing 3K planes marched for K outputs,
+// in two rounds of blocks), the interior sweep starts at the lower boundary, signals a device counter
+// once those planes are stored, and the halo stream waits for that counter; only the upper region
+// keeps its launch (one round). MDFX_FOLD=0 turns it off.
+bool Solver::fold_ok(const Slab& s, int k) const {
+  static const bool off = [] {
+    const char* v = std::getenv("MDFX_FOLD");
+    return v && std::string(v) == "0";
+  }();
+  return !off && s.sig && s.lo_e > s.lo_b && s.in_e > s.in_b && hip_region_signals(spec_, s.lay, k);
+}
+
 int Solver::min_rounds() const { return opt_.min_rounds > 0 ? opt_.min_rounds : (nranks_ > 1 ? 2 : 1); }
 
 bool Solver::boundary_on_cs() const {
@@ -298,7 +321,16 @@ bool Solver::boundary_on_cs() const {
 // The boundary regions of a step: the `halo` planes at each z face with a neighbour (all owned
 // rows), and for a pencil the `halo` rows at each y face with a neighbour (interior planes).
 // Everything the exchange sends is written here.
-void Solver::boundary_kernels(Slab& s, RegionArgs a, void* stream) {
+void Solver::boundary_kernels(Slab& s, RegionArgs a, void* stream, bool skip_lo) {
+  if (skip_lo) {
+    // the lower region is folded into the interior sweep (fold_ok)
+    if (s.hi_e > s.hi_b) {
+      a.lz_begin = s.hi_b;
+      a.lz_end = s.hi_e;
+      s.be->stencil(spec_, a, stream);
+    }
+    return;
+  }
   if (s.lo_e > s.lo_b && s.hi_e > s.hi_b) {
     // both z boundary regions in one call (one launch where the kernel supports it)
     a.lz_begin = s.lo_b;
@@ -329,7 +361,17 @@ void Solver::boundary_kernels(Slab& s, RegionArgs a, void* stream) {
 }
 
 // The interior region: interior planes, and for a pencil its interior rows.
-void Solver::interior_kernel(Slab& s, RegionArgs a, void* stream) {
+void Solver::interior_kernel(Slab& s, RegionArgs a, void* stream, bool with_lo) {
+  if (with_lo) {
+    // folded lower boundary: one upward sweep over [lo_b, in_e) that signals once [lo_b, lo_e) is stored
+    a.lz_begin = s.lo_b;
+    a.lz_end = s.in_e;
+    a.lz2_begin = a.lz2_end = 0;
+    a.sig = s.sig;
+    a.sig_z = s.lo_e;
+    s.be->stencil(spec_, a, stream);
+    return;
+  }
   if (s.in_e <= s.in_b) return;
   a.lz_begin = s.in_b;
   a.lz_end = s.in_e;
@@ -371,7 +413,8 @@ void Solver::step(bool want_resid, int k) {
     else s.be->wait(s.hs, s.ev_int);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)bs));
     a.resid = want_resid ? s.resid : nullptr;
-    boundary_kernels(s, a, bs);
+    const bool fold = bcs && fold_ok(s, k);
+    boundary_kernels(s, a, bs, fold);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)bs));
     if (opt_.sync_debug) s.be->sync_device();
     if (prof && !prof_hip && &s == &slabs_[0]) c1 = clk::now();
@@ -386,11 +429,17 @@ void Solver::step(bool want_resid, int k) {
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)is));
     a.resid = want_resid ? s.resid + 1 : nullptr;
-    interior_kernel(s, a, is);
+    interior_kernel(s, a, is, fold);
+    // the exchange sends the lower face once the interior sweep has signalled it stored
+    if (fold)
+      hip_counter_wait((const uint64_t*)(s.sig + 16), (uint64_t*)(s.sig + 32), opt_.timeout_s > 0 ? opt_.timeout_s : 300.0,
+                       s.hs, 0, nullptr);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[3], (hipStream_t)is));
     if (prof && !prof_hip && &s == &slabs_[0]) c2 = clk::now();
-    if (!bcs) s.be->record(s.ev_bnd, s.hs);
-    s.be->record(s.ev_int, is);
+    if (!bcs) {
+      s.be->record(s.ev_bnd, s.hs);
+      s.be->record(s.ev_int, is);  // (with bcs nothing in the step loop waits for it: no marker between sweeps)
+    }
     if (opt_.sync_debug) s.be->sync_device();
     s.be->trace_pop();
   }
@@ -757,6 +806,11 @@ void Solver::run_graph(int64_t pairs, int k) {
     }
   }
   GDBG("launch");
+  // (the bcs step schedule records no per-step interior event: mark every compute stream's tail now)
+  for (auto& s : slabs_) {
+    s.be->activate();
+    s.be->record(s.ev_int, s.cs);
+  }
   Slab& o = slabs_[0];
   o.be->activate();
   // the replay starts after all eager work on every slab's streams

@@ -37,7 +37,17 @@ struct RegionArgs {
   // after half the interior sweep. It is part of the launch, so a captured hipGraph replays exactly
   // the geometry the engine asked for when it captured.
   int min_rounds = 0;
+  // Folded boundary (slabs, fused 7-point sweeps through heat7_wxk: hip_region_signals): the region
+  // starts at the lower boundary planes [lz_begin, sig_z), and once every block has stored them the
+  // kernel bumps the device counter sig[16] by one (sig[0] counts the blocks' arrivals; both in
+  // memory from hip_alloc_uncached). The halo stream waits for that counter instead of a separate
+  // boundary launch, so the lower face is sent while the same sweep continues upward.
+  unsigned long long* sig = nullptr;
+  int64_t sig_z = 0;
 };
+
+// Whether a slab sweep of `steps` fused steps runs through a kernel that honours RegionArgs::sig.
+bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int steps);
 
 // Whether a fused multi-step sweep is implemented for this stencil / grid on the device.
 bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps);

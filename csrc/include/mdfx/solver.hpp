@@ -133,10 +133,14 @@ class Solver {
     // pencils: storage-row regions of the interior planes (y-boundary strips and interior rows;
     // all 0 for slabs: every owned row)
     int64_t ylo_b = 0, ylo_e = 0, yhi_b = 0, yhi_e = 0, yin_b = 0, yin_e = 0;
+    // folded lower boundary (fold_ok()): device counters from hip_alloc_uncached, [0] the interior
+    // blocks' arrivals, [16] sweeps whose lower face is stored, [32] the halo stream's private expect
+    unsigned long long* sig = nullptr;
   };
   void step(bool want_resid, int k);
-  void boundary_kernels(Slab& s, RegionArgs a, void* stream);
-  void interior_kernel(Slab& s, RegionArgs a, void* stream);
+  void boundary_kernels(Slab& s, RegionArgs a, void* stream, bool skip_lo = false);
+  void interior_kernel(Slab& s, RegionArgs a, void* stream, bool with_lo = false);
+  bool fold_ok(const Slab& s, int k) const;
   void maybe_inject_fault();
   void sync_all();
   bool drain(double limit_s);                  // bounded stream drain (teardown after an abort)

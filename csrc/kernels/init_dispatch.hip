@@ -278,6 +278,12 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   return spec.dtype == DType::F32 ? dev::heat7_tb2_supported<float>(g) : dev::heat7_tb2_supported<double>(g);
 }
 
+bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int steps) {
+  return !lay.pencil() && spec.kind == StencilKind::Heat7 && (steps == 3 || steps == 4) && lay.halo >= steps &&
+         dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx) &&
+         !(spec.dtype == DType::F64 && steps == 4);
+}
+
 int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
   switch (spec.kind) {
     case StencilKind::Jacobi5: return 8;
@@ -331,6 +337,13 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   g.lz2_begin = a.lz2_begin;
   g.lz2_end = a.lz2_end;
   g.min_rounds = std::max(1, std::min(4, a.min_rounds));
+  if (a.sig) {
+    MDFX_CHECK(hip_region_signals(spec, a.lay, a.steps) && a.lz2_end <= a.lz2_begin && a.sig_z > a.lz_begin &&
+                   a.sig_z <= a.lz_end,
+               "a folded boundary (RegionArgs::sig) needs a one-region slab sweep through heat7_wxk");
+    g.sig = a.sig;
+    g.sig_z = a.sig_z;
+  }
   if (a.ly_end > a.ly_begin) {
     MDFX_CHECK(a.ly_begin >= a.lay.hy && a.ly_end <= a.lay.hy + a.lay.nyl(), "row range must lie inside the owned rows");
     g.ly_begin = a.ly_begin;

@@ -40,6 +40,11 @@ struct Geo {
   // storage rows [ly_begin, ly_end) to write (slabs: gny = ny, gy_off = 0, every row). Kernels
   // without pencil support only ever see slab geometry (hip_stencil routes pencils to naive / wxk)
   int64_t gny = 0, gy_off = 0, ly_begin = 0, ly_end = 0;
+  // folded lower boundary (heat7_wxk SIG copy, RegionArgs::sig): every block of the chunks that start
+  // at lz_begin signals once its output planes [lz_begin, sig_z) are stored; the last of them bumps
+  // sig[16] (sig[0] counts arrivals)
+  unsigned long long* sig = nullptr;
+  int64_t sig_z = 0;
   unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };
 

@@ -63,7 +63,28 @@ int64_t resident_blocks(const void* kfn, int block);
 // PEN: the pencil copy (output rows [ly_begin, ly_end) of storage rows holding ghost rows, global
 // row = storage row + gy_off). Slabs run the copy without it: the four extra row bounds held in
 // scalars cost the slab sweep ~4 % (six more vmcnt(0) waits in front of window reads, round 4).
-template <class T, int RY, int RE, int K, int WB, bool RES, bool DG = false, bool PEN = false>
+// One block's arrival at the folded boundary (one out-of-line copy for every march variant): the
+// wave's stores complete and are written back past this XCD's L2 (agent-scope release); after the
+// block barrier one lane counts the arrival, and the block that completes the count re-arms it and
+// bumps the sweep counter sig[16] the halo stream waits for. The next sweep's launch follows this
+// one on its stream, so no block of it can arrive before the re-arm.
+__device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles, bool leader) {
+  wait_vm0();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  lds_barrier();
+  if (leader) {
+    const unsigned long long n = __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
+    if (n == (unsigned long long)tiles) {
+      __hip_atomic_store(sig, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(sig + 16, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// SIG: the folded-boundary copy (Geo::sig): the blocks of the chunks starting at lz_begin publish their
+// output planes [lz_begin, sig_z) and signal, so the halo exchange of the lower face overlaps the
+// rest of the same sweep (no separate boundary launch for that face).
+template <class T, int RY, int RE, int K, int WB, bool RES, bool DG = false, bool PEN = false, bool SIG = false>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
                                                      int diag = 0) {
@@ -148,6 +169,8 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   };
 
   const int qlast = ze - 1 + K;  // last u0 plane of the march
+  const bool sig_blk = SIG && zs == (int)g.lz_begin;
+  const int sig_last = SIG ? (int)g.sig_z - 1 : 0;
   issue(zs - K, 0);
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
@@ -286,6 +309,14 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         }
       }
       nst = valid ? nsto : 0;
+      if constexpr (SIG) {
+        if (sig_blk && lz == sig_last) {  // block-uniform: every wave takes this branch together
+          // this wave's stores of the lower planes complete, then are written back past this XCD's
+          // L2 (agent-scope release); after the barrier one lane counts the block's arrival, and the
+          // last block of the launch to arrive bumps the sweep counter the halo stream waits for
+          wxk_fold_signal(g.sig, tiles, w == 0 && lane == 0);
+        }
+      }
     };
     // an odd plane count ends with one extra step (q = qlast + 1): no DMA, nothing stored
     for (int q = zs - K; q <= qlast; q += 2) {
@@ -342,6 +373,16 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   const bool pen = g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny;
+  if (g.sig) {
+    MDFX_CHECK(!pen && g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
+    if (resid)
+      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true, false, false, true>), grd, blk, 0, s, in, out, g, r, zc,
+                         XT, YT, (int)ntasks, resid, 0);
+    else
+      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, false, false, true>), grd, blk, 0, s, in, out, g, r, zc,
+                         XT, YT, (int)ntasks, resid, 0);
+    return;
+  }
   if (resid) {
     if (pen)
       hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT,
