@@ -64,19 +64,21 @@ int64_t resident_blocks(const void* kfn, int block);
 // row = storage row + gy_off). Slabs run the copy without it: the four extra row bounds held in
 // scalars cost the slab sweep ~4 % (six more vmcnt(0) waits in front of window reads, round 4).
 // One block's arrival at the folded boundary (one out-of-line copy for every march variant): the
-// wave's stores complete and are written back past this XCD's L2 (agent-scope release); after the
-// block barrier one lane counts the arrival, and the block that completes the count re-arms it and
-// bumps the sweep counter sig[16] the halo stream waits for. The next sweep's launch follows this
+// wave's stores of the lower planes complete (vmcnt 0: acknowledged by this XCD's L2), the block
+// barrier, then one lane counts the arrival; the block that completes the count re-arms it and bumps
+// the sweep counter sig[16]. No cache maintenance here: the halo stream's counter-wait kernel ends
+// with the dispatch packet's release, which writes back every XCD's L2 before the exchange reads the
+// face. (A per-block agent-scope release - an L2 writeback, and with acq_rel an L2 invalidate, by
+// each of the 235 blocks - slowed the whole sweep by ~25 %.) The next sweep's launch follows this
 // one on its stream, so no block of it can arrive before the re-arm.
 __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles, bool leader) {
   wait_vm0();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   lds_barrier();
   if (leader) {
-    const unsigned long long n = __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
+    const unsigned long long n = __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
     if (n == (unsigned long long)tiles) {
       __hip_atomic_store(sig, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(sig + 16, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(sig + 16, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
