@@ -97,6 +97,7 @@ static Knobs read_knobs() {
   k.life_bits = env_int("MDFX_LIFE_BITS", 1);
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.wxk_diag = env_int("MDFX_WXK_DIAG", 0);
+  k.wxk_strip = env_int("MDFX_WXK_STRIP", 1);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
 }

@@ -375,7 +375,9 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   const bool pen = g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny;
-  if (g.sig) {
+  if constexpr (WB != 8) {
+    MDFX_CHECK(!g.sig, "heat7_wxk: folded boundaries run in bands of 8 waves");
+  } else if (g.sig) {
     MDFX_CHECK(!pen && g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
     if (resid)
       hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true, false, false, true>), grd, blk, 0, s, in, out, g, r, zc,
@@ -441,6 +443,19 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
                  g.gnz < ((int64_t)1 << 30) && g.gy_off > -((int64_t)1 << 30) && g.gy_off < ((int64_t)1 << 30) &&
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
              "heat7_wxk: row / plane counts must fit 32-bit indices");
+  // a pencil's y-boundary strip (K rows next to a y neighbour, over the interior planes): bands of
+  // 2 + 2 rows in 2-wave blocks instead of 22-row bands of 8 waves that would compute 4 useful rows
+  // (and 4 blocks per CU, so the strip's few tiles split into many z chunks). MDFX_WXK_STRIP=0: off.
+  const bool strip = g.ly_end - g.ly_begin <= 4 && (g.ly_begin != 0 || g.ly_end != g.ny) && knobs().wxk_strip != 0;
+  if (strip) {
+    if constexpr (sizeof(T) == 8) {
+      launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);  // (fp64 K = 4 went to heat7_wtk above)
+    } else {
+      if (steps == 3) launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
+      else launch_wxk<T, 2, 2, 4, 2>(g, in, out, r, resid, s);
+    }
+    return;
+  }
   if constexpr (sizeof(T) == 4) {
     if (steps == 3) launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
     else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);

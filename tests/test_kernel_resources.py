@@ -54,6 +54,8 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, false, false>", 2),
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, true, false>", 2),   # its pencil copy
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, false, true>", 2),   # folded-boundary copy (N > 1)
+    ("mdfx::dev::heat7_wxk<float, 2, 2, 4, 2, false, false, true, false>", 2),   # pencil y strips (2-wave bands)
+    ("mdfx::dev::heat7_wxk<double, 2, 2, 3, 2, false, false, true, false>", 2),
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, false, true>", 2),
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, false, false>", 2),         # its residual sweeps
     ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false, false, false, false>", 2),        # K = 3 (step-count remainders)
