@@ -323,10 +323,13 @@ bool Solver::boundary_on_cs() const {
 // Everything the exchange sends is written here.
 void Solver::boundary_kernels(Slab& s, RegionArgs a, void* stream, bool skip_lo) {
   if (skip_lo) {
-    // the lower region is folded into the interior sweep (fold_ok)
+    // the lower region is folded into the interior sweep (fold_ok); the upper region's launch
+    // signals the same device counter once its planes are stored (no event between the two launches)
     if (s.hi_e > s.hi_b) {
       a.lz_begin = s.hi_b;
       a.lz_end = s.hi_e;
+      a.sig = s.sig;
+      a.sig_z = s.hi_e;
       s.be->stencil(spec_, a, stream);
     }
     return;
@@ -420,20 +423,25 @@ void Solver::step(bool want_resid, int k) {
     if (prof && !prof_hip && &s == &slabs_[0]) c1 = clk::now();
     // compute stream: interior, after the previous step's boundary kernels
     void* is = opt_.overlap ? s.cs : s.hs;
-    if (bcs) {
+    if (bcs && !fold) {
       s.be->record(s.ev_bnd, s.cs);  // this step's boundary kernels: the exchange follows them
       s.be->wait(s.hs, s.ev_bnd);
-    } else if (opt_.overlap) {
+    } else if (!bcs && opt_.overlap) {
       s.be->record(s.ev_bnd, s.hs);  // this step's boundary kernels (the interior waits for them)
       s.be->wait(s.cs, s.ev_bnd);
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)is));
     a.resid = want_resid ? s.resid + 1 : nullptr;
     interior_kernel(s, a, is, fold);
-    // the exchange sends the lower face once the interior sweep has signalled it stored
-    if (fold)
-      hip_counter_wait((const uint64_t*)(s.sig + 16), (uint64_t*)(s.sig + 32), opt_.timeout_s > 0 ? opt_.timeout_s : 300.0,
-                       s.hs, 0, nullptr);
+    // the exchange sends the faces once the upper boundary launch and the interior sweep have
+    // signalled them stored (in that order: both launches are on the compute stream). Folded steps
+    // need no boundary event: the interior's signal also orders the exchange, which rewrites the
+    // ghosts of `nb`, after the previous step's kernels that read them.
+    if (fold) {
+      const double to = opt_.timeout_s > 0 ? opt_.timeout_s : 300.0;
+      for (int i = s.hi_e > s.hi_b ? 2 : 1; i > 0; --i)
+        hip_counter_wait((const uint64_t*)(s.sig + 16), (uint64_t*)(s.sig + 32), to, s.hs, 0, nullptr);
+    }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[3], (hipStream_t)is));
     if (prof && !prof_hip && &s == &slabs_[0]) c2 = clk::now();
     if (!bcs) {

@@ -356,7 +356,9 @@ static WxGeo wxk_geo(const Geo& g) {
   w.YT = (int)((g.ly_end - g.ly_begin + BR - 1) / BR);
   const int64_t tiles = (int64_t)w.XT * w.YT;
   w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false>, 64 * WB);
-  w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds);
+  // (2-wave strip bands: the strip is on the sweep's critical path, before the exchange; chunks down
+  // to K planes spread its few tiles over the device)
+  w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds, WB == 2 ? K : 0);
   if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
   w.ntasks = tiles * ZT;

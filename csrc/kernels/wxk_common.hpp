@@ -27,9 +27,10 @@ using IC = std::integral_constant<int, V>;
 
 // chunked schedule of a streaming sweep over `planes` planes of `tiles` tiles on `resident` block
 // slots, every chunk paying `fill` extra plane steps: the chunk count minimising rounds x (zc + fill)
-// (chunks of at least 4K planes; at least `min_rounds` rounds when asked)
-inline int wx_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int64_t fill, int min_rounds) {
-  const int64_t zmax = std::max<int64_t>(1, planes / (4 * K));
+// (chunks of at least `min_chunk` planes, default 4K; at least `min_rounds` rounds when asked)
+inline int wx_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int64_t fill, int min_rounds,
+                 int64_t min_chunk = 0) {
+  const int64_t zmax = std::max<int64_t>(1, planes / (min_chunk > 0 ? min_chunk : 4 * K));
   double best = 1e300;
   int64_t bz = 1;
   for (int64_t zt = 1; zt <= zmax; ++zt) {
