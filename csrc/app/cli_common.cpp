@@ -39,6 +39,7 @@ struct Opts {
   bool compat = false;
   bool ref_precision = false;
   int temporal = 0;  // 0 = auto: hip_fused_depth on HIP where a fused kernel exists, else 1
+  int py = 1;        // --py: ranks along y of a (z, y) pencil split
   bool profile = false;
   int dim = 0;
   std::string dump;
@@ -55,6 +56,7 @@ void usage(const char* prog) {
       "  --backend auto|hip|cpu    device backend\n"
       "  --gpus N                  slabs on GPUs 0..N-1 driven by this one process\n"
       "  --ranks P                 P slabs in this process (several per GPU allowed: loopback)\n"
+      "  --py Y                    (z, y) pencils: Y ranks along y, P / Y along z (3D; loopback, host, ipc)\n"
       "  --transport auto|rccl|ipc|loopback|host|tcp\n"
       "                            multi-process runs (mpirun / torchrun): rccl on GPUs, tcp on CPUs\n"
       "  --init random|dirichlet|constant|life|compat  --seed --lo --hi --value --edge --interior --density\n"
@@ -130,6 +132,7 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--compat") o.compat = true;
     else if (a == "--ref-precision") o.ref_precision = true;
     else if (a == "--temporal") o.temporal = std::atoi(need(i));
+    else if (a == "--py") o.py = std::atoi(need(i));
     else if (a == "--profile") o.profile = true;
     else if (a == "--dim") o.dim = std::atoi(need(i));
     else if (a == "--dump") o.dump = need(i);
@@ -287,6 +290,12 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     } else {
       MDFX_FAIL("unknown transport " + tname);
     }
+    if (o.temporal <= 0 && o.py > 1) {
+      // pencils: the fused 7-point sweep (heat7_wxk K = 4 fp32 / 3 fp64) is the one with y ghost rows
+      const int want = spec.kind == StencilKind::Heat7 ? (spec.dtype == DType::F32 ? 4 : 3) : 1;
+      const int64_t pz = nranks / o.py;
+      o.temporal = hip && want > 1 && g.nz >= 4 * want * pz && g.ny >= 4 * want * o.py ? want : 1;
+    }
     if (o.temporal <= 0) {  // auto: deepest fused sweep with a kernel, slabs >= 4 sweeps deep
       int want = hip ? hip_fused_depth(spec, g.nx) : 1;
       while (want > 1 && g.nz < 4 * (int64_t)want * nranks) want = shallower_depth(want);
@@ -302,6 +311,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     so.graph = o.graph;
     so.timeout_s = o.timeout;
     so.temporal = o.temporal;
+    so.py = o.py;
     Solver solver(spec, g, nranks, local_ranks, std::move(bes), std::move(tr), so);
 
     // ---- initial condition ----------------------------------------------------------------

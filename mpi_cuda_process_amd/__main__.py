@@ -33,6 +33,7 @@ def _parser() -> argparse.ArgumentParser:
     p.add_argument("--dtype", default="f32")
     p.add_argument("--device", default="auto", help="auto | hip | cpu")
     p.add_argument("--ranks", type=int, default=None, help="P virtual slabs in this process")
+    p.add_argument("--py", type=int, default=1, help="(z, y) pencils: ranks along y (3D stencils)")
     p.add_argument("--transport", default="auto", help="auto | rccl | torch | staged | loopback | host")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--temporal", type=int, default=1, help="time steps fused per sweep (2: 3D 7-pt)")
@@ -79,7 +80,7 @@ def main(argv=None) -> int:
     prob = _problem(a)
     sim = Simulation(prob, device=a.device, ranks=a.ranks, transport=a.transport, distributed=distributed,
                      overlap=not a.no_overlap, sync_debug=a.sync_debug, residual_every=a.residual_every,
-                     graph=a.graph, timeout_s=a.timeout, temporal=a.temporal)
+                     graph=a.graph, timeout_s=a.timeout, temporal=a.temporal, py=a.py)
     with sim:
         if a.resume:
             sim.load_checkpoint(a.resume)
