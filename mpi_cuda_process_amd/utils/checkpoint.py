@@ -1,6 +1,7 @@
 """Checkpoint / dump files: one raw little-endian slab per rank plus a JSON header
-(``slab_<r>.bin`` / ``slab_<r>.json``, format ``mdfx-slab-v1``), in global plane order so any
-decomposition can be reassembled (csrc/engine/solver.cpp save_checkpoint)."""
+(``slab_<r>.bin`` / ``slab_<r>.json``, format ``mdfx-slab-v1``; a pencil's header adds its rows
+``y0``, ``y1``), in global plane order so any decomposition can be reassembled
+(csrc/engine/solver.cpp save_checkpoint)."""
 
 from __future__ import annotations
 
@@ -37,14 +38,16 @@ def read_checkpoint(path: str) -> Tuple[np.ndarray, List[dict]]:
                              % (m["rank"], m["nranks"], m["step"], m0["nranks"], m0["step"]))
     dt = _DT[m0["dtype"]]
     grid = np.zeros((m0["nz"], m0["ny"], m0["nx"]), dtype=dt)
-    covered = np.zeros(m0["nz"], dtype=bool)
+    covered = np.zeros((m0["nz"], m0["ny"]), dtype=bool)
     for m in metas:
-        n = (m["z1"] - m["z0"]) * m["ny"] * m["nx"]
+        # slabs own every row; a (z, y) pencil's header also names its rows [y0, y1)
+        y0, y1 = m.get("y0", 0), m.get("y1", m["ny"])
+        shape = (m["z1"] - m["z0"], y1 - y0, m["nx"])
         raw = np.fromfile(os.path.join(path, "slab_%d.bin" % m["rank"]), dtype=dt)
-        if raw.size != n:
-            raise ValueError("slab %d: %d values, expected %d" % (m["rank"], raw.size, n))
-        grid[m["z0"]:m["z1"]] = raw.reshape(m["z1"] - m["z0"], m["ny"], m["nx"])
-        covered[m["z0"]:m["z1"]] = True
+        if raw.size != shape[0] * shape[1] * shape[2]:
+            raise ValueError("slab %d: %d values, expected %d" % (m["rank"], raw.size, shape[0] * shape[1] * shape[2]))
+        grid[m["z0"]:m["z1"], y0:y1] = raw.reshape(shape)
+        covered[m["z0"]:m["z1"], y0:y1] = True
     if not covered.all():
         raise ValueError("the slabs do not cover every plane")
     return grid, metas

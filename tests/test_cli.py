@@ -182,3 +182,21 @@ def test_utils_format_array_and_checkpoint_reader(tmp_path):
     os.remove(os.path.join(ck, "slab_1.json"))
     with pytest.raises(ValueError):
         read_checkpoint(ck)
+
+
+@pytest.mark.parametrize("stencil,temporal", [("7", "2"), ("27", "1")])
+def test_pencils_via_dump_match_slabs(tmp_path, stencil, temporal):
+    # --py 2 / --py 3 pencils (host transport) dump the same grid as one slab; the dump reader places
+    # every pencil's (z, y) block
+    from mpi_cuda_process_amd.utils.checkpoint import read_checkpoint
+
+    base = [os.path.join(BIN, "mdfx"), "--backend", "cpu", "--stencil", stencil, "--nx", "18", "--ny", "16",
+            "--nz", "14", "--steps", "5", "--temporal", temporal, "--quiet"]
+    run(base + ["--dump", str(tmp_path / "a")])
+    run(base + ["--ranks", "4", "--py", "2", "--dump", str(tmp_path / "b")])
+    run(base + ["--ranks", "6", "--py", "3", "--dump", str(tmp_path / "c")])
+    a, _ = read_checkpoint(str(tmp_path / "a"))
+    b, mb = read_checkpoint(str(tmp_path / "b"))
+    c, _ = read_checkpoint(str(tmp_path / "c"))
+    assert sorted((m["y0"], m["y1"]) for m in mb)[0] == (0, 8)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
