@@ -422,7 +422,7 @@ def main(argv=None):
         ny = 1  # 2D grids: nx = width, nz = height
     prob = make_problem(a, nx, ny, nz)
     # (z, y) pencils: py ranks along y. Auto: at 4+ processes the 3D 7-point (whose fused sweep
-    # takes y ghost rows) tries 2 along y next to the z slabs, on every transport but rccl
+    # takes y ghost rows) tries 2 along y next to the z slabs, on every transport
     if a.py > 0:
         pys = [a.py]
     else:
@@ -441,8 +441,7 @@ def main(argv=None):
     elif not env:
         transports = [a.transport if a.transport in ("loopback", "host") else "auto"]
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True] if hip else [False])
-    # rccl exchanges z faces only: no pencils there
-    cands = [(t, g, q) for t in transports for q in pys for g in graphs if q == 1 or t != "rccl"]
+    cands = [(t, g, q) for t in transports for q in pys for g in graphs]
     if hip and a.graph == "auto" and len(graphs) > 1:
         # rccl steps are captured only under HIP >= 7.2 (RcclTransport::graph_capturable); under the
         # runtime PyTorch bundles a graph candidate would just repeat the eager one

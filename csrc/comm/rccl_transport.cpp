@@ -56,6 +56,10 @@ class RcclTransport final : public Transport {
         (void)hipSetDevice(locals_[i].be->device());
         (void)hipFree(scratch_[i]);
       }
+      if (i < ystage_.size() && ystage_[i]) {
+        (void)hipSetDevice(locals_[i].be->device());
+        (void)hipFree(ystage_[i]);
+      }
       if (aux_[i]) (void)hipStreamDestroy(aux_[i]);
       if (comms_[i]) (void)ncclCommDestroy(comms_[i]);
     }
@@ -86,7 +90,6 @@ class RcclTransport final : public Transport {
   // other rank abort its half-built communicator and fail with a message instead of blocking in
   // ncclCommInitRank forever (the reference's D4 hang class starts at its MPI_Init / first send).
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
-    require_slabs(locals, "rccl");
     locals_ = locals;
     nranks_ = nranks;
     comms_.assign(locals_.size(), nullptr);
@@ -113,9 +116,66 @@ class RcclTransport final : public Transport {
       HIPC(hipMalloc(&scratch_[i], 2 * sizeof(double)));
       HIPC(hipStreamCreateWithFlags(&aux_[i], hipStreamNonBlocking));
     }
+    // (z, y) pencils: a y face is `nzl` pieces of `hy` rows, one per plane; RCCL moves contiguous
+    // bytes, so each y face travels through a staging buffer (2-D copies on the halo stream around
+    // a first send / recv group; the z faces, which carry the fresh y ghost rows, follow in a second)
+    ystage_.assign(locals_.size(), nullptr);
+    for (size_t i = 0; i < locals_.size(); ++i) {
+      const LocalSlab& ls = locals_[i];
+      if (ls.py <= 1 || ls.lay.hy == 0) continue;
+      const size_t yb = halo_span(ls, 0, 2, nranks_).bytes ? halo_span(ls, 0, 2, nranks_).bytes
+                                                            : halo_span(ls, 0, 3, nranks_).bytes;
+      if (!yb) continue;
+      ls.be->activate();
+      HIPC(hipMalloc(&ystage_[i], 4 * yb));  // send / recv for each of the two y sides
+      ystage_bytes_ = yb;
+      pencil_ = true;
+    }
   }
 
   void exchange(int b) override {
+    if (pencil_) {
+      // phase 1: the y faces through the staging buffers
+      for (size_t i = 0; i < locals_.size(); ++i) {
+        const LocalSlab& s = locals_[i];
+        if (!ystage_[i]) continue;
+        s.be->activate();
+        for (int side = 2; side < 4; ++side) {
+          const HaloSpan h = halo_span(s, b, side, nranks_);
+          if (h.peer < 0) continue;
+          MDFX_CHECK(h.bytes == ystage_bytes_, "rccl: y face sizes differ between pencils");
+          char* snd = (char*)ystage_[i] + (size_t)(2 * (side - 2)) * ystage_bytes_;
+          HIPC(hipMemcpy2DAsync(snd, h.width, h.send, h.stride, h.width, h.height, hipMemcpyDeviceToDevice,
+                                (hipStream_t)s.halo_stream));
+        }
+      }
+      NCCLC(ncclGroupStart());
+      for (size_t i = 0; i < locals_.size(); ++i) {
+        const LocalSlab& s = locals_[i];
+        if (!ystage_[i]) continue;
+        for (int side = 2; side < 4; ++side) {
+          const HaloSpan h = halo_span(s, b, side, nranks_);
+          if (h.peer < 0) continue;
+          char* snd = (char*)ystage_[i] + (size_t)(2 * (side - 2)) * ystage_bytes_;
+          char* rcv = snd + ystage_bytes_;
+          accept(ncclRecv(rcv, h.bytes, ncclUint8, h.peer, comms_[i], (hipStream_t)s.halo_stream), "ncclRecv");
+          accept(ncclSend(snd, h.bytes, ncclUint8, h.peer, comms_[i], (hipStream_t)s.halo_stream), "ncclSend");
+        }
+      }
+      if (accept(ncclGroupEnd(), "ncclGroupEnd (y faces)") == ncclInProgress) wait_ready("halo exchange launch", 50);
+      for (size_t i = 0; i < locals_.size(); ++i) {
+        const LocalSlab& s = locals_[i];
+        if (!ystage_[i]) continue;
+        s.be->activate();
+        for (int side = 2; side < 4; ++side) {
+          const HaloSpan h = halo_span(s, b, side, nranks_);
+          if (h.peer < 0) continue;
+          const char* rcv = (char*)ystage_[i] + (size_t)(2 * (side - 2) + 1) * ystage_bytes_;
+          HIPC(hipMemcpy2DAsync(h.recv, h.stride, rcv, h.width, h.width, h.height, hipMemcpyDeviceToDevice,
+                                (hipStream_t)s.halo_stream));
+        }
+      }
+    }
     NCCLC(ncclGroupStart());
     for (size_t i = 0; i < locals_.size(); ++i) {
       const LocalSlab& s = locals_[i];
@@ -237,6 +297,9 @@ class RcclTransport final : public Transport {
   std::vector<LocalSlab> locals_;
   int nranks_ = 1;
   std::vector<ncclComm_t> comms_;
+  std::vector<void*> ystage_;  // pencils: per slab 4 y-face staging buffers (send / recv x 2 sides)
+  size_t ystage_bytes_ = 0;
+  bool pencil_ = false;
   std::vector<void*> scratch_;
   std::vector<hipStream_t> aux_;
   double timeout_s_ = 0.0;

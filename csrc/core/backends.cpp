@@ -274,7 +274,7 @@ void require_slabs(const std::vector<LocalSlab>& locals, const char* transport) 
   for (const LocalSlab& s : locals)
     MDFX_CHECK(s.py <= 1 && s.lay.hy == 0,
                format("the %s transport exchanges z faces only; a pencil decomposition (y split) needs the "
-                      "loopback, host, proxy or ipc transport", transport));
+                      "loopback, host, proxy, ipc, rccl or torch transport", transport));
 }
 
 }  // namespace mdfx

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 4 session M: the whole GPU tier, smoke(), the driver's default bench and N = 1 form, after
+# the fold / pencil / CLI changes.
+set -o pipefail
+cd "$(dirname "$0")/.."
+LIMIT=900 scripts/gpu_session.sh "gputests=python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests" || exit $?
+grep -E "passed|failed" gpurun_out/gputests.log | tail -2
+scripts/gpu_session.sh smoke "b_default=python bench.py" "b_driver=python bench.py --gpus 1 --steps 20 --warmup 5" || exit $?
+for f in b_default b_driver; do echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/$f.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$f.log | head -1)"; done
