@@ -48,6 +48,18 @@ static void test_layout() {
   EXPECT(d.pitch * 8 % 256 == 0);
 }
 
+static void test_pencil_layout() {
+  // 2 x 3 pencils of a 10 x 11 x 9 grid: ranks, neighbours, row ranges and the ghost-row layout
+  PencilDecomposition d(Extent3{10, 11, 9}, 2, 3);
+  EXPECT(d.pz() == 2 && d.py() == 3 && d.ranks() == 6);
+  EXPECT(d.rz(4) == 1 && d.ry(4) == 1);
+  EXPECT(d.neighbor(4, 0) == 1 && d.neighbor(4, 1) == -1 && d.neighbor(4, 2) == 3 && d.neighbor(4, 3) == 5);
+  EXPECT(d.neighbor(0, 0) == -1 && d.neighbor(0, 2) == -1 && d.neighbor(5, 3) == -1);
+  FieldLayout l = FieldLayout::make(Extent3{10, 11, 9}, d.z.z0(1), d.z.z1(1), 2, DType::F32, d.y.z0(1), d.y.z1(1), 2);
+  EXPECT(l.pencil() && l.nyl() == d.y.size(1) && l.rows() == l.nyl() + 4 && l.plane == l.pitch * l.rows());
+  EXPECT(l.owned_cells() == (int64_t)l.nzl() * l.nyl() * 10);
+}
+
 static std::vector<char> run_engine(StencilKind k, DType dt, Extent3 g, int P, int steps, bool gpu) {
   StencilSpec s;
   s.kind = k;
@@ -71,6 +83,51 @@ static std::vector<char> run_engine(StencilKind k, DType dt, Extent3 g, int P, i
     out.insert(out.end(), b.begin(), b.end());
   }
   return out;
+}
+
+// The dense global grid after `steps` steps of a pz x py pencil run (py = 1: slabs).
+static std::vector<char> run_pencils(StencilKind k, DType dt, Extent3 g, int P, int py, int steps, int temporal,
+                                     bool gpu) {
+  StencilSpec s;
+  s.kind = k;
+  s.dtype = dt;
+  std::vector<int> ranks;
+  std::vector<std::unique_ptr<Backend>> bes;
+  for (int r = 0; r < P; ++r) {
+    ranks.push_back(r);
+    bes.push_back(gpu ? make_hip_backend(0) : make_cpu_backend());
+  }
+  SolverOptions o;
+  o.py = py;
+  o.temporal = temporal;
+  Solver sol(s, g, P, ranks, std::move(bes), gpu ? make_loopback_transport() : make_host_transport(), o);
+  InitSpec is;
+  is.kind = InitKind::Random;
+  sol.init(is);
+  sol.run(steps);
+  const size_t es = dt == DType::F64 ? 8 : 4;
+  std::vector<char> out((size_t)g.nx * g.ny * g.nz * es);
+  for (int i = 0; i < P; ++i) {
+    const FieldLayout& l = sol.layout(i);
+    std::vector<char> b((size_t)l.owned_cells() * es);
+    sol.read_owned(i, b.data());
+    const size_t row = (size_t)g.nx * es;
+    for (int64_t z = 0; z < l.nzl(); ++z)
+      for (int64_t y = 0; y < l.nyl(); ++y)
+        std::memcpy(&out[(((size_t)(l.z0 + z) * g.ny) + (size_t)(l.y0 + y)) * row],
+                    &b[((size_t)z * l.nyl() + (size_t)y) * row], row);
+  }
+  return out;
+}
+
+static void test_pencil_invariance(bool gpu) {
+  // pencils = one slab, bitwise: 7-point (single and fused steps) and 27-point (edge / corner ghosts)
+  const Extent3 g{gpu ? 256 : 20, 18, 16};
+  const auto h7 = run_pencils(StencilKind::Heat7, DType::F32, g, 1, 1, 7, 1, gpu);
+  EXPECT(run_pencils(StencilKind::Heat7, DType::F32, g, 4, 2, 7, 1, gpu) == h7);
+  EXPECT(run_pencils(StencilKind::Heat7, DType::F32, g, 6, 3, 7, gpu ? 3 : 2, gpu) == h7);
+  const auto b27 = run_pencils(StencilKind::Box27, DType::F64, g, 1, 1, 5, 1, gpu);
+  EXPECT(run_pencils(StencilKind::Box27, DType::F64, g, 4, 2, 5, 1, gpu) == b27);
 }
 
 static void test_invariance(bool gpu) {
@@ -179,10 +236,13 @@ static void test_temporal(bool gpu) {
 int main() {
   test_slab();
   test_layout();
+  test_pencil_layout();
   test_invariance(false);
+  test_pencil_invariance(false);
   test_temporal(false);
   if (hip_device_count() > 0) {
     test_invariance(true);
+    test_pencil_invariance(true);
     test_temporal(true);
     test_graph();
 #ifdef MDFX_DEVICE_CHECKS
