@@ -3,6 +3,8 @@
 # the fold / pencil / CLI changes.
 set -o pipefail
 cd "$(dirname "$0")/.."
+scripts/gpu_session.sh native || exit $?
+tail -2 gpurun_out/native.log
 LIMIT=900 scripts/gpu_session.sh "gputests=python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests" || exit $?
 grep -E "passed|failed" gpurun_out/gputests.log | tail -2
 scripts/gpu_session.sh smoke "b_default=python bench.py" "b_driver=python bench.py --gpus 1 --steps 20 --warmup 5" || exit $?
