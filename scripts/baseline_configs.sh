@@ -11,6 +11,7 @@ run c2_heat7_512_f32_t1 --n 512 --steps 100 --warmup 10 --temporal 1 || exit 1
 run c3_heat7_1024_f32 --n 1024 --steps 50 --warmup 10 --repeats 2 || exit 1
 run c3_heat7_1024_f32_driver --n 1024 --steps 20 --warmup 5 || exit 1
 for n in 2 4 8; do run c3_proxy$n --rank-proxy $n --steps 48 --warmup 12 || exit 1; done
+run c3_proxy8_pencil --rank-proxy 8 --py 2 --steps 48 --warmup 12 || exit 1
 run c4_box27_512_f32 --stencil box27 --n 512 --steps 100 --warmup 10 || exit 1
 run c4_box27_512_f64 --stencil box27 --n 512 --dtype f64 --steps 50 --warmup 5 || exit 1
 run c5_heat7_2048_f64_resid --n 2048 --dtype f64 --steps 24 --warmup 3 --residual-every 12 || exit 1
