@@ -592,26 +592,79 @@ static bool multislab_graph_ok() {
   return ok;
 }
 
+int Solver::max_depth() const {
+  for (int kk = std::min(opt_.temporal, 16); kk > 1; --kk)
+    if (depth_ok_[kk]) return kk;
+  return 1;
+}
+
+// Sweep plan of a stretch of `len` steps (the steps up to the next residual evaluation, or to the
+// end of the run): the fewest sweeps of at most `temporal` steps, with depths as even as possible
+// (hi = ceil(len / n) and hi - 1), instead of the deepest sweeps first and the remainder in one
+// shallow sweep. A fused sweep costs about the same HBM traffic whatever its depth, and the shallow
+// kernels run fewer steps per byte: a 10-step residual interval at temporal 4 runs 4 + 3 + 3 rather
+// than 4 + 4 + 2, and 5 steps 3 + 2 rather than 4 + 1. The residual sweep is planned last and takes
+// the shallower depth when there is one, so the max_depth() sweeps stay paired for graph replay;
+// only max_depth() sweeps are replayed (the cycles prepare_graphs() captured), any other depth runs
+// eagerly instead of re-capturing a cycle. When a depth of the even plan has no kernel on some
+// slab, the deepest depth that fits is taken (the plan before round 4).
+int Solver::plan_sweep(int64_t len, bool res_end, int64_t* graphable) const {
+  *graphable = 0;
+  if (len <= 1) return 1;
+  const int T = max_depth();
+  const int64_t n = (len + T - 1) / T;
+  const int hi = (int)((len + n - 1) / n), lo = hi - 1;
+  const int64_t c_hi = len - n * lo, c_lo = n - c_hi;
+  if (depth_ok_[hi] && (c_lo == 0 || depth_ok_[lo])) {
+    const bool res_hi = res_end && c_lo == 0;  // the residual sweep's depth is hi only if all are
+    const int64_t plain_hi = c_hi - (res_hi ? 1 : 0);
+    if (plain_hi > 0) {
+      if (hi == T) *graphable = plain_hi;
+      return hi;
+    }
+    return c_lo > 0 ? lo : hi;
+  }
+  int k = 1;
+  for (int kk = (int)std::min<int64_t>(T, len); kk > 1; --kk)
+    if (depth_ok_[kk]) {
+      k = kk;
+      break;
+    }
+  *graphable = (len - (res_end ? 1 : 0)) / k;
+  return k;
+}
+
+std::vector<std::pair<int, bool>> Solver::sweep_plan(int64_t steps) const {
+  // run()'s loop without the work (a replayed pair covers two sweeps of the same plan)
+  std::vector<std::pair<int, bool>> out;
+  int64_t done = 0, at = stats_.steps;
+  while (done < steps) {
+    int64_t to_res = steps - done + 1;
+    if (opt_.residual_every > 0) to_res = ((at / opt_.residual_every) + 1) * opt_.residual_every - at;
+    int64_t graphable = 0;
+    const int k = plan_sweep(std::min(steps - done, to_res), to_res <= steps - done, &graphable);
+    out.emplace_back(k, to_res == k);
+    done += k;
+    at += k;
+  }
+  return out;
+}
+
 void Solver::run(int64_t steps) {
   MDFX_CHECK(steps >= 0, "negative step count");
   MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
   if (ghosts_dirty_) exchange_ghosts();
   transport_->check();
-  const int T = opt_.temporal;
   int64_t done = 0;
   while (done < steps) {
     // time steps until the next residual evaluation (inclusive), unbounded if none
     int64_t to_res = steps - done + 1;
     if (opt_.residual_every > 0)
       to_res = ((stats_.steps / opt_.residual_every) + 1) * opt_.residual_every - stats_.steps;
-    // a fused sweep may not jump over a residual step; shorter stretches (a step count that is not
-    // a multiple of T, a residual point inside a sweep) use the deepest fused depth that fits
-    int k = 1;
-    for (int kk = std::min<int64_t>({(int64_t)T, steps - done, to_res}); kk > 1; --kk)
-      if (depth_ok_[kk]) {
-        k = kk;
-        break;
-      }
+    // a fused sweep may not jump over a residual step: the stretch up to the next residual step (or
+    // the end of the run) is cut into sweeps by plan_sweep
+    int64_t graphable = 0;
+    const int k = plan_sweep(std::min(steps - done, to_res), to_res <= steps - done, &graphable);
     const bool res = (to_res == k);
     // graph replay for plain (non-residual, non-debug) stretches of >= 2 sweeps, when the
     // transport's exchange is pure stream work (rccl, loopback, ipc; the callback / host / tcp
@@ -625,8 +678,7 @@ void Solver::run(int64_t steps) {
     // before it sent the other parity (a repeated parity needs the ipc transport's eager look-ahead
     // wait, ipc_transport.cpp).
     if (!res && graph_eligible() && transport_->last_parity() != 1 - cur_) {
-      const int64_t plain = std::min<int64_t>(steps - done, to_res - 1);
-      const int64_t pairs = plain / (2 * k);
+      const int64_t pairs = graphable / 2;
       if (pairs > 0) {
         run_graph(pairs, k);
         done += 2 * k * pairs;
@@ -661,22 +713,8 @@ bool Solver::graph_eligible() const {
 void Solver::warm_kernels(int64_t steps) {
   MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
   if (slabs_.empty() || slabs_[0].be->kind() != DeviceKind::HIP) return;  // (nothing to warm on the CPU)
-  // the sweeps run(steps) would issue: (depth, residual) as its loop picks them
   bool used[17][2] = {};
-  int64_t done = 0, at = stats_.steps;
-  while (done < steps) {
-    int64_t to_res = steps - done + 1;
-    if (opt_.residual_every > 0) to_res = ((at / opt_.residual_every) + 1) * opt_.residual_every - at;
-    int k = 1;
-    for (int kk = std::min<int64_t>({(int64_t)opt_.temporal, steps - done, to_res}); kk > 1; --kk)
-      if (depth_ok_[kk]) {
-        k = kk;
-        break;
-      }
-    used[k][to_res == k ? 1 : 0] = true;
-    done += k;
-    at += k;
-  }
+  for (const auto& kr : sweep_plan(steps)) used[kr.first][kr.second ? 1 : 0] = true;
   synchronize();
   const int nb = 1 - cur_;
   for (int k = 1; k <= 16; ++k)
@@ -701,12 +739,7 @@ void Solver::warm_kernels(int64_t steps) {
 int Solver::prepare_graphs() {
   MDFX_CHECK(!poisoned_, "the engine was aborted by its watchdog; create a new Simulation");
   if (!graph_eligible()) return 0;
-  int k = 1;
-  for (int kk = opt_.temporal; kk > 1; --kk)
-    if (depth_ok_[kk]) {
-      k = kk;
-      break;
-    }
+  const int k = max_depth();
   // one eager exchange first (it re-sends the current faces, so it changes nothing): transports
   // that set up peer connections on first use (RCCL p2p) do so outside the capture
   exchange_ghosts();

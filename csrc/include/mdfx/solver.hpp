@@ -83,6 +83,8 @@ class Solver {
   // the first launch of an instance pays one-time costs (code-object and occupancy queries) that a
   // timed run without warm-up steps would otherwise count. The field state is unchanged.
   void warm_kernels(int64_t steps);
+  // The sweeps run(steps) would issue from the current step count: (fused depth, residual sweep).
+  std::vector<std::pair<int, bool>> sweep_plan(int64_t steps) const;
   // Whether run() would replay captured cycles in this configuration.
   bool graph_eligible() const;
   void synchronize();
@@ -147,6 +149,10 @@ class Solver {
   [[noreturn]] void poison(const std::string& why);  // watchdog escalation, then throw
   void finish_residual();
   void run_graph(int64_t pairs, int k);
+  int max_depth() const;  // deepest fused depth every slab runs (the prepared graphs' depth)
+  // depth of the next sweep of a `len`-step stretch (ending at a residual step if res_end), and in
+  // *graphable how many sweeps of that depth follow back to back without a residual
+  int plan_sweep(int64_t len, bool res_end, int64_t* graphable) const;
   void capture_graph(int parity, int k);
   void destroy_graph();
 

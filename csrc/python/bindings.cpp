@@ -457,6 +457,8 @@ PYBIND11_MODULE(_mdfx, m) {
       .def_property_readonly("graph_captures", [](PySolver& p) { return p.chk().stats().graph_captures; })
       .def("prepare_graphs", [](PySolver& p) { return p.chk().prepare_graphs(); },
            "capture both parities' 2-sweep hipGraph cycles now (0 if graphs are off / not capturable)")
+      .def("sweep_plan", [](PySolver& p, int64_t steps) { return p.chk().sweep_plan(steps); }, py::arg("steps"),
+           "the sweeps run(steps) would issue from here: a list of (fused depth, residual sweep)")
       .def("warm_kernels", [](PySolver& p, int64_t steps) { p.chk().warm_kernels(steps); }, py::arg("steps"),
            py::call_guard<py::gil_scoped_release>(),
            "launch every kernel instance run(steps) would use once, into the scratch buffer (state unchanged)")

@@ -233,6 +233,13 @@ class Simulation:
         one-time costs of a first launch stay out of a timed run. The field state is unchanged."""
         self._s.warm_kernels(int(steps))
 
+    def sweep_plan(self, steps: int) -> list:
+        """The sweeps run(steps) would issue from the current step: a list of (fused depth,
+        residual sweep). Each stretch up to a residual step (or the end) is cut into the fewest
+        sweeps of at most `temporal` steps with depths as even as possible (10 steps at temporal 4:
+        4, 3, 3)."""
+        return [(int(k), bool(r)) for k, r in self._s.sweep_plan(int(steps))]
+
     def prepare_graphs(self) -> int:
         """Capture the hipGraph cycles of both buffer parities now (graph=True and capturable), so
         that later run() calls only replay them: benchmarks call this before their warmup so no

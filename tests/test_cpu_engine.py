@@ -317,6 +317,29 @@ def test_deep_temporal_2d_equals_single_steps_cpu(mdfx, prob, temporal):
         assert np.array_equal(ref, sim.gather()) and abs(sim.residual - rr) <= 1e-9 * max(1.0, rr)
 
 
+def test_sweep_plan_even_depths(mdfx):
+    """run() cuts every stretch up to a residual step into the fewest sweeps of at most `temporal`
+    steps with depths as even as possible (the residual sweep last, shallower when depths differ),
+    and the result equals single steps bitwise whatever the plan."""
+    prob = m.heat3d(nx=40, ny=24, nz=36)
+    with m.Simulation(prob, device="cpu", ranks=2, temporal=4, residual_every=10) as sim:
+        assert sim.sweep_plan(20) == [(4, False), (3, False), (3, True)] * 2
+        assert sim.sweep_plan(12) == [(4, False), (3, False), (3, True), (2, False)]
+        sim.init()
+        sim.run(5)  # 5 steps: 3 + 2 (not 4 + 1); the next residual is then 5 steps away
+        assert sim.sweep_plan(5) == [(3, False), (2, True)]
+        assert sim.sweep_plan(17) == [(3, False), (2, True), (4, False), (3, False), (3, True), (2, False)]
+        sim.run(17)
+        got, gr = sim.gather(), sim.residual
+    with m.Simulation(prob, device="cpu", temporal=4) as sim:
+        assert sim.sweep_plan(9) == [(3, False)] * 3 and sim.sweep_plan(8) == [(4, False)] * 2
+    with m.Simulation(prob, device="cpu", residual_every=10) as sim:
+        assert sim.sweep_plan(3) == [(1, False)] * 3
+        sim.init()
+        sim.run(22)
+        assert np.array_equal(got, sim.gather()) and abs(gr - sim.residual) <= 1e-12 * max(1.0, gr)
+
+
 def test_cpu_avx2_and_baseline_builds_bitwise_equal(tmp_path):
     """The CPU stencils exist twice (baseline x86-64 with libm's software fma, and AVX2 + FMA chosen
     at run time); both are exact, so every stencil must agree bit for bit."""
