@@ -599,37 +599,21 @@ int Solver::max_depth() const {
 }
 
 // Sweep plan of a stretch of `len` steps (the steps up to the next residual evaluation, or to the
-// end of the run): the fewest sweeps of at most `temporal` steps, with depths as even as possible
-// (hi = ceil(len / n) and hi - 1), instead of the deepest sweeps first and the remainder in one
-// shallow sweep. A fused sweep costs about the same HBM traffic whatever its depth, and the shallow
-// kernels run fewer steps per byte: a 10-step residual interval at temporal 4 runs 4 + 3 + 3 rather
-// than 4 + 4 + 2, and 5 steps 3 + 2 rather than 4 + 1. The residual sweep is planned last and takes
-// the shallower depth when there is one, so the max_depth() sweeps stay paired for graph replay;
-// only max_depth() sweeps are replayed (the cycles prepare_graphs() captured), any other depth runs
-// eagerly instead of re-capturing a cycle. When a depth of the even plan has no kernel on some
-// slab, the deepest depth that fits is taken (the plan before round 4).
+// end of the run): the deepest sweeps first, the remainder in the deepest depth that fits. An even
+// plan (the fewest sweeps with depths as equal as possible: 10 steps at depth 3 as 3 + 3 + 2 + 2
+// instead of 3 + 3 + 3 + 1) measured slower, because the single-step sweep runs near the copy roof
+// while the shallow fused kernels do not: 2048^3 fp64 with a residual every 10 steps, 731.9 against
+// 754.0 GCells/s (profiles/r04_session_n/); per-sweep costs at 1024^3 fp32 make the two plans tie
+// (4 + 4 + 2 vs 4 + 3 + 3: 3.43 vs 3.40 single-sweep units from the K = 1..4 rates).
 int Solver::plan_sweep(int64_t len, bool res_end, int64_t* graphable) const {
   *graphable = 0;
-  if (len <= 1) return 1;
-  const int T = max_depth();
-  const int64_t n = (len + T - 1) / T;
-  const int hi = (int)((len + n - 1) / n), lo = hi - 1;
-  const int64_t c_hi = len - n * lo, c_lo = n - c_hi;
-  if (depth_ok_[hi] && (c_lo == 0 || depth_ok_[lo])) {
-    const bool res_hi = res_end && c_lo == 0;  // the residual sweep's depth is hi only if all are
-    const int64_t plain_hi = c_hi - (res_hi ? 1 : 0);
-    if (plain_hi > 0) {
-      if (hi == T) *graphable = plain_hi;
-      return hi;
-    }
-    return c_lo > 0 ? lo : hi;
-  }
   int k = 1;
-  for (int kk = (int)std::min<int64_t>(T, len); kk > 1; --kk)
+  for (int kk = (int)std::min<int64_t>(max_depth(), len); kk > 1; --kk)
     if (depth_ok_[kk]) {
       k = kk;
       break;
     }
+  // sweeps of depth k that follow back to back before the residual sweep
   *graphable = (len - (res_end ? 1 : 0)) / k;
   return k;
 }

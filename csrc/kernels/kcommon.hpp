@@ -239,9 +239,8 @@ struct Knobs {
   int life_tbk = 0;    // MDFX_LIFE_TBK: the same for Life
   int life_bits = 1;   // MDFX_LIFE_BITS: Life sweeps of K > 2 generations bit-sliced (0: SWAR life_tbk)
   int b27_tbk = 0;     // MDFX_B27_TBK: 27-point fused kernel (0: per dtype, -1: box27_tb2, 1/2/4: box27_tbk rows)
-  int wxk_diag = 0;
-  int wxk_strip = 1;
-  int b27_ry = 0;      // MDFX_B27_RY: box27_wxk band experiments (1: 1-row waves, 4: 4-wave bands)   // MDFX_WXK_STRIP: 2-wave heat7_wxk bands for pencil y strips (0 = the 8-wave bands)    // MDFX_WXK_DIAG: heat7_wxk timing diagnostics (bits: 1 no DMA, 2 no stores, 4 no barrier; garbage results)
+  int wxk_diag = 0;    // MDFX_WXK_DIAG: heat7_wxk timing diagnostics (bits: 1 no DMA, 2 no stores, 4 no barrier; garbage results)
+  int wxk_strip = 1;   // MDFX_WXK_STRIP: 2-wave heat7_wxk bands for pencil y strips (0: the 8-wave bands)
   int debug_zc = 0;    // MDFX_DEBUG_ZC: print the z chunking of the streaming kernels
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
 };

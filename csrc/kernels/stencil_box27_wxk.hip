@@ -296,10 +296,9 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
              "box27_wxk: row / plane counts must fit 32-bit indices");
   // 2-row inner waves, 1-row edge waves, bands of 8 (14 rows): the 3-row shapes need more than
-  // 256 VGPRs
-  if (knobs().b27_ry == 1) launch_b27x<T, 1, 1, 3, 8>(g, in, out, cf, resid, s);
-  else if (knobs().b27_ry == 4) launch_b27x<T, 2, 1, 3, 4>(g, in, out, cf, resid, s);
-  else launch_b27x<T, 2, 1, 3, 8>(g, in, out, cf, resid, s);
+  // 256 VGPRs; 1-row waves in bands of 8 and 2-row waves in bands of 4 measured slower at 512^3
+  // (fp64 500 / 603 vs 640 GCells/s, fp32 845 / 957 vs 1007: profiles/r04_session_n/)
+  launch_b27x<T, 2, 1, 3, 8>(g, in, out, cf, resid, s);
 }
 template void launch_box27_wxk<float>(const Geo&, const float*, float*, const StencilCoef&, int, double*, hipStream_t);
 template void launch_box27_wxk<double>(const Geo&, const double*, double*, const StencilCoef&, int, double*, hipStream_t);

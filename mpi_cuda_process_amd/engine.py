@@ -235,9 +235,9 @@ class Simulation:
 
     def sweep_plan(self, steps: int) -> list:
         """The sweeps run(steps) would issue from the current step: a list of (fused depth,
-        residual sweep). Each stretch up to a residual step (or the end) is cut into the fewest
-        sweeps of at most `temporal` steps with depths as even as possible (10 steps at temporal 4:
-        4, 3, 3)."""
+        residual sweep). Each stretch up to a residual step (or the end) runs sweeps of the deepest
+        depth first and the remainder in the deepest depth that fits (10 steps at temporal 4:
+        4, 4, 2)."""
         return [(int(k), bool(r)) for k, r in self._s.sweep_plan(int(steps))]
 
     def prepare_graphs(self) -> int:

@@ -317,22 +317,22 @@ def test_deep_temporal_2d_equals_single_steps_cpu(mdfx, prob, temporal):
         assert np.array_equal(ref, sim.gather()) and abs(sim.residual - rr) <= 1e-9 * max(1.0, rr)
 
 
-def test_sweep_plan_even_depths(mdfx):
-    """run() cuts every stretch up to a residual step into the fewest sweeps of at most `temporal`
-    steps with depths as even as possible (the residual sweep last, shallower when depths differ),
-    and the result equals single steps bitwise whatever the plan."""
+def test_sweep_plan(mdfx):
+    """run() cuts every stretch up to a residual step into sweeps of the deepest depth and a
+    remainder of the deepest depth that fits (the residual sweep last); sweep_plan() reports the
+    sweeps a run would issue, and the result equals single steps bitwise."""
     prob = m.heat3d(nx=40, ny=24, nz=36)
     with m.Simulation(prob, device="cpu", ranks=2, temporal=4, residual_every=10) as sim:
-        assert sim.sweep_plan(20) == [(4, False), (3, False), (3, True)] * 2
-        assert sim.sweep_plan(12) == [(4, False), (3, False), (3, True), (2, False)]
+        assert sim.sweep_plan(20) == [(4, False), (4, False), (2, True)] * 2
+        assert sim.sweep_plan(12) == [(4, False), (4, False), (2, True), (2, False)]
         sim.init()
-        sim.run(5)  # 5 steps: 3 + 2 (not 4 + 1); the next residual is then 5 steps away
-        assert sim.sweep_plan(5) == [(3, False), (2, True)]
-        assert sim.sweep_plan(17) == [(3, False), (2, True), (4, False), (3, False), (3, True), (2, False)]
+        sim.run(5)
+        assert sim.steps == 5 and sim.sweep_plan(5) == [(4, False), (1, True)]
+        assert sim.sweep_plan(17) == [(4, False), (1, True), (4, False), (4, False), (2, True), (2, False)]
         sim.run(17)
         got, gr = sim.gather(), sim.residual
     with m.Simulation(prob, device="cpu", temporal=4) as sim:
-        assert sim.sweep_plan(9) == [(3, False)] * 3 and sim.sweep_plan(8) == [(4, False)] * 2
+        assert sim.sweep_plan(9) == [(4, False), (4, False), (1, False)]
     with m.Simulation(prob, device="cpu", residual_every=10) as sim:
         assert sim.sweep_plan(3) == [(1, False)] * 3
         sim.init()
