@@ -431,7 +431,7 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 template <class T>
 void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  if (sizeof(T) == 8 && steps == 4) {
+  if (sizeof(T) == 8 && steps == 4 && knobs().f64k4 == 0) {
     launch_heat7_wtk<T>(g, in, out, r, steps, resid, s);
     return;
   }
@@ -462,7 +462,9 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
     if (steps == 3) launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
     else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
   } else {
-    launch_wxk<T, 3, 1, 3, 8>(g, in, out, r, resid, s);
+    // (K = 4: 2 + 1-row bands, 254 VGPRs; 2 + 2, 3 + 1 and 3 + 2 rows spill)
+    if (steps == 3) launch_wxk<T, 3, 1, 3, 8>(g, in, out, r, resid, s);
+    else launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);
   }
 }
 template void launch_heat7_wxk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);

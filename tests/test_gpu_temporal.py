@@ -480,6 +480,7 @@ def test_heat7_wxk_bitwise(hip, prob, k, resid, knob):
     barrier per plane) == K naive single steps, bitwise, with the residual of step K, for every
     shipped band and row count, including bands taller than the grid and waves wholly outside it."""
     knob("MDFX_H7_WXK", 1)
+    knob("MDFX_WXK_F64K4", 1)  # fp64 K = 4 through heat7_wxk too (its 2 + 1-row bands)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -536,7 +537,7 @@ def test_heat7_fp64_wide_rows_default_path(hip, resid):
 B27X = [models.box27(n=40), models.box27(n=24, dtype="f64"), models.box27(nx=700, ny=37, nz=15),
         models.box27(nx=1030, ny=9, nz=12), models.box27(nx=300, ny=70, nz=10, dtype="f64"),
         models.box27(nx=8, ny=5, nz=9),
-        # x-pair kernel (box27_wxp): rows of 257..512 cells, two 256-cell halves per block
+        # rows of 257..512 cells (3 overlapping x segments; round 3's x-pair kernel was removed)
         models.box27(nx=512, ny=29, nz=14), models.box27(nx=300, ny=17, nz=11), models.box27(nx=257, ny=9, nz=8),
         models.box27(nx=512, ny=5, nz=9), models.box27(nx=448, ny=40, nz=23)]
 
