@@ -59,18 +59,20 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
 double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
 // 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
-static bool use_wxk(DType dt, int64_t nx = 0);
+static bool use_wxk(DType dt, int64_t nx, int steps);
 static bool use_wtk(int steps, DType dt) {
   (void)dt;
   return knobs().h7_wtk >= 0 && heat7_wtk_supported(steps);
 }
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
 // 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
-// 0 / 1 forces it off / on (fp64 on: K = 3 only, heat7_wtk's K = 4). fp64 takes it from 2048-cell
-// rows on, in 3 + 1-row bands: 2048^3 fp64 + residual every 12 897 vs 796 GCells/s for heat7_wtk,
-// while at 1024-cell rows heat7_wtk's 3-row waves stay ahead (907 vs 874) (profiles/r03_session_p/)
-static bool use_wxk(DType dt, int64_t nx) {
-  return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (dt == DType::F32 || nx >= 2048));
+// 0 / 1 forces it off / on. fp64 K = 3 takes it from 2048-cell rows on, in 3 + 1-row bands: 2048^3
+// fp64 + residual every 12 897 vs 796 GCells/s for heat7_wtk, while at 1024-cell rows heat7_wtk's
+// 3-row waves stay ahead (907 vs 874) (profiles/r03_session_p/). fp64 K = 4 always runs it, in
+// 2 + 1-row bands (heat7_wtk's K = 4 needs 1-row waves: 1024^3 1112-1124 vs 418 GCells/s,
+// profiles/r04_session_o/)
+static bool use_wxk(DType dt, int64_t nx, int steps) {
+  return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (dt == DType::F32 || nx >= 2048 || steps == 4));
 }
 
 static int env_int(const char* name, int dflt) {
@@ -98,7 +100,6 @@ static Knobs read_knobs() {
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.wxk_diag = env_int("MDFX_WXK_DIAG", 0);
   k.wxk_strip = env_int("MDFX_WXK_STRIP", 1);
-  k.f64k4 = env_int("MDFX_WXK_F64K4", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
 }
@@ -282,8 +283,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
 
 bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int steps) {
   return !lay.pencil() && spec.kind == StencilKind::Heat7 && (steps == 3 || steps == 4) && lay.halo >= steps &&
-         dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx) &&
-         !(spec.dtype == DType::F64 && steps == 4);
+         dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx, steps);
 }
 
 int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
@@ -303,10 +303,13 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2 (round 2), 2048^3 fp32 1666 vs 1136,
       // 1024^3 fp64 823-825 vs 546, 2048^3 fp64 818 vs 556; since the natural-layout rows also
       // 512^3 fp32 (3 segments of 256 for 512 cells): 1311 vs 1230 (profiles/r03_wtk/). K = 4
-      // where heat7_wxk runs (fp32): its per-wave rows no longer grow with K, so the fourth step
-      // per pass costs less than the HBM pass it saves
-      if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
-        return (dev::use_wxk(spec.dtype, nx) && spec.dtype == DType::F32) ? 4 : 3;  // (fp64 K = 4 only in 1-row waves)
+      // where heat7_wxk runs: its per-wave rows no longer grow with K, so the fourth step per pass
+      // costs less than the HBM pass it saves (fp32; fp64 from 1024-cell rows on: 1024^3 1099 vs
+      // 885 GCells/s at K = 3, 2048^3 + residual every 12 969 vs 890, profiles/r04_session_o/)
+      if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66) {
+        if (!dev::use_wxk(spec.dtype, nx, 4)) return 3;
+        return (spec.dtype == DType::F32 || nx >= 1024) ? 4 : 3;
+      }
       return 2;
   }
   return 1;
@@ -318,7 +321,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
     // slab: one fill of the device, one launch gap); every other kernel runs them one after the other
     const bool fuse = a.lz_end > a.lz_begin &&
                       ((a.steps > 1 && spec.kind == StencilKind::Heat7 && dev::use_wtk(a.steps, spec.dtype) &&
-                        dev::use_wxk(spec.dtype, a.lay.global.nx)) ||
+                        dev::use_wxk(spec.dtype, a.lay.global.nx, a.steps)) ||
                        (spec.kind == StencilKind::Box27 && a.steps == 3));
     if (!fuse) {
       RegionArgs r1 = a, r2 = a;
@@ -405,7 +408,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       } else {
         dev::launch_jacobi5_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.resid, s);
       }
-    } else if (dev::use_wtk(a.steps, spec.dtype) && dev::use_wxk(spec.dtype, a.lay.global.nx)) {
+    } else if (dev::use_wtk(a.steps, spec.dtype) && dev::use_wxk(spec.dtype, a.lay.global.nx, a.steps)) {
       if (spec.dtype == DType::F32)
         dev::launch_heat7_wxk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
       else

@@ -424,17 +424,15 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 // box and 2095-2138 on two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row band also
 // fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
 // (profiles/r03_wxk/). fp32 K = 3 (step-count remainders): 4-row waves. fp64 K = 3: 3 + 1-row bands
-// (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2); fp64 K = 4 stays on heat7_wtk. Round 3's
+// (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2); fp64 K = 4: 2 + 1-row bands (254 VGPRs;
+// the 2 + 2, 3 + 1 and 3 + 2-row bands spill), 1024^3 1112-1124 GCells/s against 418 for heat7_wtk's
+// 1-row K = 4 and 870-885 at K = 3 (profiles/r04_session_o/). Round 3's
 // other shapes (4-wave bands, 2-row and 3 + 1-row fp32 bands, the 5-step sweep, 3 window buffers /
 // one seam table) measured slower and were removed in round 4; their numbers stay in
 // profiles/r03_wxk/ and profiles/r03_session_r/.
 template <class T>
 void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  if (sizeof(T) == 8 && steps == 4 && knobs().f64k4 == 0) {
-    launch_heat7_wtk<T>(g, in, out, r, steps, resid, s);
-    return;
-  }
   MDFX_CHECK((steps == 3 || steps == 4) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_wxk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
@@ -451,7 +449,8 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   const bool strip = g.ly_end - g.ly_begin <= 4 && (g.ly_begin != 0 || g.ly_end != g.ny) && knobs().wxk_strip != 0;
   if (strip) {
     if constexpr (sizeof(T) == 8) {
-      launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);  // (fp64 K = 4 went to heat7_wtk above)
+      MDFX_CHECK(steps == 3, "heat7_wxk: fp64 pencil strips run K = 3");
+      launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
     } else {
       if (steps == 3) launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
       else launch_wxk<T, 2, 2, 4, 2>(g, in, out, r, resid, s);

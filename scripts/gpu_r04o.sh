@@ -7,7 +7,7 @@ mkdir -p gpurun_out/o
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
   tests/test_gpu_temporal.py -k "wxk" > gpurun_out/o/tests.log 2>&1 || { tail -30 gpurun_out/o/tests.log; exit 1; }
 tail -2 gpurun_out/o/tests.log
-for n in 1024 2048; do
+for n in 1024; do  # (2048^3 fp64: kernel_ab's fields do not fit; the bench below covers it)
   timeout -k 10 300 python bench/kernel_ab.py --kind heat7 --n $n --dtype f64 --iters 6 --rounds 3 \
     --variants "STEPS=3;STEPS=4;STEPS=4,F64K4=1,WXK=1;STEPS=3,WXK=1" > gpurun_out/o/ab_$n.log 2>&1 || { tail -20 gpurun_out/o/ab_$n.log; exit 1; }
   tail -5 gpurun_out/o/ab_$n.log

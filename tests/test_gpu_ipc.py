@@ -129,6 +129,24 @@ def test_ipc_protocols_and_copy_engines(hip, tmp_path, transport, direct, world,
     assert abs(meta["residual"] - rres) <= 1e-9 * rres
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_ipc_fp64_fused_k4_folded(hip, tmp_path, graph):
+    """fp64 K = 4 sweeps (heat7_wxk 2 + 1-row bands, the lower boundary folded into the interior
+    sweep) over three processes: bitwise equal to one process, residual included."""
+    import mpi_cuda_process_amd as m
+
+    prob_src = "m.heat3d(nx=256, ny=40, nz=50, dtype='f64')"
+    out = str(tmp_path / "g.npy")
+    steps = 13
+    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=4, graph=graph, steps=steps,
+                         transport="ipc")
+    _spawn(3, lambda r: [sys.executable, "-c", code])
+    ref, rres = _reference(eval(prob_src), steps)
+    assert np.array_equal(np.load(out), ref)
+    meta = json.load(open(out + ".json"))
+    assert abs(meta["residual"] - rres) <= 1e-9 * rres
+
+
 @pytest.mark.parametrize("world,py,temporal,graph,transport,prob_src", [
     (4, 2, 4, False, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),   # 2 x 2 pencils, the fused K = 4 sweep
     (4, 2, 3, True, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),    # ... K = 3, replayed

@@ -480,7 +480,6 @@ def test_heat7_wxk_bitwise(hip, prob, k, resid, knob):
     barrier per plane) == K naive single steps, bitwise, with the residual of step K, for every
     shipped band and row count, including bands taller than the grid and waves wholly outside it."""
     knob("MDFX_H7_WXK", 1)
-    knob("MDFX_WXK_F64K4", 1)  # fp64 K = 4 through heat7_wxk too (its 2 + 1-row bands)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -506,10 +505,10 @@ def test_heat7_wxk_bitwise(hip, prob, k, resid, knob):
 
 @pytest.mark.parametrize("resid", [False, True])
 def test_heat7_fp64_wide_rows_default_path(hip, resid):
-    """fp64 rows of 2048 cells and more take heat7_wxk (3 + 1-row bands) at K = 3 by default: the
-    engine's default fused depth and kernel == 3 naive single steps, bitwise."""
+    """fp64 rows of 1024 cells and more take heat7_wxk (2 + 1-row bands) at K = 4 by default: the
+    engine's default fused depth and kernel == 4 naive single steps, bitwise."""
     prob = models.heat3d(nx=2048, ny=23, nz=11, dtype="f64")
-    k = 3
+    k = 4
     assert native().hip_fused_depth(prob.kind, prob.dtype, prob.nx, False) == k
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")

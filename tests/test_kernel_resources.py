@@ -61,6 +61,9 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false, false, false, false>", 2),        # K = 3 (step-count remainders)
     ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false, false, false, false>", 2),       # fp64 K = 3 (2048^3 + residual)
     ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true, false, false, false>", 2),
+    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, false, false>", 2),       # fp64 K = 4 (the default from 1024-cell rows)
+    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, true, false, false, false>", 2),
+    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, false, true>", 2),        # its folded-boundary copy
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false>", 2),              # 27-point K = 3 (1024-cell rows, fp64)
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false>", 2),
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true>", 2),
