@@ -52,9 +52,13 @@ bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int ste
 // Whether a fused multi-step sweep is implemented for this stencil / grid on the device.
 bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps);
 // The deepest fused sweep that is a measured win for this stencil at row width nx (before any
-// cap by slab depth): 8 for the 2D MDF, 12 for Life, 3 for the 3D 7-point where heat7_wtk's x
-// segments cover the row efficiently, else 2 (profiles/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt).
+// cap by slab depth): 8 for the 2D MDF, 12 for Life, 4 for the 3D 7-point where heat7_wxk's x
+// segments cover the row efficiently (fp64: rows of 1024+ cells, else 3), else 2
+// (profiles/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt, r04_session_o/).
 int hip_fused_depth(const StencilSpec& spec, int64_t nx);
+// Relative time of one `steps`-step sweep on the device, in single-step sweeps of the same grid
+// (the engine's sweep plan minimises the sum over a residual stretch).
+double hip_sweep_cost(const StencilSpec& spec, int64_t nx, int steps);
 // One step shallower than `steps` among the fused depths (12 -> 6 -> 3 -> 2 -> 1).
 inline int shallower_depth(int steps) { return steps == 3 ? 2 : steps / 2; }
 

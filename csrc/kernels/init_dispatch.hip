@@ -315,6 +315,21 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
   return 1;
 }
 
+// From the per-step rates of each fused depth on one MI355X (GCells/s; the time of a k-step sweep
+// is k / rate_k): 3D 7-point fp32 1024^3 694 / 1300 / 1896 / 2350 for K = 1..4, fp64 347 / 546 /
+// 885 / 1110 (profiles/r03_wxk/first_ab.txt, r04_session_o/). Elsewhere a
+// deeper sweep is taken to cost 5 % more per pass than a single step, which makes the plan the
+// fewest sweeps with the deepest first.
+double hip_sweep_cost(const StencilSpec& spec, int64_t nx, int steps) {
+  if (steps <= 1) return 1.0;
+  if (spec.kind == StencilKind::Heat7 && steps <= 4 && nx >= 1024) {
+    static const double f32[5] = {0.0, 1.0, 1.07, 1.10, 1.18};
+    static const double f64[5] = {0.0, 1.0, 1.27, 1.18, 1.25};
+    return (spec.dtype == DType::F64 ? f64 : f32)[steps];
+  }
+  return 1.0 + 0.05 * (steps - 1);
+}
+
 void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   if (a.lz2_end > a.lz2_begin) {
     // two regions in one call: heat7_wtk sweeps them in ONE launch (both boundary regions of a

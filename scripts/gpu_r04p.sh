@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4, session P: fp64 K = 4 through heat7_wxk as the default (fused depth 4 from 1024-cell
-# rows): GPU tests of the kernels / engine / ipc / proxy, then the fp64 bench configs.
+# rows) and the cost-based sweep plan: GPU tests of the kernels / engine / ipc / proxy, then the
+# fp64 bench configs.
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/p

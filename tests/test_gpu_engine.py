@@ -247,6 +247,27 @@ def test_advance_on_gpu_equals_cpu(hip, prob, steps):
     assert gpu.is_cuda and torch.equal(gpu.cpu(), cpu)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_sweep_plan_by_cost_on_gpu(hip, dtype):
+    """On the GPU the residual stretch is cut by the measured sweep costs: 10 steps at depth 4 on
+    1024-cell rows run 4 + 3 + 3 (4 + 4 + 2 would spend a sweep on the slow two-step kernel), the
+    residual by the last sweep; narrower rows keep 4 + 4 + 2. Bitwise equal to single steps."""
+    prob = m.heat3d(nx=1024, ny=20, nz=40, dtype=dtype)
+    with m.Simulation(prob, device="hip", ranks=2, temporal=4, residual_every=10) as sim:
+        assert sim.sweep_plan(20) == [(4, False), (3, False), (3, True)] * 2
+        sim.init()
+        sim.run(23)
+        got, gr = sim.gather(), sim.residual
+    with m.Simulation(prob, device="hip", temporal=1, residual_every=10) as sim:
+        sim.init()
+        sim.run(23)
+        assert np.array_equal(got, sim.gather()) and abs(gr - sim.residual) <= 1e-9 * max(1.0, gr)
+    with m.Simulation(m.heat3d(nx=512, ny=20, nz=40, dtype=dtype), device="hip", temporal=4 if dtype == "f32" else 3,
+                      residual_every=10) as sim:
+        assert sim.sweep_plan(10) == ([(4, False), (4, False), (2, True)] if dtype == "f32" else
+                                      [(3, False), (3, False), (3, False), (1, True)])
+
+
 def test_auto_temporal_on_gpu(hip):
     from mpi_cuda_process_amd.engine import auto_temporal
 
