@@ -649,9 +649,11 @@ double Solver::tail_plan(int r, int T, int* first) const {
 
 int Solver::plan_sweep(int64_t len, bool res_end, int64_t* graphable) const {
   *graphable = 0;
-  if (len <= 1) return 1;
   const int T = max_depth();
-  if (T <= 1) return 1;
+  if (T <= 1 || len <= 1) {  // single steps: all but the residual step replay in pairs
+    *graphable = len - (res_end ? 1 : 0);
+    return 1;
+  }
   // candidate tails: len mod T and one more sweep's worth; the rest runs at depth T
   const int64_t m = len % T;
   int64_t best_r = -1;
