@@ -61,7 +61,7 @@ def test_proxy_pencil_matches_full_grid_away_from_boundaries(hip, n, py, r, temp
     from mpi_cuda_process_amd.parallel.decomp import pencil_neighbors
 
     prob = m.heat3d(nx=1024 if temporal >= 3 else 256, ny=40 * py, nz=36 * (n // py))
-    steps = 6
+    steps = 2 * temporal  # one replayed 2-sweep cycle at the full depth
     full = _full(prob, steps, temporal)
     with m.Simulation(prob, device="hip", ranks=n, proxy_rank=r, temporal=temporal, graph=graph, py=py) as sim:
         sim.init()
