@@ -199,7 +199,7 @@ def pick_temporal(a, prob, nslab, hip):
     if a.temporal > 0:
         return a.temporal
     # the deepest measured-win fused depth (native hip_fused_depth: 4 for the 3D 7-point through
-    # heat7_wxk where its x segments cover the row (fp64: rows of 1024+ cells, else 3); 3 for the
+    # heat7_wxk where its x segments cover the row; 3 for the
     # 27-point at 1024-cell rows
     # and in fp64, else 2; 8 (MDF) / 12 (Life) for the 2D ones; profiles/r03_wxk/, r02_mdf2d/,
     # r02_life.txt), made shallower until every slab is at least 4 sweeps deep

@@ -69,7 +69,7 @@ void usage(const char* prog) {
       "  --json                    one JSON metrics line ; --verbose per-rank detail ; --quiet\n"
       "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n"
       "  --temporal 0..16          time steps fused per memory sweep (0 = auto on GPUs: 4 for the 3D\n"
-      "                            7-point (fp64: rows of 1024+ cells, else 3), 3 for the 27-point in\n"
+      "                            7-point where heat7_wxk covers the row, 3 for the 27-point in\n"
       "                            fp64 or at rows of 1024+ cells, else 2 for 3D; 8 for the 2D MDF,\n"
       "                            12 for Life; 1 on the CPU; shallower until slabs are 4 sweeps deep)\n"
       "  --profile                 per-phase timing of rank 0 (boundary / interior / exchange)\n"

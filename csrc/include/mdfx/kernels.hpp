@@ -53,7 +53,7 @@ bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int ste
 bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int steps);
 // The deepest fused sweep that is a measured win for this stencil at row width nx (before any
 // cap by slab depth): 8 for the 2D MDF, 12 for Life, 4 for the 3D 7-point where heat7_wxk's x
-// segments cover the row efficiently (fp64: rows of 1024+ cells, else 3), else 2
+// segments cover the row efficiently, else 2
 // (profiles/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt, r04_session_o/).
 int hip_fused_depth(const StencilSpec& spec, int64_t nx);
 // Relative time of one `steps`-step sweep on the device, in single-step sweeps of the same grid

@@ -304,12 +304,10 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // 1024^3 fp64 823-825 vs 546, 2048^3 fp64 818 vs 556; since the natural-layout rows also
       // 512^3 fp32 (3 segments of 256 for 512 cells): 1311 vs 1230 (profiles/r03_wtk/). K = 4
       // where heat7_wxk runs: its per-wave rows no longer grow with K, so the fourth step per pass
-      // costs less than the HBM pass it saves (fp32; fp64 from 1024-cell rows on: 1024^3 1099 vs
-      // 885 GCells/s at K = 3, 2048^3 + residual every 12 969 vs 890, profiles/r04_session_o/)
-      if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66) {
-        if (!dev::use_wxk(spec.dtype, nx, 4)) return 3;
-        return (spec.dtype == DType::F32 || nx >= 1024) ? 4 : 3;
-      }
+      // costs less than the HBM pass it saves (fp32; fp64 in round 4: 512^3 983 vs 740 GCells/s at
+      // K = 3, 1024^3 1121 vs 885, 2048^3 + residual every 12 953 vs 890, profiles/r04_session_{o,p}/)
+      if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
+        return dev::use_wxk(spec.dtype, nx, 4) ? 4 : 3;
       return 2;
   }
   return 1;
