@@ -292,8 +292,8 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
       MDFX_FAIL("unknown transport " + tname);
     }
     if (o.temporal <= 0 && o.py > 1) {
-      // pencils: the fused 7-point sweep (heat7_wxk K = 4 fp32 / 3 fp64) is the one with y ghost rows
-      const int want = spec.kind == StencilKind::Heat7 ? (spec.dtype == DType::F32 ? 4 : 3) : 1;
+      // pencils: the fused 7-point sweep (heat7_wxk K = 4) is the one with y ghost rows
+      const int want = spec.kind == StencilKind::Heat7 ? 4 : 1;
       const int64_t pz = nranks / o.py;
       o.temporal = hip && want > 1 && g.nz >= 4 * want * pz && g.ny >= 4 * want * o.py ? want : 1;
     }

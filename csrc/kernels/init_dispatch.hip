@@ -259,7 +259,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
   if (steps < 2 || lay.halo < steps) return false;
   if (lay.pencil())  // pencils (y ghost rows): the fused 7-point sweep of heat7_wxk only
     return spec.kind == StencilKind::Heat7 && dev::heat7_wxk_supported(steps) && lay.hy >= steps &&
-           dev::knobs().h7_wxk != 0 && !(spec.dtype == DType::F64 && steps == 4);
+           dev::knobs().h7_wxk != 0;
   const bool k2d = steps == 2 || steps == 3 || steps == 4 || steps == 6 || steps == 8;
   if (spec.kind == StencilKind::Jacobi5)  // deep temporal blocking of the 2D problems
     return (spec.dtype == DType::F32 || spec.dtype == DType::F64) && k2d;  // ref precision too (jacobi5_tbk REF)

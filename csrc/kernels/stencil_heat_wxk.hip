@@ -448,13 +448,8 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   // (and 4 blocks per CU, so the strip's few tiles split into many z chunks). MDFX_WXK_STRIP=0: off.
   const bool strip = g.ly_end - g.ly_begin <= 4 && (g.ly_begin != 0 || g.ly_end != g.ny) && knobs().wxk_strip != 0;
   if (strip) {
-    if constexpr (sizeof(T) == 8) {
-      MDFX_CHECK(steps == 3, "heat7_wxk: fp64 pencil strips run K = 3");
-      launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
-    } else {
-      if (steps == 3) launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
-      else launch_wxk<T, 2, 2, 4, 2>(g, in, out, r, resid, s);
-    }
+    if (steps == 3) launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
+    else launch_wxk<T, 2, 2, 4, 2>(g, in, out, r, resid, s);  // (fp64: 256 VGPRs, no spills)
     return;
   }
   if constexpr (sizeof(T) == 4) {

@@ -43,11 +43,11 @@ def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1) -> in
     if device != "hip":
         return 1
     if py > 1:
-        # pencils: the fused 7-point sweep (heat7_wxk, K = 4 fp32 / 3 fp64) is the one that takes
-        # y ghost rows; the other stencils step singly
+        # pencils: the fused 7-point sweep (heat7_wxk, K = 4) is the one that takes y ghost rows;
+        # the other stencils step singly
         if problem.kind != "heat7":
             return 1
-        want = 4 if problem.dtype == "f32" else 3
+        want = 4
         pz = nranks // py
         return want if problem.nz >= 4 * want * pz and problem.ny >= 4 * want * py else 1
     want = native().hip_fused_depth(problem.kind, problem.dtype, problem.nx, problem.ref_precision)

@@ -342,6 +342,22 @@ def test_pencil_loopback_other_stencils(hip, prob, temporal):
         assert abs(sim.residual - rres) <= 1e-9 * rres
 
 
+@pytest.mark.parametrize("ranks,py", [(4, 2), (8, 4)])
+def test_pencil_loopback_fp64_k4(hip, ranks, py):
+    # fp64 K = 4 pencils: heat7_wxk's 2 + 1-row bands inside, 2 + 2-row 2-wave strips along the y
+    # neighbours; residual sweeps included, replayed cycles in between
+    prob = m.heat3d(nx=256, ny=72, nz=64, dtype="f64")
+    with m.Simulation(prob, device="hip", residual_every=8) as sim:
+        ref = sim.init().run(17).gather()
+        rres = sim.residual
+    with m.Simulation(prob, device="hip", ranks=ranks, py=py, temporal=4, graph=True, residual_every=8) as sim:
+        sim.init()
+        sim.prepare_graphs()
+        sim.run(17)
+        assert np.array_equal(sim.gather(), ref)
+        assert abs(sim.residual - rres) <= 1e-9 * rres
+
+
 def test_pencil_headline_shape_matches_slabs(hip):
     # the 1024^3 fp32 grid as 4 x 2 pencils (520-row pencils: the fused sweep's band / z-chunk
     # geometry at the N = 8 shape) against the slab split of the same ranks
