@@ -454,6 +454,8 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   }
   if constexpr (sizeof(T) == 4) {
     if (steps == 3) launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
+    else if (knobs().wxk_shape == 1) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);  // (experiment)
+    else if (knobs().wxk_shape == 2) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);  // (experiment)
     else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
   } else {
     // (K = 4: 2 + 1-row bands, 254 VGPRs; 2 + 2, 3 + 1 and 3 + 2 rows spill)
