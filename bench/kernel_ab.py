@@ -26,7 +26,7 @@ from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, i
 
 KEYS = {"RY": "MDFX_RY", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
         "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBKRY": "MDFX_TBK_RY", "B27TBK": "MDFX_B27_TBK", "WB": "MDFX_WTK_WB", "WXK": "MDFX_H7_WXK", "B27WXK": "MDFX_B27_WXK",
-        "DIAG": "MDFX_WXK_DIAG", "STRIP": "MDFX_WXK_STRIP", "SHAPE": "MDFX_WXK_SHAPE", "DBGZC": "MDFX_DEBUG_ZC"}
+        "DIAG": "MDFX_WXK_DIAG", "STRIP": "MDFX_WXK_STRIP", "DBGZC": "MDFX_DEBUG_ZC"}
 
 
 def parse_variant(s):

@@ -100,7 +100,6 @@ static Knobs read_knobs() {
   k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
   k.wxk_diag = env_int("MDFX_WXK_DIAG", 0);
   k.wxk_strip = env_int("MDFX_WXK_STRIP", 1);
-  k.wxk_shape = env_int("MDFX_WXK_SHAPE", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
 }

@@ -241,7 +241,6 @@ struct Knobs {
   int b27_tbk = 0;     // MDFX_B27_TBK: 27-point fused kernel (0: per dtype, -1: box27_tb2, 1/2/4: box27_tbk rows)
   int wxk_diag = 0;    // MDFX_WXK_DIAG: heat7_wxk timing diagnostics (bits: 1 no DMA, 2 no stores, 4 no barrier; garbage results)
   int wxk_strip = 1;   // MDFX_WXK_STRIP: 2-wave heat7_wxk bands for pencil y strips (0: the 8-wave bands)
-  int wxk_shape = 0;   // MDFX_WXK_SHAPE: fp32 K = 4 band experiment (1: 3 + 1 rows, 2: 2 + 1 rows)
   int debug_zc = 0;    // MDFX_DEBUG_ZC: print the z chunking of the streaming kernels
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
 };

@@ -426,8 +426,10 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 // (profiles/r03_wxk/). fp32 K = 3 (step-count remainders): 4-row waves. fp64 K = 3: 3 + 1-row bands
 // (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2); fp64 K = 4: 2 + 1-row bands (254 VGPRs;
 // the 2 + 2, 3 + 1 and 3 + 2-row bands spill), 1024^3 1112-1124 GCells/s against 418 for heat7_wtk's
-// 1-row K = 4 and 870-885 at K = 3 (profiles/r04_session_o/). Round 3's
-// other shapes (4-wave bands, 2-row and 3 + 1-row fp32 bands, the 5-step sweep, 3 window buffers /
+// 1-row K = 4 and 870-885 at K = 3 (profiles/r04_session_o/). fp32 K = 4 in 3 + 1 and 2 + 1-row
+// bands measured slower (1024^3 kernel A/B 2256 / 2223 vs 2523 GCells/s, driver form 2148 / 2121 vs
+// 2372; profiles/r04_session_r/). Round 3's other shapes (4-wave bands, 2-row fp32 bands, the 5-step
+// sweep, 3 window buffers /
 // one seam table) measured slower and were removed in round 4; their numbers stay in
 // profiles/r03_wxk/ and profiles/r03_session_r/.
 template <class T>
@@ -454,8 +456,6 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   }
   if constexpr (sizeof(T) == 4) {
     if (steps == 3) launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
-    else if (knobs().wxk_shape == 1) launch_wxk<T, 3, 1, 4, 8>(g, in, out, r, resid, s);  // (experiment)
-    else if (knobs().wxk_shape == 2) launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);  // (experiment)
     else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
   } else {
     // (K = 4: 2 + 1-row bands, 254 VGPRs; 2 + 2, 3 + 1 and 3 + 2 rows spill)
