@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 4 session S: the whole GPU tier, smoke(), the driver's default bench and N = 1 form, and every
+# BASELINE config, after the fp64 K = 4 default, fp64 pencils and the cost-based sweep plan.
+set -o pipefail
+cd "$(dirname "$0")/.."
+scripts/gpu_session.sh native || exit $?
+tail -2 gpurun_out/native.log
+LIMIT=900 scripts/gpu_session.sh "gputests=python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests" || exit $?
+grep -E "passed|failed" gpurun_out/gputests.log | tail -2
+scripts/gpu_session.sh smoke "b_default=python bench.py" "b_driver=python bench.py --gpus 1 --steps 20 --warmup 5" || exit $?
+for f in b_default b_driver; do echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/$f.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$f.log | head -1)"; done
+LIMIT=700 scripts/gpu_session.sh "baseline=bash scripts/baseline_configs.sh" || exit $?
+for f in gpurun_out/baseline_*.json; do echo "$(basename $f .json) $(grep -o '"value": [0-9.]*' $f | head -1)"; done
