@@ -31,12 +31,17 @@ def child(a):
     combos = [("ipc", 1), ("ipc", 2), ("ipc_sdma", 1), ("ipc_sdma", 2)] * a.passes
     t0 = time.time()
     for i, (t, py) in enumerate(combos):
-        sim = m.Simulation(prob, device="hip", distributed=True, transport=t, py=py, temporal=4, devices=[0],
-                           timeout_s=60.0)
-        sim.init()
-        sim.run(8)
-        sim.synchronize()
-        sim.close()
+        try:
+            sim = m.Simulation(prob, device="hip", distributed=True, transport=t, py=py, temporal=4, devices=[0],
+                               timeout_s=60.0)
+            sim.init()
+            sim.run(8)
+            sim.synchronize()
+            sim.close()
+        except Exception as e:  # noqa: BLE001 - name the rank and engine, then fail
+            print("CHURN rank %d engine %d %s py=%d FAILED: %s: %s" % (env.rank, i, t, py, type(e).__name__, e),
+                  file=sys.stderr, flush=True)
+            raise
         if env.rank == 0:
             print("engine %d %s py=%d ok (+%.1fs)" % (i, t, py, time.time() - t0), flush=True)
     dist.barrier()
@@ -63,8 +68,10 @@ def main():
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--child", "--n", str(a.n),
                                        "--passes", str(a.passes)], env=env))
     rc = 0
-    for q in procs:
+    for r, q in enumerate(procs):
         q.wait()
+        if q.returncode != 0:
+            print("ipc_churn rank %d exit status %d" % (r, q.returncode), flush=True)
         rc = rc or q.returncode
     print("ipc_churn world=%d rc=%d" % (a.world, rc), flush=True)
     return rc

@@ -270,5 +270,11 @@ def test_ipc_engines_rebuilt_in_turn_by_eight_processes(hip):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "ipc_churn.py"), "--world", "8"],
                        capture_output=True, timeout=240, cwd=ROOT)
     out = p.stdout.decode()
-    assert p.returncode == 0, out + p.stderr.decode()[-3000:]
+    if p.returncode != 0:
+        err = p.stderr.decode()
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", "ipc_churn_stderr.log"), "w") as f:
+            f.write(err)
+        key = [l for l in err.splitlines() if "CHURN" in l or "HIP" in l or "mdfx" in l.lower()]
+        raise AssertionError(out + "\n".join(key[:40]) + "\n" + err[-1500:])
     assert "engine 7 ipc_sdma py=2 ok" in out
