@@ -353,6 +353,30 @@ class IpcTransport final : public Transport {
     join();
     if (!capturing) last_b_ = b;
   }
+  std::string debug_state() override {
+    if (!dev_ok_ || !ctr_) return "";
+    self_.be->activate();
+    uint64_t c[128] = {0};
+    if (hipMemcpy(c, ctr_, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();
+      return "ipc: counters unreadable";
+    }
+    std::string out = format("ipc rank %d (%s): ready %llu readyZ %llu", self_.rank, direct_ ? "direct" : "mailbox",
+                             (unsigned long long)c[kReady], (unsigned long long)c[kReadyZ]);
+    for (int side = 0; side < 4; ++side) {
+      const Peer& p = peers_[side];
+      if (p.rank < 0) continue;
+      uint64_t r[128] = {0};
+      const bool ok = p.ctr && hipMemcpy(r, p.ctr, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess;
+      if (!ok) (void)hipGetLastError();
+      out += format("; side %d (rank %d): pulled %llu expReady %llu expPulled %llu | its ready %lld readyZ %lld "
+                    "pulled[mine] %lld",
+                    side, p.rank, (unsigned long long)c[kPulled + side], (unsigned long long)c[kExpReady + side],
+                    (unsigned long long)c[kExpPulled + side], ok ? (long long)r[kReady] : -1LL,
+                    ok ? (long long)r[kReadyZ] : -1LL, ok ? (long long)r[kPulled + (side ^ 1)] : -1LL);
+    }
+    return out;
+  }
   void set_last_parity(int b) override { last_b_ = b; }
   // a captured 2-exchange cycle bakes the look-ahead of its first wait: the engine replays one only
   // when the exchange before it used the other parity (Solver::run)

@@ -116,6 +116,9 @@ class Transport {
   // Watchdog escalation: make every outstanding transport operation return (ncclCommAbort, the
   // device abort word) so the streams drain and the process can exit instead of hanging.
   virtual void abort() {}
+  // Watchdog diagnostics: the transport's device counters (the ipc protocol's ready / pulled
+  // words, its private expect counters and its neighbours' words), printed before an abort.
+  virtual std::string debug_state() { return ""; }
   // Parity of the buffer the last exchange() sent (-1: none yet, or the transport does not track
   // it). The ipc transport uses it to reuse a mailbox slot safely when a parity repeats.
   virtual int last_parity() const { return -1; }
