@@ -236,10 +236,12 @@ void Solver::poison(const std::string& why) {
     for (auto& s : slabs_) {
       if (!s.sig || s.be->kind() != DeviceKind::HIP) continue;
       s.be->activate();
-      unsigned long long v[33] = {0};
+      unsigned long long v[96] = {0};
       if (hipMemcpy(v, s.sig, sizeof(v), hipMemcpyDeviceToHost) == hipSuccess)
-        std::fprintf(stderr, "[mdfx] rank %d fold counters: arrivals %llu signals %llu expected %llu\n", s.rank, v[0],
-                     v[16], v[32]);
+        std::fprintf(stderr,
+                     "[mdfx] rank %d fold counters: upper launch arrivals %llu signals %llu expected %llu; interior "
+                     "arrivals %llu signals %llu expected %llu\n",
+                     s.rank, v[0], v[16], v[64], v[32], v[48], v[80]);
       else
         (void)hipGetLastError();
     }
@@ -345,7 +347,7 @@ void Solver::boundary_kernels(Slab& s, RegionArgs a, void* stream, bool skip_lo)
     if (s.hi_e > s.hi_b) {
       a.lz_begin = s.hi_b;
       a.lz_end = s.hi_e;
-      a.sig = s.sig;
+      a.sig = s.sig;  // (its own counter block: never shared with the interior sweep's)
       a.sig_z = s.hi_e;
       s.be->stencil(spec_, a, stream);
     }
@@ -387,7 +389,7 @@ void Solver::interior_kernel(Slab& s, RegionArgs a, void* stream, bool with_lo) 
     a.lz_begin = s.lo_b;
     a.lz_end = s.in_e;
     a.lz2_begin = a.lz2_end = 0;
-    a.sig = s.sig;
+    a.sig = s.sig + 32;
     a.sig_z = s.lo_e;
     s.be->stencil(spec_, a, stream);
     return;
@@ -456,8 +458,9 @@ void Solver::step(bool want_resid, int k) {
     // ghosts of `nb`, after the previous step's kernels that read them.
     if (fold) {
       const double to = opt_.timeout_s > 0 ? opt_.timeout_s : 300.0;
-      for (int i = s.hi_e > s.hi_b ? 2 : 1; i > 0; --i)
-        hip_counter_wait((const uint64_t*)(s.sig + 16), (uint64_t*)(s.sig + 32), to, s.hs, 0, nullptr);
+      if (s.hi_e > s.hi_b)
+        hip_counter_wait((const uint64_t*)(s.sig + 16), (uint64_t*)(s.sig + 64), to, s.hs, 0, nullptr);
+      hip_counter_wait((const uint64_t*)(s.sig + 48), (uint64_t*)(s.sig + 80), to, s.hs, 0, nullptr);
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[3], (hipStream_t)is));
     if (prof && !prof_hip && &s == &slabs_[0]) c2 = clk::now();

@@ -40,7 +40,7 @@ struct RegionArgs {
   // Folded boundary (slabs, fused 7-point sweeps through heat7_wxk: hip_region_signals): the region
   // starts at the lower boundary planes [lz_begin, sig_z), and once every block has stored them the
   // kernel bumps the device counter sig[16] by one (sig[0] counts the blocks' arrivals; both in
-  // memory from hip_alloc_uncached). The halo stream waits for that counter instead of a separate
+  // memory from hip_alloc_uncached, one counter block per signalling launch). The halo stream waits for that counter instead of a separate
   // boundary launch, so the lower face is sent while the same sweep continues upward.
   unsigned long long* sig = nullptr;
   int64_t sig_z = 0;

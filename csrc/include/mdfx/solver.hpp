@@ -135,8 +135,10 @@ class Solver {
     // pencils: storage-row regions of the interior planes (y-boundary strips and interior rows;
     // all 0 for slabs: every owned row)
     int64_t ylo_b = 0, ylo_e = 0, yhi_b = 0, yhi_e = 0, yin_b = 0, yin_e = 0;
-    // folded lower boundary (fold_ok()): device counters from hip_alloc_uncached, [0] the interior
-    // blocks' arrivals, [16] sweeps whose lower face is stored, [32] the halo stream's private expect
+    // folded lower boundary (fold_ok()): device counters from hip_alloc_uncached, one block of 32
+    // words per signalling launch (the upper boundary launch at [0], the interior sweep at [32]):
+    // [+0] the launch's block arrivals, [+16] its completed signals; [64] / [80] the halo stream's
+    // private expect counters for the two
     unsigned long long* sig = nullptr;
   };
   void step(bool want_resid, int k);

@@ -69,8 +69,11 @@ int64_t resident_blocks(const void* kfn, int block);
 // the sweep counter sig[16]. No cache maintenance here: the halo stream's counter-wait kernel ends
 // with the dispatch packet's release, which writes back every XCD's L2 before the exchange reads the
 // face. (A per-block agent-scope release - an L2 writeback, and with acq_rel an L2 invalidate, by
-// each of the 235 blocks - slowed the whole sweep by ~25 %.) The next sweep's launch follows this
-// one on its stream, so no block of it can arrive before the re-arm.
+// each of the 235 blocks - slowed the whole sweep by ~25 %.) The upper boundary launch and the
+// interior sweep count on separate counter blocks (Solver::Slab::sig), and each launch follows the
+// previous one on its stream, so no block of a launch arrives before the re-arm of the last one
+// that used its counters. (A monotonic count compared modulo `tiles` would need no re-arm, but
+// its 64-bit division around this out-of-line call makes the sweep spill.)
 __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles, bool leader) {
   wait_vm0();
   lds_barrier();
