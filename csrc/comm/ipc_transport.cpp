@@ -166,9 +166,7 @@ class IpcTransport final : public Transport {
     dev_ok_ = true;
     // the hi-side pull runs on a second stream, concurrently with the lo-side pull on the halo
     // stream: two neighbours are two different xGMI links (or two blits on one device)
-    int lo = 0, hi = 0;
-    HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, hi));
+    HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, halo_stream_priority(true)));
     HIPC(hipEventCreateWithFlags(&ev_fork_, sync_event_flags()));
     HIPC(hipEventCreateWithFlags(&ev_join_, sync_event_flags()));
     // every face has the same size (halo planes of one field layout)

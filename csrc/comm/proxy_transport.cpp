@@ -75,9 +75,7 @@ class ProxyTransport final : public Transport {
       HIPC(hipMalloc(&mbox_, 4 * face_));
       HIPC(hipMemset(mbox_, 0, 4 * face_));
     }
-    int lo = 0, hi = 0;
-    HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, hi));
+    HIPC(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, halo_stream_priority(true)));
     HIPC(hipEventCreateWithFlags(&ev_fork_, sync_event_flags()));
     HIPC(hipEventCreateWithFlags(&ev_join_, sync_event_flags()));
     HIPC(hipDeviceSynchronize());

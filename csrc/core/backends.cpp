@@ -75,12 +75,10 @@ class HipBackend final : public Backend {
   }
   void* create_stream(int priority) override {
     activate();
-    int lo = 0, hi = 0;
-    HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
     hipStream_t s;
     // the halo stream gets the highest priority so boundary planes and the RCCL kernels are
     // scheduled ahead of the interior sweep and the exchange starts as early as possible.
-    HIPC(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority > 0 ? hi : lo));
+    HIPC(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, halo_stream_priority(priority > 0)));
     return s;
   }
   void destroy_stream(void* s) override {
@@ -201,6 +199,16 @@ void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode)
   if (mode < 0) mode = face_copy_mode();
   HIPC(hipMemcpyAsync(dst, src, n, mode == 1 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice,
                       (hipStream_t)stream));
+}
+
+// HIP priority of the engine's streams: the halo stream (and the transports' second pull stream)
+// high, the compute stream normal. MDFX_HALO_PRIORITY=0 gives the halo streams normal priority too.
+int halo_stream_priority(bool halo) {
+  int lo = 0, hi = 0;
+  HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  const char* v = std::getenv("MDFX_HALO_PRIORITY");
+  const bool high = halo && !(v && std::strcmp(v, "0") == 0);
+  return high ? hi : lo;
 }
 
 // Flags of the engine's stream-ordering events (boundary -> exchange, interior -> next boundary,
