@@ -3,7 +3,7 @@
 // One process per GPU (torchrun / mpirun; the 128-byte ncclUniqueId is distributed by the
 // caller: torch.distributed in Python, a TCP rendezvous in the C++ CLI), or one process driving
 // several GPUs (every local rank's comm initialised inside one ncclGroup). Each step the sends
-// and receives of all local slabs go into ONE ncclGroupStart/End on each slab's high-priority
+// and receives of all local slabs go into ONE ncclGroupStart/End on each slab's
 // halo stream, so the exchange is ordered after the boundary kernel and before the next step's
 // boundary kernel by stream order alone, while the interior sweep runs on the compute stream.
 // Slab neighbours are single peers: each face rides one xGMI link (≈153 GB/s); a 1024^2 fp32 face

@@ -76,8 +76,7 @@ class HipBackend final : public Backend {
   void* create_stream(int priority) override {
     activate();
     hipStream_t s;
-    // the halo stream gets the highest priority so boundary planes and the RCCL kernels are
-    // scheduled ahead of the interior sweep and the exchange starts as early as possible.
+    // (halo_stream_priority: normal unless MDFX_HALO_PRIORITY=1)
     HIPC(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, halo_stream_priority(priority > 0)));
     return s;
   }
@@ -201,13 +200,19 @@ void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode)
                       (hipStream_t)stream));
 }
 
-// HIP priority of the engine's streams: the halo stream (and the transports' second pull stream)
-// high, the compute stream normal. MDFX_HALO_PRIORITY=0 gives the halo streams normal priority too.
+// HIP priority of the engine's streams: normal for all of them by default; MDFX_HALO_PRIORITY=1
+// gives the halo stream (and the transports' second pull stream) high priority, the round-3/4
+// default. High priority measured no faster (rank proxy N = 8: 1967 / 1954 vs 1953 / 1977 GCells/s
+// per GPU, N = 4 2066 / 2085 vs 2121 / 2065; two processes sharing the GPU over ipc 2226 / 2200 vs
+// 2244 / 2281, profiles/r04_session_t/), and with 8 processes on one GPU (more user queues than
+// the hardware maps at once) the high-priority queues of the spinning counter waits starved a
+// normal-priority compute queue whose sweep they were waiting for: scripts/ipc_churn.py hung on
+// its 5th-11th engine in 3 of 3 runs, and ran 16 engines clean at normal priority.
 int halo_stream_priority(bool halo) {
   int lo = 0, hi = 0;
   HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
   const char* v = std::getenv("MDFX_HALO_PRIORITY");
-  const bool high = halo && !(v && std::strcmp(v, "0") == 0);
+  const bool high = halo && v && std::strcmp(v, "1") == 0;
   return high ? hi : lo;
 }
 

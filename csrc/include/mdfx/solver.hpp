@@ -5,7 +5,7 @@
 // serialised everything with cudaDeviceSynchronize (MDF_kernel.cu:175), raced the two streams on
 // d_new_univ (D6) and d_univ (D7), and never swapped buffers (D1). Here, per step and per slab:
 //
-//   halo stream (high priority):  wait(interior t-1) -> boundary planes (cur -> nxt)
+//   halo stream:  wait(interior t-1) -> boundary planes (cur -> nxt)
 //                                 -> record(bnd) -> exchange faces of nxt (RCCL / loopback)
 //   compute stream:               wait(boundary t-1) -> interior planes (cur -> nxt)
 //                                 -> record(int)
