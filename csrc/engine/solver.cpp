@@ -1,5 +1,6 @@
 // mdfx engine implementation (see solver.hpp for the schedule).
 #include "mdfx/solver.hpp"
+#include "mdfx/sweep_plan.hpp"
 
 #include <dirent.h>
 #include <hip/hip_runtime_api.h>
@@ -618,99 +619,34 @@ int Solver::max_depth() const {
   return 1;
 }
 
-// Sweep plan of a stretch of `len` steps (the steps up to the next residual evaluation, or to the
-// end of the run): max_depth() sweeps and a tail of at most 2 max_depth() - 1 steps, the tail cut
-// so that the summed sweep cost (hip_sweep_cost: time per sweep of each fused depth, in single-step
-// sweeps) is least; ties keep the deepest sweeps first. The max_depth() sweeps run first (replayed
-// in pairs from the prepared graphs), the tail's sweeps deepest first, and the residual is
-// evaluated by the stretch's last sweep. Measured: 2048^3 fp64 with a residual every 10 steps at
-// depth 3, 3 + 3 + 3 + 1 754.0 vs an even 3 + 3 + 2 + 2 731.9 GCells/s (the single-step sweep runs
-// near the copy roof, the fp64 two-step kernel does not; profiles/r04_session_n/), which the
-// cost table reproduces; at depth 4 it picks 4 + 3 + 3 over 4 + 4 + 2.
+// Sweep plan of a stretch of `len` steps (plan_next_sweep, csrc/engine/sweep_plan.cpp): max_depth()
+// sweeps and a tail of at most 2 max_depth() - 1 steps, the tail cut so that the summed sweep cost
+// (hip_sweep_cost: time per sweep of each fused depth, in single-step sweeps) is least. Measured:
+// 2048^3 fp64 with a residual every 10 steps at depth 3, 3 + 3 + 3 + 1 754.0 vs an even
+// 3 + 3 + 2 + 2 731.9 GCells/s (the single-step sweep runs near the copy roof, the fp64 two-step
+// kernel does not; profiles/r04_session_n/), which the cost table reproduces; at depth 4 it picks
+// 4 + 3 + 3 over 4 + 4 + 2 (937.6 GCells/s, profiles/r04_session_u/).
 double Solver::sweep_cost(int k) const {
   if (k <= 1) return 1.0;
   return slabs_[0].be->kind() == DeviceKind::HIP ? hip_sweep_cost(spec_, global_.nx, k) : 1.0 + 0.05 * (k - 1);
 }
 
-// The cheapest cut of a tail of r < 2T steps into supported depths: best[l][d] is the least cost of
-// l steps in sweeps of at most d steps (ties take the deeper sweep); *first gets the plan's deepest
-// sweep, which runs first.
-double Solver::tail_plan(int r, int T, int* first) const {
-  double best[33][17];
-  bool use[33][17];
-  for (int l = 0; l <= r; ++l)
-    for (int d = 1; d <= T; ++d) {
-      use[l][d] = false;
-      if (l == 0) {
-        best[l][d] = 0.0;
-        continue;
-      }
-      if (d == 1) {
-        best[l][d] = best[l - 1][1] + sweep_cost(1);
-        use[l][d] = true;
-        continue;
-      }
-      best[l][d] = best[l][d - 1];
-      if (depth_ok_[d] && l >= d) {
-        const double c = sweep_cost(d) + best[l - d][d];
-        if (c <= best[l][d] + 1e-9) {
-          best[l][d] = c;
-          use[l][d] = true;
-        }
-      }
-    }
-  if (first) {
-    int d = T;
-    while (d > 1 && !use[r][d]) --d;
-    *first = r > 0 ? d : 1;
+SweepCosts Solver::sweep_costs() const {
+  SweepCosts c;
+  c.T = max_depth();
+  for (int k = 1; k <= 16; ++k) {
+    c.cost[k] = sweep_cost(k);
+    c.ok[k] = depth_ok_[k];
   }
-  return best[r][T];
+  return c;
 }
 
 int Solver::plan_sweep(int64_t len, bool res_end, int64_t* graphable) const {
-  *graphable = 0;
-  const int T = max_depth();
-  if (T <= 1 || len <= 1) {  // single steps: all but the residual step replay in pairs
-    *graphable = len - (res_end ? 1 : 0);
-    return 1;
-  }
-  // candidate tails: len mod T and one more sweep's worth; the rest runs at depth T
-  const int64_t m = len % T;
-  int64_t best_r = -1;
-  double best_c = 0.0;
-  for (int64_t r : {m, m + T}) {
-    if (r > len || r >= 2 * T) continue;
-    const double c = (double)((len - r) / T) * sweep_cost(T) + tail_plan((int)r, T, nullptr);
-    if (best_r < 0 || c < best_c - 1e-9) {
-      best_r = r;
-      best_c = c;
-    }
-  }
-  const int64_t full = (len - best_r) / T;  // depth-T sweeps ahead of the tail
-  if (full > 0) {
-    // back-to-back depth-T sweeps before the residual sweep (the last one when the tail is empty)
-    *graphable = full - ((res_end && best_r == 0) ? 1 : 0);
-    return T;
-  }
-  int first = 1;
-  tail_plan((int)best_r, T, &first);
-  return first;
+  return plan_next_sweep(sweep_costs(), len, res_end, graphable);
 }
 
 std::vector<std::pair<int, bool>> Solver::sweep_plan(int64_t steps) const {
-  // run()'s loop without the work (a replayed pair covers two sweeps of the same plan)
-  std::vector<std::pair<int, bool>> out;
-  int64_t done = 0, at = stats_.steps;
-  while (done < steps) {
-    int64_t to_res = steps - done + 1;
-    if (opt_.residual_every > 0) to_res = ((at / opt_.residual_every) + 1) * opt_.residual_every - at;
-    int64_t graphable = 0;
-    const int k = plan_sweep(std::min(steps - done, to_res), to_res <= steps - done, &graphable);
-    out.emplace_back(k, to_res == k);
-    done += k;
-    at += k;
-  }
-  return out;
+  return plan_sweeps(sweep_costs(), steps, stats_.steps, opt_.residual_every);
 }
 
 void Solver::run(int64_t steps) {

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "mdfx/runtime.hpp"
+#include "mdfx/sweep_plan.hpp"
 
 namespace mdfx {
 
@@ -155,8 +156,8 @@ class Solver {
   // depth of the next sweep of a `len`-step stretch (ending at a residual step if res_end), and in
   // *graphable how many sweeps of that depth follow back to back without a residual
   int plan_sweep(int64_t len, bool res_end, int64_t* graphable) const;
-  double sweep_cost(int k) const;                     // relative time of a k-step sweep
-  double tail_plan(int r, int T, int* first) const;   // cheapest cut of r < 2T steps
+  double sweep_cost(int k) const;  // relative time of a k-step sweep
+  SweepCosts sweep_costs() const;  // the plan's inputs: max_depth(), sweep_cost(k), depth_ok_
   void capture_graph(int parity, int k);
   void destroy_graph();
 

@@ -12,6 +12,7 @@
 
 #include "mdfx/devsync.hpp"
 #include "mdfx/solver.hpp"
+#include "mdfx/sweep_plan.hpp"
 
 namespace py = pybind11;
 using namespace mdfx;
@@ -360,6 +361,19 @@ PYBIND11_MODULE(_mdfx, m) {
     StencilSpec s = make_spec(kind, dtype, -1, 0, 0, 0, 0, ref_precision);
     return hip_fused_depth(s, nx);
   }, py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ref_precision") = false);
+  m.def("plan_sweeps", [](int64_t steps, int64_t start, int64_t residual_every, int temporal,
+                          std::vector<double> cost, std::vector<bool> ok) {
+    SweepCosts c;
+    c.T = temporal;
+    for (size_t k = 0; k < cost.size() && k < 17; ++k) c.cost[k] = cost[k];
+    for (size_t k = 0; k < ok.size() && k < 17; ++k) c.ok[k] = ok[k];
+    c.ok[1] = true;
+    return plan_sweeps(c, steps, start, residual_every);
+  }, py::arg("steps"), py::arg("start"), py::arg("residual_every"), py::arg("temporal"), py::arg("cost"),
+     py::arg("ok"), "the engine's sweep plan for given per-depth costs (cost[k], ok[k] indexed by depth)");
+  m.def("hip_sweep_cost", [](const std::string& kind, const std::string& dtype, int64_t nx, int steps) {
+    return hip_sweep_cost(make_spec(kind, dtype, -1, 0, 0, 0, 0, false), nx, steps);
+  }, py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("steps"));
   m.def("life_compat_init", [](int64_t h, int64_t w, double density, unsigned seed) {
     py::array_t<uint8_t> a({h, w});
     cpu_life_compat_init(a.mutable_data(), h, w, density, seed);

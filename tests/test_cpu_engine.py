@@ -340,6 +340,35 @@ def test_sweep_plan(mdfx):
         assert np.array_equal(got, sim.gather()) and abs(gr - sim.residual) <= 1e-12 * max(1.0, gr)
 
 
+def test_sweep_plan_cost_tables(mdfx):
+    """The planner with the GPU's cost tables (hip_sweep_cost, host-side): on 1024-cell 7-point rows
+    a 10-step residual stretch at depth 4 runs 4 + 3 + 3 (the two-step kernels are the least
+    efficient per step), at depth 3 in fp64 3 + 3 + 3 + 1 (the single step runs near the copy roof;
+    the measured order, profiles/r04_session_n/); other stencils keep the deepest sweeps first; a
+    missing depth (pencils have no two-step kernel) is planned around; the residual sweep is last."""
+    import mpi_cuda_process_amd as m
+
+    n = m.native()
+
+    def plan(steps, every, T, kind="heat7", dtype="f32", nx=1024, start=0, missing=()):
+        cost = [0.0] + [n.hip_sweep_cost(kind, dtype, nx, k) for k in range(1, 17)]
+        ok = [False] + [k not in missing for k in range(1, 17)]
+        return [tuple(x) for x in n.plan_sweeps(steps, start, every, T, cost, ok)]
+
+    F, R = False, True
+    for dt in ("f32", "f64"):
+        assert plan(10, 10, 4, dtype=dt) == [(4, F), (3, F), (3, R)]
+        assert plan(12, 12, 4, dtype=dt) == [(4, F), (4, F), (4, R)]
+        assert plan(20, 0, 4, dtype=dt) == [(4, F)] * 5
+    assert plan(10, 10, 3, dtype="f64") == [(3, F), (3, F), (3, F), (1, R)]
+    assert plan(5, 0, 4, dtype="f64") == [(4, F), (1, F)]
+    assert plan(10, 10, 4, kind="box27", nx=512) == [(4, F), (4, F), (2, R)]    # generic costs
+    assert plan(6, 0, 4, missing=(2,)) == [(3, F), (3, F)]                      # no 2-step kernel
+    assert plan(2, 0, 4, missing=(2, 3)) == [(1, F), (1, F)]
+    assert plan(17, 10, 4, start=5) == [(3, F), (2, R), (4, F), (3, F), (3, R), (2, F)]  # fp32: 3 + 2 < 4 + 1
+    assert plan(7, 0, 1) == [(1, F)] * 7
+
+
 def test_cpu_avx2_and_baseline_builds_bitwise_equal(tmp_path):
     """The CPU stencils exist twice (baseline x86-64 with libm's software fma, and AVX2 + FMA chosen
     at run time); both are exact, so every stencil must agree bit for bit."""
