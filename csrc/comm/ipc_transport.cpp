@@ -355,18 +355,14 @@ class IpcTransport final : public Transport {
     if (!dev_ok_ || !ctr_) return "";
     self_.be->activate();
     uint64_t c[128] = {0};
-    if (hipMemcpy(c, ctr_, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess) {
-      (void)hipGetLastError();
-      return "ipc: counters unreadable";
-    }
+    if (!hip_read_words(c, ctr_, sizeof(c), 2.0)) return "ipc: counters unreadable";
     std::string out = format("ipc rank %d (%s): ready %llu readyZ %llu", self_.rank, direct_ ? "direct" : "mailbox",
                              (unsigned long long)c[kReady], (unsigned long long)c[kReadyZ]);
     for (int side = 0; side < 4; ++side) {
       const Peer& p = peers_[side];
       if (p.rank < 0) continue;
       uint64_t r[128] = {0};
-      const bool ok = p.ctr && hipMemcpy(r, p.ctr, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess;
-      if (!ok) (void)hipGetLastError();
+      const bool ok = p.ctr && hip_read_words(r, p.ctr, sizeof(r), 2.0);
       out += format("; side %d (rank %d): pulled %llu expReady %llu expPulled %llu | its ready %lld readyZ %lld "
                     "pulled[mine] %lld",
                     side, p.rank, (unsigned long long)c[kPulled + side], (unsigned long long)c[kExpReady + side],

@@ -7,9 +7,11 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <dlfcn.h>
+#include <thread>
 
 #include "mdfx/runtime.hpp"
 
@@ -214,6 +216,35 @@ int halo_stream_priority(bool halo) {
   const char* v = std::getenv("MDFX_HALO_PRIORITY");
   const bool high = halo && v && std::strcmp(v, "1") == 0;
   return high ? hi : lo;
+}
+
+// Diagnostic read of device words (watchdog reports): an async copy on a private stream into pinned
+// memory, polled for at most `timeout_s`, so a wedged device cannot turn a report into a hang (on
+// timeout the stream and buffer are left behind on purpose: the process is about to fail anyway).
+bool hip_read_words(void* host, const void* dev, size_t bytes, double timeout_s) {
+  hipStream_t st = nullptr;
+  void* pin = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(&pin, bytes, hipHostMallocDefault) != hipSuccess ||
+      hipMemcpyAsync(pin, dev, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady ||
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+      (void)hipGetLastError();
+      return false;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  std::memcpy(host, pin, bytes);
+  (void)hipHostFree(pin);
+  (void)hipStreamDestroy(st);
+  return true;
 }
 
 // Flags of the engine's stream-ordering events (boundary -> exchange, interior -> next boundary,

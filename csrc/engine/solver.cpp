@@ -232,19 +232,17 @@ void Solver::poison(const std::string& why) {
   poisoned_ = true;
   std::fprintf(stderr, "[mdfx] %s: aborting the transport and releasing device waits\n", why.c_str());
   // what the device waits were waiting for: the fold counters of each slab and the transport's
-  // protocol counters (read with plain copies; the stuck streams are not involved)
+  // protocol counters (bounded copies on private streams; the stuck streams are not involved)
   try {
     for (auto& s : slabs_) {
       if (!s.sig || s.be->kind() != DeviceKind::HIP) continue;
       s.be->activate();
       unsigned long long v[96] = {0};
-      if (hipMemcpy(v, s.sig, sizeof(v), hipMemcpyDeviceToHost) == hipSuccess)
+      if (hip_read_words(v, s.sig, sizeof(v), 2.0))
         std::fprintf(stderr,
                      "[mdfx] rank %d fold counters: upper launch arrivals %llu signals %llu expected %llu; interior "
                      "arrivals %llu signals %llu expected %llu\n",
                      s.rank, v[0], v[16], v[64], v[32], v[48], v[80]);
-      else
-        (void)hipGetLastError();
     }
     const std::string ts = transport_->debug_state();
     if (!ts.empty()) std::fprintf(stderr, "[mdfx] %s\n", ts.c_str());

@@ -90,6 +90,7 @@ void hip_face_copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, s
 void hip_face_copy(void* dst, const HaloSpan& d, const void* src, const HaloSpan& s, void* stream, int mode = -1);
 int face_copy_mode();
 // hipEventCreateWithFlags flags of the engine's and transports' stream-ordering events (MDFX_EVENT_FENCE)
+bool hip_read_words(void* host, const void* dev, size_t bytes, double timeout_s);  // bounded D2H read (diagnostics)
 int halo_stream_priority(bool halo);  // HIP stream priority of a halo (true) or compute stream
 unsigned sync_event_flags();
 
