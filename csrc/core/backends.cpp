@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <dlfcn.h>
+#include <mutex>
 #include <thread>
 
 #include "mdfx/runtime.hpp"
@@ -53,6 +54,8 @@ bool trace_enabled() {
   return on;
 }
 
+void diag_init(int dev);  // (below: the watchdog's report buffers)
+
 class HipBackend final : public Backend {
  public:
   explicit HipBackend(int dev) : dev_(dev) {
@@ -60,6 +63,7 @@ class HipBackend final : public Backend {
     HIPC(hipGetDeviceCount(&n));
     MDFX_CHECK(dev >= 0 && dev < n, format("HIP device %d not present (%d visible)", dev, n));
     HIPC(hipSetDevice(dev_));
+    diag_init(dev_);  // (watchdog report buffers: made now, while the device is healthy)
   }
   DeviceKind kind() const override { return DeviceKind::HIP; }
   int device() const override { return dev_; }
@@ -218,21 +222,42 @@ int halo_stream_priority(bool halo) {
   return high ? hi : lo;
 }
 
-// Diagnostic read of device words (watchdog reports): an async copy on a private stream into pinned
-// memory, polled for at most `timeout_s`, so a wedged device cannot turn a report into a hang (on
-// timeout the stream and buffer are left behind on purpose: the process is about to fail anyway).
-bool hip_read_words(void* host, const void* dev, size_t bytes, double timeout_s) {
+// Diagnostic read of device words (watchdog reports): an async copy on a private stream into a
+// pinned buffer, polled for at most `timeout_s`, so a wedged device cannot turn a report into a
+// hang. The stream and the buffer are made once per device when its backend is created
+// (hipHostMalloc / hipHostFree and stream teardown can wait for the whole device, i.e. for the very
+// kernel that is stuck).
+namespace {
+constexpr size_t kDiagBytes = 4096;
+struct DiagRead {
   hipStream_t st = nullptr;
   void* pin = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc(&pin, bytes, hipHostMallocDefault) != hipSuccess ||
-      hipMemcpyAsync(pin, dev, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) {
+};
+DiagRead g_diag[64];
+std::mutex g_diag_mu;
+void diag_init(int dev) {
+  std::lock_guard<std::mutex> lk(g_diag_mu);
+  if (dev < 0 || dev >= 64 || g_diag[dev].st) return;
+  if (hipStreamCreateWithFlags(&g_diag[dev].st, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(&g_diag[dev].pin, kDiagBytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    g_diag[dev] = DiagRead();
+  }
+}
+}  // namespace
+
+bool hip_read_words(void* host, const void* dev, size_t bytes, double timeout_s) {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64 || bytes > kDiagBytes) return false;
+  std::lock_guard<std::mutex> lk(g_diag_mu);
+  const DiagRead& r = g_diag[d];
+  if (!r.st || hipMemcpyAsync(r.pin, dev, bytes, hipMemcpyDeviceToHost, r.st) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
-    const hipError_t q = hipStreamQuery(st);
+    const hipError_t q = hipStreamQuery(r.st);
     if (q == hipSuccess) break;
     if (q != hipErrorNotReady ||
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
@@ -241,9 +266,7 @@ bool hip_read_words(void* host, const void* dev, size_t bytes, double timeout_s)
     }
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
-  std::memcpy(host, pin, bytes);
-  (void)hipHostFree(pin);
-  (void)hipStreamDestroy(st);
+  std::memcpy(host, r.pin, bytes);
   return true;
 }
 
