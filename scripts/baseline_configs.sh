@@ -4,6 +4,8 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
+# (c5: the warm-up is a whole residual interval, so the timed window starts on a residual
+# boundary; with --warmup 3 the window held a 4 + 4 + 1 and a 3-step stretch, profiles/r04_session_z/)
 run() { local tag=$1; shift; echo "== $tag: $*"; timeout -k 10 600 python bench.py "$@" > gpurun_out/baseline_$tag.json 2> gpurun_out/baseline_$tag.err || { tail -5 gpurun_out/baseline_$tag.err; return 1; }; cat gpurun_out/baseline_$tag.json; }
 run c1_mdf2d_256_f32_cpu --device cpu --stencil jacobi5 --nx 256 --nz 256 --steps 200 --warmup 10 || exit 1
 run c2_heat7_512_f32 --n 512 --steps 100 --warmup 10 || exit 1
@@ -14,9 +16,9 @@ for n in 2 4 8; do run c3_proxy$n --rank-proxy $n --steps 48 --warmup 12 || exit
 run c3_proxy8_pencil --rank-proxy 8 --py 2 --steps 48 --warmup 12 || exit 1
 run c4_box27_512_f32 --stencil box27 --n 512 --steps 100 --warmup 10 || exit 1
 run c4_box27_512_f64 --stencil box27 --n 512 --dtype f64 --steps 50 --warmup 5 || exit 1
-run c5_heat7_2048_f64_resid --n 2048 --dtype f64 --steps 24 --warmup 3 --residual-every 12 || exit 1
-run c5_heat7_2048_f64_resid10 --n 2048 --dtype f64 --steps 20 --warmup 2 --residual-every 10 || exit 1
-run c5_proxy8_2048_f64_resid --rank-proxy 8 --n 2048 --dtype f64 --steps 24 --warmup 3 --residual-every 12 || exit 1
+run c5_heat7_2048_f64_resid --n 2048 --dtype f64 --steps 24 --warmup 12 --residual-every 12 || exit 1
+run c5_heat7_2048_f64_resid10 --n 2048 --dtype f64 --steps 20 --warmup 10 --residual-every 10 || exit 1
+run c5_proxy8_2048_f64_resid --rank-proxy 8 --n 2048 --dtype f64 --steps 24 --warmup 12 --residual-every 12 || exit 1
 run x_heat7_1024_f64 --n 1024 --dtype f64 --steps 30 --warmup 5 || exit 1
 run x_mdf2d_16k_f32 --stencil jacobi5 --nx 16384 --nz 16384 --steps 96 --warmup 16 || exit 1
 run x_mdf2d_16k_f32_ref --stencil jacobi5 --nx 16384 --nz 16384 --steps 96 --warmup 16 --ref-precision || exit 1
