@@ -84,8 +84,8 @@ def parse(argv=None):
                         "overlap (auto); every candidate is timed twice, interleaved, and its faster run counts")
     p.add_argument("--temporal", type=int, default=0,
                    help="time steps fused per memory sweep (temporal blocking); 0 = auto (native "
-                        "hip_fused_depth): 4 for the 3D 7-point fp32 where heat7_wxk's x segments cover the "
-                        "row (3 in fp64), 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 (2D "
+                        "hip_fused_depth): 4 for the 3D 7-point (fp32 and fp64) where heat7_wxk's x segments "
+                        "cover the row, 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 (2D "
                         "MDF) / 12 (Life)")
     p.add_argument("--ref-precision", action="store_true",
                    help="jacobi5: the reference program's mixed fp32/fp64 update (MDF_kernel.cu:20)")
