@@ -29,8 +29,18 @@ blocking, --temporal 4 through heat7_wxk at 1024-cell rows; bitwise identical to
 steps, tests/test_gpu_temporal.py): every step is still computed in full, the fused kernel keeps
 u^{t+1}..u^{t+3} on chip. A step count that is not a multiple of 4 ends with a shorter fused sweep.
 --temporal 1 measures one sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
-torch.cuda.synchronize() on both sides; the slowest rank's time is reported. GCells/s =
-nx*ny*nz*K / t / 1e9 for the whole job. Rank 0 prints one JSON line. The DRAM fields report the
+torch.cuda.synchronize() on both sides; the slowest rank's time is reported (N > 1: three such
+repetitions by default, the median reported and all three listed). GCells/s = nx*ny*nz*K / t / 1e9
+for the whole job.
+
+Verification of the timed run itself. After timing, every rank re-runs the exact step sequence of
+the timed engine (init, warm-up, every timed repetition) on the FULL grid as one slab on its own
+device with the naive single-step kernels, and compares its owned cells bitwise; the verdict is
+all-reduced into the JSON ("verified"), and any difference exits non-zero without a number. So the
+reported run, not only the small gate, is checked against an independent computation (N = 1
+included: the fused heat7_wxk sweeps against naive single steps on the whole 1024^3 grid).
+
+Rank 0 prints one JSON line. The DRAM fields report the
 traffic actually required per time step (one read + one write of every cell per fused sweep, i.e.
 divided by the temporal depth) against the measured 6.29 TB/s copy roof.
 """
@@ -98,7 +108,11 @@ def parse(argv=None):
                         "3D 7-point tries slabs and 2-along-y pencils on the ipc transports and times the faster)")
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
     p.add_argument("--device", default="auto", choices=["auto", "hip", "cpu"])
-    p.add_argument("--repeats", type=int, default=1, help="timed repetitions; the best is reported")
+    p.add_argument("--repeats", type=int, default=0,
+                   help="timed repetitions of --steps steps each; the median is reported and every one is "
+                        "listed (0 = auto: 3 with several ranks, 1 on one GPU)")
+    p.add_argument("--no-verify", action="store_true",
+                   help="skip the check of the timed run against a full-grid naive run on each rank's device")
     p.add_argument("--timeout", type=float, default=120.0,
                    help="watchdog (s): a rank whose streams make no progress for this long aborts the "
                         "transport and exits non-zero")
@@ -112,7 +126,9 @@ def parse(argv=None):
     p.add_argument("--proxy-rank", type=int, default=-1,
                    help="which slab the proxy runs (default: a middle rank, two neighbours)")
     p.add_argument("--share-gpu", action="store_true",
-                   help="allow more ranks than GPUs (processes share devices; tests of the ipc/staged paths)")
+                   help="allow more ranks than GPUs (processes share devices; tests of the ipc/staged paths "
+                        "only: the ipc exchange's device spin waits assume one engine process per GPU and the "
+                        "transport refuses shared GPUs without this)")
     return p.parse_args(argv)
 
 
@@ -238,7 +254,8 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False, py=1):
         if fault.startswith("gate:") and transport in fault[5:].split(","):
             # fault injection for the fallback test: this transport's gate fails on every rank
             raise RuntimeError("injected gate failure (MDFX_FAULT=%s)" % fault)
-        with Simulation(prob, distributed=True, transport=transport, graph=graph, py=py, **kw) as sim:
+        with Simulation(prob, distributed=True, transport=transport, graph=graph, py=py, share_gpu=a.share_gpu,
+                        **kw) as sim:
             trace("gate: engine up")
             sim.init()
             sim.prepare_graphs()  # the timed run's path: cycles captured before any step
@@ -270,6 +287,82 @@ def run_gate(a, hip, transport, temporal, world, rank, graph=False, py=1):
     rec = {"grid": [prob.nx, prob.ny, prob.nz], "steps": steps, "transport": transport, "graph": graph, "py": py,
            "ranks_failed": bad, "passed": bad == 0}
     return bad == 0, rec
+
+
+def _owned(sim, i, nx):
+    """Owned cells of local part i as a zero-copy (nzl, nyl, nx) view of the current buffer."""
+    lay = sim.layout(i)
+    h, hy = lay["halo"], lay["hy"]
+    return sim.view(i)[h:h + lay["nzl"], hy:hy + lay["nyl"], :nx]
+
+
+def inject_timed_fault(sim, rank, world):
+    """MDFX_FAULT=ghost@<r>:timed (tests): once the timed run's warm-up is done, rank r adds 1 to one
+    cell of its lower ghost plane, as a broken or racy exchange would leave it. The gate and the
+    trials ran clean before, so only the verification of the timed run can catch it."""
+    f = os.environ.get("MDFX_FAULT", "")
+    if not (f.startswith("ghost@") and f.endswith(":timed")):
+        return False
+    if int(f[6:-6]) != rank or rank == 0 or world < 2:
+        return False
+    sim.synchronize()
+    lay = sim.layout(0)
+    v = sim.view(0)
+    v[lay["halo"] - 1, lay["hy"] + lay["nyl"] // 2, sim.problem.nx // 2] += 1
+    if v.is_cuda:
+        torch.cuda.synchronize()
+    print("[bench rank %d] injected a ghost-plane fault into the timed run (MDFX_FAULT=%s)" % (rank, f),
+          file=sys.stderr, flush=True)
+    return True
+
+
+def verify_timed(a, sim, prob, hip, env, rank, world, seq):
+    """Check the timed run itself, not only the gate: rank r re-runs the exact step sequence of the
+    timed engine (init, then run(n) for every n in `seq`) on the FULL grid as one slab on its own
+    device with the naive single-step kernels (HIP) or the CPU oracle, and compares its owned cells
+    bitwise (and the last residual, when one was evaluated). The verdict is all-reduced; returns the
+    JSON record. The reference program never read its result back (MDF_kernel.cu:164,177)."""
+    import torch.distributed as dist
+
+    from mpi_cuda_process_amd import Simulation, native
+
+    parts = [(sim.layout(i), _owned(sim, i, prob.nx)) for i in range(sim.num_local)]
+    res_mine = sim.residual
+    diff, err = float("inf"), ""
+    if hip:
+        native().set_kernel_variant("naive")
+    try:
+        kw = dict(device="hip" if hip else "cpu", temporal=1, residual_every=a.residual_every,
+                  timeout_s=a.timeout if hip else 0.0)
+        with Simulation(prob, ranks=1, distributed=False, **kw) as ref:
+            ref.init()
+            for n in seq:
+                ref.run(n)
+            ref.synchronize()
+            rl = ref.layout(0)
+            diff = 0.0
+            for lay, mine in parts:
+                full = ref.view(0)[rl["halo"] + lay["z0"]:rl["halo"] + lay["z1"], lay["y0"]:lay["y1"], :prob.nx]
+                if not torch.equal(mine, full):
+                    d = (mine.double() - full.double()).abs()
+                    diff = max(diff, float(d.nan_to_num(nan=float("inf")).max()))
+            if res_mine >= 0 and abs(res_mine - ref.residual) > 1e-9 * max(1.0, abs(ref.residual)):
+                err = "residual %r vs %r" % (res_mine, ref.residual)
+    except Exception as e:  # noqa: BLE001 - reported and agreed on below
+        err = "%s: %s" % (type(e).__name__, e)
+    finally:
+        if hip:
+            native().set_kernel_variant(a.variant)
+    if err or diff != 0.0:
+        print("bench verify: rank %d: owned cells differ from the full-grid run by up to %g %s" % (rank, diff, err),
+              file=sys.stderr, flush=True)
+    t = torch.tensor([diff if not err else float("inf"), 1.0 if (err or diff != 0.0) else 0.0], dtype=torch.float64)
+    if env:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"ranks": world, "max_abs_diff": float(t[0].item()), "passed": t[1].item() == 0.0,
+            "steps": [int(n) for n in seq],
+            "reference": "full grid, one slab on each rank's own device, %s" % (
+                "naive single-step HIP kernels" if hip else "CPU oracle")}
 
 
 def run_proxy(a):
@@ -493,7 +586,8 @@ def main(argv=None):
 
     def make_sim(transport, graph, rounds=0, overlap=True, py=1):
         if env:
-            sim = Simulation(prob, distributed=True, transport=transport, graph=graph, py=py, **kw)
+            sim = Simulation(prob, distributed=True, transport=transport, graph=graph, py=py, share_gpu=a.share_gpu,
+                             **kw)
         else:
             sim = Simulation(prob, ranks=a.virtual_ranks or 1, distributed=False, transport=transport, graph=graph,
                              py=py, **kw)
@@ -569,12 +663,30 @@ def main(argv=None):
     trace("warmup enqueued")
     timed(sim, 0)
     trace("warmup done")
+    inject_timed_fault(sim, rank, world)
     replays0, captures0 = sim.graph_replays, sim.graph_captures
-    best = None
-    for _ in range(max(1, a.repeats)):
-        dt = timed(sim, a.steps)
-        best = dt if best is None else min(best, dt)
-        trace("timed %.4f s" % dt)
+    repeats = a.repeats if a.repeats > 0 else (3 if (env and world > 1) else 1)
+    dts = []
+    for _ in range(repeats):
+        dts.append(timed(sim, a.steps))
+        trace("timed %.4f s" % dts[-1])
+    best = sorted(dts)[len(dts) // 2]  # the median repetition (the only one at N = 1)
+    verified = None
+    if not a.no_verify:
+        trace("verifying the timed run")
+        verified = verify_timed(a, sim, prob, hip, env, rank, world, [a.warmup] + [a.steps] * repeats)
+        trace("verified: %s" % verified)
+        if not verified["passed"]:
+            if rank == 0:
+                print("bench: timed-run verification FAILED (max |diff| %g over %d ranks; the gate %s): not "
+                      "reporting a number" % (verified["max_abs_diff"], world,
+                                              "passed" if gate and gate["passed"] else "was not run"),
+                      file=sys.stderr, flush=True)
+            sim.close()
+            if env:
+                dist.barrier()
+                dist.destroy_process_group()
+            return 4
 
     devices = [device_id]
     if env:
@@ -600,8 +712,7 @@ def main(argv=None):
     if rank == 0:
         sim_transport = sim.transport
         decomp = "slab-z%d" % world if chosen[4] == 1 else "pencil-z%dy%d" % (world // chosen[4], chosen[4])
-        par = ("%s (1 process/GPU, %s halo, %s)" % (
-            decomp, sim_transport, "interior||boundary streams" if chosen[3] else "exchange then one sweep")
+        par = ("%s (1 process/GPU, %s halo, %s schedule)" % (decomp, sim_transport, sim.schedule)
                if env else ("slab-z%d virtual in 1 process (%s)" % (a.virtual_ranks, sim_transport)
                             if a.virtual_ranks > 1 else "single GPU" if hip else "cpu"))
         model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF",
@@ -641,6 +752,9 @@ def main(argv=None):
                 "trials": trials,
                 "overlap": chosen[3],
                 "timed_vs_trial": timed_vs_trial,
+                "schedule": sim.schedule,
+                "repeats_ms_per_step": [round(d / a.steps * 1e3, 4) for d in dts],
+                "verified": verified,
                 "face_copy": ("sdma" if sim_transport == "ipc_sdma" else native().face_copy_mode())
                 if sim_transport in ("ipc", "ipc_sdma") else None,
                 "ipc_protocol": (("direct" if native().ipc_direct_ok(sim.layout(0)["bytes"]) else "mailbox")

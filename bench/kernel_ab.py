@@ -2,12 +2,12 @@
 """A/B harness for the stencil kernels on one MI355X (cdna_hip_programming.md §5.4 rule 24:
 variants interleaved in ONE process, several rounds, best and median reported).
 
-Variants are the native dispatcher's tuning knobs (MDFX_RY, MDFX_ZC, MDFX_BLOCKS, MDFX_TB_RY,
-MDFX_TBK_RY, MDFX_J5_TBK, MDFX_LIFE_TBK, MDFX_B27_TBK; cached by the native layer and re-read per
-variant) plus the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
+Variants are the native dispatcher's kernel-family selectors (MDFX_TB_RY, MDFX_WTK_WB, MDFX_H7_WXK,
+MDFX_B27_WXK, MDFX_B27_TBK, and MDFX_WXK_EXP for experimental heat7_wxk copies; cached by the native
+layer and re-read per variant) plus the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
 bitwise against the naive kernel.
 
-    python bench/kernel_ab.py --kind heat7 --n 1024 --variants "RY=4;RY=2;STEPS=2;STEPS=2,TBKRY=2"
+    python bench/kernel_ab.py --kind heat7 --n 1024 --variants "STEPS=4;STEPS=3;STEPS=3,WXK=0;STEPS=2"
 """
 
 import argparse
@@ -24,9 +24,8 @@ import mpi_cuda_process_amd as m  # noqa: E402
 from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, init_field,  # noqa: E402
                                       set_kernel_variant)
 
-KEYS = {"RY": "MDFX_RY", "ZC": "MDFX_ZC", "BLOCKS": "MDFX_BLOCKS", "TBRY": "MDFX_TB_RY",
-        "J5TBK": "MDFX_J5_TBK", "LTBK": "MDFX_LIFE_TBK", "TBKRY": "MDFX_TBK_RY", "B27TBK": "MDFX_B27_TBK", "WB": "MDFX_WTK_WB", "WXK": "MDFX_H7_WXK", "B27WXK": "MDFX_B27_WXK",
-        "DIAG": "MDFX_WXK_DIAG", "STRIP": "MDFX_WXK_STRIP", "DBGZC": "MDFX_DEBUG_ZC"}
+KEYS = {"TBRY": "MDFX_TB_RY", "B27TBK": "MDFX_B27_TBK", "WB": "MDFX_WTK_WB", "WXK": "MDFX_H7_WXK",
+        "B27WXK": "MDFX_B27_WXK", "EXP": "MDFX_WXK_EXP"}
 
 
 def parse_variant(s):

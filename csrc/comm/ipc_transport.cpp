@@ -1,13 +1,15 @@
 // HIP-IPC halo transport: one process per slab; the neighbours pull each other's boundary faces
-// straight into their ghost planes with the SDMA copy engines (hipMemcpyDeviceToDeviceNoCU, over
-// xGMI between GPUs), ordered by device-side counters instead of host synchronisation.
+// straight into their ghost planes (over xGMI between GPUs), ordered by device-side counters instead
+// of host synchronisation. Two copy engines: "ipc" (the default) pulls with the runtime's blit
+// kernels (hipMemcpyDeviceToDevice: __amd_rocclr_copyBuffer on the CUs), "ipc_sdma" with the SDMA
+// copy engines (hipMemcpyDeviceToDeviceNoCU: no CUs beyond one-wave counter kernels, but slower
+// than a blit between buffers of one device); bench.py times both (hip_face_copy, backends.cpp).
 //
 // Why a second device-resident transport next to RCCL: RCCL's p2p send/recv runs as kernels that
-// occupy CUs the interior sweep wants, and RCCL refuses two ranks on one GPU. An SDMA pull takes no
-// CUs beyond one-wave counter kernels, and works for any number of processes sharing a device —
-// which is how the device-resident multi-process path is tested on a one-GPU box
-// (tests/test_gpu_ipc.py). (A plain hipMemcpyDeviceToDevice between buffers of one device runs as
-// __amd_rocclr_copyBuffer blit kernels on the CUs: MDFX_XCOPY=blit, the round-3 behaviour.)
+// occupy CUs the interior sweep wants, and RCCL refuses two ranks on one GPU. The ipc transport
+// also runs with several processes on one device, which is how the device-resident multi-process
+// path is tested on a one-GPU box (tests/test_gpu_ipc.py; share_gpu: a test-only opt-in, see
+// ipc_shared_gpu_problem).
 //
 // Two protocols, by field-buffer size:
 //   direct  (buffers below ~1.9 GiB, e.g. 1024^3 fp32 at N >= 4): each process exports its two
@@ -115,7 +117,7 @@ int local_device_of(const char* pci) {
 
 class IpcTransport final : public Transport {
  public:
-  IpcTransport(CallbackFns f, int copy_mode) : f_(std::move(f)), copy_(copy_mode) {
+  IpcTransport(CallbackFns f, int copy_mode, bool share_gpu) : f_(std::move(f)), copy_(copy_mode), share_gpu_(share_gpu) {
     MDFX_CHECK((bool)f_.allgather, "ipc transport needs an allgather control plane");
   }
   ~IpcTransport() override {
@@ -137,9 +139,8 @@ class IpcTransport final : public Transport {
     // re-allocate memory a neighbour still had mapped, and the next engine's hipIpcGetMemHandle on
     // the new buffer failed with "invalid argument" (round-4 8-process rehearsal of bench.py's
     // trial loop, which builds and closes engines in turn; scripts/ipc_churn.py). Skipped once the
-    // transport was aborted (a peer may be gone) and with MDFX_IPC_CLOSE_BARRIER=0.
-    const char* cb = std::getenv("MDFX_IPC_CLOSE_BARRIER");
-    if (mapped && setup_done_ && !aborted_ && f_.barrier && !(cb && std::string(cb) == "0")) {
+    // transport was aborted (a peer may be gone).
+    if (mapped && setup_done_ && !aborted_ && f_.barrier) {
       try {
         f_.barrier();
       } catch (...) {
@@ -151,7 +152,7 @@ class IpcTransport final : public Transport {
   }
   const char* name() const override { return copy_ == 1 ? "ipc_sdma" : "ipc"; }
   bool in_process_only() const override { return false; }
-  bool graph_capturable() const override { return true; }
+  bool stream_ordered() const override { return true; }
   void set_timeout(double s) override { timeout_s_ = s > 0 ? s : 300.0; }
 
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
@@ -206,13 +207,18 @@ class IpcTransport final : public Transport {
     MDFX_CHECK((int)all.size() == nranks_, format("ipc allgather returned %zu records for %d ranks", all.size(), nranks_));
     direct_ = true;
     bool any_pencil = false;
+    std::vector<std::pair<int, std::string>> pid_pci;
     for (const std::string& rec : all) {
       MDFX_CHECK(rec.size() == sizeof(IpcRecord), "ipc: malformed handle record");
       IpcRecord r;
       std::memcpy(&r, rec.data(), sizeof(r));
       direct_ = direct_ && r.direct != 0;
       any_pencil = any_pencil || r.pencil != 0;
+      r.pci[sizeof(r.pci) - 1] = 0;
+      pid_pci.emplace_back(r.pid, std::string(r.pci));
     }
+    const std::string shared = ipc_shared_gpu_problem(pid_pci, share_gpu_);
+    MDFX_CHECK(shared.empty(), shared);
     // (every rank reaches the same verdict from the same records: all fail together)
     MDFX_CHECK(direct_ || !any_pencil, "ipc transport: a pencil decomposition needs the direct protocol (field buffers "
                                        "up to 1900 MiB on every rank, or MDFX_IPC_DIRECT=1)");
@@ -272,7 +278,7 @@ class IpcTransport final : public Transport {
     const bool capturing = cap != hipStreamCaptureStatusNone;
     // the two pulls: lo side on the halo stream, hi side on the aux stream (forked after the
     // publish / ready signal, joined back before the exchange ends)
-    const bool both = concurrent_pulls() && peers_[0].rank >= 0 && peers_[1].rank >= 0;
+    const bool both = peers_[0].rank >= 0 && peers_[1].rank >= 0;
     auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
     auto fork = [&]() {
       if (!both) return;
@@ -287,7 +293,7 @@ class IpcTransport final : public Transport {
     if (direct_) {
       // one pair of faces: the lo side's pull on the halo stream, the hi side's on the aux stream
       auto phase = [&](int s0, int ready) {
-        const bool two = concurrent_pulls() && peers_[s0].rank >= 0 && peers_[s0 + 1].rank >= 0;
+        const bool two = peers_[s0].rank >= 0 && peers_[s0 + 1].rank >= 0;
         if (two) {
           HIPC(hipEventRecord(ev_fork_, hs));
           HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
@@ -417,7 +423,7 @@ class IpcTransport final : public Transport {
   bool dev_ok_ = false;
   bool direct_ = false;
   bool pencil_ = false;  // (z, y) pencil: y faces first, then the z faces (which carry the y ghosts)
-  bool setup_done_ = false, aborted_ = false;
+  bool setup_done_ = false, aborted_ = false, share_gpu_ = false;
   Peer peers_[4];
   double timeout_s_ = 300.0;
 };
@@ -457,12 +463,6 @@ void ipc_enable_peer(int mine, int peer, int peer_rank) {
 
 // The direct protocol maps the neighbours' field buffers; torch's HIP 7.0 runtime stalls in
 // hipIpcOpenMemHandle from 2 GiB up, so only buffers of at most 1900 MiB (probed good) go direct.
-// Whether the two pulls of a pair of faces run on two streams (default) or one after the other on
-// the halo stream (MDFX_XPULL=serial; read per call).
-bool concurrent_pulls() {
-  const char* v = std::getenv("MDFX_XPULL");
-  return !(v && std::string(v) == "serial");
-}
 
 bool ipc_direct_ok(size_t field_bytes) {
   const char* v = std::getenv("MDFX_IPC_DIRECT");  // (read per call: tests switch it within a process)
@@ -471,8 +471,25 @@ bool ipc_direct_ok(size_t field_bytes) {
   return field_bytes <= ((size_t)1900 << 20);
 }
 
-std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode) {
-  return std::unique_ptr<Transport>(new IpcTransport(std::move(fns), copy_mode < 0 ? face_copy_mode() : copy_mode));
+std::string ipc_shared_gpu_problem(const std::vector<std::pair<int, std::string>>& pid_pci, bool share_gpu) {
+  if (share_gpu) return "";
+  for (size_t i = 0; i < pid_pci.size(); ++i)
+    for (size_t j = i + 1; j < pid_pci.size(); ++j) {
+      const auto& a = pid_pci[i];
+      const auto& b = pid_pci[j];
+      if (a.second.empty() || a.second != b.second || a.first == b.first) continue;
+      return format("ipc transport: ranks %zu and %zu are two engine processes on one GPU (%s). Their halo "
+                    "exchange waits on device counters that need the hardware scheduler to run every producer "
+                    "queue, which several processes oversubscribing one GPU do not guarantee: run one process "
+                    "per GPU (share_gpu=True / bench.py --share-gpu allow it for tests)",
+                    i, j, a.second.c_str());
+    }
+  return "";
+}
+
+std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode, bool share_gpu) {
+  return std::unique_ptr<Transport>(
+      new IpcTransport(std::move(fns), copy_mode < 0 ? face_copy_mode() : copy_mode, share_gpu));
 }
 
 }  // namespace mdfx

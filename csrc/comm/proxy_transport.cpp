@@ -52,7 +52,7 @@ class ProxyTransport final : public Transport {
     hip_words_free(words_);
   }
   const char* name() const override { return "proxy"; }
-  bool graph_capturable() const override { return true; }
+  bool stream_ordered() const override { return true; }
   void set_timeout(double s) override { timeout_s_ = s > 0 ? s : 300.0; }
 
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
@@ -94,7 +94,7 @@ class ProxyTransport final : public Transport {
     // the ipc transport's stream layout: per pair of faces the hi-side pull on a second stream,
     // concurrent with the lo-side pull on the halo stream
     auto phase = [&](int s0, int ready) {
-      const bool both = concurrent_pulls() && halo_span(self_, b, s0, nranks_).peer >= 0 &&
+      const bool both = halo_span(self_, b, s0, nranks_).peer >= 0 &&
                         halo_span(self_, b, s0 + 1, nranks_).peer >= 0;
       if (both) {
         HIPC(hipEventRecord(ev_fork_, hs));
@@ -113,7 +113,7 @@ class ProxyTransport final : public Transport {
         HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
       }
     };
-    const bool both = concurrent_pulls() && halo_span(self_, b, 0, nranks_).peer >= 0 &&
+    const bool both = halo_span(self_, b, 0, nranks_).peer >= 0 &&
                       halo_span(self_, b, 1, nranks_).peer >= 0;
     auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
     auto fork = [&]() {

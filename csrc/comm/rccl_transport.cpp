@@ -41,6 +41,19 @@ std::string rccl_unique_id() {
   return std::string(id.internal, NCCL_UNIQUE_ID_BYTES);
 }
 
+// The grouped send / recv is pure stream work on the halo stream under every runtime
+bool rccl_stream_ordered() { return true; }
+// ... but RCCL's group joins its own internal streams to the caller's with events, and the HIP 7.0
+// runtime PyTorch bundles segfaults in hipStreamEndCapture on such multi-stream captures
+// (profiles/r02_graph_runtime.txt): RCCL steps are captured only under HIP >= 7.2
+bool rccl_graph_capturable() {
+  static const bool ok = [] {
+    int v = 0;
+    return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
+  }();
+  return ok;
+}
+
 namespace {
 
 class RcclTransport final : public Transport {
@@ -66,17 +79,10 @@ class RcclTransport final : public Transport {
   }
   const char* name() const override { return "rccl"; }
   bool in_process_only() const override { return false; }
-  // RCCL's grouped send/recv joins its own internal streams to the caller's with events; the HIP
-  // 7.0 runtime PyTorch bundles segfaults in hipStreamEndCapture on such multi-stream captures
-  // (profiles/r02_graph_runtime.txt), so RCCL steps are captured only under HIP >= 7.2 and run
-  // eagerly otherwise.
-  bool graph_capturable() const override {
-    static const bool ok = [] {
-      int v = 0;
-      return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
-    }();
-    return ok;
-  }
+  // RCCL gets the engine's folded single-stream boundary schedule under every runtime
+  // (stream_ordered), and graph capture only where the runtime supports it (eager otherwise)
+  bool stream_ordered() const override { return rccl_stream_ordered(); }
+  bool graph_capturable() const override { return rccl_graph_capturable(); }
   void set_timeout(double s) override { timeout_s_ = s; }
   void abort() override {
     if (aborted_) return;

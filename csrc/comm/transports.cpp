@@ -79,7 +79,7 @@ class LoopbackTransport final : public InProcessBase {
     for (size_t i = 0; i < ev_y_.size(); ++i) locals_[i].be->destroy_event(ev_y_[i]);
   }
   const char* name() const override { return "loopback"; }
-  bool graph_capturable() const override { return true; }
+  bool stream_ordered() const override { return true; }
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
     InProcessBase::setup(locals, nranks);
     for (auto& s : locals_) {

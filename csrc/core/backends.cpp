@@ -82,7 +82,7 @@ class HipBackend final : public Backend {
   void* create_stream(int priority) override {
     activate();
     hipStream_t s;
-    // (halo_stream_priority: normal unless MDFX_HALO_PRIORITY=1)
+    // (halo_stream_priority: normal priority for both streams)
     HIPC(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, halo_stream_priority(priority > 0)));
     return s;
   }
@@ -194,11 +194,9 @@ int hip_device_count() {
 // instead. On one device the SDMA copies are the slower choice (N = 8 rank proxy: 1,499 vs 1,923
 // GCells/s per GPU with the mailbox protocol's four 16 MiB copies per sweep, 1,906 vs 1,872 with
 // the direct protocol's two; profiles/r04_session_a/), so blit is the default; between GPUs the
-// bench's trials time both (transport "ipc" vs "ipc_sdma"). MDFX_XCOPY=sdma changes the default.
-int face_copy_mode() {
-  const char* v = std::getenv("MDFX_XCOPY");  // (read per call: tests switch it within a process)
-  return v && std::strcmp(v, "sdma") == 0 ? 1 : 0;
-}
+// bench's trials time both (transport "ipc" vs "ipc_sdma"). (Round 4's environment switch of
+// the default was removed in round 5: the transport name selects the engine.)
+int face_copy_mode() { return 0; }
 
 void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode) {
   if (mode < 0) mode = face_copy_mode();
@@ -206,20 +204,18 @@ void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode)
                       (hipStream_t)stream));
 }
 
-// HIP priority of the engine's streams: normal for all of them by default; MDFX_HALO_PRIORITY=1
-// gives the halo stream (and the transports' second pull stream) high priority, the round-3/4
-// default. High priority measured no faster (rank proxy N = 8: 1967 / 1954 vs 1953 / 1977 GCells/s
+// HIP priority of the engine's streams: normal for all of them. High priority for the halo stream
+// (and the transports' second pull stream), the round-3/4 default (its switch was removed in round
+// 5), measured no faster (rank proxy N = 8: 1967 / 1954 vs 1953 / 1977 GCells/s
 // per GPU, N = 4 2066 / 2085 vs 2121 / 2065; two processes sharing the GPU over ipc 2226 / 2200 vs
 // 2244 / 2281, profiles/r04_session_t/), and with 8 processes on one GPU (more user queues than
 // the hardware maps at once) the high-priority queues of the spinning counter waits starved a
 // normal-priority compute queue whose sweep they were waiting for: scripts/ipc_churn.py hung on
 // its 5th-11th engine in 3 of 3 runs, and ran 16 engines clean at normal priority.
-int halo_stream_priority(bool halo) {
+int halo_stream_priority(bool) {
   int lo = 0, hi = 0;
   HIPC(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  const char* v = std::getenv("MDFX_HALO_PRIORITY");
-  const bool high = halo && v && std::strcmp(v, "1") == 0;
-  return high ? hi : lo;
+  return lo;
 }
 
 // Diagnostic read of device words (watchdog reports): an async copy on a private stream into a
@@ -271,15 +267,10 @@ bool hip_read_words(void* host, const void* dev, size_t bytes, double timeout_s)
 }
 
 // Flags of the engine's stream-ordering events (boundary -> exchange, interior -> next boundary,
-// exchange -> next boundary, the transports' fork / join). MDFX_EVENT_FENCE: "system" (the HIP
-// default: a system-scope release, i.e. an L2 writeback, when the event is recorded) or "device"
-// (hipEventDisableSystemFence: these events only order work on one device; data that another GPU
-// reads is published by the counter signal kernels' own system-scope release).
-unsigned sync_event_flags() {
-  const char* v = std::getenv("MDFX_EVENT_FENCE");
-  const bool device = v && std::string(v) == "device";
-  return hipEventDisableTiming | (device ? hipEventDisableSystemFence : 0u);
-}
+// exchange -> next boundary, the transports' fork / join): the HIP default system-scope release (an
+// L2 writeback when the event is recorded), no timing. (Device-scope events, round 4's
+// switch to them, measured no faster and was removed in round 5.)
+unsigned sync_event_flags() { return hipEventDisableTiming; }
 
 void hip_face_copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height, void* stream,
                      int mode) {

@@ -183,6 +183,9 @@ Solver::~Solver() {
 
 void Solver::set_options(const SolverOptions& o) {
   if (o.graph != opt_.graph || o.overlap != opt_.overlap || o.min_rounds != opt_.min_rounds) destroy_graph();
+  // a different overlap mode switches the schedule (boundary_on_cs), whose steps wait on events the
+  // other schedule never records (ev_x) or stops recording (ev_int): drain the queued steps first
+  if (o.overlap != opt_.overlap) sync_all();
   MDFX_CHECK(o.temporal == opt_.temporal, "the temporal blocking depth is fixed at construction");
   opt_ = o;
   transport_->set_timeout(opt_.timeout_s);
@@ -321,19 +324,27 @@ void Solver::exchange_ghosts() {
 // separate launch over both K-plane boundary regions (each needing 3K planes marched for K outputs,
 // in two rounds of blocks), the interior sweep starts at the lower boundary, signals a device counter
 // once those planes are stored, and the halo stream waits for that counter; only the upper region
-// keeps its launch (one round). MDFX_FOLD=0 turns it off.
+// keeps its launch (one round). (Round 4's switch back to two launches was removed in round 5; the
+// two-launch schedule measured 6-9 % slower at the N = 8 proxy, profiles/r04_session_{i,k}/.)
 bool Solver::fold_ok(const Slab& s, int k) const {
-  static const bool off = [] {
-    const char* v = std::getenv("MDFX_FOLD");
-    return v && std::string(v) == "0";
-  }();
-  return !off && s.sig && s.lo_e > s.lo_b && s.in_e > s.in_b && hip_region_signals(spec_, s.lay, k);
+  return s.sig && s.lo_e > s.lo_b && s.in_e > s.in_b && hip_region_signals(spec_, s.lay, k);
 }
 
 int Solver::min_rounds() const { return opt_.min_rounds > 0 ? opt_.min_rounds : (nranks_ > 1 ? 2 : 1); }
 
+const char* step_schedule(bool overlap, size_t local_slabs, bool stream_ordered, bool fold) {
+  if (!overlap) return "serialised";
+  if (local_slabs != 1 || !stream_ordered) return "two-stream";
+  return fold ? "folded" : "boundary-on-compute";
+}
+
 bool Solver::boundary_on_cs() const {
-  return opt_.overlap && slabs_.size() == 1 && transport_->graph_capturable();
+  return opt_.overlap && slabs_.size() == 1 && transport_->stream_ordered();
+}
+
+std::string Solver::schedule() const {
+  const bool fold = boundary_on_cs() && fold_ok(slabs_[0], max_depth());  // (eager steps; captures never fold)
+  return step_schedule(opt_.overlap, slabs_.size(), transport_->stream_ordered(), fold);
 }
 
 // The boundary regions of a step: the `halo` planes at each z face with a neighbour (all owned
@@ -434,7 +445,10 @@ void Solver::step(bool want_resid, int k) {
     else s.be->wait(s.hs, s.ev_int);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)bs));
     a.resid = want_resid ? s.resid : nullptr;
-    const bool fold = bcs && fold_ok(s, k);
+    // (never inside a capture: the folded exchange is ordered after the interior sweep's stores by a
+    // device spin wait alone, with no graph edge, so a replay that put the wait node on a queue ahead
+    // of the sweep could spin until the watchdog; captured cycles use the boundary launch + event)
+    const bool fold = bcs && !capturing_ && fold_ok(s, k);
     boundary_kernels(s, a, bs, fold);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)bs));
     if (opt_.sync_debug) s.be->sync_device();
@@ -798,8 +812,15 @@ void Solver::capture_graph(int parity, int k) {
   }
   const StepStats saved = stats_;
   GDBG("capture: steps");
-  step(false, k);
-  step(false, k);
+  capturing_ = true;
+  try {
+    step(false, k);
+    step(false, k);
+  } catch (...) {
+    capturing_ = false;
+    throw;
+  }
+  capturing_ = false;
   GDBG("capture: join");
   stats_ = saved;  // replay accounts for them
   ++stats_.graph_captures;

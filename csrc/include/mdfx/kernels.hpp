@@ -47,6 +47,17 @@ struct RegionArgs {
 };
 
 // Whether a slab sweep of `steps` fused steps runs through a kernel that honours RegionArgs::sig.
+//
+// Visibility assumption of the folded boundary (measured, not specified): a signalling block only
+// waits until its stores are acknowledged by its XCD's L2 (vmcnt 0) before counting its arrival; it
+// issues no release, so the face may still sit dirty in up to 8 XCD L2s when the count completes.
+// What makes it visible to the exchange is the halo stream's counter-wait kernel: the exchange is
+// the next operation on that stream, and the runtime ends every kernel dispatch with a system-scope
+// release that writes back each XCD's L2 before a dependent operation (blit kernel, SDMA copy, RCCL
+// kernel, peer read over xGMI) starts. Per-block agent-scope releases instead (an L2 writeback by
+// each of 235 blocks) made the whole sweep ~25 % slower (round 4). The ipc / proxy tests run this
+// bitwise with both readers on one device; a cross-device reader relies on the same end-of-dispatch
+// release.
 bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int steps);
 
 // Whether a fused multi-step sweep is implemented for this stencil / grid on the device.

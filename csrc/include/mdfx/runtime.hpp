@@ -79,7 +79,7 @@ void require_slabs(const std::vector<LocalSlab>& locals, const char* transport);
 // Stream-ordered device-to-device copy of a halo face (same device or a mapped peer): mode 0 the
 // runtime's blit kernels (hipMemcpyDeviceToDevice: copy shaders on the CUs), 1 the SDMA copy
 // engines (hipMemcpyDeviceToDeviceNoCU: no CUs, lower bandwidth on one device), -1 the process
-// default (face_copy_mode(): MDFX_XCOPY=blit / sdma, blit unless set).
+// default (face_copy_mode(): blit).
 void hip_face_copy(void* dst, const void* src, size_t n, void* stream, int mode = -1);
 // The same for a 2-D face (a pencil's y face: `height` pieces of `width` bytes, each side at its own
 // pitch) ...
@@ -89,7 +89,7 @@ void hip_face_copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, s
 // 1-D or 2-D by the spans' geometry.
 void hip_face_copy(void* dst, const HaloSpan& d, const void* src, const HaloSpan& s, void* stream, int mode = -1);
 int face_copy_mode();
-// hipEventCreateWithFlags flags of the engine's and transports' stream-ordering events (MDFX_EVENT_FENCE)
+// hipEventCreateWithFlags flags of the engine's and transports' stream-ordering events
 bool hip_read_words(void* host, const void* dev, size_t bytes, double timeout_s);  // bounded D2H read (diagnostics)
 int halo_stream_priority(bool halo);  // HIP stream priority of a halo (true) or compute stream
 unsigned sync_event_flags();
@@ -110,9 +110,13 @@ class Transport {
   virtual bool in_process_only() const { return true; }  // every rank lives in this process
   // Optional async-error poll (RCCL, IPC counters); throws if a peer failed.
   virtual void check() {}
-  // Whether exchange() only enqueues stream work (no host-side data movement or blocking), so a
-  // hipGraph capture of the step loop replays it faithfully: rccl, loopback, ipc.
-  virtual bool graph_capturable() const { return false; }
+  // Whether exchange() only enqueues stream work on the halo streams (no host-side data movement
+  // or blocking): rccl (grouped send / recv), loopback, ipc, proxy. The engine's folded,
+  // boundary-on-the-compute-stream schedule (Solver::boundary_on_cs) needs exactly this.
+  virtual bool stream_ordered() const { return false; }
+  // Whether the loaded HIP runtime can also capture that stream work into a hipGraph that replays
+  // it faithfully (stream_ordered() and capturable: RCCL's grouped send / recv only under HIP >= 7.2).
+  virtual bool graph_capturable() const { return stream_ordered(); }
   // Watchdog bound for blocking transport calls and device-side waits (seconds; 0 = default).
   virtual void set_timeout(double) {}
   // Watchdog escalation: make every outstanding transport operation return (ncclCommAbort, the
@@ -135,6 +139,10 @@ std::unique_ptr<Transport> make_host_transport();
 std::unique_ptr<Transport> make_loopback_transport();
 // RCCL send/recv over xGMI. `unique_id` is the 128-byte ncclUniqueId shared by all processes.
 std::unique_ptr<Transport> make_rccl_transport(const std::string& unique_id);
+// The rccl transport's schedule traits (what its Transport overrides return; the CPU tier asserts
+// the engine schedule they select without constructing a communicator)
+bool rccl_stream_ordered();
+bool rccl_graph_capturable();
 std::string rccl_unique_id();
 // Host callbacks (the Python layer plugs torch.distributed in here, e.g. gloo on CPU).
 struct CallbackFns {
@@ -151,12 +159,12 @@ std::unique_ptr<Transport> make_callback_transport(CallbackFns fns);
 // (csrc/comm/ipc_transport.cpp). Needs fns.allgather; residual / barrier go through fns too.
 // copy_mode: the face copy engine (hip_face_copy; -1 = process default). Named "ipc" (blit) or
 // "ipc_sdma".
-std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode = -1);
+// share_gpu: allow several engine processes on one GPU (tests only; see ipc_shared_gpu_problem).
+std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode = -1, bool share_gpu = false);
 // Whether the ipc transport pulls faces straight from the neighbours' exported field buffers (one
 // copy per face) rather than through mailboxes (two): buffers of at most 1900 MiB, since torch's
 // HIP 7.0 runtime stalls mapping exported buffers of 2 GiB and more; MDFX_IPC_DIRECT=0 / 1 forces.
 bool ipc_direct_ok(size_t field_bytes);
-bool concurrent_pulls();
 // Rank proxy (HIP): ONE slab of an N-way decomposition alone on a GPU, exchanging with itself
 // through the ipc transport's mailbox copies and device counters (csrc/comm/proxy_transport.cpp):
 // the per-GPU schedule of an N-GPU run, measurable on one GPU. Ghost values are the slab's own
@@ -173,5 +181,13 @@ struct IpcPeerInfo {
 // why not. `peer_access` is hipDeviceCanAccessPeer(mine.device -> peer.device) for devices that
 // differ (ignored on one device).
 std::string ipc_peer_problem(const IpcPeerInfo& mine, const IpcPeerInfo& peer, int expect_rank, bool peer_access);
+// Host-only check over every rank's (pid, GPU PCI bus id) record (CPU-testable): "" unless two
+// engine processes would share one GPU without share_gpu. The exchange and the folded boundary order
+// their work by device-side spin waits (counter_wait_kernel, csrc/kernels/sync_kernels.hip), which
+// rely on the hardware scheduler running every producer queue: with several processes' queues
+// oversubscribing one GPU a waiting queue can starve the producing one (round 4, session T:
+// profiles/r04_session_t/). One process per GPU, the production layout, never does; the one-GPU
+// multi-process tests opt in with share_gpu. Every rank sees the same records, so all refuse together.
+std::string ipc_shared_gpu_problem(const std::vector<std::pair<int, std::string>>& pid_pci, bool share_gpu);
 
 }  // namespace mdfx

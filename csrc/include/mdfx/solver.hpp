@@ -61,6 +61,15 @@ struct StepStats {
   int64_t graph_captures = 0;  // cycles captured + instantiated (prepare_graphs() or on demand)
 };
 
+// The per-step schedule the engine runs for a layout and transport (Solver::boundary_on_cs and
+// fold_ok decide it; Solver::schedule() reports it): "serialised" (no overlap: the exchange, then one
+// sweep on the halo stream), "two-stream" (boundary kernels + exchange on the halo stream, interior
+// on the compute stream; several slabs per process or a host-side exchange), "boundary-on-compute"
+// (one slab per process and a stream-ordered exchange: boundary kernels then interior on the
+// compute stream, only the exchange on the halo stream) and "folded" (the same with the lower
+// boundary region computed inside the interior sweep, heat7_wxk fused sweeps).
+const char* step_schedule(bool overlap, size_t local_slabs, bool stream_ordered, bool fold);
+
 class Solver {
  public:
   // local_ranks[i] is the global slab index owned by backends[i] in this process.
@@ -88,6 +97,8 @@ class Solver {
   std::vector<std::pair<int, bool>> sweep_plan(int64_t steps) const;
   // Whether run() would replay captured cycles in this configuration.
   bool graph_eligible() const;
+  // The schedule eager steps of the deepest fused sweep run (step_schedule).
+  std::string schedule() const;
   void synchronize();
   // Refresh ghost planes of the current buffer (after write_owned / resume).
   void exchange_ghosts();
@@ -183,6 +194,7 @@ class Solver {
   bool boundary_on_cs() const;
   int min_rounds() const;  // effective rounds per streaming sweep (RegionArgs::min_rounds)
   bool poisoned_ = false;  // the watchdog aborted the transport: no further steps, bounded teardown
+  bool capturing_ = false;  // capture_graph() is recording steps (no folded boundary inside a graph)
   // hipGraphExec_t of the 2-sweep cycle starting at buffer p (index p), and its fused depth
   void* graph_exec_[2] = {nullptr, nullptr};
   int graph_k_[2] = {0, 0};

@@ -58,11 +58,12 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
                       hipStream_t s);
 double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
-// 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt); MDFX_H7_WTK = -1 keeps heat7_tbk
+// 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt; heat7_tbk's K = 3 / 4 were
+// removed in round 5)
 static bool use_wxk(DType dt, int64_t nx, int steps);
 static bool use_wtk(int steps, DType dt) {
   (void)dt;
-  return knobs().h7_wtk >= 0 && heat7_wtk_supported(steps);
+  return heat7_wtk_supported(steps);
 }
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
 // 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
@@ -83,23 +84,11 @@ static int env_int(const char* name, int dflt) {
 
 static Knobs read_knobs() {
   Knobs k;
-  k.zc = env_int("MDFX_ZC", 0);
-  k.blocks = env_int("MDFX_BLOCKS", 4096);
-  k.ry = env_int("MDFX_RY", 0);
   k.tb_ry = env_int("MDFX_TB_RY", 0);
-  k.tbk_ry = env_int("MDFX_TBK_RY", 0);
-  k.h7_wtk = env_int("MDFX_H7_WTK", 0);
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
-  k.wtk_ry8 = env_int("MDFX_WTK_RY8", 0);
-  k.j5_tbk = env_int("MDFX_J5_TBK", 0);
-  k.life_tbk = env_int("MDFX_LIFE_TBK", 0);
-  k.b27_tbk = env_int("MDFX_B27_TBK", 0);
-  k.life_bits = env_int("MDFX_LIFE_BITS", 1);
-  k.debug_zc = env_int("MDFX_DEBUG_ZC", 0);
-  k.wxk_diag = env_int("MDFX_WXK_DIAG", 0);
-  k.wxk_strip = env_int("MDFX_WXK_STRIP", 1);
+  k.wxk_exp = env_int("MDFX_WXK_EXP", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
 }
@@ -306,7 +295,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // where heat7_wxk runs: its per-wave rows no longer grow with K, so the fourth step per pass
       // costs less than the HBM pass it saves (fp32; fp64 in round 4: 512^3 983 vs 740 GCells/s at
       // K = 3, 1024^3 1121 vs 885, 2048^3 + residual every 12 953 vs 890, profiles/r04_session_{o,p}/)
-      if (dev::knobs().h7_wtk >= 0 && nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
+      if (nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
         return dev::use_wxk(spec.dtype, nx, 4) ? 4 : 3;
       return 2;
   }
@@ -402,14 +391,14 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
       else
         dev::launch_box27_tb2<double>(g, (const double*)a.in, (double*)a.out, spec.coef, a.resid, s);
     } else if (spec.kind == StencilKind::Life) {
-      if (a.steps > 2 || dev::knobs().life_tbk)
+      if (a.steps > 2)
         dev::launch_life_tbk(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.steps, a.resid, s);
       else
         dev::launch_life_tb2(g, (const uint8_t*)a.in, (uint8_t*)a.out, a.resid, s);
     } else if (spec.kind == StencilKind::Jacobi5) {
       // ref_precision takes the mixed kernels only where it can change a bit (mixed_update())
       const bool mixed = spec.mixed_update();
-      if (a.steps > 2 || dev::knobs().j5_tbk || mixed) {
+      if (a.steps > 2 || mixed) {
         if (spec.dtype == DType::F32)
           dev::launch_jacobi5_tbk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s,
                                          mixed);

@@ -351,6 +351,8 @@ struct RowOpsN {
   // partial sum across the back edge and forms it in the next iteration, where the lane-shift
   // moves can no longer fold into the adds as DPP operands (DPP combining works inside a block)
   static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.p), "+v"(r.q)); }
+  // the same without `volatile`: still materialises the row, but is no scheduling barrier
+  static __device__ __forceinline__ void pin_nv(Row& r) { asm("" : "+v"(r.p), "+v"(r.q)); }
 };
 
 }  // namespace dev

@@ -196,8 +196,7 @@ static void launch_box27_t(const Geo& g, const T* in, T* out, const StencilCoef&
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + WXN * WX - 1) / (WXN * WX));
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  int zc = knobs().zc;
-  if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, 2048);
+  const int zc = pick_zc(planes, (int64_t)XT * YT, 128, 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XT * YT * ZT)), blk(256);
   const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
@@ -225,8 +224,8 @@ template <class T>
 void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
                   hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  // 2 rows per tile (MDFX_RY=1 for one), 1 on short columns
-  if (knobs().ry == 1 || g.ny < 8)
+  // 2 rows per tile, 1 on short columns
+  if (g.ny < 8)
     launch_box27_ry<T, 1>(g, in, out, c, resid, s);
   else
     launch_box27_ry<T, 2>(g, in, out, c, resid, s);
@@ -246,162 +245,14 @@ template void launch_box27<double>(const Geo&, const double*, double*, const Ste
 // between planes, so the registers stay close to the 7-point fused kernel. One barrier per plane
 // publishes the wave-seam values of the new u0 plane and of the pending u1 plane together. Rows
 // must fit one block (nx <= 4 * 64 * N); the result is bitwise equal to two box27_zw steps.
-template <class T, int RY, int WXN, bool RES, int PF>
-__global__ __launch_bounds__(256) void box27_tb2(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0,
-                                                 T c1, T c2, T c3, int zc, int YT, double* __restrict__ resid) {
-  using V = typename VT<T>::type;
-  using RO = RowOps<T>;  // rows in the pair layout: packed fp32 ops without lane-element shuffles
-  using Row = typename RO::Row;
-  constexpr int N = VT<T>::N;
-  constexpr int WX = 64 * N;
-  constexpr int WYN = 4 / WXN;
-  constexpr int R0 = RY + 4;  // u0 rows y0-2 .. y0+RY+1
-  constexpr int R1 = RY + 2;  // u1 rows y0-1 .. y0+RY
-  __shared__ T edge[2][4][R0 + R1][2];
-  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
-  const int yt = t % YT;
-  const int zt = t / YT;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wx = w % WXN, wy = w / WXN;
-  const int64_t xw = (int64_t)wx * WX;
-  const uint32_t xo = (uint32_t)lane * N;
-  const int64_t x = xw + xo;
-  const int64_t y0 = ((int64_t)yt * WYN + wy) * RY;
-  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
-  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
-  const bool xin = x < g.pitch;
-  const int64_t pitch = g.pitch, plane = g.plane;
-  const T* ib = in + (y0 - 2) * pitch + xw;
-  T* ob = out + y0 * pitch + xw;
-  bool xb[N];
-#pragma unroll
-  for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
-
-  auto ld = [&](int64_t lz, int k) -> Row {
-    const int64_t y = y0 - 2 + k;
-    if (xin && lz >= 0 && lz < g.lz_max && y >= 0 && y < g.ny) {
-      dcheck(g, in, ib + lz * plane + (int64_t)k * pitch + xo, N);
-      return RO::lds(ib + lz * plane + (int64_t)k * pitch + xo);  // 16-B load, regrouped into pairs
-    }
-    return RO::zero();
-  };
-  // x-neighbour sum of one row; `slot` = its seam slot in edge[buf][*] (the wave-edge lanes take
-  // the neighbouring wave's edge cell as DPP's `old` operand)
-  auto hsum = [&](const Row& v, int buf, int slot) -> Row {
-    const T le = wx > 0 ? edge[buf][w - 1][slot][1] : T(0);
-    const T re = wx < WXN - 1 ? edge[buf][w + 1][slot][0] : T(0);
-    return RO::hsum(v, lane_up1_or(le, RO::last(v)), lane_down1_or(re, RO::first(v)));
-  };
-
-  Row Rw[R0];                   // u0 plane k
-  Row A0p[R1], S0[R1], C0[R1];  // A0(k-1); A0(k-2) + B0(k-1); u0 plane k-1 (u1 window rows)
-  Row U1[R1];                   // u1 plane k-2
-  Row A1p[RY], S1[RY], C1[RY];  // A1(k-3); A1(k-4) + B1(k-3); u1 plane k-3 (owned rows)
-#pragma unroll
-  for (int j = 0; j < R0; ++j) Rw[j] = ld(zs - 2, j);
-#pragma unroll
-  for (int j = 0; j < R1; ++j) A0p[j] = S0[j] = C0[j] = U1[j] = RO::zero();
-#pragma unroll
-  for (int i = 0; i < RY; ++i) A1p[i] = S1[i] = C1[i] = RO::zero();
-  double acc = 0.0;
-  int buf = 0;
-  for (int64_t k = zs - 2; k <= ze + 2; ++k) {
-    Row NX[R0];
-    if (PF) {
-#pragma unroll
-      for (int j = 0; j < R0; ++j) NX[j] = ld(k + 1, j);
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < R0; ++j) edge[buf][w][j][0] = RO::first(Rw[j]);
-#pragma unroll
-      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][0] = RO::first(U1[j]);
-    }
-    if (lane == 63) {
-#pragma unroll
-      for (int j = 0; j < R0; ++j) edge[buf][w][j][1] = RO::last(Rw[j]);
-#pragma unroll
-      for (int j = 0; j < R1; ++j) edge[buf][w][R0 + j][1] = RO::last(U1[j]);
-    }
-    lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
-
-    // ---- level 1: partials of u1 plane k-2, u2(k-3) ------------------------------------------
-    if (k >= zs + 1) {
-      Row Hm = hsum(U1[0], buf, R0), Hc = hsum(U1[1], buf, R0 + 1);
-      const int64_t lz = k - 3;
-      const int64_t gz = lz + g.gz_off;
-      const bool zb = gz == 0 || gz == g.gnz - 1;
-#pragma unroll
-      for (int i = 0; i < RY; ++i) {
-        const int j = i + 1;
-        const Row Hp = hsum(U1[j + 1], buf, R0 + j + 1);
-        const Row cross = RO::add(Hc, RO::add(U1[j - 1], U1[j + 1]));
-        const Row diag = RO::add(Hm, Hp);
-        const Row A = RO::lin3(U1[j], cross, diag, c1, c2, c3);  // sm::box27_A
-        const Row B = RO::lin3(U1[j], cross, diag, c0, c1, c2);  // sm::box27_B
-        Hm = Hc;
-        Hc = Hp;
-        const int64_t y = y0 + i;
-        if (k >= zs + 3 && y < g.ny) {
-          Row o = C1[i];
-          if (!zb && y != 0 && y != g.ny - 1) o = RO::sel(xb, C1[i], RO::add(S1[i], A));
-          if (xin) {
-            dcheck(g, (const T*)out, ob + lz * plane + (int64_t)i * pitch + xo, N);
-            store_nt((V*)(ob + lz * plane + (int64_t)i * pitch + xo), RO::vec(o));
-            if (RES) {
-#pragma unroll
-              for (int e = 0; e < N; ++e)
-                if (x + e < g.nx) {
-                  const double d = (double)RO::get(o, e) - (double)RO::get(C1[i], e);
-                  acc += d * d;
-                }
-            }
-          }
-        }
-        S1[i] = RO::add(A1p[i], B);
-        A1p[i] = A;
-        C1[i] = U1[j];
-      }
-    }
-    // ---- level 0: partials of u0 plane k, u1(k-1) (written over U1, consumed above) ----------
-    {
-      const int64_t gz = k - 1 + g.gz_off;
-      const bool zb = gz <= 0 || gz >= g.gnz - 1;
-      Row Hm = hsum(Rw[0], buf, 0), Hc = hsum(Rw[1], buf, 1);
-#pragma unroll
-      for (int jj = 0; jj < R1; ++jj) {
-        const int j = jj + 1;
-        const Row Hp = hsum(Rw[j + 1], buf, j + 1);
-        const Row cross = RO::add(Hc, RO::add(Rw[j - 1], Rw[j + 1]));
-        const Row diag = RO::add(Hm, Hp);
-        const Row A = RO::lin3(Rw[j], cross, diag, c1, c2, c3);
-        const Row B = RO::lin3(Rw[j], cross, diag, c0, c1, c2);
-        Hm = Hc;
-        Hc = Hp;
-        const int64_t y = y0 - 1 + jj;
-        Row u = C0[jj];
-        if (!zb && y > 0 && y < g.ny - 1) u = RO::sel(xb, C0[jj], RO::add(S0[jj], A));
-        U1[jj] = u;
-        S0[jj] = RO::add(A0p[jj], B);
-        A0p[jj] = A;
-        C0[jj] = Rw[j];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < R0; ++j) Rw[j] = PF ? NX[j] : ld(k + 1, j);
-    buf ^= 1;
-  }
-  if (RES) wave_atomic_add(resid, acc);
-}
-
-// box27_tb2 for fp32 in the natural pair layout (RowOpsN: (e0,e1),(e2,e3) straight from a 16-B
+//
+// box27_tb2n: that scheme for fp32 in the natural pair layout (RowOpsN: (e0,e1),(e2,e3) straight from a 16-B
 // load, x sums as scalar adds) with the plane loop unrolled by two: every loop-carried row (the
 // running sums, the last A, the centres, the pending u1 plane and the prefetched u0 plane) lives in
 // two copies that swap roles between the planes of a trip, so no carried row is ever copied (the
-// pair-layout kernel spent 161 of its 400 VALU instructions per plane on register moves). Same
-// arithmetic and order as box27_tb2, so bitwise equal to it and to two box27_zw steps. An odd
-// plane count ends with one extra plane that stores nothing.
+// pair-layout kernel, removed in round 5 with its last fp64 use, spent 161 of its 400 VALU
+// instructions per plane on register moves). Bitwise equal to two box27_zw steps. An odd plane
+// count ends with one extra plane that stores nothing.
 template <int RY, int WXN, bool RES>
 __global__ __launch_bounds__(256) void box27_tb2n(const float* __restrict__ in, float* __restrict__ out, Geo g,
                                                   float c0, float c1, float c2, float c3, int zc, int YT,
@@ -775,8 +626,7 @@ static void launch_box27_tbk_w(const Geo& g, const T* in, T* out, const StencilC
   constexpr int WYN = 4 / WXN;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  int zc = knobs().zc;
-  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks((const void*)&box27_tbk<T, RY, K, WXN, false>), K, g.min_rounds);
+  const int zc = tbk_zc(planes, YT, resident_blocks((const void*)&box27_tbk<T, RY, K, WXN, false>), K, g.min_rounds);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
@@ -811,34 +661,25 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   constexpr int WYN = 4 / WXN;
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  int zc = knobs().zc;
-  if (zc <= 0) {  // balanced ~43-plane chunks, as the 7-point fused kernel (5 pipeline planes here)
-    int64_t zt = (planes + 43) / 44;
+  // balanced ~43-plane chunks, as the 7-point fused kernel (5 pipeline planes here)
+  int64_t zt = (planes + 43) / 44;
+  int zc = (int)((planes + zt - 1) / zt);
+  while ((int64_t)YT * zt < 1024 && zc > 16) {
+    ++zt;
     zc = (int)((planes + zt - 1) / zt);
-    while ((int64_t)YT * zt < 1024 && zc > 16) {
-      ++zt;
-      zc = (int)((planes + zt - 1) / zt);
-    }
-    zc = std::max(zc, 1);
   }
+  zc = std::max(zc, 1);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
-  // fp32: the natural-layout kernel with the 2-plane unroll (box27_tb2n; round 2's pair-layout
-  // fp32 box27_tb2, 937-944 vs 1005-1013 GCells/s at 512^3, was removed in round 4,
-  // profiles/r03_wtk/b27f32_*); fp64 (MDFX_B27_TBK = -1 only: box27_tbk is its default): box27_tb2
-  // with the next-plane prefetch (491.8 vs 479.8 without, profiles/r01_box27_tb2.txt)
-  if constexpr (std::is_same<T, float>::value) {
-    if (resid)
-      hipLaunchKernelGGL((box27_tb2n<RY, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-    else
-      hipLaunchKernelGGL((box27_tb2n<RY, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-  } else {
-    if (resid)
-      hipLaunchKernelGGL((box27_tb2<T, RY, WXN, true, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-    else
-      hipLaunchKernelGGL((box27_tb2<T, RY, WXN, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-  }
+  // the natural-layout kernel with the 2-plane unroll (box27_tb2n; round 2's pair-layout fp32
+  // box27_tb2, 937-944 vs 1005-1013 GCells/s at 512^3, was removed in round 4,
+  // profiles/r03_wtk/b27f32_*; its fp64 instance, 491.8 GCells/s against box27_tbk's 553, in round 5)
+  static_assert(std::is_same<T, float>::value, "box27_tb2n: fp32 rows (fp64 runs box27_tbk)");
+  if (resid)
+    hipLaunchKernelGGL((box27_tb2n<RY, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
+  else
+    hipLaunchKernelGGL((box27_tb2n<RY, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
 }
 
 template <class T, int RY>
@@ -859,20 +700,14 @@ void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, d
   // fp64: box27_tbk with 4 rows per tile, fp32: box27_tb2 (interleaved A/B on one MI355X, GCells/s,
   // tb2 / tbk RY 2 / tbk RY 4: 512^3 fp32 987 / 942 / 884, 1024^3 fp32 995 / 873 / 985, 512^3 fp64
   // 492 / 468 / 553; profiles/r02_box27_tbk.txt). box27_tb2 exists for fp32 only (its pair-layout
-  // rows cost the fp64 instance occupancy: 489 -> 341). MDFX_B27_TBK: -1 box27_tb2 (fp32; fp64:
-  // box27_tbk with 2 rows), 1 / 2 / 4 box27_tbk with that many rows.
-  int ry = knobs().b27_tbk != 0 ? knobs().b27_tbk : std::is_same<T, double>::value ? 4 : -1;
-  if (ry < 0 && std::is_same<T, double>::value) ry = 2;
-  if (ry > 0) {
-    if (ry == 1 || g.ny < 8)
+  // rows cost the fp64 instance occupancy: 489 -> 341). One row per tile on short columns. (The
+  // switch to the other combinations, measured slower, was removed in round 5.)
+  if constexpr (std::is_same<T, double>::value) {
+    if (g.ny < 8)
       launch_box27_tbk_ry<T, 1, 2>(g, in, out, c, resid, s);
-    else if (ry == 4)
-      launch_box27_tbk_ry<T, 4, 2>(g, in, out, c, resid, s);
     else
-      launch_box27_tbk_ry<T, 2, 2>(g, in, out, c, resid, s);
-    return;
-  }
-  if constexpr (std::is_same<T, float>::value) {
+      launch_box27_tbk_ry<T, 4, 2>(g, in, out, c, resid, s);
+  } else {
     if (knobs().tb_ry == 1 || g.ny < 8)
       launch_box27_tb2_ry<T, 1>(g, in, out, c, resid, s);
     else

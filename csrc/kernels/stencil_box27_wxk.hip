@@ -46,7 +46,7 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 
-template <class T, int RY, int RE, int K, int WB, bool RES>
+template <class T, int RY, int RE, int K, int WB, bool RES, int EXP = 0>
 __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
                                                      T c2, T c3, int zc, int XT, int YT, int ntasks,
                                                      double* __restrict__ resid) {
@@ -156,6 +156,20 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
       if (q < qdma) issue(q + 1, P ^ 1);
       const int lzo = q - LAG;  // level K's output plane
       const bool valid = lzo >= zs && lzo < ze;
+      // EXP 1: the step's LDS rows (level 1's u0 window rows, every upper level's two seam rows) are
+      // read up front, so the reads overlap each other instead of each waiting out a round trip
+      constexpr int NU = EXP ? SH::n(1) + 2 : 1;
+      Row U[NU], SU[K], SD[K];
+      if constexpr (EXP != 0) {
+#pragma unroll
+        for (int k = 0; k < NU; ++k) U[k] = RO::fromv(V(wrow[P * WIN_BUF + (SH::lo(1) - 1 + k + K) * 64]));
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+          SU[j] = SD[j] = RO::zero();
+          if (SH::lo(j + 1) - 1 < SH::lo(j)) SU[j] = RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
+          if (SH::hi(j + 1) >= SH::hi(j)) SD[j] = RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
+        }
+      }
       // levels top-down: level l reads its inputs (the level below's plane from the previous step)
       // before that level overwrites its other stored plane
 #pragma unroll
@@ -171,11 +185,19 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
         }
         // input rows of level l-1 at plane p: rows lo(l)-1 .. hi(l)
         auto vin = [&](int i) -> Row {
-          if (l == 1) return RO::fromv(V(wrow[P * WIN_BUF + (i + K) * 64]));
-          const int j = l - 1;
-          if (i < SH::lo(j)) return RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
-          if (i >= SH::hi(j)) return RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
-          return H[j - 1][P ^ 1][i - SH::lo(j)];
+          if constexpr (EXP != 0) {
+            if (l == 1) return U[i - (SH::lo(1) - 1)];
+            const int j = l - 1;
+            if (i < SH::lo(j)) return SU[j];
+            if (i >= SH::hi(j)) return SD[j];
+            return H[j - 1][P ^ 1][i - SH::lo(j)];
+          } else {
+            if (l == 1) return RO::fromv(V(wrow[P * WIN_BUF + (i + K) * 64]));
+            const int j = l - 1;
+            if (i < SH::lo(j)) return RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
+            if (i >= SH::hi(j)) return RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
+            return H[j - 1][P ^ 1][i - SH::lo(j)];
+          }
         };
         Row vm = vin(SH::lo(l) - 1), vc = vin(SH::lo(l));
         Row hm = hs(vm), hc = hs(vc);
@@ -264,19 +286,19 @@ static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf
   const int64_t tiles = (int64_t)XT * YT;
   const void* kfn = (const void*)&box27_wxk<T, RY, RE, K, WB, false>;
   const int64_t resident = resident_blocks(kfn, 64 * WB);
-  int zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, resident, K, 3 * K - 1, g.min_rounds);
+  int zc = wx_zc(planes, tiles, resident, K, 3 * K - 1, g.min_rounds);
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = tiles * ZT;
-  if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] box27_wxk K=%d RY=%d RE=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d\n", K, RY,
-            RE, WB, (long long)planes, XT, YT, (long long)resident, zc);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "box27_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
   if (resid)
     hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
                        (int)ntasks, resid);
+  else if (knobs().wxk_exp == 1)
+    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT,
+                       YT, (int)ntasks, resid);
   else
     hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
                        (int)ntasks, resid);

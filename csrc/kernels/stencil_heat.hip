@@ -312,9 +312,8 @@ static void launch_heat7_t(const Geo& g, const T* in, T* out, T r, double* resid
   const int64_t planes = g.lz_end - g.lz_begin;
   const int XT = (int)((g.nx + WXN * WX - 1) / (WXN * WX));
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
-  int zc = knobs().zc;
   // ~16 blocks per CU: 512^3 fp32 ran 0.2018 ms at 4096 blocks vs 0.2296 ms at 2048
-  if (zc <= 0) zc = pick_zc(planes, (int64_t)XT * YT, 128, knobs().blocks);
+  const int zc = pick_zc(planes, (int64_t)XT * YT, 128, 4096);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XT * YT * ZT)), blk(256);
   if (resid)
@@ -354,15 +353,12 @@ void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStre
   // defaults from bench/kernel_ab.py on MI355X, 1024^3 fp32 (profiles/r01_ab_heat7_f32.json):
   // RY=2 PF=1 1.546 ms (694.5 GCells/s) > RY=4 PF=1 1.584 > RY=4 PF=2 1.603 > RY=2 PF=2 1.662
   // fp64 1024^3: RY=4 PF=2 3.395 ms (316 GCells/s) > RY=4 PF=1 3.415 > RY=2 PF=1 3.479
-  // (profiles/r01_ab_heat7_f64.json). MDFX_RY picks 1, 2 or 4 rows per tile.
-  int ry = knobs().ry;
-  if (ry <= 0) ry = sizeof(T) == 4 ? 2 : 4;
-  if (g.ny < 8) ry = 1;
-  switch (ry) {
-    case 1: launch_heat7_ry<T, 1>(g, in, out, r, resid, s); break;
-    case 2: launch_heat7_ry<T, 2>(g, in, out, r, resid, s); break;
-    default: launch_heat7_ry<T, 4>(g, in, out, r, resid, s); break;
-  }
+  // (profiles/r01_ab_heat7_f64.json); one row on short columns.
+  constexpr int RY = sizeof(T) == 4 ? 2 : 4;
+  if (g.ny < 8)
+    launch_heat7_ry<T, 1>(g, in, out, r, resid, s);
+  else
+    launch_heat7_ry<T, RY>(g, in, out, r, resid, s);
 }
 template void launch_heat7<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
 template void launch_heat7<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
@@ -373,8 +369,7 @@ void launch_jacobi5(const Geo& g, const T* in, T* out, T r, double* resid, hipSt
   if (planes <= 0) return;
   constexpr int WX = 64 * VT<T>::N;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = knobs().zc;
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int zc = pick_zc(planes, XT, 256, 4 * 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);

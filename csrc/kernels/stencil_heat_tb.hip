@@ -276,7 +276,6 @@ int64_t resident_blocks(const void* kfn, int block) {
   int cus = 0, nb = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, block, 0) != hipSuccess || nb <= 0) nb = block > 256 ? 1 : 2;
-  if (knobs().debug_zc) fprintf(stderr, "[mdfx] residency: %d CUs x %d blocks of %d threads\n", cus, nb, block);
   return cache[{dev, {kfn, block}}] = (int64_t)cus * nb;
 }
 int64_t resident_blocks(const void* kfn) { return resident_blocks(kfn, 256); }
@@ -308,8 +307,7 @@ static void launch_tb2_xt(const Geo& g, const T* in, T* out, T r, double* resid,
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + RY - 1) / RY);
   const void* kfn = (const void*)&heat7_tb2<T, RY, 4, false, 1, true>;
-  int zc = knobs().zc;
-  if (zc <= 0) zc = tb2_zc(planes, (int64_t)XTn * YT, resident_blocks(kfn));
+  const int zc = tb2_zc(planes, (int64_t)XTn * YT, resident_blocks(kfn));
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)XTn * YT * ZT)), blk(256);
   if (resid)
@@ -465,8 +463,7 @@ void launch_jacobi5_tb2(const Geo& g, const T* in, T* out, T r, double* resid, h
   if (planes <= 0) return;
   constexpr int WX = 64 * VT<T>::N;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = knobs().zc;
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int zc = pick_zc(planes, XT, 256, 4 * 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
@@ -619,8 +616,7 @@ static void launch_jacobi5_tbk_km(const Geo& g, const T* in, T* out, T r, double
   if (planes <= 0) return;
   constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
-  int zc = knobs().zc;
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int zc = pick_zc(planes, XT, 256, 4 * 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);

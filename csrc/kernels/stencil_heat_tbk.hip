@@ -284,7 +284,9 @@ bool heat7_tbk_supported(const Geo& g, int steps) {
   constexpr int WX = 64 * VT<T>::N;
   // the row in one block (wider rows at K = 2: heat7_tb2 x tiles, 533 vs 483 GCells/s for these
   // kernels' x tiles at 2048^3 fp64, profiles/r02_ab_f64_2048.txt)
-  return steps >= 2 && steps <= 4 && g.pitch <= 4 * WX && g.nx >= 1 && g.ny >= 1;
+  // (K = 3 / 4 run heat7_wtk / heat7_wxk: this kernel's deeper sweeps measured slower and were
+  // removed in round 5 with the switch that reached them, profiles/r01_tbk/, r02_wtk/README.txt)
+  return steps == 2 && g.pitch <= 4 * WX && g.nx >= 1 && g.ny >= 1;
 }
 template bool heat7_tbk_supported<float>(const Geo&, int);
 template bool heat7_tbk_supported<double>(const Geo&, int);
@@ -295,9 +297,7 @@ static void launch_tbk_w(const Geo& g, const T* in, T* out, T r, double* resid, 
   const int64_t planes = g.lz_end - g.lz_begin;
   const int YT = (int)((g.ny + WYN * RY - 1) / (WYN * RY));
   const void* kfn = (const void*)&heat7_tbk<T, RY, K, WXN, false>;
-  int zc = knobs().zc;
-  if (zc <= 0) zc = tbk_zc(planes, YT, resident_blocks(kfn), K, g.min_rounds);
-  if (knobs().debug_zc) fprintf(stderr, "[mdfx] tbk K=%d RY=%d: %lld planes x %d tiles -> zc %d\n", K, RY, (long long)planes, YT, zc);
+  const int zc = tbk_zc(planes, YT, resident_blocks(kfn), K, g.min_rounds);
   const int ZT = (int)((planes + zc - 1) / zc);
   const dim3 grd((unsigned)((int64_t)YT * ZT)), blk(256);
   if (resid)
@@ -317,40 +317,23 @@ static void launch_tbk_t(const Geo& g, const T* in, T* out, T r, double* resid, 
     launch_tbk_w<T, RY, K, 1>(g, in, out, r, resid, s);
 }
 
-// K fused steps. Rows per tile: 4 at K = 2 and 2 deeper (1 on very short columns); MDFX_TBK_RY
-// picks 1, 2 or 4 (K = 2) / 1 or 2 (K = 3, 4). K = 2: RY 4 1351 GCells/s vs 3 1199, 2 1189;
-// K = 3: RY 2 1146 vs 3 844 (register spills) (profiles/r01_tbk/ab_1024_f32.log).
+// Two fused steps. Rows per tile: 4 (1 on very short columns): RY 4 1351 GCells/s vs 3 1199, 2 1189
+// (profiles/r01_tbk/ab_1024_f32.log).
 template <class T>
 void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
   // region contract: u0 is read on [lz_begin - K, lz_end + K)
-  MDFX_CHECK(steps >= 2 && steps <= 4 && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+  MDFX_CHECK(steps == 2 && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_tbk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.pitch <= 4 * 64 * VT<T>::N, "heat7_tbk: the row must fit one block");
   MDFX_CHECK(g.ny < ((int64_t)1 << 30) && g.lz_max < ((int64_t)1 << 30) && g.gnz < ((int64_t)1 << 30) &&
                  g.gz_off > -((int64_t)1 << 30) && g.gz_off < ((int64_t)1 << 30),
              "heat7_tbk: row / plane counts must fit 32-bit indices");
-  int ry = knobs().tbk_ry;
-  if (ry <= 0) ry = steps == 2 ? 4 : 2;
-  if (g.ny < 8) ry = 1;
-  if (steps == 2) {
-    switch (ry) {
-      case 1: launch_tbk_t<T, 1, 2>(g, in, out, r, resid, s); break;
-      case 2: launch_tbk_t<T, 2, 2>(g, in, out, r, resid, s); break;
-      default: launch_tbk_t<T, 4, 2>(g, in, out, r, resid, s); break;
-    }
-  } else if (steps == 3) {
-    if (ry == 1)
-      launch_tbk_t<T, 1, 3>(g, in, out, r, resid, s);
-    else
-      launch_tbk_t<T, 2, 3>(g, in, out, r, resid, s);
-  } else {
-    if (ry == 1)
-      launch_tbk_t<T, 1, 4>(g, in, out, r, resid, s);
-    else
-      launch_tbk_t<T, 2, 4>(g, in, out, r, resid, s);
-  }
+  if (g.ny < 8)
+    launch_tbk_t<T, 1, 2>(g, in, out, r, resid, s);
+  else
+    launch_tbk_t<T, 4, 2>(g, in, out, r, resid, s);
 }
 template void launch_heat7_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
 template void launch_heat7_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);

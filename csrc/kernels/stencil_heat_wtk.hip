@@ -275,14 +275,11 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
   const void* kfn = (const void*)&heat7_wtk<T, RY, K, WB, false, MODE>;
   const int64_t tiles = (int64_t)XT * YT;  // blocks per z chunk
   const int64_t resident = resident_blocks(kfn, 64 * WB);
-  int zc = knobs().zc > 0 ? knobs().zc : wtk_zc(planes, tiles, resident, K, g.min_rounds);
+  int zc = wtk_zc(planes, tiles, resident, K, g.min_rounds);
   const int64_t planes2 = g.lz2_end - g.lz2_begin;  // a second region (boundary pair): one chunk each
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = (int64_t)XT * YT * ZT;
-  if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] wtk K=%d RY=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n", K, RY,
-            WB, (long long)planes, XT, YT, (long long)resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wtk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   // residual instances exist where they fit 256 VGPRs without spills: every fp64 shape, fp32 in
@@ -347,14 +344,9 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
   if (steps == 3) {
     if (wb == 8) {
       // fp64 8-wave bands: 3 rows per wave at rows up to 1024 cells (1024^3 923-925 vs 849-852
-      // GCells/s), 2 rows on wider rows (2048^3 835 vs 802); MDFX_WTK_RY8 = 2 / 3 forces
-      bool ry2 = false;
+      // GCells/s), 2 rows on wider rows (2048^3 835 vs 802)
       if constexpr (sizeof(T) == 8) {
-        const int k = knobs().wtk_ry8;
-        ry2 = k == 2 || (k != 3 && g.nx > 1024);
-      }
-      if constexpr (sizeof(T) == 8) {
-        if (ry2) launch_wtk_k<T, 2, 3, 8>(g, in, out, r, resid, s);
+        if (g.nx > 1024) launch_wtk_k<T, 2, 3, 8>(g, in, out, r, resid, s);
         else launch_wtk_k<T, 3, 3, 8>(g, in, out, r, resid, s);
       } else {
         launch_wtk_k<T, 3, 3, 8>(g, in, out, r, resid, s);

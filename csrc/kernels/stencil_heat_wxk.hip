@@ -57,9 +57,6 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 
-// DG: a diagnostic copy (MDFX_WXK_DIAG, timing only, results are garbage) whose `diag` bits drop
-// parts of the sweep to see where its time goes: 1 the window DMAs after the first plane, 2 the
-// output stores, 4 the per-plane barrier
 // PEN: the pencil copy (output rows [ly_begin, ly_end) of storage rows holding ghost rows, global
 // row = storage row + gy_off). Slabs run the copy without it: the four extra row bounds held in
 // scalars cost the slab sweep ~4 % (six more vmcnt(0) waits in front of window reads, round 4).
@@ -89,11 +86,9 @@ __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles,
 // SIG: the folded-boundary copy (Geo::sig): the blocks of the chunks starting at lz_begin publish their
 // output planes [lz_begin, sig_z) and signal, so the halo exchange of the lower face overlaps the
 // rest of the same sweep (no separate boundary launch for that face).
-template <class T, int RY, int RE, int K, int WB, bool RES, bool DG = false, bool PEN = false, bool SIG = false>
+template <class T, int RY, int RE, int K, int WB, bool RES, bool PEN = false, bool SIG = false, int EXP = 0>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
-                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid,
-                                                     int diag = 0) {
-  const int dg = DG ? diag : 0;
+                                                     int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
@@ -152,7 +147,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // needs the per-row held test (bands at global y = 0 / gny-1 run the tested copy, all their waves
   // together)
   const bool yint = yb - (K - 1) + gyoff >= 1 && yb + BR + K - 2 + gyoff <= gny - 2;
-  const int nsto = (__builtin_amdgcn_ballot_w64(own) != 0 && !(dg & 2)) ? max(0, min(rown, ly1 - y0)) : 0;
+  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(rown, ly1 - y0)) : 0;
   int nst = 0;  // output stores issued since this wave's last DMA
 
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
@@ -221,9 +216,8 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // publishes it and last step's seam rows, and certifies that every wave is done with the
       // other window buffer and the other seam parity
       wait_vm_le(nst);
-      if (!(dg & 4)) lds_barrier();
-      else wait_lgkm0();
-      if (q < qlast && !(dg & 1)) issue(q + 1, P ^ 1);
+      lds_barrier();
+      if (q < qlast) issue(q + 1, P ^ 1);
       constexpr int SR = P ^ 1;  // seam parity read this step
       // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact)
       Row rl[K + 1];
@@ -232,13 +226,35 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         const int gz = q - l + gzoff;
         rl[l] = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
       }
+      LV* const wbuf = wrow + P * WIN_BUF;
+      auto u0row = [&](int i) -> Row { return RO::fromv(V(wbuf[(i + K) * 64])); };
+      // EXP 1: every LDS row this step reads (the seam rows of levels 1..K-1 and the u0 window
+      // rows) is read up front, so the reads overlap each other and the level-(1) arithmetic
+      // instead of each waiting out a full LDS round trip right before its use
+      constexpr int NU = EXP ? SH::n(1) + 2 : 1;
+      Row UP[K - 1], DN[K - 1], U[NU];
+      if constexpr (EXP != 0) {
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+          UP[j - 1] = DN[j - 1] = RO::zero();
+          if (ROLE != 0) UP[j - 1] = RO::fromv(seam[SR][j - 1][wu][1][lane]);
+          if (ROLE != 2) DN[j - 1] = RO::fromv(seam[SR][j - 1][wd][0][lane]);
+        }
+#pragma unroll
+        for (int k = 0; k < NU; ++k) U[k] = u0row(SH::lo(1) - 1 + k);
+      }
       // (1) levels 2..K: S_l(m), m = q - l, into the slot of u_{l-1}(m-1) (its zm, consumed here)
 #pragma unroll
       for (int l = 2; l <= K; ++l) {
         const int j = l - 1;  // level of the inputs
         Row up = RO::zero(), dn = RO::zero();
-        if (ROLE != 0) up = RO::fromv(seam[SR][j - 1][wu][1][lane]);
-        if (ROLE != 2) dn = RO::fromv(seam[SR][j - 1][wd][0][lane]);
+        if constexpr (EXP != 0) {
+          up = UP[j - 1];
+          dn = DN[j - 1];
+        } else {
+          if (ROLE != 0) up = RO::fromv(seam[SR][j - 1][wu][1][lane]);
+          if (ROLE != 2) dn = RO::fromv(seam[SR][j - 1][wd][0][lane]);
+        }
 #pragma unroll
         for (int i = SH::lo(l); i < SH::hi(l); ++i) {
           const int ij = i - SH::lo(j);
@@ -249,21 +265,24 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
           const T rgt = lane_down1(RO::first(c));
           Row& a = H[j - 1][P][ij];
           a = RO::partial(c, lft, rgt, ym, yp, a);
-          RO::pin(a);
+          if constexpr (EXP >= 2) RO::pin_nv(a);
+          else RO::pin(a);
         }
       }
       // (2) level 1 row by row from the u0 window, each new row cascading up through the levels
-      LV* const wbuf = wrow + P * WIN_BUF;
-      auto u0row = [&](int i) -> Row { return RO::fromv(V(wbuf[(i + K) * 64])); };
       Row X[3];
-      X[0] = u0row(SH::lo(1) - 1);
-      X[1] = u0row(SH::lo(1));
+      auto urow = [&](int i) -> Row {
+        if constexpr (EXP != 0) return U[i - (SH::lo(1) - 1)];
+        else return u0row(i);
+      };
+      X[0] = urow(SH::lo(1) - 1);
+      X[1] = urow(SH::lo(1));
       const bool valid = q - K >= zs && q <= qlast;  // u_K(q - K) is an owned output plane
       const int lz = q - K;
 #pragma unroll
       for (int i = SH::lo(1); i < SH::hi(1); ++i) {
         const int i1 = i - SH::lo(1);
-        X[(i1 + 2) % 3] = u0row(i + 1);
+        X[(i1 + 2) % 3] = urow(i + 1);
         const Row& xm = X[i1 % 3];
         const Row& cen = X[(i1 + 1) % 3];
         const Row& xp = X[(i1 + 2) % 3];
@@ -275,13 +294,14 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         const T lft = lane_up1(RO::last(cen));
         const T rgt = lane_down1(RO::first(cen));
         S1[i1] = RO::partial(cen, lft, rgt, xm, xp, cold);
-        RO::pin(S1[i1]);
+        if constexpr (EXP >= 2) RO::pin_nv(S1[i1]);
+        else RO::pin(S1[i1]);
         Cout[i1] = cen;
         // cascade: cur = u_j(q - j) for j = 1, 2, ...
 #pragma unroll
         for (int j = 1; j <= K; ++j) {
           if (j == K) {  // the sweep's output row
-            if (valid && i >= 0 && i < SH::R && y0 + i < ly1 && own && !(dg & 2)) {
+            if (valid && i >= 0 && i < SH::R && y0 + i < ly1 && own) {
               T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
               dcheck(g, (const T*)out, a, N);
               store_nt((V*)a, RO::vec(cur));
@@ -316,9 +336,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       nst = valid ? nsto : 0;
       if constexpr (SIG) {
         if (sig_blk && lz == sig_last) {  // block-uniform: every wave takes this branch together
-          // this wave's stores of the lower planes complete, then are written back past this XCD's
-          // L2 (agent-scope release); after the barrier one lane counts the block's arrival, and the
-          // last block of the launch to arrive bumps the sweep counter the halo stream waits for
+          // this wave's stores of the lower planes are acknowledged by this XCD's L2 (vmcnt 0; no
+          // release: they may still sit dirty in that L2); after the barrier one lane counts the
+          // block's arrival, and the last block of the launch to arrive bumps the sweep counter the
+          // halo stream waits for. Visibility to the exchange rests on the counter-wait kernel's
+          // end-of-dispatch release (hip_region_signals, kernels.hpp)
           wxk_fold_signal(g.sig, tiles, w == 0 && lane == 0);
         }
       }
@@ -361,7 +383,7 @@ static WxGeo wxk_geo(const Geo& g) {
   w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false>, 64 * WB);
   // (2-wave strip bands: the strip is on the sweep's critical path, before the exchange; chunks down
   // to K planes spread its few tiles over the device)
-  w.zc = knobs().zc > 0 ? knobs().zc : wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds, WB == 2 ? K : 0);
+  w.zc = wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds, WB == 2 ? K : 0);
   if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
   w.ntasks = tiles * ZT;
@@ -373,48 +395,51 @@ template <class T, int RY, int RE, int K, int WB>
 static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   const WxGeo wg = wxk_geo<T, RY, RE, K, WB>(g);
   const int XT = wg.XT, YT = wg.YT, zc = wg.zc;
+  // only the blocks of the first z chunk signal: it must hold every plane the signal covers (a
+  // chunk shorter than that would leave the halo stream waiting for a signal never sent)
+  MDFX_CHECK(!g.sig || zc >= g.sig_z - g.lz_begin,
+             format("heat7_wxk: z chunks of %d planes cannot carry the folded boundary's %lld planes", zc,
+                    (long long)(g.sig_z - g.lz_begin)));
   const int64_t ntasks = wg.ntasks;
-  if (knobs().debug_zc)
-    fprintf(stderr, "[mdfx] wxk K=%d RY=%d RE=%d WB=%d: %lld planes x %d x %d tiles, %lld slots -> zc %d (%lld blocks)\n",
-            K, RY, RE, WB, (long long)(g.lz_end - g.lz_begin), XT, YT, (long long)wg.resident, zc, (long long)ntasks);
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   const bool pen = g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny;
+  // one instance per (residual, pencil rows, folded-boundary signal) combination the engine uses
+  auto go = [&](auto res_c, auto pen_c, auto sig_c, auto exp_c) {
+    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, decltype(res_c)::value, decltype(pen_c)::value,
+                                  decltype(sig_c)::value, decltype(exp_c)::value>),
+                       grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
+  };
+  using F = std::false_type;
+  using Tr = std::true_type;
   if constexpr (WB != 8) {
     MDFX_CHECK(!g.sig, "heat7_wxk: folded boundaries run in bands of 8 waves");
   } else if (g.sig) {
     MDFX_CHECK(!pen && g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
-    if (resid)
-      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true, false, false, true>), grd, blk, 0, s, in, out, g, r, zc,
-                         XT, YT, (int)ntasks, resid, 0);
-    else
-      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, false, false, true>), grd, blk, 0, s, in, out, g, r, zc,
-                         XT, YT, (int)ntasks, resid, 0);
+    if (resid) go(Tr{}, F{}, Tr{}, IC<0>{});
+    else go(F{}, F{}, Tr{}, IC<0>{});
     return;
   }
   if (resid) {
-    if (pen)
-      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT,
-                         (int)ntasks, resid, 0);
-    else
-      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
-                         resid, 0);
+    if (pen) go(Tr{}, Tr{}, F{}, IC<0>{});
+    else go(Tr{}, F{}, F{}, IC<0>{});
     return;
   }
   if (pen) {
-    hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT,
-                       (int)ntasks, resid, 0);
+    go(F{}, Tr{}, F{}, IC<0>{});
     return;
   }
   if constexpr (sizeof(T) == 4 && RY == 3 && RE == 2 && K == 4 && WB == 8) {  // the headline shape only
-    if (knobs().wxk_diag) {
-      hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false, true>), grd, blk, 0, s, in, out, g, r, zc, XT, YT,
-                         (int)ntasks, resid, knobs().wxk_diag);
+    if (knobs().wxk_exp == 1) {
+      go(F{}, F{}, F{}, IC<1>{});
+      return;
+    }
+    if (knobs().wxk_exp == 2) {
+      go(F{}, F{}, F{}, IC<2>{});
       return;
     }
   }
-  hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks,
-                     resid, 0);
+  go(F{}, F{}, F{}, IC<0>{});
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -450,8 +475,8 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
              "heat7_wxk: row / plane counts must fit 32-bit indices");
   // a pencil's y-boundary strip (K rows next to a y neighbour, over the interior planes): bands of
   // 2 + 2 rows in 2-wave blocks instead of 22-row bands of 8 waves that would compute 4 useful rows
-  // (and 4 blocks per CU, so the strip's few tiles split into many z chunks). MDFX_WXK_STRIP=0: off.
-  const bool strip = g.ly_end - g.ly_begin <= 4 && (g.ly_begin != 0 || g.ly_end != g.ny) && knobs().wxk_strip != 0;
+  // (and 4 blocks per CU, so the strip's few tiles split into many z chunks)
+  const bool strip = g.ly_end - g.ly_begin <= 4 && (g.ly_begin != 0 || g.ly_end != g.ny);
   if (strip) {
     if (steps == 3) launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
     else launch_wxk<T, 2, 2, 4, 2>(g, in, out, r, resid, s);  // (fp64: 256 VGPRs, no spills)

@@ -140,10 +140,9 @@ void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, h
   if (planes <= 0) return;
   constexpr int WX = 64 * 16;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = knobs().zc;
   // 32768^2: zc 64 beats 128 (profiles/r01_ab_life_u8.json), zc 32 beats 64 once the carry bytes
   // moved to DPP (2414 vs 2351 GCells/s, profiles/r01_life_tb2.txt)
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
+  const int zc = pick_zc(planes, XT, 256, 4 * 8192);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
@@ -294,8 +293,7 @@ void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resi
   if (planes <= 0) return;
   constexpr int WX = 64 * 16;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  int zc = knobs().zc;
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
+  const int zc = pick_zc(planes, XT, 256, 4 * 8192);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
@@ -305,125 +303,8 @@ void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resi
     hipLaunchKernelGGL(life_tb2<false>, grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
 }
 
-// ---- K generations per sweep --------------------------------------------------------------------
-//
-// Deep temporal blocking with overlapping wave segments, as jacobi5_tbk: a wave owns lanes 1..62
-// and lanes 0 / 63 carry the neighbours' edge cells; every generation corrupts one more byte of
-// those two lanes from the outside in, so K <= 16 generations leave the owned lanes exact.
-template <int K, bool RES>
-__global__ __launch_bounds__(256) void life_tbk(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                Geo g, int zc, int XT, int ntasks, double* __restrict__ resid) {
-  constexpr int N = 16;
-  constexpr int SEG = 62 * N;
-  static_assert(K >= 1 && K <= N, "generations must not reach past the halo lanes");
-  const int lane = threadIdx.x & 63;
-  const int task = (int)xcd_remap(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (task >= ntasks) return;  // wave-uniform, no barriers
-  const int xt = task % XT, zt = task / XT;
-  const int64_t x = (int64_t)xt * SEG - N + (int64_t)lane * N;
-  const int64_t zs = g.lz_begin + (int64_t)zt * zc;
-  const int64_t ze = min(g.lz_end, zs + (int64_t)zc);
-  const bool xin = x >= 0 && x < g.pitch;
-  const bool own = lane >= 1 && lane <= 62 && xin;
-  const bool frame = x == 0 || (x >= 0 && x + N > g.nx - 1);
-  const int64_t plane = g.plane;
-  auto ld = [&](int64_t lz) -> U2 {
-    if (xin && lz >= 0 && lz < g.lz_max) {
-      dcheck(g, in, in + lz * plane + x, N);
-      return ld_u2(in + lz * plane + x);
-    }
-    return U2{0, 0};
-  };
-  // one generation of a row from S = its column sums (north + centre + south) and its centre C
-  auto gen = [&](const U2& S, const U2& C, int64_t gz, bool inner_only) -> U2 {
-    const bool bnd = inner_only ? (gz == 0 || gz == g.gnz - 1) : (gz <= 0 || gz >= g.gnz - 1);
-    if (bnd) return C;
-    const uint64_t sl = (uint32_t)lane_up1((int)(S.hi >> 56));
-    const uint64_t sr = (uint32_t)lane_down1((int)(S.lo & 0xFF));
-    const U2 L{(S.lo << 8) | sl, (S.hi << 8) | (S.lo >> 56)};
-    const U2 R{(S.lo >> 8) | (S.hi << 56), (S.hi >> 8) | (sr << 56)};
-    const U2 T{L.lo + S.lo + R.lo, L.hi + S.hi + R.hi};
-    U2 o{life_next(T.lo, C.lo), life_next(T.hi, C.hi)};
-    if (frame) {
-#pragma unroll
-      for (int e = 0; e < N; ++e) {
-        const int64_t xe = x + e;
-        if (xe == 0 || xe >= g.nx - 1) {
-          const uint64_t m = 0xFFull << (8 * (e & 7));
-          if (e < 8)
-            o.lo = (o.lo & ~m) | (C.lo & m);
-          else
-            o.hi = (o.hi & ~m) | (C.hi & m);
-        }
-      }
-    }
-    return o;
-  };
-  // streaming levels: level l (1..K) keeps V = the sum of the last two rows of its input u_{l-1}
-  // and C = the last row; when input row r arrives, S = V + r finishes u_l(r-1) = gen(S, C), then
-  // V = C + r and C = r. No row ring to rotate (the sums are byte-exact, so the order is free).
-  U2 V[K], Cl[K];
-#pragma unroll
-  for (int l = 0; l < K; ++l) V[l] = Cl[l] = U2{0, 0};
-  {
-    const U2 a = ld(zs - K - 1), b = ld(zs - K);
-    V[0] = U2{a.lo + b.lo, a.hi + b.hi};
-    Cl[0] = b;
-  }
-  U2 nx = ld(zs - K + 1);
-  double acc = 0.0;
-  for (int64_t q = zs - K + 1; q <= ze - 1 + K; ++q) {
-    U2 X = nx;  // u0(q)
-    nx = ld(q + 1);
-    const int64_t lz = q - K;
-#pragma unroll
-    for (int l = 1; l <= K; ++l) {
-      const U2 S{V[l - 1].lo + X.lo, V[l - 1].hi + X.hi};
-      const U2 C = Cl[l - 1];
-      V[l - 1] = U2{C.lo + X.lo, C.hi + X.hi};
-      Cl[l - 1] = X;
-      if (l < K) {
-        X = gen(S, C, q - l + g.gz_off, false);  // u_l(q - l)
-      } else if (lz >= zs) {
-        const U2 o = gen(S, C, lz + g.gz_off, true);
-        if (own) {
-          uint4 qv;
-          qv.x = (uint32_t)o.lo;
-          qv.y = (uint32_t)(o.lo >> 32);
-          qv.z = (uint32_t)o.hi;
-          qv.w = (uint32_t)(o.hi >> 32);
-          dcheck(g, (const uint8_t*)out, out + lz * plane + x, N);
-          *(uint4*)(out + lz * plane + x) = qv;
-          if (RES) {
-            const uint64_t dlo = o.lo ^ C.lo, dhi = o.hi ^ C.hi;
-            int cnt = 0;
-            for (int e = 0; e < N; ++e)
-              if (x + e < g.nx) cnt += (int)(((e < 8 ? dlo : dhi) >> (8 * (e & 7))) & 1);
-            acc += (double)cnt;
-          }
-        }
-      }
-    }
-  }
-  if (RES) wave_atomic_add(resid, acc);
-}
-
-template <int K>
-static void launch_life_tbk_k(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, hipStream_t s) {
-  const int64_t planes = g.lz_end - g.lz_begin;
-  if (planes <= 0) return;
-  constexpr int SEG = 62 * 16;
-  const int XT = (int)((g.nx + SEG - 1) / SEG);
-  int zc = knobs().zc;
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 8192);
-  const int ZT = (int)((planes + zc - 1) / zc);
-  const int ntasks = XT * ZT;
-  const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
-  if (resid)
-    hipLaunchKernelGGL((life_tbk<K, true>), grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
-  else
-    hipLaunchKernelGGL((life_tbk<K, false>), grd, blk, 0, s, in, out, g, zc, XT, ntasks, resid);
-}
+// (Round 4's SWAR K-generation kernel, life_tbk: 7,656-7,960 GCells/s at 32768^2 against life_bits'
+// 21,268-22,430, profiles/r02_life.txt, reachable only through a switch, was removed in round 5.)
 
 // ---- K generations per sweep, bit-sliced (life_bits) ---------------------------------------------
 //
@@ -437,8 +318,8 @@ static void launch_life_tbk_k(const Geo& g, const uint8_t* in, uint8_t* out, dou
 //   neighbours of row r: N = s(r-1) + s(r+1) + c(r) (a 4-bit ripple of full adders, 10 ops)
 //   B3/S23: alive' = (N | alive) == 3  ->  n1 & (n0 | alive) & ~(n2 | n3)
 // Each level keeps the 3-sums of its last two input rows, the 2-sum and the cells of the last row.
-// Waves overlap by one lane per side like life_tbk (a generation corrupts one more cell of the
-// halo lanes from the outside in: K <= 32). Held cells (x = 0, x >= nx - 1, the first / last row)
+// Waves overlap by one lane per side (a generation corrupts one more cell of the halo lanes from the
+// outside in: K <= 32). Held cells (x = 0, x >= nx - 1, the first / last row)
 // keep their state through a per-lane bit mask. Bitwise equal to K single generations.
 __device__ __forceinline__ uint32_t life_pack4(uint32_t d) {  // bytes 0/1 -> bits 0..3
   return __builtin_amdgcn_ubfe(d * 0x01020408u, 24, 4);
@@ -566,8 +447,7 @@ static void launch_life_bits_k(const Geo& g, const uint8_t* in, uint8_t* out, do
   if (planes <= 0) return;
   constexpr int SEG = 62 * 32;
   const int XT = (int)((g.nx + SEG - 1) / SEG);
-  int zc = knobs().zc;
-  if (zc <= 0) zc = pick_zc(planes, XT, 256, 4 * 2048);
+  const int zc = pick_zc(planes, XT, 256, 4 * 2048);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
   const dim3 grd((unsigned)((ntasks + 3) / 4)), blk(256);
@@ -578,26 +458,15 @@ static void launch_life_bits_k(const Geo& g, const uint8_t* in, uint8_t* out, do
 }
 
 void launch_life_tbk(const Geo& g, const uint8_t* in, uint8_t* out, int steps, double* resid, hipStream_t s) {
-  // the bit-sliced kernel by default (MDFX_LIFE_BITS=0: the SWAR one, depths up to 8)
-  if (knobs().life_bits || steps > 8) {
-    switch (steps) {
-      case 2: launch_life_bits_k<2>(g, in, out, resid, s); return;
-      case 3: launch_life_bits_k<3>(g, in, out, resid, s); return;
-      case 4: launch_life_bits_k<4>(g, in, out, resid, s); return;
-      case 6: launch_life_bits_k<6>(g, in, out, resid, s); return;
-      case 8: launch_life_bits_k<8>(g, in, out, resid, s); return;
-      case 12: launch_life_bits_k<12>(g, in, out, resid, s); return;
-      case 16: launch_life_bits_k<16>(g, in, out, resid, s); return;
-      default: return;
-    }
-  }
+  // K > 2 generations per sweep, bit-sliced (two generations: life_tb2)
   switch (steps) {
-    case 2: launch_life_tbk_k<2>(g, in, out, resid, s); break;
-    case 3: launch_life_tbk_k<3>(g, in, out, resid, s); break;
-    case 4: launch_life_tbk_k<4>(g, in, out, resid, s); break;
-    case 6: launch_life_tbk_k<6>(g, in, out, resid, s); break;
-    case 8: launch_life_tbk_k<8>(g, in, out, resid, s); break;
-    default: break;
+    case 3: launch_life_bits_k<3>(g, in, out, resid, s); return;
+    case 4: launch_life_bits_k<4>(g, in, out, resid, s); return;
+    case 6: launch_life_bits_k<6>(g, in, out, resid, s); return;
+    case 8: launch_life_bits_k<8>(g, in, out, resid, s); return;
+    case 12: launch_life_bits_k<12>(g, in, out, resid, s); return;
+    case 16: launch_life_bits_k<16>(g, in, out, resid, s); return;
+    default: MDFX_FAIL(format("life: no %d-generation sweep (3, 4, 6, 8, 12, 16)", steps));
   }
 }
 

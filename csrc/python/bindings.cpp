@@ -206,7 +206,7 @@ class PySolver {
            int nranks, std::vector<int> local_ranks, std::vector<int> devices,
            const std::string& transport, py::bytes unique_id, py::object callbacks, bool overlap,
            bool sync_debug, int residual_every, bool graph, double timeout_s, double r, double c0,
-           double c1, double c2, double c3, int temporal, bool ref_precision, int pencil_py) {
+           double c1, double c2, double c3, int temporal, bool ref_precision, int pencil_py, bool share_gpu) {
     const StencilSpec spec = make_spec(kind, dtype, r, c0, c1, c2, c3, ref_precision);
     if (devices.size() == 1 && local_ranks.size() > 1) devices.assign(local_ranks.size(), devices[0]);
     if (devices.size() != local_ranks.size())
@@ -227,7 +227,7 @@ class PySolver {
     } else if (transport == "ipc" || transport == "ipc_sdma") {
       CallbackFns f = callback_fns(callbacks);
       if (!f.allgather) throw Error("ipc transport needs an allgather callback");
-      tr = make_ipc_transport(std::move(f), transport == "ipc_sdma" ? 1 : -1);
+      tr = make_ipc_transport(std::move(f), transport == "ipc_sdma" ? 1 : -1, share_gpu);
     } else if (transport == "proxy" || transport == "proxy_sdma") {
       tr = make_proxy_transport(transport == "proxy_sdma" ? 1 : -1);
     } else {
@@ -282,7 +282,17 @@ PYBIND11_MODULE(_mdfx, m) {
         return ipc_peer_problem(info(mine), info(peer), expect_rank, peer_access);
       },
       "host-side check of an ipc neighbour record: '' if usable, else the reason");
+  m.def("ipc_shared_gpu_problem", &ipc_shared_gpu_problem, py::arg("pid_pci"), py::arg("share_gpu") = false,
+        "host-side check of every rank's (pid, GPU PCI bus id): '' unless engine processes share a GPU");
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("rccl_traits", []() {
+    py::dict d;
+    d["stream_ordered"] = rccl_stream_ordered();
+    d["graph_capturable"] = rccl_graph_capturable();
+    return d;
+  }, "what the rccl transport reports to the engine (it is never constructed for this)");
+  m.def("step_schedule", &step_schedule, py::arg("overlap"), py::arg("local_slabs"), py::arg("stream_ordered"),
+        py::arg("fold"), "the engine's per-step schedule for a layout and transport (Solver::schedule)");
   m.def("set_kernel_variant", [](const std::string& v) { hip_set_kernel_variant(v.c_str()); });
   m.def("reload_knobs", &hip_reload_knobs, "re-read the MDFX_* kernel tuning knobs from the environment");
   m.def("poison_lds", &hip_poison_lds, "fill every CU's LDS with NaN (tests for stale-LDS reads)");
@@ -290,7 +300,7 @@ PYBIND11_MODULE(_mdfx, m) {
         "version of the HIP runtime the process loaded (PyTorch's bundled one under torch), 0 if none");
   m.def("kernel_variant", []() { return std::string(hip_kernel_variant()); });
   m.def("face_copy_mode", []() { return std::string(face_copy_mode() == 1 ? "sdma" : "blit"); },
-        "engine of the ipc / proxy halo face copies (MDFX_XCOPY)");
+        "default engine of the ipc / proxy halo face copies (blit; ipc_sdma / proxy_sdma pick SDMA)");
   m.def("ipc_direct_ok", [](size_t bytes) { return ipc_direct_ok(bytes); },
         "whether the ipc transport pulls straight from field buffers of this size (MDFX_IPC_DIRECT)");
   m.def("layout", [](int64_t nx, int64_t ny, int64_t nz, int64_t z0, int64_t z1, int halo,
@@ -383,14 +393,15 @@ PYBIND11_MODULE(_mdfx, m) {
   py::class_<PySolver>(m, "Solver")
       .def(py::init<const std::string&, const std::string&, int64_t, int64_t, int64_t, int,
                     std::vector<int>, std::vector<int>, const std::string&, py::bytes, py::object,
-                    bool, bool, int, bool, double, double, double, double, double, double, int, bool, int>(),
+                    bool, bool, int, bool, double, double, double, double, double, double, int, bool, int, bool>(),
            py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ny"), py::arg("nz"),
            py::arg("nranks"), py::arg("local_ranks"), py::arg("devices"), py::arg("transport"),
            py::arg("unique_id") = py::bytes(""), py::arg("callbacks") = py::none(),
            py::arg("overlap") = true, py::arg("sync_debug") = false, py::arg("residual_every") = 0,
            py::arg("graph") = false, py::arg("timeout_s") = 0.0, py::arg("r") = -1.0,
            py::arg("c0") = 0.25, py::arg("c1") = 0.05, py::arg("c2") = 0.025,
-           py::arg("c3") = 3.0 / 160.0, py::arg("temporal") = 1, py::arg("ref_precision") = false, py::arg("py") = 1)
+           py::arg("c3") = 3.0 / 160.0, py::arg("temporal") = 1, py::arg("ref_precision") = false, py::arg("py") = 1,
+           py::arg("share_gpu") = false)
       .def("close", &PySolver::close)
       .def("phase_times",
            [](PySolver& p) {
@@ -477,6 +488,8 @@ PYBIND11_MODULE(_mdfx, m) {
            py::call_guard<py::gil_scoped_release>(),
            "launch every kernel instance run(steps) would use once, into the scratch buffer (state unchanged)")
       .def_property_readonly("graph_eligible", [](PySolver& p) { return p.chk().graph_eligible(); })
+      .def_property_readonly("schedule", [](PySolver& p) { return p.chk().schedule(); },
+                             "the per-step schedule eager steps run (step_schedule)")
       .def_property_readonly("current_index", [](PySolver& p) { return p.chk().current_index(); })
       .def_property_readonly("transport_name", [](PySolver& p) { return std::string(p.chk().transport().name()); })
       .def("local_rank", [](PySolver& p, int i) { return p.chk().local_rank(i); })

@@ -34,9 +34,14 @@ def _parser() -> argparse.ArgumentParser:
     p.add_argument("--device", default="auto", help="auto | hip | cpu")
     p.add_argument("--ranks", type=int, default=None, help="P virtual slabs in this process")
     p.add_argument("--py", type=int, default=1, help="(z, y) pencils: ranks along y (3D stencils)")
-    p.add_argument("--transport", default="auto", help="auto | rccl | torch | staged | loopback | host")
+    p.add_argument("--transport", default="auto",
+                   help="auto | rccl | ipc | ipc_sdma | torch | staged (one process per rank) | loopback | host "
+                        "(one process); ipc pulls faces with blit kernels, ipc_sdma with the SDMA engines")
     p.add_argument("--residual-every", type=int, default=0)
-    p.add_argument("--temporal", type=int, default=1, help="time steps fused per sweep (2: 3D 7-pt)")
+    p.add_argument("--temporal", type=int, default=0,
+                   help="time steps fused per sweep: 0 = auto (as mdfx and bench.py: 4 for the 3D 7-point on "
+                        "the GPU, 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 for the 2D MDF, 12 "
+                        "for Life), 1 = one step per sweep")
     p.add_argument("--graph", action="store_true")
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--sync-debug", action="store_true")

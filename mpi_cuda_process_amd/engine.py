@@ -68,14 +68,17 @@ class Simulation:
     planes + exchange; ``sync_debug`` serialise every phase (race screen); ``residual_every`` k:
     global L2 norm of the update every k steps (NaN/Inf guard); ``graph`` replay two-sweep cycles
     as hipGraphs; ``timeout_s`` watchdog; ``temporal`` fused steps per sweep (1 = none, 0 = auto,
-    see :func:`auto_temporal`; halo planes = temporal).
+    see :func:`auto_temporal`; halo planes = temporal); ``share_gpu`` let several engine processes
+    use one GPU with the ipc transport (tests only: its device spin waits assume one process per
+    GPU, native ipc_shared_gpu_problem).
     """
 
     def __init__(self, problem: Problem, *, device: str = "auto", ranks: Optional[int] = None,
                  devices: Optional[Sequence[int]] = None, transport: str = "auto",
                  distributed: Optional[bool] = None, overlap: bool = True, sync_debug: bool = False,
                  residual_every: int = 0, graph: bool = False, timeout_s: float = 0.0,
-                 temporal: int = 1, group=None, proxy_rank: Optional[int] = None, py: int = 1):
+                 temporal: int = 1, group=None, proxy_rank: Optional[int] = None, py: int = 1,
+                 share_gpu: bool = False):
         self.problem = problem
         if device == "auto":
             device = "hip" if hip_available() else "cpu"
@@ -168,7 +171,7 @@ class Simulation:
         self._s = native().Solver(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                   nranks, local_ranks, dev_list, overlap=overlap,
                                   sync_debug=sync_debug, residual_every=residual_every, graph=graph,
-                                  timeout_s=timeout_s, temporal=temporal, py=int(py),
+                                  timeout_s=timeout_s, temporal=temporal, py=int(py), share_gpu=bool(share_gpu),
                                   **problem.coef_kwargs(), **args)
         if self._torch_transport is not None:
             self._torch_transport.solver = self._s
@@ -258,6 +261,12 @@ class Simulation:
         return bool(self._s.graph_eligible)
 
     @property
+    def schedule(self) -> str:
+        """The per-step schedule eager steps run: 'serialised', 'two-stream', 'boundary-on-compute'
+        or 'folded' (native step_schedule; docs/DESIGN.md §3)."""
+        return str(self._s.schedule)
+
+    @property
     def graph_replays(self) -> int:
         """2-sweep cycles replayed from a captured hipGraph so far (0: every step ran eagerly, e.g.
         graph replay off or not capturable under this HIP runtime)."""
@@ -265,7 +274,11 @@ class Simulation:
 
     @property
     def options(self) -> dict:
-        return dict(self._s.options())
+        from . import GRAPH_QUEUES
+
+        d = dict(self._s.options())
+        d["graph_queues"] = GRAPH_QUEUES  # whether hipGraph replay runs on one hardware queue (__init__.py)
+        return d
 
     @property
     def temporal(self) -> int:

@@ -33,7 +33,7 @@ def child(a):
     for i, (t, py) in enumerate(combos):
         try:
             sim = m.Simulation(prob, device="hip", distributed=True, transport=t, py=py, temporal=4, devices=[0],
-                               timeout_s=60.0)
+                               timeout_s=60.0, share_gpu=True)
             sim.init()
             sim.run(8)
             sim.synchronize()

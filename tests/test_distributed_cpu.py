@@ -176,6 +176,12 @@ def test_bench_self_launches_8_ranks_cpu(mdfx):
     assert sorted({r["py"] for r in cfg["gate"]["runs"]}) == [1, 2]
     assert sorted({t["py"] for t in cfg["trials"]}) == [1, 2]
     assert cfg["py"] in (1, 2) and cfg["parallelism"].startswith("slab-z8" if cfg["py"] == 1 else "pencil-z4y2")
+    # the timed run itself (not only the gate) was checked on every rank against a full-grid run,
+    # and timed three times (the median reported)
+    ver = cfg["verified"]
+    assert ver["passed"] and ver["ranks"] == 8 and ver["max_abs_diff"] == 0.0 and ver["steps"] == [1, 4, 4, 4]
+    assert len(cfg["repeats_ms_per_step"]) == 3 and rec["ms_per_step"] == sorted(cfg["repeats_ms_per_step"])[1]
+    assert cfg["schedule"] in cfg["parallelism"]
 
 
 def test_bench_json_reports_effective_graph_mode(mdfx):
@@ -205,6 +211,34 @@ def test_bench_gate_catches_a_broken_rank(mdfx):
     assert rc != 0, out
     assert "gate FAILED" in err or "gate" in err
     assert not [l for l in out.splitlines() if l.startswith("{")]
+
+
+def test_bench_verification_catches_a_fault_the_gate_missed(mdfx):
+    """MDFX_FAULT=ghost@1:timed corrupts one ghost cell of rank 1 only after the timed run's warm-up:
+    the gate passes, the verification of the timed run against the full-grid run fails on the ranks
+    the fault reaches, and the bench exits non-zero without printing a number."""
+    rc, out, err = _bench(["--device", "cpu", "--gpus", "2", "--n", "32", "--steps", "4", "--warmup", "1"],
+                          env_extra={"MDFX_FAULT": "ghost@1:timed"})
+    assert rc != 0, out
+    assert "injected a ghost-plane fault" in err
+    assert "verification FAILED" in err and "the gate passed" in err
+    assert not [l for l in out.splitlines() if l.startswith("{")]
+
+
+def test_rccl_gets_the_folded_single_stream_schedule(mdfx):
+    """RCCL's grouped send / recv is stream work on the halo stream under every HIP runtime, so one
+    slab per process gets the folded boundary-on-compute schedule with it, eager where the runtime
+    cannot capture it (it used to fall back to the two-stream schedule under HIP 7.0)."""
+    nat = mdfx.native()
+    tr = nat.rccl_traits()
+    assert tr["stream_ordered"] is True
+    assert tr["graph_capturable"] == (nat.hip_runtime_version() >= 70200000)
+    assert nat.step_schedule(True, 1, tr["stream_ordered"], True) == "folded"
+    assert nat.step_schedule(True, 1, tr["stream_ordered"], False) == "boundary-on-compute"
+    # several slabs in one process, or a host-side exchange (torch / staged callbacks): two streams
+    assert nat.step_schedule(True, 2, tr["stream_ordered"], False) == "two-stream"
+    assert nat.step_schedule(True, 1, False, False) == "two-stream"
+    assert nat.step_schedule(False, 1, True, True) == "serialised"
 
 
 CONTROL = r"""
@@ -275,6 +309,23 @@ def test_ipc_peer_record_checks_cpu(mdfx):
     assert nat.ipc_peer_problem(me, other, 1, True) == ""
     why = nat.ipc_peer_problem(me, other, 1, False)
     assert "cannot access device 3" in why and "rccl" in why
+
+
+def test_ipc_refuses_engine_processes_sharing_a_gpu_cpu(mdfx):
+    """Two engine processes on one GPU are refused unless share_gpu (test-only): the ipc exchange's
+    device spin waits need the hardware scheduler to run every producer queue.
+    Every rank checks the same allgathered records, so all refuse together."""
+    nat = mdfx.native()
+    pci = ["0000:05:00.0", "0000:15:00.0", "0000:65:00.0", "0000:75:00.0"]
+    node = [(1000 + r, pci[r]) for r in range(4)]  # one process per GPU: fine
+    assert nat.ipc_shared_gpu_problem(node) == ""
+    shared = node + [(1004, pci[1])]
+    why = nat.ipc_shared_gpu_problem(shared)
+    assert "ranks 1 and 4" in why and pci[1] in why and "share_gpu" in why
+    assert nat.ipc_shared_gpu_problem(shared, True) == ""
+    # no PCI id (an old runtime): nothing to compare, no refusal; one process on one GPU: fine
+    assert nat.ipc_shared_gpu_problem([(1, ""), (2, "")]) == ""
+    assert nat.ipc_shared_gpu_problem([(7, pci[0]), (7, pci[0])]) == ""
 
 
 def test_ipc_transport_needs_hip(mdfx):

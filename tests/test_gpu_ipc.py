@@ -32,7 +32,8 @@ env = init_distributed("gloo")
 torch.cuda.set_device(0)
 prob = %(prob)s
 with m.Simulation(prob, device="hip", distributed=True, transport=%(transport)r, residual_every=4,
-                  temporal=%(temporal)d, devices=[0], graph=%(graph)s, timeout_s=60.0, py=%(py)d) as sim:
+                  temporal=%(temporal)d, devices=[0], graph=%(graph)s, timeout_s=60.0, py=%(py)d,
+                  share_gpu=True) as sim:
     assert sim.transport == %(transport)r, sim.transport
     sim.init()
     sim.run(%(steps)d)
@@ -241,7 +242,7 @@ def test_ipc_slabs_larger_than_2gib(hip):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu", "--transport",
                         "ipc", "--n", "1024", "--steps", "4", "--warmup", "2", "--timeout", "30"],
-                       env=env, capture_output=True, timeout=110, cwd=ROOT)
+                       env=env, capture_output=True, timeout=170, cwd=ROOT)
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     rec = json.loads([l for l in p.stdout.decode().splitlines() if l.startswith("{")][0])
     assert rec["n_gpus"] == 2 and rec["config"]["gate"]["passed"] and rec["config"]["transport"] == "ipc"
@@ -254,12 +255,29 @@ def test_ipc_direct_protocol_at_the_headline_size(hip):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--share-gpu", "--transport",
                         "ipc", "--n", "1024", "--steps", "8", "--warmup", "4", "--timeout", "30"],
-                       env=env, capture_output=True, timeout=110, cwd=ROOT)
+                       env=env, capture_output=True, timeout=170, cwd=ROOT)
     assert p.returncode == 0, p.stderr.decode()[-3000:]
     rec = json.loads([l for l in p.stdout.decode().splitlines() if l.startswith("{")][0])
     cfg = rec["config"]
     assert rec["n_gpus"] == 4 and cfg["gate"]["passed"] and cfg["transport"] == "ipc"
     assert cfg["ipc_protocol"] == "direct" and cfg["face_copy"] == "blit"
+    # the timed run itself was checked on all four ranks against a full-grid naive run
+    assert cfg["verified"]["passed"] and cfg["verified"]["ranks"] == 4 and cfg["verified"]["max_abs_diff"] == 0.0
+
+
+def test_ipc_refuses_two_engine_processes_on_one_gpu(hip, tmp_path):
+    """Without share_gpu, two ipc engine processes on one GPU are refused at setup with a message
+    (their device spin waits assume one process per GPU), on both ranks, quickly."""
+    out = str(tmp_path / "g.npy")
+    code = WORKER.replace(",\n                  share_gpu=True)", ")") % dict(
+        py=1, root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=4,
+        transport="ipc")
+    assert "share_gpu" not in code
+    t0 = time.time()
+    procs, outs = _spawn(2, lambda r: [sys.executable, "-c", code], timeout=120, expect_ok=False)
+    assert all(p.returncode != 0 for p in procs), outs
+    assert all("two engine processes on one GPU" in o for o in outs), outs
+    assert time.time() - t0 < 90
 
 
 def test_ipc_engines_rebuilt_in_turn_by_eight_processes(hip):

@@ -77,12 +77,12 @@ BOX27 = [models.box27(nx=1024, ny=11, nz=9), models.box27(nx=512, ny=21, nz=15),
 
 
 @pytest.mark.parametrize("prob", BOX27, ids=lambda p: p.describe().replace(" ", "_"))
-@pytest.mark.parametrize("kernel", ["-1", "1", "2", "4"])
-def test_box27_fused_kernels_bitwise(hip, prob, kernel, knob):
-    """Both fused 27-point kernels (MDFX_B27_TBK=-1: box27_tb2, fp32 in the natural layout with
-    the 2-plane unroll (box27_tb2n); 1 / 2 / 4: box27_tbk with that many rows per tile) == two
-    naive single steps, bitwise, with the residual of step 2."""
-    knob("MDFX_B27_TBK", kernel)
+@pytest.mark.parametrize("tbry", ["0", "1"])
+def test_box27_fused_kernels_bitwise(hip, prob, tbry, knob):
+    """Both fused 27-point kernels (fp32: box27_tb2 in the natural layout with the 2-plane unroll,
+    2 rows per tile or MDFX_TB_RY=1; fp64: box27_tbk with 4 rows per tile, 1 on short columns) ==
+    two naive single steps, bitwise, with the residual of step 2."""
+    knob("MDFX_TB_RY", tbry)
     lay = FieldLayout.make(prob, halo=2)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
@@ -196,12 +196,11 @@ DEEP = [models.mdf2d(h=45, w=1000), models.mdf2d(h=33, w=300, dtype="f64"), mode
 
 @pytest.mark.parametrize("prob", DEEP, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k", [2, 3, 4, 6, 8])
-def test_deep_fused_steps_bitwise(hip, prob, k, knob):
-    """K fused steps per sweep (overlapping wave segments) == K naive single steps, bitwise; K = 2
-    also through the overlapped-segment kernels (MDFX_J5_TBK / MDFX_LIFE_TBK)."""
-    for force in ((0, 1) if k == 2 else (0,)):
-        knob("MDFX_J5_TBK", force)
-        knob("MDFX_LIFE_TBK", force)
+def test_deep_fused_steps_bitwise(hip, prob, k):
+    """K fused steps per sweep (K = 2: jacobi5_tb2 / life_tb2, or jacobi5_tbk REF where the mixed
+    update can change a bit; deeper: the overlapping-segment kernels jacobi5_tbk / life_bits) == K
+    naive single steps, bitwise."""
+    for force in (0,):
         lay = FieldLayout.make(prob, halo=k)
         src = alloc_field(lay, "cuda")
         init_field(prob, lay, src)
@@ -259,12 +258,10 @@ LIFE_DEEP = [models.life2d(h=50, w=3000), models.life2d(h=19, w=100), models.lif
 
 @pytest.mark.parametrize("prob", LIFE_DEEP, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k", [2, 3, 4, 6, 8, 12, 16])
-def test_life_kernels_bitwise(hip, prob, k, knob):
-    """K Life generations per sweep through the bit-sliced kernel (life_bits, up to 16) and the SWAR
-    one (life_tbk, up to 8) == K naive generations, bitwise, with the change count of the last."""
-    knob("MDFX_LIFE_TBK", 1)
-    for bits in ((1, 0) if k <= 8 else (1,)):
-        knob("MDFX_LIFE_BITS", bits)
+def test_life_kernels_bitwise(hip, prob, k):
+    """K Life generations per sweep (two: life_tb2; deeper: the bit-sliced life_bits, up to 16) == K
+    naive generations, bitwise, with the change count of the last."""
+    for bits in (1,):
         lay = FieldLayout.make(prob, halo=k)
         src = alloc_field(lay, "cuda")
         init_field(prob, lay, src)
@@ -308,12 +305,11 @@ DEEP3D = [models.heat3d(nx=1024, ny=37, nz=23), models.heat3d(nx=700, ny=19, nz=
 
 @pytest.mark.parametrize("prob", DEEP3D, ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k", [2, 3, 4])
-@pytest.mark.parametrize("ry", ["1", "2", "4"])
-def test_heat7_deep_fused_bitwise(hip, prob, k, ry, knob):
-    """heat7_tbk's K fused 3D steps per sweep == K naive single steps, bitwise, with the residual of
-    step K (K >= 3 through heat7_tbk only with MDFX_H7_WTK=-1; the default is heat7_wtk)."""
-    knob("MDFX_TBK_RY", ry)
-    knob("MDFX_H7_WTK", "-1")
+def test_heat7_deep_fused_bitwise(hip, prob, k):
+    """The 3D 7-point's K fused steps per sweep (K = 2: heat7_tbk, 4 rows per tile, 1 on short
+    columns; K = 3 / 4: heat7_wxk / heat7_wtk) == K naive single steps, bitwise, with the residual
+    of step K."""
+    ry = "auto"
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
     init_field(prob, lay, src)
