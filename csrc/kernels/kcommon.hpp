@@ -99,6 +99,23 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
+// The same with the non-temporal policy (aux 2: nt on gfx950), for rows read once per sweep.
+__device__ __forceinline__ void glds16_nt(const void* g, void* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 2);
+}
+// An L2 prefetch: one dword per lane from `g` into 256 B of LDS at `lds` (wave-uniform), by an LDS
+// DMA the compiler does not see, so it neither drains it before later LDS reads nor counts it in its
+// own vmcnt waits: the caller accounts for it in its wait_vm_le counts.
+// M0 is the compiler's: saved and restored around the DMA.
+__device__ __forceinline__ void l2_touch(const void* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+
 // Raw waits: s_waitcnt encodings for gfx9 (vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]).
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 // vmcnt(n) for a wave-uniform n in 0..15 (an immediate per case): wait until at most the wave's n

@@ -46,6 +46,7 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 
+// EXP (A/B only): bit 0 non-temporal window DMAs
 template <class T, int RY, int RE, int K, int WB, bool RES, int EXP = 0>
 __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
                                                      T c2, T c3, int zc, int XT, int YT, int ntasks,
@@ -111,7 +112,8 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
         const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
         const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xcb);
         dcheck(g, in, a, N);
-        glds16(a, &win[buf][k][0]);
+        if constexpr ((EXP & 1) != 0) glds16_nt(a, &win[buf][k][0]);
+        else glds16(a, &win[buf][k][0]);
       }
     }
   };
@@ -156,19 +158,18 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
       if (q < qdma) issue(q + 1, P ^ 1);
       const int lzo = q - LAG;  // level K's output plane
       const bool valid = lzo >= zs && lzo < ze;
-      // EXP 1: the step's LDS rows (level 1's u0 window rows, every upper level's two seam rows) are
-      // read up front, so the reads overlap each other instead of each waiting out a round trip
-      constexpr int NU = EXP ? SH::n(1) + 2 : 1;
+      // the step's LDS rows (level 1's u0 window rows, every upper level's two seam rows) are read up
+      // front, so the reads overlap each other instead of each waiting out a round trip right before
+      // its use (round 5: 512^3 fp64 678 vs 640 GCells/s, fp32 1056 vs 971, profiles/r05_session_a/)
+      constexpr int NU = SH::n(1) + 2;
       Row U[NU], SU[K], SD[K];
-      if constexpr (EXP != 0) {
 #pragma unroll
-        for (int k = 0; k < NU; ++k) U[k] = RO::fromv(V(wrow[P * WIN_BUF + (SH::lo(1) - 1 + k + K) * 64]));
+      for (int k = 0; k < NU; ++k) U[k] = RO::fromv(V(wrow[P * WIN_BUF + (SH::lo(1) - 1 + k + K) * 64]));
 #pragma unroll
-        for (int j = 1; j < K; ++j) {
-          SU[j] = SD[j] = RO::zero();
-          if (SH::lo(j + 1) - 1 < SH::lo(j)) SU[j] = RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
-          if (SH::hi(j + 1) >= SH::hi(j)) SD[j] = RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
-        }
+      for (int j = 1; j < K; ++j) {
+        SU[j] = SD[j] = RO::zero();
+        if (SH::lo(j + 1) - 1 < SH::lo(j)) SU[j] = RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
+        if (SH::hi(j + 1) >= SH::hi(j)) SD[j] = RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
       }
       // levels top-down: level l reads its inputs (the level below's plane from the previous step)
       // before that level overwrites its other stored plane
@@ -185,19 +186,11 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
         }
         // input rows of level l-1 at plane p: rows lo(l)-1 .. hi(l)
         auto vin = [&](int i) -> Row {
-          if constexpr (EXP != 0) {
-            if (l == 1) return U[i - (SH::lo(1) - 1)];
-            const int j = l - 1;
-            if (i < SH::lo(j)) return SU[j];
-            if (i >= SH::hi(j)) return SD[j];
-            return H[j - 1][P ^ 1][i - SH::lo(j)];
-          } else {
-            if (l == 1) return RO::fromv(V(wrow[P * WIN_BUF + (i + K) * 64]));
-            const int j = l - 1;
-            if (i < SH::lo(j)) return RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
-            if (i >= SH::hi(j)) return RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
-            return H[j - 1][P ^ 1][i - SH::lo(j)];
-          }
+          if (l == 1) return U[i - (SH::lo(1) - 1)];
+          const int j = l - 1;
+          if (i < SH::lo(j)) return SU[j];
+          if (i >= SH::hi(j)) return SD[j];
+          return H[j - 1][P ^ 1][i - SH::lo(j)];
         };
         Row vm = vin(SH::lo(l) - 1), vc = vin(SH::lo(l));
         Row hm = hs(vm), hc = hs(vc);

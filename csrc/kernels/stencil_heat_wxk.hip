@@ -86,6 +86,10 @@ __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles,
 // SIG: the folded-boundary copy (Geo::sig): the blocks of the chunks starting at lz_begin publish their
 // output planes [lz_begin, sig_z) and signal, so the halo exchange of the lower face overlaps the
 // rest of the same sweep (no separate boundary launch for that face).
+// EXP (A/B only): bit 0 non-temporal window DMAs, bit 1 an L2 prefetch of plane q + 2 by one 4-byte
+// LDS DMA per window row line (outside the compiler's view), bit 2 the z-test-free middle of the
+// march, bit 3 the window DMA two planes ahead in the same two buffers (a second barrier per plane
+// step, right after the step's window reads, frees the buffer just read)
 template <class T, int RY, int RE, int K, int WB, bool RES, bool PEN = false, bool SIG = false, int EXP = 0>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
@@ -109,6 +113,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   __shared__ V win[2][RB][64];
   // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
   __shared__ V seam[2][K - 1][WB - 1][2][64];
+  __shared__ uint32_t pfd[(EXP & 2) ? WB : 1][64];  // (EXP bit 1) the prefetch DMAs' landing slots
   // (A second plane in flight does not help this sweep: a third window buffer with one seam table
   // and a second barrier lost in round 3 (profiles/r03_session_r/), and an L2 prefetch of plane
   // q + 2 by 4-byte LDS DMAs lost 15-24 % in round 4 (profiles/r04_session_b/).)
@@ -161,17 +166,47 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       if (k < RB) {
         const int y = yb - K + k;
         const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-        const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xcb);
+        // the row's address is wave-uniform: pinned in SGPRs, so the DMA takes the scalar-base +
+        // 32-bit lane-offset form instead of a 64-bit VGPR address per row held across the loop
+        uint64_t rb = (uint64_t)(uintptr_t)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
+        asm volatile("" : "+s"(rb));
+        const T* a = (const T*)((const char*)(uintptr_t)rb + xcb);
         dcheck(g, in, a, N);
-        glds16(a, &win[buf][k][0]);
+        if constexpr ((EXP & 1) != 0) glds16_nt(a, &win[buf][k][0]);
+        else glds16(a, &win[buf][k][0]);
       }
     }
+  };
+  // (EXP bit 1) plane lz -> L2: waves 0 .. ceil(RB / 8) - 1 each touch every 128-B line of 8 window
+  // rows with one dword per lane (lane l: row 8w + l / 8, line l % 8); npf: prefetches issued since
+  // the wave's newest window DMA (they stay in flight across the next plane's wait)
+  constexpr bool PFW = (EXP & 2) != 0;
+  const bool pfw = PFW && 8 * w < RB;
+  uint32_t pfo = 0;
+  if (PFW) {
+    const int k = min(8 * w + lane / 8, RB - 1);
+    const int y = yb - K + k;
+    const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
+    int64_t xo = (xs < 0 ? 0 : xs) * (int64_t)sizeof(T) + (int64_t)(lane % 8) * 128;
+    if (xo > pitch * (int64_t)sizeof(T) - 4) xo = pitch * (int64_t)sizeof(T) - 4;
+    pfo = (uint32_t)((int64_t)yc * pitch * (int64_t)sizeof(T) + xo);
+  }
+  const unsigned pfl = PFW ? (unsigned)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)&pfd[PFW ? w : 0][0]) : 0u;
+  int npf = 0;
+  // (EXP bit 3) vector-memory ops issued after the DMA the next step waits for / after the newest DMA
+  constexpr bool DL2 = (EXP & 8) != 0;
+  const int ndma = (RB - w + WB - 1) / WB;  // window rows this wave fetches per plane
+  int c_prev = DL2 ? ndma : 0, c_next = 0;
+  auto prefetch = [&](int lz) {
+    const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
+    l2_touch((const char*)(in + (int64_t)lzc * plane) + pfo, pfl);
   };
 
   const int qlast = ze - 1 + K;  // last u0 plane of the march
   const bool sig_blk = SIG && zs == (int)g.lz_begin;
   const int sig_last = SIG ? (int)g.sig_z - 1 : 0;
   issue(zs - K, 0);
+  if (DL2) issue(zs - K + 1, 1);
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
   double acc = 0.0;
@@ -205,7 +240,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
 #pragma unroll
       for (int l = 0; l < K - 1; ++l) H[l][0][i] = H[l][1][i] = RO::zero();
     }
-    auto step = [&](int q, auto par_c) __attribute__((always_inline)) {
+    auto step = [&](int q, auto par_c, auto zt_c) __attribute__((always_inline)) {
       constexpr int P = decltype(par_c)::value;
       Row(&Cin)[NM] = P == 0 ? CA : CB;
       Row(&Cout)[NM] = P == 0 ? CB : CA;
@@ -215,46 +250,60 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // plane q's DMA has landed (the stores issued after it stay in flight); the barrier
       // publishes it and last step's seam rows, and certifies that every wave is done with the
       // other window buffer and the other seam parity
-      wait_vm_le(nst);
+      wait_vm_le(DL2 ? c_prev : nst + npf);
       lds_barrier();
-      if (q < qlast) issue(q + 1, P ^ 1);
+      if (!DL2 && q < qlast) issue(q + 1, P ^ 1);
+      npf = 0;
+      if (pfw && q + 2 <= qlast) {
+        prefetch(q + 2);
+        npf = 1;
+      }
       constexpr int SR = P ^ 1;  // seam parity read this step
-      // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact)
+      // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact); none in the march's
+      // middle (ZT false: every level's plane is z-interior)
+      constexpr bool ZTEST = decltype(zt_c)::value;
       Row rl[K + 1];
 #pragma unroll
       for (int l = 1; l <= K; ++l) {
         const int gz = q - l + gzoff;
-        rl[l] = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
+        rl[l] = ZTEST ? RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1)) : rx;
       }
       LV* const wbuf = wrow + P * WIN_BUF;
-      auto u0row = [&](int i) -> Row { return RO::fromv(V(wbuf[(i + K) * 64])); };
-      // EXP 1: every LDS row this step reads (the seam rows of levels 1..K-1 and the u0 window
-      // rows) is read up front, so the reads overlap each other and the level-(1) arithmetic
-      // instead of each waiting out a full LDS round trip right before its use
-      constexpr int NU = EXP ? SH::n(1) + 2 : 1;
+      // every LDS row this step reads (the seam rows of levels 1..K-1 and the u0 window rows) is
+      // read up front: the reads overlap each other and the level-(1) arithmetic instead of each
+      // waiting out a full LDS round trip right before its use (round 5: 1024^3 kernel A/B 0.4170
+      // vs 0.4313 ms per step, profiles/r05_session_a/)
+      constexpr int NU = SH::n(1) + 2;
       Row UP[K - 1], DN[K - 1], U[NU];
-      if constexpr (EXP != 0) {
+      auto seam_reads = [&] {
 #pragma unroll
         for (int j = 1; j < K; ++j) {
           UP[j - 1] = DN[j - 1] = RO::zero();
           if (ROLE != 0) UP[j - 1] = RO::fromv(seam[SR][j - 1][wu][1][lane]);
           if (ROLE != 2) DN[j - 1] = RO::fromv(seam[SR][j - 1][wd][0][lane]);
         }
+      };
+      if constexpr (!DL2) seam_reads();
 #pragma unroll
-        for (int k = 0; k < NU; ++k) U[k] = u0row(SH::lo(1) - 1 + k);
+      for (int k = 0; k < NU; ++k) U[k] = RO::fromv(V(wbuf[(SH::lo(1) - 1 + k + K) * 64]));
+      if constexpr (DL2) {
+        // every wave has read plane q out of buffer P: it takes plane q + 2 (the seam rows, which no
+        // DMA writes, are read after it: fewer rows live across the barrier)
+        lds_barrier();
+        c_prev = c_next;
+        if (q + 2 <= qlast) {
+          issue(q + 2, P);
+          c_prev += ndma;
+        }
+        c_next = 0;
+        seam_reads();
       }
       // (1) levels 2..K: S_l(m), m = q - l, into the slot of u_{l-1}(m-1) (its zm, consumed here)
 #pragma unroll
       for (int l = 2; l <= K; ++l) {
         const int j = l - 1;  // level of the inputs
-        Row up = RO::zero(), dn = RO::zero();
-        if constexpr (EXP != 0) {
-          up = UP[j - 1];
-          dn = DN[j - 1];
-        } else {
-          if (ROLE != 0) up = RO::fromv(seam[SR][j - 1][wu][1][lane]);
-          if (ROLE != 2) dn = RO::fromv(seam[SR][j - 1][wd][0][lane]);
-        }
+        const Row& up = UP[j - 1];
+        const Row& dn = DN[j - 1];
 #pragma unroll
         for (int i = SH::lo(l); i < SH::hi(l); ++i) {
           const int ij = i - SH::lo(j);
@@ -265,16 +314,12 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
           const T rgt = lane_down1(RO::first(c));
           Row& a = H[j - 1][P][ij];
           a = RO::partial(c, lft, rgt, ym, yp, a);
-          if constexpr (EXP >= 2) RO::pin_nv(a);
-          else RO::pin(a);
+          RO::pin(a);
         }
       }
       // (2) level 1 row by row from the u0 window, each new row cascading up through the levels
       Row X[3];
-      auto urow = [&](int i) -> Row {
-        if constexpr (EXP != 0) return U[i - (SH::lo(1) - 1)];
-        else return u0row(i);
-      };
+      auto urow = [&](int i) -> Row { return U[i - (SH::lo(1) - 1)]; };
       X[0] = urow(SH::lo(1) - 1);
       X[1] = urow(SH::lo(1));
       const bool valid = q - K >= zs && q <= qlast;  // u_K(q - K) is an owned output plane
@@ -294,8 +339,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         const T lft = lane_up1(RO::last(cen));
         const T rgt = lane_down1(RO::first(cen));
         S1[i1] = RO::partial(cen, lft, rgt, xm, xp, cold);
-        if constexpr (EXP >= 2) RO::pin_nv(S1[i1]);
-        else RO::pin(S1[i1]);
+        RO::pin(S1[i1]);
         Cout[i1] = cen;
         // cascade: cur = u_j(q - j) for j = 1, 2, ...
 #pragma unroll
@@ -334,6 +378,10 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         }
       }
       nst = valid ? nsto : 0;
+      if (DL2) {
+        c_prev += nst;
+        c_next += nst;
+      }
       if constexpr (SIG) {
         if (sig_blk && lz == sig_last) {  // block-uniform: every wave takes this branch together
           // this wave's stores of the lower planes are acknowledged by this XCD's L2 (vmcnt 0; no
@@ -346,9 +394,27 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       }
     };
     // an odd plane count ends with one extra step (q = qlast + 1): no DMA, nothing stored
-    for (int q = zs - K; q <= qlast; q += 2) {
-      step(q, IC<0>{});
-      step(q + 1, IC<1>{});
+    if constexpr ((EXP & 4) != 0) {
+      // (EXP bit 2) steps whose K levels all finish z-interior planes skip the z-held factors
+      auto zfree = [&](int q) { return q - K + gzoff >= 1 && q - 1 + gzoff <= gnz - 2; };
+      int q = zs - K;
+      for (; q <= qlast && !(zfree(q) && zfree(q + 1)); q += 2) {
+        step(q, IC<0>{}, std::true_type{});
+        step(q + 1, IC<1>{}, std::true_type{});
+      }
+      for (; q <= qlast && zfree(q + 1); q += 2) {
+        step(q, IC<0>{}, std::false_type{});
+        step(q + 1, IC<1>{}, std::false_type{});
+      }
+      for (; q <= qlast; q += 2) {
+        step(q, IC<0>{}, std::true_type{});
+        step(q + 1, IC<1>{}, std::true_type{});
+      }
+    } else {
+      for (int q = zs - K; q <= qlast; q += 2) {
+        step(q, IC<0>{}, std::true_type{});
+        step(q + 1, IC<1>{}, std::true_type{});
+      }
     }
   };
   if (w == 0) {
@@ -430,13 +496,16 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
     return;
   }
   if constexpr (sizeof(T) == 4 && RY == 3 && RE == 2 && K == 4 && WB == 8) {  // the headline shape only
-    if (knobs().wxk_exp == 1) {
-      go(F{}, F{}, F{}, IC<1>{});
-      return;
-    }
-    if (knobs().wxk_exp == 2) {
-      go(F{}, F{}, F{}, IC<2>{});
-      return;
+    switch (knobs().wxk_exp) {
+      case 1: go(F{}, F{}, F{}, IC<1>{}); return;
+      case 2: go(F{}, F{}, F{}, IC<2>{}); return;
+      case 4: go(F{}, F{}, F{}, IC<4>{}); return;
+      case 5: go(F{}, F{}, F{}, IC<5>{}); return;
+      case 7: go(F{}, F{}, F{}, IC<7>{}); return;
+      case 8: go(F{}, F{}, F{}, IC<8>{}); return;
+      case 9: go(F{}, F{}, F{}, IC<9>{}); return;
+      case 12: go(F{}, F{}, F{}, IC<12>{}); return;
+      default: break;
     }
   }
   go(F{}, F{}, F{}, IC<0>{});

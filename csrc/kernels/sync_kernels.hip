@@ -64,6 +64,17 @@ __global__ __launch_bounds__(64) void counter_signal_kernel(uint64_t* ctr) {
   __hip_atomic_store(ctr, v + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Forward-progress assumption. This one-wave kernel spins on the halo stream until a producer (the
+// interior sweep's folded-boundary signal, or a neighbour's ready / pulled counter) advances. The
+// producer runs on ANOTHER hardware queue, so nothing orders the two: the wait relies on the
+// hardware scheduler keeping the producing queue mapped and dispatching its blocks while this wave
+// spins. With one engine process per GPU (two queues of ours plus the runtime's) that holds. With
+// several processes oversubscribing one GPU's hardware queues it did not: round 4 session T, 8
+// processes, one sweep stopped at 177 of 235 tile arrivals while high-priority waits spun
+// (profiles/r04_session_t/). Hence normal stream priority everywhere, the ipc transport's refusal of
+// shared GPUs without share_gpu (ipc_shared_gpu_problem), captured graphs never containing a folded
+// wait (Solver::step), and the wall-clock bound below: a wait that cannot complete turns into an
+// error word the host watchdog reports, never into a hang.
 __global__ __launch_bounds__(64) void counter_wait_kernel(const uint64_t* remote, uint64_t* expect, uint64_t ahead,
                                                           uint64_t ticks, const int* abort_w, int* err_w) {
   if (threadIdx.x != 0) return;

@@ -7,10 +7,10 @@ cd "$(dirname "$0")/.."
 O=gpurun_out/r05a
 mkdir -p $O
 timeout -k 10 300 python bench/kernel_ab.py --kind heat7 --n 1024 --iters 10 --rounds 4 \
-  --variants "STEPS=4;STEPS=4,EXP=1;STEPS=4;STEPS=4,EXP=1" > $O/ab_1024.log 2>&1 || { tail -20 $O/ab_1024.log; exit 1; }
+  --variants "STEPS=4;STEPS=4,EXP=1;STEPS=4,EXP=3;STEPS=4;STEPS=4,EXP=1" > $O/ab_1024.log 2>&1 || { tail -20 $O/ab_1024.log; exit 1; }
 tail -6 $O/ab_1024.log
 timeout -k 10 300 python bench/kernel_ab.py --kind heat7 --nx 992 --ny 1024 --nz 1024 --iters 10 --rounds 3 \
-  --variants "STEPS=4;STEPS=4,EXP=1" > $O/ab_992.log 2>&1 || { tail -20 $O/ab_992.log; exit 1; }
+  --variants "STEPS=4;STEPS=4,EXP=1;STEPS=4,EXP=3" > $O/ab_992.log 2>&1 || { tail -20 $O/ab_992.log; exit 1; }
 tail -4 $O/ab_992.log
 timeout -k 10 300 python bench/kernel_ab.py --kind box27 --n 512 --iters 10 --rounds 3 \
   --variants "STEPS=2;STEPS=3;STEPS=3,EXP=1" > $O/ab_b27_512_f32.log 2>&1 || { tail -20 $O/ab_b27_512_f32.log; exit 1; }
