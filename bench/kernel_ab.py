@@ -3,8 +3,7 @@
 variants interleaved in ONE process, several rounds, best and median reported).
 
 Variants are the native dispatcher's kernel-family selectors (MDFX_TB_RY, MDFX_WTK_WB, MDFX_H7_WXK,
-MDFX_B27_WXK, MDFX_B27_TBK, and MDFX_WXK_EXP for experimental heat7_wxk copies; cached by the native
-layer and re-read per variant) plus the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
+and MDFX_B27_WXK; cached by the native layer and re-read per variant) plus the kernel family (tuned / naive) and the fused depth. Every variant's output is first checked
 bitwise against the naive kernel.
 
     python bench/kernel_ab.py --kind heat7 --n 1024 --variants "STEPS=4;STEPS=3;STEPS=3,WXK=0;STEPS=2"
@@ -24,8 +23,7 @@ import mpi_cuda_process_amd as m  # noqa: E402
 from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, init_field,  # noqa: E402
                                       set_kernel_variant)
 
-KEYS = {"TBRY": "MDFX_TB_RY", "B27TBK": "MDFX_B27_TBK", "WB": "MDFX_WTK_WB", "WXK": "MDFX_H7_WXK",
-        "B27WXK": "MDFX_B27_WXK", "EXP": "MDFX_WXK_EXP"}
+KEYS = {"TBRY": "MDFX_TB_RY", "WB": "MDFX_WTK_WB", "WXK": "MDFX_H7_WXK", "B27WXK": "MDFX_B27_WXK"}
 
 
 def parse_variant(s):

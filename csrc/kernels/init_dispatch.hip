@@ -88,7 +88,6 @@ static Knobs read_knobs() {
   k.wtk_wb = env_int("MDFX_WTK_WB", 0);
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
-  k.wxk_exp = env_int("MDFX_WXK_EXP", 0);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   return k;
 }
@@ -280,13 +279,13 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
     case StencilKind::Jacobi5: return 8;
     case StencilKind::Life: return 12;
     case StencilKind::Box27:
-      // K = 3 through box27_wxk for fp64 (512^3: 663 vs 527 GCells/s for box27_tbk K = 2) and for
-      // fp32 rows of 1024 cells and more (1024^3: 1291 vs 1102); at 512-cell rows its overlapping x
-      // segments waste a third of the lanes and box27_tb2n's K = 2 stays ahead (1074 vs 1027)
-      // (profiles/r03_wxk/). MDFX_B27_WXK = 0 / 1 forces K = 2 / 3
+      // K = 3 through box27_wxk for fp64 (512^3: 663 vs 527 GCells/s for box27_tbk K = 2), for fp32
+      // rows of 1024 cells and more (1024^3: 1291 vs 1102, profiles/r03_wxk/) and, since round 5's
+      // whole-row blocks, for fp32 rows of 257..512 cells (512^3: 1332 vs 1092 for box27_tb2n K = 2,
+      // profiles/r05_session_f/). MDFX_B27_WXK = 0 / 1 forces K = 2 / 3
       if (dev::knobs().b27_wxk == 1) return 3;
       if (dev::knobs().b27_wxk == 0) return 2;
-      return (spec.dtype == DType::F64 || nx >= 1024) ? 3 : 2;
+      return (spec.dtype == DType::F64 || nx >= 1024 || (nx > 256 && nx <= 512)) ? 3 : 2;
     case StencilKind::Heat7:
       // K = 3 through heat7_wtk wherever its x segments cover at least 2/3 of the lane cells:
       // 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2 (round 2), 2048^3 fp32 1666 vs 1136,

@@ -99,23 +99,6 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-// The same with the non-temporal policy (aux 2: nt on gfx950), for rows read once per sweep.
-__device__ __forceinline__ void glds16_nt(const void* g, void* l) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 2);
-}
-// An L2 prefetch: one dword per lane from `g` into 256 B of LDS at `lds` (wave-uniform), by an LDS
-// DMA the compiler does not see, so it neither drains it before later LDS reads nor counts it in its
-// own vmcnt waits: the caller accounts for it in its wait_vm_le counts.
-// M0 is the compiler's: saved and restored around the DMA.
-__device__ __forceinline__ void l2_touch(const void* g, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(lds)
-               : "memory");
-}
-
 // Raw waits: s_waitcnt encodings for gfx9 (vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]).
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 // vmcnt(n) for a wave-uniform n in 0..15 (an immediate per case): wait until at most the wave's n
@@ -231,8 +214,7 @@ struct Knobs {
   int tb_ry = 0;       // MDFX_TB_RY: rows per tile of heat7_tb2 (x-tiled rows) / box27_tb2 (1; 0: 2, 1 on short columns)
   int wtk_wb = 0;      // MDFX_WTK_WB: heat7_wtk waves per y band (4 or 8; 0: by region depth)
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: by dtype / width, 0: never, 1: always)
-  int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64 and rows >= 1024; 0 / 1)
-  int wxk_exp = 0;     // MDFX_WXK_EXP: experimental heat7_wxk code variants (headline shape; A/B only)
+  int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64, fp32 rows of 257..512 or >= 1024 cells; 0 / 1)
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
 };
 const Knobs& knobs();

@@ -253,9 +253,9 @@ template void launch_box27<double>(const Geo&, const double*, double*, const Ste
 // pair-layout kernel, removed in round 5 with its last fp64 use, spent 161 of its 400 VALU
 // instructions per plane on register moves). Bitwise equal to two box27_zw steps. An odd plane
 // count ends with one extra plane that stores nothing.
-// HOIST (A/B, MDFX_WXK_EXP=8): the plane's seam cells are read into registers right after the
-// barrier instead of one LDS round trip per row inside hsum
-template <int RY, int WXN, bool RES, bool HOIST = false>
+// (Reading the plane's seam cells into registers right after the barrier, instead of one LDS round
+// trip per row inside hsum, measured 1091 vs 1099 GCells/s at 512^3: profiles/r05_session_c/.)
+template <int RY, int WXN, bool RES>
 __global__ __launch_bounds__(256) void box27_tb2n(const float* __restrict__ in, float* __restrict__ out, Geo g,
                                                   float c0, float c1, float c2, float c3, int zc, int YT,
                                                   double* __restrict__ resid) {
@@ -311,10 +311,9 @@ __global__ __launch_bounds__(256) void box27_tb2n(const float* __restrict__ in, 
   const auto eL = lds_vptr(&edge[0][wl][0][1]);
   const auto eR = lds_vptr(&edge[0][wr][0][0]);
   const auto eW = lds_vptr(&edge[0][w][0][lane == 0 ? 0 : 1]);
-  T EL[HOIST ? SL : 1], ER[HOIST ? SL : 1];
   auto hsum = [&](const Row& v, int buf, int slot) -> Row {
-    const T le = HOIST ? EL[HOIST ? slot : 0] : eL[(buf * 4 * SL + slot) * 2];
-    const T re = HOIST ? ER[HOIST ? slot : 0] : eR[(buf * 4 * SL + slot) * 2];
+    const T le = eL[(buf * 4 * SL + slot) * 2];
+    const T re = eR[(buf * 4 * SL + slot) * 2];
     return RO::hsum(v, lane_up1_or(le, RO::last(v)), lane_down1_or(re, RO::first(v)));
   };
   struct St {
@@ -347,13 +346,6 @@ __global__ __launch_bounds__(256) void box27_tb2n(const float* __restrict__ in, 
         eW[(buf * 4 * SL + R0 + j) * 2] = lane == 0 ? RO::first(si.U1[j]) : RO::last(si.U1[j]);
     }
     lds_barrier();  // s_barrier after the LDS writes only: the register prefetch stays in flight
-    if constexpr (HOIST) {
-#pragma unroll
-      for (int j = 0; j < SL; ++j) {
-        EL[j] = eL[(buf * 4 * SL + j) * 2];
-        ER[j] = eR[(buf * 4 * SL + j) * 2];
-      }
-    }
 
     // ---- level 1: partials of u1 plane k-2, u2(k-3) ------------------------------------------
     if (k >= zs + 1) {
@@ -686,9 +678,7 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   // box27_tb2, 937-944 vs 1005-1013 GCells/s at 512^3, was removed in round 4,
   // profiles/r03_wtk/b27f32_*; its fp64 instance, 491.8 GCells/s against box27_tbk's 553, in round 5)
   static_assert(std::is_same<T, float>::value, "box27_tb2n: fp32 rows (fp64 runs box27_tbk)");
-  if (!resid && (knobs().wxk_exp & 8))
-    hipLaunchKernelGGL((box27_tb2n<RY, WXN, false, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
-  else if (resid)
+  if (resid)
     hipLaunchKernelGGL((box27_tb2n<RY, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
   else
     hipLaunchKernelGGL((box27_tb2n<RY, WXN, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);

@@ -46,28 +46,39 @@ namespace dev {
 
 int64_t resident_blocks(const void* kfn, int block);
 
-// EXP (A/B only): bit 0 non-temporal window DMAs
-template <class T, int RY, int RE, int K, int WB, bool RES, int EXP = 0>
-__global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T c0, T c1,
-                                                     T c2, T c3, int zc, int XT, int YT, int ntasks,
-                                                     double* __restrict__ resid) {
+// XW = 0: one wave per x segment, neighbouring segments overlapping by OV lanes (any row width).
+// XW >= 1: the whole row in one block (nx <= XW * 64 * N): XW waves side by side in x with no
+// overlap. The x neighbour of a wave's first / last cell comes from the LDS: level 1 reads it from
+// the neighbour's window row, level l > 1 from an edge table in which every wave leaves the first
+// and last cell of each row it finishes at levels 1..K-1 (written one step before it is read, like
+// the y seams). A block is then XW x WB waves.
+template <class T, int RY, int RE, int K, int WB, bool RES, int XW = 0>
+__global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T* __restrict__ in, T* __restrict__ out,
+                                                                         Geo g, T c0, T c1, T c2, T c3, int zc, int XT,
+                                                                         int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
   using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
   using Row = typename RO::Row;
   constexpr int N = VT<T>::N;
-  constexpr int OV = (K + N - 1) / N;
+  constexpr int XN = XW > 0 ? XW : 1;
+  constexpr int OV = XW > 0 ? 0 : (K + N - 1) / N;
   constexpr int SEG = (64 - 2 * OV) * N;
   constexpr int BR = 2 * RE + (WB - 2) * RY;
   constexpr int RB = BR + 2 * K;
+  constexpr int RX = BR + 2 * (K - 1);  // band rows levels 1..K-1 finish: -(K-1) .. BR+K-2
   constexpr int NM = RY > RE + K - 1 ? RY : RE + K - 1;
   constexpr int LAG = 2 * K - 1;  // level K finishes plane q - LAG at step q
   static_assert(WB >= 2 && K >= 2, "box27_wxk: bands of at least two waves, at least two levels");
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w = wid / XN, wx = wid % XN;  // y wave of the band, x wave of the row
   const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   if (b >= ntasks) return;
-  __shared__ V win[2][RB][64];
-  __shared__ V seam[2][K - 1][WB - 1][2][64];
+  __shared__ V win[2][XN][RB][64];
+  __shared__ V seam[2][XN][K - 1][WB - 1][2][64];
+  // x-edge table (XW >= 1) and the slots the other 62 lanes of an edge store write into
+  constexpr int XE = XW > 0 ? 2 * (K - 1) * XN * RX * 2 : 1;
+  __shared__ T xe[XE], xd[XW > 0 ? XE + 64 : 1];
   const int tiles = XT * YT;
   const int t = b % tiles, zt = b / tiles;
   const int P0 = (int)(g.lz_end - g.lz_begin);
@@ -81,9 +92,11 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
     ze = min((int)g.lz2_end, zs + zc);
   }
   const int xt = t % XT, yt = t / XT;
-  const int64_t x = (int64_t)xt * SEG - OV * N + (int64_t)lane * N;
+  const int64_t x = XW > 0 ? (int64_t)(wx * 64 + lane) * N : (int64_t)xt * SEG - OV * N + (int64_t)lane * N;
   const int ny = (int)g.ny, lzmax = (int)g.lz_max, gzoff = (int)g.gz_off, gnz = (int)g.gnz;
-  const int yb = yt * BR;
+  // bands tile the interior rows 1 .. ny-2; the held rows 0 / ny-1 a band does not reach are copied
+  // from the window (their value never changes) by the band's edge wave next to them
+  const int yb = 1 + yt * BR;
   const int y0 = yb + (w == 0 ? 0 : RE + (w - 1) * RY);
   const int rown = (w == 0 || w == WB - 1) ? RE : RY;
   const int64_t pitch = g.pitch, plane = g.plane;
@@ -98,22 +111,33 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
   // the fast march: no band row at y = 0 / ny-1 and no global boundary plane anywhere in the chunk
   const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
   const bool zint = zs - K + gzoff >= 1 && ze + K - 1 + gzoff <= gnz - 2;
-  const int nsto = __builtin_amdgcn_ballot_w64(own) != 0 ? max(0, min(rown, ny - y0)) : 0;
+  const bool anyown = __builtin_amdgcn_ballot_w64(own) != 0;
+  const int nsto = anyown ? max(0, min(rown, ny - y0)) : 0;
+  const bool held0 = anyown && yt == 0 && w == 0;                   // row 0 = this wave's row -1
+  const bool held1 = anyown && w == WB - 1 && yb + BR == ny - 1;  // row ny-1 = this wave's row RE
   int nst = 0;
 
-  const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
+  // byte offset of this lane's vector in x chunk kx (clamped into the row: finite values for the
+  // held cells past the pitch)
+  auto xcb_of = [&](int kx) -> uint32_t {
+    const int64_t xx = XW > 0 ? (int64_t)(kx * 64 + lane) * N : x;
+    return (uint32_t)((xx < 0 ? 0 : xx >= pitch ? pitch - N : xx) * (int64_t)sizeof(T));
+  };
+  const uint32_t xcb = xcb_of(0);
   auto issue = [&](int lz, int buf) {
     const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
+    constexpr int NW = XN * WB, NR = XN * RB;
 #pragma unroll
-    for (int j = 0; j < (RB + WB - 1) / WB; ++j) {
-      const int k = w + j * WB;
-      if (k < RB) {
-        const int y = yb - K + k;
+    for (int j = 0; j < (NR + NW - 1) / NW; ++j) {
+      const int k = wid + j * NW;
+      if (k < NR) {
+        const int kx = k / RB, kr = k - kx * RB;
+        const int y = yb - K + kr;
         const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-        const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xcb);
+        const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) +
+                                (XW > 1 ? xcb_of(kx) : xcb));
         dcheck(g, in, a, N);
-        if constexpr ((EXP & 1) != 0) glds16_nt(a, &win[buf][k][0]);
-        else glds16(a, &win[buf][k][0]);
+        glds16(a, &win[buf][kx][kr][0]);
       }
     }
   };
@@ -125,16 +149,43 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
   double acc = 0.0;
   typedef __attribute__((address_space(3))) V LV;
-  LV* const wrow = lds_vptr(&win[0][y0 - yb][lane]);
+  typedef __attribute__((address_space(3))) T LT;
+  LV* const wrow = lds_vptr(&win[0][wx][y0 - yb][lane]);
   const int wu = w > 0 ? w - 1 : 0, wd = w < WB - 1 ? w : WB - 2;
-  LV* const s_first = lds_vptr(&seam[0][0][wu][0][lane]);
-  LV* const s_last = lds_vptr(&seam[0][0][wd][1][lane]);
-  constexpr int WIN_BUF = RB * 64;
-  constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
+  LV* const s_first = lds_vptr(&seam[0][wx][0][wu][0][lane]);
+  LV* const s_last = lds_vptr(&seam[0][wx][0][wd][1][lane]);
+  // the neighbours' rows this wave reads (through laundered pointers: indexed with the runtime x
+  // wave, the direct seam reads made hipcc drain the window DMA just issued, vmcnt(0), every step)
+  LV* const s_rdu = lds_vptr(&seam[0][wx][0][wu][1][lane]);
+  LV* const s_rdd = lds_vptr(&seam[0][wx][0][wd][0][lane]);
+  constexpr int WIN_BUF = XN * RB * 64;
+  constexpr int SEAM_PAR = XN * (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
+  // x edges (XW >= 1). Lane 0 takes its left neighbour's last cell, lane 63 its right neighbour's
+  // first; at the row's ends (held cells, the value only meets a zero coefficient) a lane reads a
+  // finite cell of its own wave instead. Window: row r of buffer P at e_win[(P * WIN_BUF + r * 64) * N]
+  // with r = y0 - yb + i + K; table: [P][level][x wave][i + K - 1][side] from this wave's row i.
+  const int wl = wx > 0 ? wx - 1 : 0, wr = wx < XN - 1 ? wx + 1 : XN - 1;
+  auto cell = [](V* v, int e) -> T* { return (T*)v + e; };
+  LT* const e_win = lds_vptr(lane == 63 ? (wx < XN - 1 ? cell(&win[0][wx + 1][y0 - yb][0], 0) : cell(&win[0][wx][y0 - yb][63], N - 1))
+                                        : (wx > 0 ? cell(&win[0][wx - 1][y0 - yb][63], N - 1) : cell(&win[0][wx][y0 - yb][0], 0)));
+  constexpr int XE_PAR = (K - 1) * XN * RX * 2, XE_LVL = XN * RX * 2;
+  const int xrow0 = (y0 - yb) * 2;  // row i = -(K-1) of this wave in the table
+  LT* const e_tab = lds_vptr(lane == 63 ? &xe[(wr * RX) * 2 + xrow0 + (wx < XN - 1 ? 0 : 1)]
+                                        : &xe[(wl * RX) * 2 + xrow0 + (wx > 0 ? 1 : 0)]);
+  LT* const e_put = lds_vptr(lane == 0 ? &xe[(wx * RX) * 2 + xrow0] : lane == 63 ? &xe[(wx * RX) * 2 + xrow0 + 1] : &xd[lane]);
   auto st = [](LV* p, const V& v) {
     asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
+  auto st1 = [](LT* p, T v) {
+    if constexpr (sizeof(T) == 4)
+      asm volatile("ds_write_b32 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+    else
+      asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+  };
   auto hs = [](const Row& v) -> Row { return RO::hsum(v, lane_up1(RO::last(v)), lane_down1(RO::first(v))); };
+  auto hsx = [](const Row& v, T e) -> Row {
+    return RO::hsum(v, lane_up1_or(e, RO::last(v)), lane_down1_or(e, RO::first(v)));
+  };
 
   auto march = [&](auto role_c, auto gen_c) __attribute__((always_inline)) {
     constexpr int ROLE = decltype(role_c)::value;
@@ -168,8 +219,20 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
 #pragma unroll
       for (int j = 1; j < K; ++j) {
         SU[j] = SD[j] = RO::zero();
-        if (SH::lo(j + 1) - 1 < SH::lo(j)) SU[j] = RO::fromv(seam[P ^ 1][j - 1][wu][1][lane]);
-        if (SH::hi(j + 1) >= SH::hi(j)) SD[j] = RO::fromv(seam[P ^ 1][j - 1][wd][0][lane]);
+        if (SH::lo(j + 1) - 1 < SH::lo(j)) SU[j] = RO::fromv(V(s_rdu[(P ^ 1) * SEAM_PAR + (j - 1) * SEAM_LVL]));
+        if (SH::hi(j + 1) >= SH::hi(j)) SD[j] = RO::fromv(V(s_rdd[(P ^ 1) * SEAM_PAR + (j - 1) * SEAM_LVL]));
+      }
+      // x edges of every level's input rows (XW > 1): level 1's from the window, level l's from the
+      // table level l-1 filled in the previous step
+      T E1[NU], EX[K][NM + 2];
+      if constexpr (XW > 1) {
+#pragma unroll
+        for (int k = 0; k < NU; ++k) E1[k] = e_win[(P * WIN_BUF + (SH::lo(1) - 1 + k + K) * 64) * N];
+#pragma unroll
+        for (int j = 1; j < K; ++j)
+#pragma unroll
+          for (int k = 0; k < SH::n(j + 1) + 2; ++k)
+            EX[j][k] = e_tab[(P ^ 1) * XE_PAR + (j - 1) * XE_LVL + (SH::lo(j + 1) - 1 + k + K - 1) * 2];
       }
       // levels top-down: level l reads its inputs (the level below's plane from the previous step)
       // before that level overwrites its other stored plane
@@ -192,13 +255,17 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
           if (i >= SH::hi(j)) return SD[j];
           return H[j - 1][P ^ 1][i - SH::lo(j)];
         };
+        auto hsi = [&](const Row& v, int i) -> Row {
+          if constexpr (XW > 1) return hsx(v, l == 1 ? E1[i - (SH::lo(1) - 1)] : EX[l - 1][i - (SH::lo(l) - 1)]);
+          else return hs(v);
+        };
         Row vm = vin(SH::lo(l) - 1), vc = vin(SH::lo(l));
-        Row hm = hs(vm), hc = hs(vc);
+        Row hm = hsi(vm, SH::lo(l) - 1), hc = hsi(vc, SH::lo(l));
 #pragma unroll
         for (int i = SH::lo(l); i < SH::hi(l); ++i) {
           const int il = i - SH::lo(l);
           const Row vp = vin(i + 1);
-          const Row hp = hs(vp);
+          const Row hp = hsi(vp, i + 1);
           const Row cross = RO::add(hc, RO::add(vm, vp));
           const Row diag = RO::add(hm, hp);
           Row a, bb;
@@ -234,6 +301,8 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
             H[l - 1][P][il] = o;
             if (ROLE != 0 && i == 0) st(s_first + P * SEAM_PAR + (l - 1) * SEAM_LVL, RO::vec(o));
             if (ROLE != 2 && i == SH::R - 1) st(s_last + P * SEAM_PAR + (l - 1) * SEAM_LVL, RO::vec(o));
+            if constexpr (XW > 1)
+              st1(e_put + P * XE_PAR + (l - 1) * XE_LVL + (i + K - 1) * 2, lane == 63 ? RO::last(o) : RO::first(o));
           }
           vm = vc;
           vc = vp;
@@ -242,6 +311,17 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
         }
       }
       nst = valid ? nsto : 0;
+      if constexpr (GEN && ROLE != 1) {
+        if ((ROLE == 0 ? held0 : held1) && q >= zs && q < ze) {  // u0 plane q is output plane q there
+          constexpr int ih = ROLE == 0 ? -1 : SH::R;
+          if (own) {
+            T* ad = (T*)((char*)(ob + (int64_t)q * plane + (int64_t)ih * pitch) + xob);
+            dcheck(g, (const T*)out, ad, N);
+            store_nt((V*)ad, RO::vec(U[ih - (SH::lo(1) - 1)]));
+          }
+          ++nst;
+        }
+      }
     };
     for (int q = zs - K; q <= qend; q += 2) {
       step(q, IC<0>{});
@@ -268,33 +348,31 @@ __global__ __launch_bounds__(WB * 64) void box27_wxk(const T* __restrict__ in, T
 // 6-row bands fetched twice the window rows per output row and it ran 909 vs 1017-1026 GCells/s
 // at 512^3 (profiles/r03_session_t/); removed in round 4.)
 
-template <class T, int RY, int RE, int K, int WB>
+template <class T, int RY, int RE, int K, int WB, int XW = 0>
 static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf, double* resid, hipStream_t s) {
-  constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
-  constexpr int BR = 2 * RE + (WB - 2) * RY;
+  constexpr int N = VT<T>::N, OV = XW > 0 ? 0 : (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  constexpr int BR = 2 * RE + (WB - 2) * RY, NT = 64 * WB * (XW > 0 ? XW : 1);
+  if (XW > 0) MDFX_CHECK(g.nx <= XW * 64 * N, "box27_wxk: whole-row blocks need nx <= XW * 64 * N");
   const int64_t planes = g.lz_end - g.lz_begin;
   const int64_t planes2 = g.lz2_end > g.lz2_begin ? g.lz2_end - g.lz2_begin : 0;
-  const int XT = (int)((g.nx + SEG - 1) / SEG);
-  const int YT = (int)((g.ny + BR - 1) / BR);
+  const int XT = XW > 0 ? 1 : (int)((g.nx + SEG - 1) / SEG);
+  const int YT = (int)std::max<int64_t>(1, (g.ny - 2 + BR - 1) / BR);  // bands over rows 1 .. ny-2
   const int64_t tiles = (int64_t)XT * YT;
-  const void* kfn = (const void*)&box27_wxk<T, RY, RE, K, WB, false>;
-  const int64_t resident = resident_blocks(kfn, 64 * WB);
+  const void* kfn = (const void*)&box27_wxk<T, RY, RE, K, WB, false, XW>;
+  const int64_t resident = resident_blocks(kfn, NT);
   int zc = wx_zc(planes, tiles, resident, K, 3 * K - 1, g.min_rounds);
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + zc - 1) / zc) + (planes2 > 0 ? (int)((planes2 + zc - 1) / zc) : 0);
   const int64_t ntasks = tiles * ZT;
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "box27_wxk: too many tasks");
-  const dim3 grd((unsigned)ntasks), blk(64 * WB);
+  const dim3 grd((unsigned)ntasks), blk(NT);
   const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
   if (resid)
-    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
+    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, true, XW>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
                        (int)ntasks, resid);
-  else if (knobs().wxk_exp == 1)
-    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false, 1>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT,
-                       YT, (int)ntasks, resid);
   else
-    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
-                       (int)ntasks, resid);
+    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false, XW>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT,
+                       YT, (int)ntasks, resid);
 }
 
 template <class T>
@@ -313,6 +391,12 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
   // 2-row inner waves, 1-row edge waves, bands of 8 (14 rows): the 3-row shapes need more than
   // 256 VGPRs; 1-row waves in bands of 8 and 2-row waves in bands of 4 measured slower at 512^3
   // (fp64 500 / 603 vs 640 GCells/s, fp32 845 / 957 vs 1007: profiles/r04_session_n/)
+  // fp32 rows of at most 512 cells: whole-row blocks of 2 x 4 waves with the x edges exchanged through
+  // the LDS (no lane of a 512-cell row computed twice; bands over rows 1..ny-2 fill 255 blocks in
+  // three z chunks): 512^3 1332 GCells/s against 1009 in three overlapping segments and 1092 for
+  // box27_tb2n K = 2 (profiles/r05_session_f/)
+  if constexpr (std::is_same<T, float>::value)
+    if (g.nx <= 512) return launch_b27x<T, 2, 1, 3, 4, 2>(g, in, out, cf, resid, s);
   launch_b27x<T, 2, 1, 3, 8>(g, in, out, cf, resid, s);
 }
 template void launch_box27_wxk<float>(const Geo&, const float*, float*, const StencilCoef&, int, double*, hipStream_t);

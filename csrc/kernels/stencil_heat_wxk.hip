@@ -86,11 +86,7 @@ __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles,
 // SIG: the folded-boundary copy (Geo::sig): the blocks of the chunks starting at lz_begin publish their
 // output planes [lz_begin, sig_z) and signal, so the halo exchange of the lower face overlaps the
 // rest of the same sweep (no separate boundary launch for that face).
-// EXP (A/B only): bit 0 non-temporal window DMAs, bit 1 an L2 prefetch of plane q + 2 by one 4-byte
-// LDS DMA per window row line (outside the compiler's view), bit 2 the z-test-free middle of the
-// march, bit 3 the window DMA two planes ahead in the same two buffers (a second barrier per plane
-// step, right after the step's window reads, frees the buffer just read)
-template <class T, int RY, int RE, int K, int WB, bool RES, bool PEN = false, bool SIG = false, int EXP = 0>
+template <class T, int RY, int RE, int K, int WB, bool RES, bool PEN = false, bool SIG = false>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
   using V = typename VT<T>::type;
@@ -113,10 +109,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   __shared__ V win[2][RB][64];
   // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
   __shared__ V seam[2][K - 1][WB - 1][2][64];
-  __shared__ uint32_t pfd[(EXP & 2) ? WB : 1][64];  // (EXP bit 1) the prefetch DMAs' landing slots
   // (A second plane in flight does not help this sweep: a third window buffer with one seam table
-  // and a second barrier lost in round 3 (profiles/r03_session_r/), and an L2 prefetch of plane
-  // q + 2 by 4-byte LDS DMAs lost 15-24 % in round 4 (profiles/r04_session_b/).)
+  // and a second barrier lost in round 3 (profiles/r03_session_r/); an L2 prefetch of plane q + 2 by
+  // 4-byte LDS DMAs lost 15-24 % in round 4 (profiles/r04_session_b/) and 15 % in round 5; the DMA
+  // two planes ahead in these two buffers (a second barrier per step right after the window reads)
+  // lost 4-6 %, non-temporal window DMAs 19 % (profiles/r05_session_b/, r05_session_c/).)
   const int tiles = XT * YT;
   const int t = b % tiles, zt = b / tiles;
   const int P0 = (int)(g.lz_end - g.lz_begin);
@@ -172,41 +169,14 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         asm volatile("" : "+s"(rb));
         const T* a = (const T*)((const char*)(uintptr_t)rb + xcb);
         dcheck(g, in, a, N);
-        if constexpr ((EXP & 1) != 0) glds16_nt(a, &win[buf][k][0]);
-        else glds16(a, &win[buf][k][0]);
+        glds16(a, &win[buf][k][0]);
       }
     }
   };
-  // (EXP bit 1) plane lz -> L2: waves 0 .. ceil(RB / 8) - 1 each touch every 128-B line of 8 window
-  // rows with one dword per lane (lane l: row 8w + l / 8, line l % 8); npf: prefetches issued since
-  // the wave's newest window DMA (they stay in flight across the next plane's wait)
-  constexpr bool PFW = (EXP & 2) != 0;
-  const bool pfw = PFW && 8 * w < RB;
-  uint32_t pfo = 0;
-  if (PFW) {
-    const int k = min(8 * w + lane / 8, RB - 1);
-    const int y = yb - K + k;
-    const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-    int64_t xo = (xs < 0 ? 0 : xs) * (int64_t)sizeof(T) + (int64_t)(lane % 8) * 128;
-    if (xo > pitch * (int64_t)sizeof(T) - 4) xo = pitch * (int64_t)sizeof(T) - 4;
-    pfo = (uint32_t)((int64_t)yc * pitch * (int64_t)sizeof(T) + xo);
-  }
-  const unsigned pfl = PFW ? (unsigned)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)&pfd[PFW ? w : 0][0]) : 0u;
-  int npf = 0;
-  // (EXP bit 3) vector-memory ops issued after the DMA the next step waits for / after the newest DMA
-  constexpr bool DL2 = (EXP & 8) != 0;
-  const int ndma = (RB - w + WB - 1) / WB;  // window rows this wave fetches per plane
-  int c_prev = DL2 ? ndma : 0, c_next = 0;
-  auto prefetch = [&](int lz) {
-    const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
-    l2_touch((const char*)(in + (int64_t)lzc * plane) + pfo, pfl);
-  };
-
   const int qlast = ze - 1 + K;  // last u0 plane of the march
   const bool sig_blk = SIG && zs == (int)g.lz_begin;
   const int sig_last = SIG ? (int)g.sig_z - 1 : 0;
   issue(zs - K, 0);
-  if (DL2) issue(zs - K + 1, 1);
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
   double acc = 0.0;
@@ -240,7 +210,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
 #pragma unroll
       for (int l = 0; l < K - 1; ++l) H[l][0][i] = H[l][1][i] = RO::zero();
     }
-    auto step = [&](int q, auto par_c, auto zt_c) __attribute__((always_inline)) {
+    auto step = [&](int q, auto par_c) __attribute__((always_inline)) {
       constexpr int P = decltype(par_c)::value;
       Row(&Cin)[NM] = P == 0 ? CA : CB;
       Row(&Cout)[NM] = P == 0 ? CB : CA;
@@ -250,23 +220,18 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // plane q's DMA has landed (the stores issued after it stay in flight); the barrier
       // publishes it and last step's seam rows, and certifies that every wave is done with the
       // other window buffer and the other seam parity
-      wait_vm_le(DL2 ? c_prev : nst + npf);
+      wait_vm_le(nst);
       lds_barrier();
-      if (!DL2 && q < qlast) issue(q + 1, P ^ 1);
-      npf = 0;
-      if (pfw && q + 2 <= qlast) {
-        prefetch(q + 2);
-        npf = 1;
-      }
+      if (q < qlast) issue(q + 1, P ^ 1);
       constexpr int SR = P ^ 1;  // seam parity read this step
-      // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact); none in the march's
-      // middle (ZT false: every level's plane is z-interior)
-      constexpr bool ZTEST = decltype(zt_c)::value;
+      // z-held planes: coefficient 0 through a wave-uniform 0 / 1 factor (exact). (A copy of the
+      // march without these factors for the z-interior middle gained 3.5 % in the kernel A/B but
+      // nothing in the driver form, sessions r05_b / r05_c: not shipped.)
       Row rl[K + 1];
 #pragma unroll
       for (int l = 1; l <= K; ++l) {
         const int gz = q - l + gzoff;
-        rl[l] = ZTEST ? RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1)) : rx;
+        rl[l] = RO::scale(rx, (gz <= 0 || gz >= gnz - 1) ? T(0) : T(1));
       }
       LV* const wbuf = wrow + P * WIN_BUF;
       // every LDS row this step reads (the seam rows of levels 1..K-1 and the u0 window rows) is
@@ -274,30 +239,19 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       // waiting out a full LDS round trip right before its use (round 5: 1024^3 kernel A/B 0.4170
       // vs 0.4313 ms per step, profiles/r05_session_a/)
       constexpr int NU = SH::n(1) + 2;
+      // (the residual copies of the 4-row K = 3 band read the window rows where they are used: with
+      // them held the band needs 4-10 VGPRs more than it has)
+      constexpr bool LAZY = RES && K == 3 && RY == 4;
       Row UP[K - 1], DN[K - 1], U[NU];
-      auto seam_reads = [&] {
 #pragma unroll
-        for (int j = 1; j < K; ++j) {
-          UP[j - 1] = DN[j - 1] = RO::zero();
-          if (ROLE != 0) UP[j - 1] = RO::fromv(seam[SR][j - 1][wu][1][lane]);
-          if (ROLE != 2) DN[j - 1] = RO::fromv(seam[SR][j - 1][wd][0][lane]);
-        }
-      };
-      if constexpr (!DL2) seam_reads();
-#pragma unroll
-      for (int k = 0; k < NU; ++k) U[k] = RO::fromv(V(wbuf[(SH::lo(1) - 1 + k + K) * 64]));
-      if constexpr (DL2) {
-        // every wave has read plane q out of buffer P: it takes plane q + 2 (the seam rows, which no
-        // DMA writes, are read after it: fewer rows live across the barrier)
-        lds_barrier();
-        c_prev = c_next;
-        if (q + 2 <= qlast) {
-          issue(q + 2, P);
-          c_prev += ndma;
-        }
-        c_next = 0;
-        seam_reads();
+      for (int j = 1; j < K; ++j) {
+        UP[j - 1] = DN[j - 1] = RO::zero();
+        if (ROLE != 0) UP[j - 1] = RO::fromv(seam[SR][j - 1][wu][1][lane]);
+        if (ROLE != 2) DN[j - 1] = RO::fromv(seam[SR][j - 1][wd][0][lane]);
       }
+#pragma unroll
+      for (int k = 0; k < NU; ++k)
+        if constexpr (!LAZY) U[k] = RO::fromv(V(wbuf[(SH::lo(1) - 1 + k + K) * 64]));
       // (1) levels 2..K: S_l(m), m = q - l, into the slot of u_{l-1}(m-1) (its zm, consumed here)
 #pragma unroll
       for (int l = 2; l <= K; ++l) {
@@ -319,7 +273,10 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       }
       // (2) level 1 row by row from the u0 window, each new row cascading up through the levels
       Row X[3];
-      auto urow = [&](int i) -> Row { return U[i - (SH::lo(1) - 1)]; };
+      auto urow = [&](int i) -> Row {
+        if constexpr (LAZY) return RO::fromv(V(wbuf[(i + K) * 64]));
+        else return U[i - (SH::lo(1) - 1)];
+      };
       X[0] = urow(SH::lo(1) - 1);
       X[1] = urow(SH::lo(1));
       const bool valid = q - K >= zs && q <= qlast;  // u_K(q - K) is an owned output plane
@@ -378,10 +335,6 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         }
       }
       nst = valid ? nsto : 0;
-      if (DL2) {
-        c_prev += nst;
-        c_next += nst;
-      }
       if constexpr (SIG) {
         if (sig_blk && lz == sig_last) {  // block-uniform: every wave takes this branch together
           // this wave's stores of the lower planes are acknowledged by this XCD's L2 (vmcnt 0; no
@@ -394,27 +347,9 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
       }
     };
     // an odd plane count ends with one extra step (q = qlast + 1): no DMA, nothing stored
-    if constexpr ((EXP & 4) != 0) {
-      // (EXP bit 2) steps whose K levels all finish z-interior planes skip the z-held factors
-      auto zfree = [&](int q) { return q - K + gzoff >= 1 && q - 1 + gzoff <= gnz - 2; };
-      int q = zs - K;
-      for (; q <= qlast && !(zfree(q) && zfree(q + 1)); q += 2) {
-        step(q, IC<0>{}, std::true_type{});
-        step(q + 1, IC<1>{}, std::true_type{});
-      }
-      for (; q <= qlast && zfree(q + 1); q += 2) {
-        step(q, IC<0>{}, std::false_type{});
-        step(q + 1, IC<1>{}, std::false_type{});
-      }
-      for (; q <= qlast; q += 2) {
-        step(q, IC<0>{}, std::true_type{});
-        step(q + 1, IC<1>{}, std::true_type{});
-      }
-    } else {
-      for (int q = zs - K; q <= qlast; q += 2) {
-        step(q, IC<0>{}, std::true_type{});
-        step(q + 1, IC<1>{}, std::true_type{});
-      }
+    for (int q = zs - K; q <= qlast; q += 2) {
+      step(q, IC<0>{});
+      step(q + 1, IC<1>{});
     }
   };
   if (w == 0) {
@@ -471,9 +406,9 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
   const bool pen = g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny;
   // one instance per (residual, pencil rows, folded-boundary signal) combination the engine uses
-  auto go = [&](auto res_c, auto pen_c, auto sig_c, auto exp_c) {
+  auto go = [&](auto res_c, auto pen_c, auto sig_c) {
     hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, decltype(res_c)::value, decltype(pen_c)::value,
-                                  decltype(sig_c)::value, decltype(exp_c)::value>),
+                                  decltype(sig_c)::value>),
                        grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
   };
   using F = std::false_type;
@@ -482,33 +417,17 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
     MDFX_CHECK(!g.sig, "heat7_wxk: folded boundaries run in bands of 8 waves");
   } else if (g.sig) {
     MDFX_CHECK(!pen && g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
-    if (resid) go(Tr{}, F{}, Tr{}, IC<0>{});
-    else go(F{}, F{}, Tr{}, IC<0>{});
+    if (resid) go(Tr{}, F{}, Tr{});
+    else go(F{}, F{}, Tr{});
     return;
   }
   if (resid) {
-    if (pen) go(Tr{}, Tr{}, F{}, IC<0>{});
-    else go(Tr{}, F{}, F{}, IC<0>{});
+    if (pen) go(Tr{}, Tr{}, F{});
+    else go(Tr{}, F{}, F{});
     return;
   }
-  if (pen) {
-    go(F{}, Tr{}, F{}, IC<0>{});
-    return;
-  }
-  if constexpr (sizeof(T) == 4 && RY == 3 && RE == 2 && K == 4 && WB == 8) {  // the headline shape only
-    switch (knobs().wxk_exp) {
-      case 1: go(F{}, F{}, F{}, IC<1>{}); return;
-      case 2: go(F{}, F{}, F{}, IC<2>{}); return;
-      case 4: go(F{}, F{}, F{}, IC<4>{}); return;
-      case 5: go(F{}, F{}, F{}, IC<5>{}); return;
-      case 7: go(F{}, F{}, F{}, IC<7>{}); return;
-      case 8: go(F{}, F{}, F{}, IC<8>{}); return;
-      case 9: go(F{}, F{}, F{}, IC<9>{}); return;
-      case 12: go(F{}, F{}, F{}, IC<12>{}); return;
-      default: break;
-    }
-  }
-  go(F{}, F{}, F{}, IC<0>{});
+  if (pen) go(F{}, Tr{}, F{});
+  else go(F{}, F{}, F{});
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 5, session G1: the native tests, the whole GPU tier (ipc churn test included) and smoke().
+set -o pipefail
+cd "$(dirname "$0")/.."
+scripts/gpu_session.sh native || exit $?
+LIMIT=900 scripts/gpu_session.sh "gputests=python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests --deselect tests/test_gpu_ipc.py" || exit $?
+grep -E "passed|failed" gpurun_out/gputests.log | tail -2
+scripts/gpu_session.sh ipc smoke || exit $?
+grep -E "passed|failed" gpurun_out/ipc.log | tail -1
