@@ -31,7 +31,7 @@ struct Opts {
   double r = -1, c0 = 0.25, c1 = 0.05, c2 = 0.025, c3 = 3.0 / 160.0;
   int residual_every = 0;
   bool print = false, json = false, sync_debug = false, overlap = true, graph = false;
-  bool verbose = false, quiet = false;
+  bool verbose = false, quiet = false, share_gpu = false;
   std::string variant = "auto";
   double timeout = 0;
   int64_t ckpt_every = 0;
@@ -57,8 +57,9 @@ void usage(const char* prog) {
       "  --gpus N                  slabs on GPUs 0..N-1 driven by this one process\n"
       "  --ranks P                 P slabs in this process (several per GPU allowed: loopback)\n"
       "  --py Y                    (z, y) pencils: Y ranks along y, P / Y along z (3D; loopback, host, ipc)\n"
-      "  --transport auto|rccl|ipc|loopback|host|tcp\n"
+      "  --transport auto|rccl|ipc|ipc_sdma|loopback|host|tcp\n"
       "                            multi-process runs (mpirun / torchrun): rccl on GPUs, tcp on CPUs\n"
+      "  --share-gpu               ipc: allow several processes on one GPU (tests; one per GPU otherwise)\n"
       "  --init random|dirichlet|constant|life|compat  --seed --lo --hi --value --edge --interior --density\n"
       "  --r R | --c0 --c1 --c2 --c3   update coefficients\n"
       "  --ref-precision           2D MDF: the reference's fp32-sum / fp64-scale evaluation of the update\n"
@@ -104,6 +105,7 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--gpus") o.gpus = std::atoi(need(i));
     else if (a == "--ranks") o.ranks = std::atoi(need(i));
     else if (a == "--transport") o.transport = need(i);
+    else if (a == "--share-gpu") o.share_gpu = true;
     else if (a == "--init") o.init = need(i);
     else if (a == "--seed") o.seed = std::strtoull(need(i), nullptr, 10);
     else if (a == "--lo") o.lo = std::atof(need(i));
@@ -287,7 +289,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
       f.allreduce_sum = [r](double v) { return r->allreduce_sum(v); };
       f.allreduce_max = [r](double v) { return r->allreduce_max(v); };
       f.barrier = [r]() { r->barrier(); };
-      tr = make_ipc_transport(std::move(f), tname == "ipc_sdma" ? 1 : -1);
+      tr = make_ipc_transport(std::move(f), tname == "ipc_sdma" ? 1 : -1, o.share_gpu);
     } else {
       MDFX_FAIL("unknown transport " + tname);
     }

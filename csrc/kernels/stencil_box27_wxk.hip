@@ -21,9 +21,10 @@
 // Held cells: per-cell coefficient rows (x): c0 -> 1 and c1 = c2 = c3 -> 0, so A = 0 and B = the
 // centre, and the cell keeps its value; rows y = 0 / ny-1 take that held coefficient set per row;
 // planes gz = 0 / gnz-1 through a 0 / 1 factor on the A terms (u' = fma(z, A, S), S = fma(z, A, B)
-// with B = the centre there). Those two run in a general copy of the march that only bands touching
-// y = 0 / ny-1 and chunks touching the first / last global plane take. (A held cell holding -0.0
-// comes back as +0.0, as in every fused kernel: 0 * t + (-0) rounds to +0.)
+// with B = the centre there). Those two run in a general copy of the plane step that only bands
+// touching y = 0 / ny-1 take, and other bands only in the step pairs that touch the first / last
+// global plane. (A held cell holding -0.0 comes back as +0.0, as in every fused kernel:
+// 0 * t + (-0) rounds to +0.)
 //
 // Region contract (as box27_tb2): output storage planes [lz_begin, lz_end) (and optionally a second
 // region [lz2_begin, lz2_end)) need u0 valid on [lz_begin - K, lz_end + K).
@@ -108,9 +109,8 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
   // per-cell coefficients: held x cells keep their centre (A = 0, B = centre)
   const Row k0 = RO::coefv(c0, T(1), xb), k1 = RO::coefv(c1, T(0), xb), k2 = RO::coefv(c2, T(0), xb),
             k3 = RO::coefv(c3, T(0), xb);
-  // the fast march: no band row at y = 0 / ny-1 and no global boundary plane anywhere in the chunk
+  // no row of the band (trapezoid included) at y = 0 / ny-1: the plane steps may skip the row tests
   const bool yint = yb - (K - 1) >= 1 && yb + BR + K - 2 <= ny - 2;
-  const bool zint = zs - K + gzoff >= 1 && ze + K - 1 + gzoff <= gnz - 2;
   const bool anyown = __builtin_amdgcn_ballot_w64(own) != 0;
   const int nsto = anyown ? max(0, min(rown, ny - y0)) : 0;
   const bool held0 = anyown && yt == 0 && w == 0;                   // row 0 = this wave's row -1
@@ -187,9 +187,9 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
     return RO::hsum(v, lane_up1_or(e, RO::last(v)), lane_down1_or(e, RO::first(v)));
   };
 
-  auto march = [&](auto role_c, auto gen_c) __attribute__((always_inline)) {
+  auto march = [&](auto role_c, auto ygen_c) __attribute__((always_inline)) {
     constexpr int ROLE = decltype(role_c)::value;
-    constexpr bool GEN = decltype(gen_c)::value;  // held rows / planes may occur
+    constexpr bool YGEN = decltype(ygen_c)::value;  // the band has rows at y = 0 / ny-1
     using SH = WxRows<ROLE, RY, RE, K>;
     // per level l (index l-1): running sums S, the last two A (ping-pong), and for l < K the two
     // stored output planes H (ping-pong) the level above reads
@@ -201,7 +201,8 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
         S[l][i] = Ap[l][0][i] = Ap[l][1][i] = RO::zero();
         if (l < K - 1) H[l][0][i] = H[l][1][i] = RO::zero();
       }
-    auto step = [&](int q, auto par_c) __attribute__((always_inline)) {
+    auto step = [&](int q, auto par_c, auto gen_c) __attribute__((always_inline)) {
+      constexpr bool GEN = decltype(gen_c)::value;  // held rows / planes may occur in this step
       constexpr int P = decltype(par_c)::value;
       __builtin_amdgcn_sched_barrier(0);
       wait_vm_le(nst);
@@ -323,20 +324,36 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
         }
       }
     };
-    for (int q = zs - K; q <= qend; q += 2) {
-      step(q, IC<0>{});
-      step(q + 1, IC<1>{});
+    // in a y-interior band, the step pairs whose levels all finish and read z-interior planes take
+    // the copy without the held-row / held-plane tests (at 512^3 two of the three z chunks touch a
+    // global boundary plane, but only in their first or last 2K - 1 steps)
+    using Tr = std::true_type;
+    using F = std::false_type;
+    int q = zs - K;
+    if constexpr (!YGEN) {
+      auto zfree = [&](int qq) { return qq - LAG + gzoff >= 1 && qq + 1 + gzoff <= gnz - 2; };  // qq and qq + 1
+      for (; q <= qend && !zfree(q); q += 2) {
+        step(q, IC<0>{}, Tr{});
+        step(q + 1, IC<1>{}, Tr{});
+      }
+      for (; q <= qend && zfree(q); q += 2) {
+        step(q, IC<0>{}, F{});
+        step(q + 1, IC<1>{}, F{});
+      }
+    }
+    for (; q <= qend; q += 2) {
+      step(q, IC<0>{}, Tr{});
+      step(q + 1, IC<1>{}, Tr{});
     }
   };
-  const bool fast = yint && zint;
   if (w == 0) {
-    if (fast) march(IC<0>{}, std::false_type{});
+    if (yint) march(IC<0>{}, std::false_type{});
     else march(IC<0>{}, std::true_type{});
   } else if (w == WB - 1) {
-    if (fast) march(IC<2>{}, std::false_type{});
+    if (yint) march(IC<2>{}, std::false_type{});
     else march(IC<2>{}, std::true_type{});
   } else {
-    if (fast) march(IC<1>{}, std::false_type{});
+    if (yint) march(IC<1>{}, std::false_type{});
     else march(IC<1>{}, std::true_type{});
   }
   wait_vm0();

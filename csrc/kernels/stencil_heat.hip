@@ -329,10 +329,11 @@ static void launch_heat7_e(const Geo& g, const T* in, T* out, T r, double* resid
   constexpr int PF = sizeof(T) == 4 ? 1 : 2;
   // one block spans the whole row: the x neighbours at the block edge are the Dirichlet
   // boundary, so the block-edge loads vanish from the kernel.
-  if (g.nx > (int64_t)WXN * WX)
-    launch_heat7_t<T, RY, WXN, true, PF>(g, in, out, r, resid, s);
-  else
-    launch_heat7_t<T, RY, WXN, false, PF>(g, in, out, r, resid, s);
+  // (launch_heat7_ry picks fewer x waves only for rows that fit them: only 4-wave rows have edges)
+  if constexpr (WXN == 4) {
+    if (g.nx > (int64_t)WXN * WX) return launch_heat7_t<T, RY, WXN, true, PF>(g, in, out, r, resid, s);
+  }
+  launch_heat7_t<T, RY, WXN, false, PF>(g, in, out, r, resid, s);
 }
 
 template <class T, int RY>

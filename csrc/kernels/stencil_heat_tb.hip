@@ -656,10 +656,10 @@ static void launch_jacobi5_tbk_r(const Geo& g, const T* in, T* out, T r, int ste
 template <class T>
 void launch_jacobi5_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s,
                         bool ref_precision) {
-  if (sizeof(T) == 4 && ref_precision)
-    launch_jacobi5_tbk_r<T, true>(g, in, out, r, steps, resid, s);
-  else
-    launch_jacobi5_tbk_r<T, false>(g, in, out, r, steps, resid, s);
+  if constexpr (sizeof(T) == 4) {
+    if (ref_precision) return launch_jacobi5_tbk_r<T, true>(g, in, out, r, steps, resid, s);
+  }
+  launch_jacobi5_tbk_r<T, false>(g, in, out, r, steps, resid, s);
 }
 template void launch_jacobi5_tbk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t, bool);
 template void launch_jacobi5_tbk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t, bool);

@@ -3,8 +3,9 @@
 (or --transport ipc: device-resident faces through HIP IPC mailboxes, copy engines, no CUs).
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/heat3d_distributed.py --n 1024 --steps 200
-    torchrun --nproc-per-node 2 --master-addr 127.0.0.1 examples/heat3d_distributed.py --transport ipc
-        (on a one-GPU machine both ranks share cuda:0: only the ipc transport allows that)
+    torchrun --nproc-per-node 2 --master-addr 127.0.0.1 examples/heat3d_distributed.py --transport ipc --share-gpu
+        (on a one-GPU machine both ranks share cuda:0: only the ipc transport allows that, and only with
+        --share-gpu, a test mode)
     python examples/heat3d_distributed.py --n 128 --steps 20 --device cpu      # single process
 
 Prints the global residual every --report steps and the throughput at the end (rank 0). With
@@ -35,13 +36,15 @@ def main(argv=None):
     p.add_argument("--device", default="auto")
     p.add_argument("--checkpoint", default="")
     p.add_argument("--transport", default="auto", help="auto (rccl on GPUs, torch on CPUs) | rccl | ipc | torch")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="ipc: allow several ranks on one GPU (tests; the exchange assumes one process per GPU)")
     a = p.parse_args(argv)
     distributed = detect_env().world > 1
     if distributed:
         init_distributed()
     rank = dist.get_rank() if distributed else 0
     prob = m.heat3d(n=a.n, dtype=a.dtype)
-    kw = dict(transport=a.transport) if distributed else {}
+    kw = dict(transport=a.transport, share_gpu=a.share_gpu) if distributed else {}
     with m.Simulation(prob, device=a.device, distributed=distributed, residual_every=a.report, temporal=0,
                       **kw) as sim:
         sim.init()

@@ -54,7 +54,7 @@ def test_example_distributed_ipc_two_ranks_one_gpu(hip):
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
-        procs.append(subprocess.Popen(args + ["--transport", "ipc"], env=env, stdout=subprocess.PIPE,
+        procs.append(subprocess.Popen(args + ["--transport", "ipc", "--share-gpu"], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, cwd=ROOT))
     outs = [p.communicate(timeout=240) for p in procs]
     for p, (o, e) in zip(procs, outs):

@@ -75,10 +75,10 @@ def test_cli_ipc_two_processes_match_one(hip):
     through HIP IPC mailboxes): the printed Life board and the heat residual equal one process's."""
     life = os.path.join(BIN, "life")
     single = _run([life, "--print"], "12\n40\n50\n")
-    multi = _launch2([life, "--print", "--transport", "ipc"], "12\n40\n50\n")
+    multi = _launch2([life, "--print", "--transport", "ipc", "--share-gpu"], "12\n40\n50\n")
     assert multi == single
     args = [os.path.join(BIN, "mdfx"), "--stencil", "7", "--n", "96", "--steps", "9", "--json", "--residual-every", "9"]
     one = json.loads(_run(args))
-    two = json.loads([l for l in _launch2(args + ["--transport", "ipc"]).splitlines() if l.startswith("{")][0])
+    two = json.loads([l for l in _launch2(args + ["--transport", "ipc", "--share-gpu"]).splitlines() if l.startswith("{")][0])
     assert two["transport"] == "ipc" and two["ranks"] == 2
     assert abs(two["residual"] - one["residual"]) <= 1e-9 * one["residual"]
