@@ -449,6 +449,7 @@ void Solver::step(bool want_resid, int k) {
     // device spin wait alone, with no graph edge, so a replay that put the wait node on a queue ahead
     // of the sweep could spin until the watchdog; captured cycles use the boundary launch + event)
     const bool fold = bcs && !capturing_ && fold_ok(s, k);
+    if (fold) ++stats_.folded_sweeps;
     boundary_kernels(s, a, bs, fold);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)bs));
     if (opt_.sync_debug) s.be->sync_device();
@@ -783,6 +784,31 @@ static bool graph_debug() {
     if (graph_debug()) std::fprintf(stderr, "[mdfx graph] %s\n", msg); \
   } while (0)
 
+// The device spin-wait nodes of a captured graph, and among them those that wait on a slab's own
+// fold counters. Solver::step never folds while capturing (a fold wait is ordered after the interior
+// sweep by the spin alone, with no graph edge, so a replay that put it on a queue ahead of the sweep
+// would spin until the watchdog); this checks the captured graph itself (tests/test_gpu_ipc.py).
+void Solver::count_wait_nodes(void* graph) {
+  hipGraph_t g = (hipGraph_t)graph;
+  size_t n = 0;
+  HIPC(hipGraphGetNodes(g, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) HIPC(hipGraphGetNodes(g, nodes.data(), &n));
+  const void* wk = hip_counter_wait_kernel();
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    HIPC(hipGraphNodeGetType(nodes[i], &t));
+    if (t != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams p{};
+    HIPC(hipGraphKernelNodeGetParams(nodes[i], &p));
+    if (p.func != wk) continue;
+    ++stats_.graph_wait_nodes;
+    const uint64_t* remote = p.kernelParams ? *(const uint64_t* const*)p.kernelParams[0] : nullptr;
+    for (auto& s : slabs_)
+      if (s.sig && remote >= (const uint64_t*)s.sig && remote < (const uint64_t*)(s.sig + 128)) ++stats_.graph_fold_waits;
+  }
+}
+
 // Capture the cycle starting at buffer `parity` (== cur_): two sweeps of depth k. Nothing runs.
 void Solver::capture_graph(int parity, int k) {
   GDBG("capture begin");
@@ -841,6 +867,7 @@ void Solver::capture_graph(int parity, int k) {
   hipGraph_t g;
   GDBG("capture: end");
   HIPC(hipStreamEndCapture(origin, &g));
+  count_wait_nodes(g);
   GDBG("instantiate");
   hipGraphExec_t ex;
   HIPC(hipGraphInstantiateWithFlags(&ex, g, 0));

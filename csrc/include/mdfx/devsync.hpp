@@ -45,6 +45,8 @@ void hip_words_free(HipWords& w);
 // `own` is given, else the process-wide one); a timeout raises the matching error word.
 void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream,
                       uint64_t ahead = 0, const HipWords* own = nullptr);
+// The wait's kernel (its first argument is `remote`): the engine finds its nodes in captured graphs.
+const void* hip_counter_wait_kernel();
 
 // Tests: leave a quiet-NaN pattern in every CU's LDS (synchronous, current device), so a kernel
 // that reads LDS it never wrote produces NaN instead of silently using stale finite data.

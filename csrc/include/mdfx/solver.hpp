@@ -59,6 +59,11 @@ struct StepStats {
   int64_t residual_step = -1;
   int64_t graph_replays = 0;  // 2-sweep cycles replayed from a captured hipGraph
   int64_t graph_captures = 0;  // cycles captured + instantiated (prepare_graphs() or on demand)
+  int64_t folded_sweeps = 0;   // eager sweeps whose lower boundary ran inside the interior sweep
+  // device spin-wait nodes found in the captured graphs: all of them, and those that wait on a
+  // slab's own fold counters (a folded boundary inside a capture; must stay 0, see Solver::step)
+  int64_t graph_wait_nodes = 0;
+  int64_t graph_fold_waits = 0;
 };
 
 // The per-step schedule the engine runs for a layout and transport (Solver::boundary_on_cs and
@@ -170,6 +175,7 @@ class Solver {
   double sweep_cost(int k) const;  // relative time of a k-step sweep
   SweepCosts sweep_costs() const;  // the plan's inputs: max_depth(), sweep_cost(k), depth_ok_
   void capture_graph(int parity, int k);
+  void count_wait_nodes(void* graph);  // StepStats::graph_wait_nodes / graph_fold_waits of a capture
   void destroy_graph();
 
   StencilSpec spec_;

@@ -141,6 +141,8 @@ void hip_counter_signal(uint64_t* ctr, void* stream) {
   check_launch("counter_signal");
 }
 
+const void* hip_counter_wait_kernel() { return (const void*)&counter_wait_kernel; }
+
 void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream, uint64_t ahead,
                       const HipWords* own) {
   int* w = own ? own->dev : dev_words();

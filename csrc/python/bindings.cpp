@@ -480,6 +480,9 @@ PYBIND11_MODULE(_mdfx, m) {
       .def_property_readonly("residual_step", [](PySolver& p) { return p.chk().stats().residual_step; })
       .def_property_readonly("graph_replays", [](PySolver& p) { return p.chk().stats().graph_replays; })
       .def_property_readonly("graph_captures", [](PySolver& p) { return p.chk().stats().graph_captures; })
+      .def_property_readonly("folded_sweeps", [](PySolver& p) { return p.chk().stats().folded_sweeps; })
+      .def_property_readonly("graph_wait_nodes", [](PySolver& p) { return p.chk().stats().graph_wait_nodes; })
+      .def_property_readonly("graph_fold_waits", [](PySolver& p) { return p.chk().stats().graph_fold_waits; })
       .def("prepare_graphs", [](PySolver& p) { return p.chk().prepare_graphs(); },
            "capture both parities' 2-sweep hipGraph cycles now (0 if graphs are off / not capturable)")
       .def("sweep_plan", [](PySolver& p, int64_t steps) { return p.chk().sweep_plan(steps); }, py::arg("steps"),

@@ -256,6 +256,17 @@ class Simulation:
         return int(self._s.graph_captures)
 
     @property
+    def folded_sweeps(self) -> int:
+        """Eager sweeps whose lower boundary region ran inside the interior sweep (schedule 'folded')."""
+        return int(self._s.folded_sweeps)
+
+    @property
+    def graph_wait_nodes(self) -> tuple:
+        """(device spin-wait nodes in the captured graphs, those among them waiting on a slab's own
+        fold counters). The second is 0 by construction: captured cycles never fold."""
+        return int(self._s.graph_wait_nodes), int(self._s.graph_fold_waits)
+
+    @property
     def graph_eligible(self) -> bool:
         """Whether run() replays captured cycles in the current configuration."""
         return bool(self._s.graph_eligible)

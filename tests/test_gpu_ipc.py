@@ -41,7 +41,8 @@ with m.Simulation(prob, device="hip", distributed=True, transport=%(transport)r,
     g = sim.gather()
     if env.rank == 0:
         np.save(%(out)r, g)
-        json.dump({"residual": sim.residual, "nranks": sim.nranks}, open(%(out)r + ".json", "w"))
+        json.dump({"residual": sim.residual, "nranks": sim.nranks, "folded": sim.folded_sweeps,
+                   "captures": sim.graph_captures, "waits": sim.graph_wait_nodes}, open(%(out)r + ".json", "w"))
 dist.barrier()
 dist.destroy_process_group()
 """
@@ -133,7 +134,8 @@ def test_ipc_protocols_and_copy_engines(hip, tmp_path, transport, direct, world,
 @pytest.mark.parametrize("graph", [False, True])
 def test_ipc_fp64_fused_k4_folded(hip, tmp_path, graph):
     """fp64 K = 4 sweeps (heat7_wxk 2 + 1-row bands, the lower boundary folded into the interior
-    sweep) over three processes: bitwise equal to one process, residual included."""
+    sweep) over three processes: bitwise equal to one process, residual included. Eager runs fold;
+    captured cycles hold device spin-waits (the ipc exchange's) but none on a fold counter."""
     import mpi_cuda_process_amd as m
 
     prob_src = "m.heat3d(nx=256, ny=40, nz=50, dtype='f64')"
@@ -146,6 +148,10 @@ def test_ipc_fp64_fused_k4_folded(hip, tmp_path, graph):
     assert np.array_equal(np.load(out), ref)
     meta = json.load(open(out + ".json"))
     assert abs(meta["residual"] - rres) <= 1e-9 * rres
+    if graph:
+        assert meta["captures"] > 0 and meta["waits"][0] > 0 and meta["waits"][1] == 0, meta
+    else:
+        assert meta["folded"] > 0 and meta["captures"] == 0, meta
 
 
 @pytest.mark.parametrize("world,py,temporal,graph,transport,prob_src", [
