@@ -31,7 +31,7 @@ from mpi_cuda_process_amd.parallel.dist import init_distributed
 env = init_distributed("gloo")
 torch.cuda.set_device(0)
 prob = %(prob)s
-with m.Simulation(prob, device="hip", distributed=True, transport=%(transport)r, residual_every=4,
+with m.Simulation(prob, device="hip", distributed=True, transport=%(transport)r, residual_every=%(resid)d,
                   temporal=%(temporal)d, devices=[0], graph=%(graph)s, timeout_s=60.0, py=%(py)d,
                   share_gpu=True) as sim:
     assert sim.transport == %(transport)r, sim.transport
@@ -39,10 +39,12 @@ with m.Simulation(prob, device="hip", distributed=True, transport=%(transport)r,
     sim.run(%(steps)d)
     sim.synchronize()
     g = sim.gather()
+    st = torch.tensor([sim.folded_sweeps, sim.graph_captures, *sim.graph_wait_nodes], dtype=torch.int64)
+    dist.all_reduce(st, op=dist.ReduceOp.MAX)  # (rank 0 has no lower neighbour and never folds)
     if env.rank == 0:
         np.save(%(out)r, g)
-        json.dump({"residual": sim.residual, "nranks": sim.nranks, "folded": sim.folded_sweeps,
-                   "captures": sim.graph_captures, "waits": sim.graph_wait_nodes}, open(%(out)r + ".json", "w"))
+        json.dump({"residual": sim.residual, "nranks": sim.nranks, "folded": int(st[0]), "captures": int(st[1]),
+                   "waits": [int(st[2]), int(st[3])]}, open(%(out)r + ".json", "w"))
 dist.barrier()
 dist.destroy_process_group()
 """
@@ -81,6 +83,13 @@ def _spawn(world, argv_of, env_extra=None, timeout=180, expect_ok=True):
     return procs, outs
 
 
+def _resid(graph, steps):
+    # graph runs of 13 steps take a residual every 12, so their first sweeps form a non-residual
+    # stretch that is captured and replayed (every 4 would make every K = 4 sweep a residual sweep,
+    # which always runs eagerly); the last residual is step 12's either way, as in _reference
+    return 12 if graph and steps >= 13 else 4
+
+
 def _reference(prob, steps, temporal=1):
     import mpi_cuda_process_amd as m
 
@@ -100,13 +109,14 @@ def test_ipc_multiprocess_matches_single(hip, tmp_path, world, temporal, graph):
     out = str(tmp_path / "g.npy")
     steps = 13
     code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
-                         transport="ipc")
+                         resid=_resid(graph, steps), transport="ipc")
     _spawn(world, lambda r: [sys.executable, "-c", code])
     got = np.load(out)
     ref, rres = _reference(eval(prob_src), steps)
     assert np.array_equal(got, ref)
     meta = json.load(open(out + ".json"))
     assert meta["nranks"] == world and abs(meta["residual"] - rres) <= 1e-9 * rres
+    assert (meta["captures"] > 0) == graph, meta  # graph runs really replay
 
 
 @pytest.mark.parametrize("transport,direct,world,temporal,graph", [
@@ -121,7 +131,7 @@ def test_ipc_protocols_and_copy_engines(hip, tmp_path, transport, direct, world,
     out = str(tmp_path / "g.npy")
     steps = 13
     code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
-                         transport=transport)
+                         resid=_resid(graph, steps), transport=transport)
     _spawn(world, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_IPC_DIRECT": direct})
     import mpi_cuda_process_amd as m  # noqa: F401 (eval below)
 
@@ -129,6 +139,7 @@ def test_ipc_protocols_and_copy_engines(hip, tmp_path, transport, direct, world,
     assert np.array_equal(np.load(out), ref)
     meta = json.load(open(out + ".json"))
     assert abs(meta["residual"] - rres) <= 1e-9 * rres
+    assert (meta["captures"] > 0) == graph, meta
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -142,7 +153,7 @@ def test_ipc_fp64_fused_k4_folded(hip, tmp_path, graph):
     out = str(tmp_path / "g.npy")
     steps = 13
     code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=4, graph=graph, steps=steps,
-                         transport="ipc")
+                         resid=_resid(graph, steps), transport="ipc")
     _spawn(3, lambda r: [sys.executable, "-c", code])
     ref, rres = _reference(eval(prob_src), steps)
     assert np.array_equal(np.load(out), ref)
@@ -170,7 +181,7 @@ def test_ipc_pencils_match_single(hip, tmp_path, world, py, temporal, graph, tra
     out = str(tmp_path / "g.npy")
     steps = 11
     code = WORKER % dict(py=py, root=ROOT, prob=prob_src, out=out, temporal=temporal, graph=graph, steps=steps,
-                         transport=transport)
+                         resid=_resid(graph, steps), transport=transport)
     _spawn(world, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_IPC_DIRECT": "1"})
     ref, rres = _reference(eval(prob_src), steps)
     assert np.array_equal(np.load(out), ref)
@@ -184,7 +195,7 @@ def test_ipc_other_stencils(hip, tmp_path, prob_src):
     import mpi_cuda_process_amd as m
 
     out = str(tmp_path / "g.npy")
-    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=9, transport="ipc")
+    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=9, resid=4, transport="ipc")
     _spawn(3, lambda r: [sys.executable, "-c", code])
     ref, _ = _reference(eval(prob_src), 9)
     assert np.array_equal(np.load(out), ref)
