@@ -243,7 +243,8 @@ def test_ipc_dead_peer_is_an_error_not_a_hang(hip, tmp_path):
     reports a transport failure and exits non-zero instead of hanging."""
     out = str(tmp_path / "g.npy")
     code = WORKER.replace("timeout_s=60.0", "timeout_s=5.0") % dict(
-        py=1, root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=40, transport="ipc")
+        py=1, root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=40, resid=4,
+        transport="ipc")
     t0 = time.time()
     procs, outs = _spawn(2, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_FAULT": "exit@1:3"},
                          timeout=150, expect_ok=False)
@@ -288,7 +289,7 @@ def test_ipc_refuses_two_engine_processes_on_one_gpu(hip, tmp_path):
     out = str(tmp_path / "g.npy")
     code = WORKER.replace(",\n                  share_gpu=True)", ")") % dict(
         py=1, root=ROOT, prob="m.heat3d(nx=128, ny=32, nz=40)", out=out, temporal=1, graph=False, steps=4,
-        transport="ipc")
+        resid=4, transport="ipc")
     assert "share_gpu" not in code
     t0 = time.time()
     procs, outs = _spawn(2, lambda r: [sys.executable, "-c", code], timeout=120, expect_ok=False)
