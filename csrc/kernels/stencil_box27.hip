@@ -224,11 +224,9 @@ template <class T>
 void launch_box27(const Geo& g, const T* in, T* out, const StencilCoef& c, double* resid,
                   hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  // 2 rows per tile, 1 on short columns
-  if (g.ny < 8)
-    launch_box27_ry<T, 1>(g, in, out, c, resid, s);
-  else
-    launch_box27_ry<T, 2>(g, in, out, c, resid, s);
+  // 2 rows per tile (short columns too: a 1-row copy for ny < 8 was dropped in round 5 with the
+  // other rarely reached instances, libmdfx.so size)
+  launch_box27_ry<T, 2>(g, in, out, c, resid, s);
 }
 template void launch_box27<float>(const Geo&, const float*, float*, const StencilCoef&, double*,
                                   hipStream_t);

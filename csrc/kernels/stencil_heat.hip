@@ -354,12 +354,11 @@ void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStre
   // defaults from bench/kernel_ab.py on MI355X, 1024^3 fp32 (profiles/r01_ab_heat7_f32.json):
   // RY=2 PF=1 1.546 ms (694.5 GCells/s) > RY=4 PF=1 1.584 > RY=4 PF=2 1.603 > RY=2 PF=2 1.662
   // fp64 1024^3: RY=4 PF=2 3.395 ms (316 GCells/s) > RY=4 PF=1 3.415 > RY=2 PF=1 3.479
-  // (profiles/r01_ab_heat7_f64.json); one row on short columns.
+  // (profiles/r01_ab_heat7_f64.json).
+  // (short columns take the same tiles: a 1-row copy for ny < 8 was dropped in round 5 with the other
+  // rarely reached instances, libmdfx.so size)
   constexpr int RY = sizeof(T) == 4 ? 2 : 4;
-  if (g.ny < 8)
-    launch_heat7_ry<T, 1>(g, in, out, r, resid, s);
-  else
-    launch_heat7_ry<T, RY>(g, in, out, r, resid, s);
+  launch_heat7_ry<T, RY>(g, in, out, r, resid, s);
 }
 template void launch_heat7<float>(const Geo&, const float*, float*, float, double*, hipStream_t);
 template void launch_heat7<double>(const Geo&, const double*, double*, double, double*, hipStream_t);
