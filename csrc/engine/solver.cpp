@@ -441,8 +441,14 @@ void Solver::step(bool want_resid, int k) {
     }
     // boundary planes of this step, after the previous interior sweep (same stream with bcs) and,
     // with bcs, after the previous exchange
-    if (bcs) s.be->wait(s.cs, s.ev_x);
-    else s.be->wait(s.hs, s.ev_int);
+    // (a single slab has no neighbour: its exchange moves nothing and the compute stream waits on
+    // nothing; the cross-stream event wait alone put ~12 us between consecutive N = 1 sweeps,
+    // profiles/r05_session_g2/prof_driver_kernel_trace.csv)
+    if (bcs) {
+      if (nranks_ > 1) s.be->wait(s.cs, s.ev_x);
+    } else {
+      s.be->wait(s.hs, s.ev_int);
+    }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)bs));
     a.resid = want_resid ? s.resid : nullptr;
     // (never inside a capture: the folded exchange is ordered after the interior sweep's stores by a
@@ -488,7 +494,7 @@ void Solver::step(bool want_resid, int k) {
   if (!slabs_.empty()) slabs_[0].be->trace_push("mdfx.exchange");
   transport_->exchange(nb);
   if (!slabs_.empty()) slabs_[0].be->trace_pop();
-  if (bcs)
+  if (bcs && nranks_ > 1)
     for (auto& s : slabs_) s.be->record(s.ev_x, s.hs);
   if (prof_hip) {
     Slab& s0 = slabs_[0];
