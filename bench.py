@@ -225,7 +225,7 @@ def pick_temporal(a, prob, nslab, hip):
     want = native().hip_fused_depth(prob.kind, prob.dtype, prob.nx, prob.ref_precision) if hip else \
         {"jacobi5": 8, "life": 12}.get(a.stencil, 2)
     while want > 1 and prob.nz < 4 * want * nslab:
-        want = 2 if want == 3 else want // 2
+        want = {5: 4, 3: 2}.get(want, want // 2)
     if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz,
                                                             want, want, prob.ref_precision)):
         return want

@@ -71,7 +71,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx);
 // (the engine's sweep plan minimises the sum over a residual stretch).
 double hip_sweep_cost(const StencilSpec& spec, int64_t nx, int steps);
 // One step shallower than `steps` among the fused depths (12 -> 6 -> 3 -> 2 -> 1).
-inline int shallower_depth(int steps) { return steps == 3 ? 2 : steps / 2; }
+inline int shallower_depth(int steps) { return steps == 5 ? 4 : steps == 3 ? 2 : steps / 2; }
 
 enum class InitKind : int {
   Constant = 0,   // every cell = value

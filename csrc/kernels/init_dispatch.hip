@@ -61,9 +61,9 @@ double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt; heat7_tbk's K = 3 / 4 were
 // removed in round 5)
 static bool use_wxk(DType dt, int64_t nx, int steps);
+// (fp32 K = 5: heat7_wxk only, in rows of 2 cells per lane)
 static bool use_wtk(int steps, DType dt) {
-  (void)dt;
-  return heat7_wtk_supported(steps);
+  return heat7_wtk_supported(steps) || (dt == DType::F32 && steps == 5);
 }
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
 // 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
@@ -73,7 +73,7 @@ static bool use_wtk(int steps, DType dt) {
 // 2 + 1-row bands (heat7_wtk's K = 4 needs 1-row waves: 1024^3 1112-1124 vs 418 GCells/s,
 // profiles/r04_session_o/)
 static bool use_wxk(DType dt, int64_t nx, int steps) {
-  return knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (dt == DType::F32 || nx >= 2048 || steps == 4));
+  return steps >= 5 || knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (dt == DType::F32 || nx >= 2048 || steps == 4));
 }
 
 static int env_int(const char* name, int dflt) {
@@ -270,7 +270,8 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
 }
 
 bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int steps) {
-  return !lay.pencil() && spec.kind == StencilKind::Heat7 && (steps == 3 || steps == 4) && lay.halo >= steps &&
+  return !lay.pencil() && spec.kind == StencilKind::Heat7 &&
+         (steps == 3 || steps == 4 || (steps == 5 && spec.dtype == DType::F32)) && lay.halo >= steps &&
          dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx, steps);
 }
 
@@ -294,8 +295,14 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // where heat7_wxk runs: its per-wave rows no longer grow with K, so the fourth step per pass
       // costs less than the HBM pass it saves (fp32; fp64 in round 4: 512^3 983 vs 740 GCells/s at
       // K = 3, 1024^3 1121 vs 885, 2048^3 + residual every 12 953 vs 890, profiles/r04_session_{o,p}/)
-      if (nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66)
+      // fp32 K = 5 (round 5): heat7_wxk in rows of 2 cells per lane (RowOps2f), whose half-size
+      // rows leave room for the fifth level: 1024^3 2689 vs 2426 GCells/s at K = 4 in one process,
+      // 1024^2 x 256 2639 vs 2399, x 128 2536 vs 2384, 768^3 2349 vs 1954, 512^3 2187 vs 2039,
+      // 2048^2 x 512 2166 vs 2144 (profiles/r05_session_t/, r05_session_u/)
+      if (nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66) {
+        if (spec.dtype == DType::F32 && dev::knobs().h7_wxk != 0) return 5;
         return dev::use_wxk(spec.dtype, nx, 4) ? 4 : 3;
+      }
       return 2;
   }
   return 1;
@@ -308,9 +315,11 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
 // fewest sweeps with the deepest first.
 double hip_sweep_cost(const StencilSpec& spec, int64_t nx, int steps) {
   if (steps <= 1) return 1.0;
-  if (spec.kind == StencilKind::Heat7 && steps <= 4 && nx >= 1024) {
-    static const double f32[5] = {0.0, 1.0, 1.07, 1.10, 1.18};
-    static const double f64[5] = {0.0, 1.0, 1.27, 1.18, 1.25};
+  if (spec.kind == StencilKind::Heat7 && steps <= 5 && nx >= 1024) {
+    // (fp32 K = 5 from the round-5 rates 1929 / 2399 / 2639 GCells/s for K = 3 / 4 / 5 at 1024^2 x
+    // 256, scaled to the K = 4 entry; fp64 has no 5-step sweep)
+    static const double f32[6] = {0.0, 1.0, 1.07, 1.10, 1.18, 1.34};
+    static const double f64[6] = {0.0, 1.0, 1.27, 1.18, 1.25, 1.6};
     return (spec.dtype == DType::F64 ? f64 : f32)[steps];
   }
   return 1.0 + 0.05 * (steps - 1);

@@ -355,5 +355,44 @@ struct RowOpsN {
   static __device__ __forceinline__ void pin_nv(Row& r) { asm("" : "+v"(r.p), "+v"(r.q)); }
 };
 
+// fp32 rows of 2 cells per lane (one 8-B vector; heat7_wxk's 5-step sweep): half the registers per
+// row of RowOpsN at the same issue count per cell (2 x adds, both with the neighbour lane's cell as
+// a DPP operand, + 6 packed ops per row update), so a wave holds the rows of a fifth level
+static constexpr int kRowOps2 = 2;
+struct RowOps2f {
+  typedef float T2 __attribute__((ext_vector_type(2)));
+  typedef T2 V;
+  struct Row {
+    T2 v;
+  };
+  static __device__ __forceinline__ Row fromv(const V& v) { return Row{v}; }
+  static __device__ __forceinline__ Row zero() { return Row{T2{0.f, 0.f}}; }
+  static __device__ __forceinline__ float first(const Row& c) { return c.v.x; }
+  static __device__ __forceinline__ float last(const Row& c) { return c.v.y; }
+  // (((xm + xp) + ym) + yp) + zm; l / rr are the cells beyond the slice's ends
+  static __device__ __forceinline__ Row partial(const Row& c, float l, float rr, const Row& ym, const Row& yp,
+                                                const Row& zm) {
+    Row s;
+    s.v.x = l + c.v.y;
+    s.v.y = c.v.x + rr;
+    s.v = ((s.v + ym.v) + yp.v) + zm.v;
+    return s;
+  }
+  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    const T2 m6 = T2{-6.f, -6.f};
+    return Row{__builtin_elementwise_fma(rc.v, __builtin_elementwise_fma(m6, c.v, S.v + zp.v), c.v)};
+  }
+  static __device__ __forceinline__ Row coef(float r, const bool* held) {
+    return Row{T2{held[0] ? 0.f : r, held[1] ? 0.f : r}};
+  }
+  static __device__ __forceinline__ Row scale(const Row& x, float s) { return Row{x.v * T2{s, s}}; }
+  static __device__ __forceinline__ float get(const Row& c, int e) { return e == 0 ? c.v.x : c.v.y; }
+  static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
+  // (as RowOpsN::pin: the row is formed where it is computed, so the lane shifts fold into the
+  // adds as DPP operands; a non-volatile pin that lets rows interleave measured the same, +0.4-0.8 %
+  // in the kernel A/B, profiles/r05_session_w/)
+  static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.v)); }
+};
+
 }  // namespace dev
 }  // namespace mdfx

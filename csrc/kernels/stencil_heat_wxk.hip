@@ -1,6 +1,6 @@
 // Deep temporal blocking for the 3D 7-point stencil with the y halo EXCHANGED between the waves of
-// a band instead of recomputed (heat7_wxk): K = 3 or 4 fused steps per sweep, one block barrier
-// per plane, bitwise equal to K single steps.
+// a band instead of recomputed (heat7_wxk): K = 3 or 4 fused steps per sweep (fp32 also K = 5, in
+// rows of 2 cells per lane), one block barrier per plane, bitwise equal to K single steps.
 //
 // heat7_wtk (stencil_heat_wtk.hip) makes every wave of a y band compute the RY + 2(K-l) rows that
 // its own level l+1 needs: at K = 3, 3-row waves, 15 row updates per plane for 9 output rows. Most
@@ -86,13 +86,19 @@ __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles,
 // SIG: the folded-boundary copy (Geo::sig): the blocks of the chunks starting at lz_begin publish their
 // output planes [lz_begin, sig_z) and signal, so the halo exchange of the lower face overlaps the
 // rest of the same sweep (no separate boundary launch for that face).
-template <class T, int RY, int RE, int K, int WB, bool RES, bool PEN = false, bool SIG = false>
+// CN = kRowOps2: fp32 rows of 2 cells per lane (RowOps2f; the 5-step sweep), the window filled by
+// 4-byte LDS DMAs (an x segment of 2-cell lanes starts 2 cells off a 16-B vector, so neither a 16-B
+// nor an 8-B DMA lane would line up with the grid's column 0).
+template <class T, int RY, int RE, int K, int WB, bool RES, bool PEN = false, bool SIG = false, int CN = 0>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
-  using V = typename VT<T>::type;
-  using RO = typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type;
+  constexpr bool NAR = CN == kRowOps2;
+  static_assert(!NAR || sizeof(T) == 4, "heat7_wxk: 2-cell lanes are fp32");
+  using RO = typename std::conditional<NAR, RowOps2f,
+                                       typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type>::type;
+  using V = typename RO::V;
   using Row = typename RO::Row;
-  constexpr int N = VT<T>::N;
+  constexpr int N = NAR ? 2 : VT<T>::N;
   constexpr int OV = (K + N - 1) / N;     // overlap lanes per side
   constexpr int SEG = (64 - 2 * OV) * N;  // owned columns per wave
   constexpr int BR = 2 * RE + (WB - 2) * RY;  // output rows of a band
@@ -155,6 +161,13 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
   // read the nearest valid row / vector. Wave w fetches rows w, w + WB, ... of the window.
   const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
+  // (2-cell lanes: the window row's two 64-cell halves, one cell per lane each)
+  uint32_t xch[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t xh = xs + h * 64 + lane;
+    xch[h] = (uint32_t)((xh < 0 ? 0 : xh >= pitch ? pitch - 1 : xh) * (int64_t)sizeof(T));
+  }
   auto issue = [&](int lz, int buf) {
     const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
 #pragma unroll
@@ -167,9 +180,18 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         // 32-bit lane-offset form instead of a 64-bit VGPR address per row held across the loop
         uint64_t rb = (uint64_t)(uintptr_t)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
         asm volatile("" : "+s"(rb));
-        const T* a = (const T*)((const char*)(uintptr_t)rb + xcb);
-        dcheck(g, in, a, N);
-        glds16(a, &win[buf][k][0]);
+        if constexpr (NAR) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const T* a = (const T*)((const char*)(uintptr_t)rb + xch[h]);
+            dcheck(g, in, a, 1);
+            glds4(a, (T*)&win[buf][k][0] + h * 64);
+          }
+        } else {
+          const T* a = (const T*)((const char*)(uintptr_t)rb + xcb);
+          dcheck(g, in, a, N);
+          glds16(a, &win[buf][k][0]);
+        }
       }
     }
   };
@@ -192,7 +214,10 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   constexpr int WIN_BUF = RB * 64;  // V elements per window buffer
   constexpr int SEAM_PAR = (K - 1) * (WB - 1) * 2 * 64, SEAM_LVL = (WB - 1) * 2 * 64;
   auto st = [](LV* p, const V& v) {
-    asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+    if constexpr (sizeof(V) == 16)
+      asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
+    else
+      asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
 
   auto march = [&](auto role_c, auto edge_c) __attribute__((always_inline)) {
@@ -371,9 +396,9 @@ struct WxGeo {
   int XT = 0, YT = 0, zc = 0;
   int64_t ntasks = 0, resident = 0, rounds = 0;
 };
-template <class T, int RY, int RE, int K, int WB>
+template <class T, int RY, int RE, int K, int WB, int CN = 0>
 static WxGeo wxk_geo(const Geo& g) {
-  constexpr int N = VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  constexpr int N = CN == kRowOps2 ? 2 : VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   constexpr int BR = 2 * RE + (WB - 2) * RY;
   WxGeo w;
   const int64_t planes = g.lz_end - g.lz_begin;
@@ -381,7 +406,7 @@ static WxGeo wxk_geo(const Geo& g) {
   w.XT = (int)((g.nx + SEG - 1) / SEG);
   w.YT = (int)((g.ly_end - g.ly_begin + BR - 1) / BR);
   const int64_t tiles = (int64_t)w.XT * w.YT;
-  w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false>, 64 * WB);
+  w.resident = resident_blocks((const void*)&heat7_wxk<T, RY, RE, K, WB, false, false, false, CN>, 64 * WB);
   // (2-wave strip bands: the strip is on the sweep's critical path, before the exchange; chunks down
   // to K planes spread its few tiles over the device)
   w.zc = wx_zc(planes, tiles, w.resident, K, 2 * K, g.min_rounds, WB == 2 ? K : 0);
@@ -392,9 +417,11 @@ static WxGeo wxk_geo(const Geo& g) {
   return w;
 }
 
-template <class T, int RY, int RE, int K, int WB>
+static bool pen_geo(const Geo& g) { return g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny; }
+
+template <class T, int RY, int RE, int K, int WB, int CN = 0>
 static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  const WxGeo wg = wxk_geo<T, RY, RE, K, WB>(g);
+  const WxGeo wg = wxk_geo<T, RY, RE, K, WB, CN>(g);
   const int XT = wg.XT, YT = wg.YT, zc = wg.zc;
   // only the blocks of the first z chunk signal: it must hold every plane the signal covers (a
   // chunk shorter than that would leave the halo stream waiting for a signal never sent)
@@ -404,30 +431,42 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   const int64_t ntasks = wg.ntasks;
   MDFX_CHECK(ntasks < (int64_t)1 << 31, "heat7_wxk: too many tasks");
   const dim3 grd((unsigned)ntasks), blk(64 * WB);
-  const bool pen = g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny;
+  const bool pen = pen_geo(g);
   // one instance per (residual, pencil rows, folded-boundary signal) combination the engine uses
   auto go = [&](auto res_c, auto pen_c, auto sig_c) {
     hipLaunchKernelGGL((heat7_wxk<T, RY, RE, K, WB, decltype(res_c)::value, decltype(pen_c)::value,
-                                  decltype(sig_c)::value>),
+                                  decltype(sig_c)::value, CN>),
                        grd, blk, 0, s, in, out, g, r, zc, XT, YT, (int)ntasks, resid);
   };
   using F = std::false_type;
   using Tr = std::true_type;
-  if constexpr (WB != 8) {
-    MDFX_CHECK(!g.sig, "heat7_wxk: folded boundaries run in bands of 8 waves");
-  } else if (g.sig) {
-    MDFX_CHECK(!pen && g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
-    if (resid) go(Tr{}, F{}, Tr{});
-    else go(F{}, F{}, Tr{});
-    return;
+  if constexpr (CN != 0) {  // (the 5-step 2-cell-lane sweep: slabs, with or without the folded boundary)
+    MDFX_CHECK(!pen, "heat7_wxk: the 5-step sweep is for slabs");
+    if (g.sig) {
+      MDFX_CHECK(g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
+      if (resid) go(Tr{}, F{}, Tr{});
+      else go(F{}, F{}, Tr{});
+    } else {
+      if (resid) go(Tr{}, F{}, F{});
+      else go(F{}, F{}, F{});
+    }
+  } else {
+    if constexpr (WB != 8) {
+      MDFX_CHECK(!g.sig, "heat7_wxk: folded boundaries run in bands of 8 waves");
+    } else if (g.sig) {
+      MDFX_CHECK(!pen && g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
+      if (resid) go(Tr{}, F{}, Tr{});
+      else go(F{}, F{}, Tr{});
+      return;
+    }
+    if (resid) {
+      if (pen) go(Tr{}, Tr{}, F{});
+      else go(Tr{}, F{}, F{});
+      return;
+    }
+    if (pen) go(F{}, Tr{}, F{});
+    else go(F{}, F{}, F{});
   }
-  if (resid) {
-    if (pen) go(Tr{}, Tr{}, F{});
-    else go(Tr{}, F{}, F{});
-    return;
-  }
-  if (pen) go(F{}, Tr{}, F{});
-  else go(F{}, F{}, F{});
 }
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -448,10 +487,16 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 // sweep, 3 window buffers /
 // one seam table) measured slower and were removed in round 4; their numbers stay in
 // profiles/r03_wxk/ and profiles/r03_session_r/.
+// fp32 K = 5 (round 5): rows of 2 cells per lane (RowOps2f: half the registers per row, so a fifth
+// level fits), 5 + 4-row bands of 8 waves (38 rows; 9 x segments of 116 columns x 27 bands = 243
+// tiles at 1024 cells, one round; 245 VGPRs). 1024^3 kernel A/B 2689 vs 2426 GCells/s for K = 4,
+// 768^3 2349 vs 1954, 512^3 2187 vs 2039, 1024^2 x 128 2536 vs 2384 (profiles/r05_session_t/,
+// r05_session_u/); 6 + 1-row bands measured 3 % slower; K = 6 spills in every band that fits one
+// round.
 template <class T>
 void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  MDFX_CHECK((steps == 3 || steps == 4) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+  MDFX_CHECK((steps >= 3 && steps <= (sizeof(T) == 4 ? 5 : 4)) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_wxk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
@@ -471,6 +516,10 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
     return;
   }
   if constexpr (sizeof(T) == 4) {
+    if (steps == 5) {
+      launch_wxk<T, 5, 4, 5, 8, kRowOps2>(g, in, out, r, resid, s);
+      return;
+    }
     if (steps == 3) launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
     else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
   } else {

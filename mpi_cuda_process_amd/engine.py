@@ -52,7 +52,7 @@ def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1) -> in
         return want if problem.nz >= 4 * want * pz and problem.ny >= 4 * want * py else 1
     want = native().hip_fused_depth(problem.kind, problem.dtype, problem.nx, problem.ref_precision)
     while want > 1 and problem.nz < 4 * want * nranks:
-        want = 2 if want == 3 else want // 2
+        want = {5: 4, 3: 2}.get(want, want // 2)
     if want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                                 want, want, problem.ref_precision):
         return want

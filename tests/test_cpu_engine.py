@@ -553,22 +553,23 @@ def test_mdf_ref_precision_at_power_of_two_rate_is_bitwise_fp32(mdfx, r):
 def test_fused_depth_policy(mdfx):
     """hip_fused_depth: the measured-win fused depth per stencil and row width (host-side policy,
     profiles/r02_wtk/README.txt, r03_wtk/, r03_wxk/): for the 3D 7-point where the x segments cover
-    at least 2/3 of the lane cells (rows of 512 cells and more) K = 4 through heat7_wxk (fp32 and
-    fp64), 2 below; the 27-point 3 (box27_wxk) in fp64, at fp32 rows of 257..512 cells (whole-row
+    at least 2/3 of the lane cells (rows of 512 cells and more) K = 5 through heat7_wxk in fp32
+    (2-cell lanes) and K = 4 in fp64, 2 below; the 27-point 3 (box27_wxk) in fp64, at fp32 rows of 257..512 cells (whole-row
     blocks) and of 1024 cells and more, else 2;
-    8 / 12 for the 2D stencils; auto_temporal makes it shallower for thin slabs (4 -> 2 -> 1,
+    8 / 12 for the 2D stencils; auto_temporal makes it shallower for thin slabs (5 -> 4 -> 2 -> 1,
     3 -> 2 -> 1)."""
     import mpi_cuda_process_amd as m
     from mpi_cuda_process_amd.engine import auto_temporal
 
     d = m.native().hip_fused_depth
-    assert d("heat7", "f32", 1024) == 4 and d("heat7", "f64", 1024) == 4
-    assert d("heat7", "f32", 2048) == 4 and d("heat7", "f64", 2048) == 4 and d("heat7", "f32", 3072) == 4
-    assert d("heat7", "f32", 512) == 4 and d("heat7", "f32", 256) == 2 and d("heat7", "f64", 512) == 4
+    assert d("heat7", "f32", 1024) == 5 and d("heat7", "f64", 1024) == 4
+    assert d("heat7", "f32", 2048) == 5 and d("heat7", "f64", 2048) == 4 and d("heat7", "f32", 3072) == 5
+    assert d("heat7", "f32", 512) == 5 and d("heat7", "f32", 256) == 2 and d("heat7", "f64", 512) == 4
     assert d("box27", "f32", 512) == 3 and d("box27", "f32", 1024) == 3 and d("box27", "f64", 512) == 3
     assert d("box27", "f32", 256) == 2 and d("box27", "f32", 768) == 2
     assert d("jacobi5", "f32", 16384) == 8 and d("life", "u8", 32768) == 12
-    assert auto_temporal(m.heat3d(n=1024), 8, "hip") == 4       # 128-plane slabs: 4 steps per sweep
+    assert auto_temporal(m.heat3d(n=1024), 8, "hip") == 5       # 128-plane slabs: 5 steps per sweep
+    assert auto_temporal(m.heat3d(nx=1024, ny=64, nz=152), 8, "hip") == 4   # 19-plane slabs: 5 -> 4
     assert auto_temporal(m.heat3d(n=1024, dtype="f64"), 8, "hip") == 4
     assert auto_temporal(m.heat3d(n=512, dtype="f64"), 8, "hip") == 4
     assert auto_temporal(m.heat3d(nx=1024, ny=64, nz=64), 8, "hip") == 2   # 8-plane slabs

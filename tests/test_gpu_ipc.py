@@ -165,6 +165,29 @@ def test_ipc_fp64_fused_k4_folded(hip, tmp_path, graph):
         assert meta["folded"] > 0 and meta["captures"] == 0, meta
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_ipc_fp32_fused_k5_folded(hip, tmp_path, graph):
+    """fp32 K = 5 sweeps (the default depth of the 3D 7-point: heat7_wxk in rows of 2 cells per lane,
+    the lower boundary folded into the interior sweep) over three processes: bitwise equal to one
+    process, residual included; eager runs fold, captured cycles never wait on a fold counter."""
+    import mpi_cuda_process_amd as m
+
+    prob_src = "m.heat3d(nx=300, ny=45, nz=66)"
+    out = str(tmp_path / "g.npy")
+    steps = 20  # (residual every 10 / 20: K = 5 sweeps throughout, the last residual step 20's as in _reference)
+    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=5, graph=graph, steps=steps,
+                         resid=20 if graph else 10, transport="ipc")
+    _spawn(3, lambda r: [sys.executable, "-c", code])
+    ref, rres = _reference(eval(prob_src), steps)
+    assert np.array_equal(np.load(out), ref)
+    meta = json.load(open(out + ".json"))
+    assert abs(meta["residual"] - rres) <= 1e-9 * rres
+    if graph:
+        assert meta["captures"] > 0 and meta["waits"][0] > 0 and meta["waits"][1] == 0, meta
+    else:
+        assert meta["folded"] > 0 and meta["captures"] == 0, meta
+
+
 @pytest.mark.parametrize("world,py,temporal,graph,transport,prob_src", [
     (4, 2, 4, False, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),   # 2 x 2 pencils, the fused K = 4 sweep
     (4, 2, 3, True, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),    # ... K = 3, replayed

@@ -51,19 +51,23 @@ def test_lds_never_limits_occupancy(recs):
 @pytest.mark.parametrize("name,min_waves", [
     # the shipped headline sweep: 1024^3 fp32, 4 fused steps, 3 + 2-row bands of 8 waves (one 512-thread
     # block per CU: 2 waves per SIMD is all a block of 8 waves can have)
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, false>", 2),
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, true, false>", 2),   # its pencil copy
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, true>", 2),   # folded-boundary copy (N > 1)
-    ("mdfx::dev::heat7_wxk<float, 2, 2, 4, 2, false, true, false>", 2),   # pencil y strips (2-wave bands)
-    ("mdfx::dev::heat7_wxk<double, 2, 2, 3, 2, false, true, false>", 2),
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, true>", 2),
-    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, false>", 2),         # its residual sweeps
-    ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false, false, false>", 2),        # K = 3 (step-count remainders)
-    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false, false, false>", 2),       # fp64 K = 3 (2048^3 + residual)
-    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true, false, false>", 2),
-    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, false>", 2),       # fp64 K = 4 (the default from 1024-cell rows)
-    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, true, false, false>", 2),
-    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, true>", 2),        # its folded-boundary copy
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, false, 0>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, true, false, 0>", 2),   # its pencil copy
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, true, 0>", 2),   # folded-boundary copy (N > 1)
+    ("mdfx::dev::heat7_wxk<float, 2, 2, 4, 2, false, true, false, 0>", 2),   # pencil y strips (2-wave bands)
+    ("mdfx::dev::heat7_wxk<double, 2, 2, 3, 2, false, true, false, 0>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, true, 0>", 2),
+    ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, false, 0>", 2),         # its residual sweeps
+    ("mdfx::dev::heat7_wxk<float, 5, 4, 5, 8, false, false, false, 2>", 2),        # fp32 K = 5 (2-cell lanes): the default
+    ("mdfx::dev::heat7_wxk<float, 5, 4, 5, 8, true, false, false, 2>", 2),
+    ("mdfx::dev::heat7_wxk<float, 5, 4, 5, 8, false, false, true, 2>", 2),         # its folded-boundary copy
+    ("mdfx::dev::heat7_wxk<float, 5, 4, 5, 8, true, false, true, 2>", 2),
+    ("mdfx::dev::heat7_wxk<float, 4, 4, 3, 8, false, false, false, 0>", 2),        # K = 3 (step-count remainders)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, false, false, false, 0>", 2),       # fp64 K = 3 (2048^3 + residual)
+    ("mdfx::dev::heat7_wxk<double, 3, 1, 3, 8, true, false, false, 0>", 2),
+    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, false, 0>", 2),       # fp64 K = 4 (the default from 1024-cell rows)
+    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, true, false, false, 0>", 2),
+    ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, true, 0>", 2),        # its folded-boundary copy
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false, 0>", 2),              # 27-point K = 3 (1024-cell rows, fp64)
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, false, 2>", 2),              # fp32 rows <= 512: whole-row blocks
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, true, 2>", 2),
@@ -92,7 +96,7 @@ def test_headline_sweep_keeps_its_memory_waits():
     # 13 places; round 4's pencil row bounds, compiled into the same kernel, made it 19 (six waits in
     # front of window LDS reads: the sweep lost 3-4 %, profiles/r04_session_c/summary.txt). The
     # slab and pencil copies are separate instances now: pin the slab one's count.
-    isa = kernel_isa(LIB, "_ZN4mdfx3dev9heat7_wxkIfLi3ELi2ELi4ELi8ELb0ELb0ELb0E")
+    isa = kernel_isa(LIB, "_ZN4mdfx3dev9heat7_wxkIfLi3ELi2ELi4ELi8ELb0ELb0ELb0ELi0E")
     assert len(isa) == 1, sorted(isa)
     body = next(iter(isa.values()))
     assert len(body) > 5000
@@ -100,10 +104,22 @@ def test_headline_sweep_keeps_its_memory_waits():
     assert n0 <= 13, n0
 
 
+def test_k5_sweep_keeps_its_memory_waits():
+    # the fp32 K = 5 sweep (2-cell lanes, 4-byte window DMAs) and its folded-boundary copy: the same
+    # 13 full vector-memory waits as the K = 4 sweep (none in front of the window reads)
+    for mangled in ("_ZN4mdfx3dev9heat7_wxkIfLi5ELi4ELi5ELi8ELb0ELb0ELb0ELi2E",
+                    "_ZN4mdfx3dev9heat7_wxkIfLi5ELi4ELi5ELi8ELb0ELb0ELb1ELi2E"):
+        isa = kernel_isa(LIB, mangled)
+        assert len(isa) == 1, sorted(isa)
+        body = next(iter(isa.values()))
+        n0 = sum(1 for l in body if l.startswith("s_waitcnt") and "vmcnt(0)" in l)
+        assert n0 <= 13, (mangled, n0)
+
+
 def test_folded_boundary_copy_keeps_the_sweep_loop():
     # the folded-boundary copy adds one out-of-line signal call; its plane loop must keep the same
     # memory waits as the plain sweep (13 vmcnt(0))
-    isa = kernel_isa(LIB, "_ZN4mdfx3dev9heat7_wxkIfLi3ELi2ELi4ELi8ELb0ELb0ELb1E")
+    isa = kernel_isa(LIB, "_ZN4mdfx3dev9heat7_wxkIfLi3ELi2ELi4ELi8ELb0ELb0ELb1ELi0E")
     assert len(isa) == 1, sorted(isa)
     body = next(iter(isa.values()))
     n0 = sum(1 for l in body if l.startswith("s_waitcnt") and "vmcnt(0)" in l)
