@@ -24,10 +24,11 @@ The grid is fixed as N grows (strong scaling, the BASELINE.json config "3D 7-pt 
 slab-decomposed across 8xMI355X"). Data is synthetic: a uniform random initial grid generated on
 the device from a counter-based hash of the global cell index (seed 1). Every timed step is a full
 Jacobi update of every cell (boundary planes + halo exchange + interior), nothing is skipped or
-cached. By default four consecutive Jacobi steps are fused into one pass over memory (temporal
-blocking, --temporal 4 through heat7_wxk at 1024-cell rows; bitwise identical to four single
-steps, tests/test_gpu_temporal.py): every step is still computed in full, the fused kernel keeps
-u^{t+1}..u^{t+3} on chip. A step count that is not a multiple of 4 ends with a shorter fused sweep.
+cached. By default five consecutive Jacobi steps are fused into one pass over memory (temporal
+blocking, --temporal 5 through heat7_wxk in rows of 2 cells per lane at 1024-cell rows; bitwise
+identical to five single steps, tests/test_gpu_temporal.py): every step is still computed in full,
+the fused kernel keeps u^{t+1}..u^{t+4} on chip. A step count that is not a multiple of 5 ends with
+a shorter fused sweep.
 --temporal 1 measures one sweep per step. Timing: W untimed warmup steps, then exactly K steps bracketed by barrier +
 torch.cuda.synchronize() on both sides; the slowest rank's time is reported (N > 1: three such
 repetitions by default, the median reported and all three listed). GCells/s = nx*ny*nz*K / t / 1e9
@@ -97,7 +98,7 @@ def parse(argv=None):
                         "overlap (auto); every candidate is timed twice, interleaved, and its faster run counts")
     p.add_argument("--temporal", type=int, default=0,
                    help="time steps fused per memory sweep (temporal blocking); 0 = auto (native "
-                        "hip_fused_depth): 4 for the 3D 7-point (fp32 and fp64) where heat7_wxk's x segments "
+                        "hip_fused_depth): 5 (fp32) / 4 (fp64) for the 3D 7-point where heat7_wxk's x segments "
                         "cover the row, 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 (2D "
                         "MDF) / 12 (Life)")
     p.add_argument("--ref-precision", action="store_true",
@@ -217,8 +218,8 @@ def pick_temporal(a, prob, nslab, hip):
 
     if a.temporal > 0:
         return a.temporal
-    # the deepest measured-win fused depth (native hip_fused_depth: 4 for the 3D 7-point through
-    # heat7_wxk where its x segments cover the row; 3 for the
+    # the deepest measured-win fused depth (native hip_fused_depth: 5 / 4 for the fp32 / fp64 3D
+    # 7-point through heat7_wxk where its x segments cover the row; 3 for the
     # 27-point at 1024-cell rows
     # and in fp64, else 2; 8 (MDF) / 12 (Life) for the 2D ones; profiles/r03_wxk/, r02_mdf2d/,
     # r02_life.txt), made shallower until every slab is at least 4 sweeps deep
@@ -429,6 +430,8 @@ def run_proxy(a):
     prob = make_problem(a, nx, ny, nz)
     py = max(1, a.py)
     temporal = pick_temporal(a, prob, max(1, n // py), True)
+    if py > 1:
+        temporal = min(temporal, 4)  # (pencils fuse at most 4 steps)
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True])
     overlaps = [True, False] if (n > 1 and not a.no_overlap and not a.overlap) else [not a.no_overlap]
     rounds = [int(a.rounds)] if a.rounds != "auto" else ([2, 1] if n > 1 else [0])
@@ -571,6 +574,12 @@ def main(argv=None):
     temporal = pick_temporal(a, prob, max(1, world, a.virtual_ranks) // max(pys), hip)
     timeout = a.timeout if hip else 0.0
 
+    slab_depth = temporal
+
+    def depth_for(q):
+        # pencils fuse at most 4 steps (heat7_wxk's pencil copies; the 5-step sweep is for slabs)
+        return min(slab_depth, 4) if (hip and q > 1) else slab_depth
+
     # ---- transport / graph mode: correctness gate (N > 1), then short timed trials ---------
     # Every (transport, graph) candidate that passes the bitwise gate gets a short timed trial on
     # the full problem; the fastest is timed for real. With one candidate there is no trial.
@@ -600,7 +609,7 @@ def main(argv=None):
             if g and (t, False, q) in cands and (t, False, q) not in ok:
                 continue  # a transport whose eager run failed is not tried with graphs
             trace("gate %s graph=%s py=%d" % (t, g, q))
-            passed, rec = run_gate(a, hip, t, temporal, world, rank, graph=g, py=q)
+            passed, rec = run_gate(a, hip, t, depth_for(q), world, rank, graph=g, py=q)
             trace("gate %s graph=%s py=%d passed=%s" % (t, g, q, passed))
             recs.append(rec)
             if passed:
@@ -634,10 +643,10 @@ def main(argv=None):
     def make_sim(transport, graph, rounds=0, overlap=True, py=1):
         if env:
             sim = Simulation(prob, distributed=True, transport=transport, graph=graph, py=py, share_gpu=a.share_gpu,
-                             **kw)
+                             **dict(kw, temporal=depth_for(py)))
         else:
             sim = Simulation(prob, ranks=a.virtual_ranks or 1, distributed=False, transport=transport, graph=graph,
-                             py=py, **kw)
+                             py=py, **dict(kw, temporal=depth_for(py)))
         sim.set_options(min_rounds=rounds, overlap=overlap)
         return sim
 
@@ -700,6 +709,7 @@ def main(argv=None):
         chosen = cands[0]
     if sim is None:
         sim = make_sim(*chosen)
+    temporal = depth_for(chosen[4])
     sim.set_options(graph=chosen[1], min_rounds=chosen[2], overlap=chosen[3])
     trace("engine up (%s, graph=%s, rounds=%s, overlap=%s)" % (sim.transport, chosen[1], chosen[2], chosen[3]))
     sim.init()  # every timed run starts from the same initial grid

@@ -301,6 +301,10 @@ def test_ipc_direct_protocol_at_the_headline_size(hip):
     rec = json.loads([l for l in p.stdout.decode().splitlines() if l.startswith("{")][0])
     cfg = rec["config"]
     assert rec["n_gpus"] == 4 and cfg["gate"]["passed"] and cfg["transport"] == "ipc"
+    # every candidate passed its gate: the z slabs at the slab depth (5) and the 2 x 2 pencils at
+    # theirs (4: pencils fuse at most 4 steps)
+    runs = cfg["gate"]["runs"]
+    assert {r["py"] for r in runs} == {1, 2} and all(r["passed"] for r in runs), runs
     assert cfg["ipc_protocol"] == "direct" and cfg["face_copy"] == "blit"
     # the timed run itself was checked on all four ranks against a full-grid naive run
     assert cfg["verified"]["passed"] and cfg["verified"]["ranks"] == 4 and cfg["verified"]["max_abs_diff"] == 0.0
