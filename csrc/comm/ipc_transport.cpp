@@ -153,6 +153,7 @@ class IpcTransport final : public Transport {
   const char* name() const override { return copy_ == 1 ? "ipc_sdma" : "ipc"; }
   bool in_process_only() const override { return false; }
   bool stream_ordered() const override { return true; }
+  bool records_ghost_event() const override { return true; }
   void set_timeout(double s) override { timeout_s_ = s > 0 ? s : 300.0; }
 
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
@@ -291,8 +292,11 @@ class IpcTransport final : public Transport {
       HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
     };
     if (direct_) {
-      // one pair of faces: the lo side's pull on the halo stream, the hi side's on the aux stream
-      auto phase = [&](int s0, int ready) {
+      // one pair of faces: the lo side's pull on the halo stream, the hi side's on the aux stream.
+      // After the last pair the ghosts are complete: the ghost event goes on the halo stream right
+      // after both pulls, ahead of the pulled signals and of the waits for the neighbours' pulls
+      // of my faces (only the sweep after next overwrites those; the halo stream still orders it)
+      auto phase = [&](int s0, int ready, bool last) {
         const bool two = peers_[s0].rank >= 0 && peers_[s0 + 1].rank >= 0;
         if (two) {
           HIPC(hipEventRecord(ev_fork_, hs));
@@ -306,7 +310,14 @@ class IpcTransport final : public Transport {
           hipStream_t ps = two && side == s0 + 1 ? aux_ : hs;
           hip_counter_wait((const uint64_t*)p.ctr + ready, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
           hip_face_copy(mine.recv, mine, (const char*)p.buf[b] + p.face_off, p.face, ps, copy_);
-          hip_counter_signal(ctr_ + kPulled + side, ps);
+        }
+        if (last && self_.ghost_event) {  // (each pull's own stream: no join on the critical path)
+          HIPC(hipEventRecord((hipEvent_t)self_.ghost_event, hs));
+          HIPC(hipEventRecord((hipEvent_t)self_.ghost_event2, two ? aux_ : hs));
+        }
+        for (int side = s0; side < s0 + 2; ++side) {
+          if (peers_[side].rank < 0) continue;
+          hip_counter_signal(ctr_ + kPulled + side, two && side == s0 + 1 ? aux_ : hs);
         }
         if (two) {
           HIPC(hipEventRecord(ev_join_, aux_));
@@ -316,11 +327,11 @@ class IpcTransport final : public Transport {
       hip_counter_signal(ctr_ + kReady, hs);
       if (pencil_) {
         // y faces first; readyZ tells the z neighbours my y ghost rows (inside my z faces) landed
-        phase(2, kReady);
+        phase(2, kReady, false);
         hip_counter_signal(ctr_ + kReadyZ, hs);
-        phase(0, kReadyZ);
+        phase(0, kReadyZ, true);
       } else {
-        phase(0, kReady);
+        phase(0, kReady, true);
       }
       for (int side = 0; side < 4; ++side) {
         const Peer& p = peers_[side];
@@ -355,6 +366,10 @@ class IpcTransport final : public Transport {
       hip_counter_signal(ctr_ + kPulled + side, ps);
     }
     join();
+    if (self_.ghost_event) {
+      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event, hs));
+      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event2, hs));
+    }
     if (!capturing) last_b_ = b;
   }
   std::string debug_state() override {

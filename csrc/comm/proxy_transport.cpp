@@ -53,6 +53,7 @@ class ProxyTransport final : public Transport {
   }
   const char* name() const override { return "proxy"; }
   bool stream_ordered() const override { return true; }
+  bool records_ghost_event() const override { return true; }
   void set_timeout(double s) override { timeout_s_ = s > 0 ? s : 300.0; }
 
   void setup(const std::vector<LocalSlab>& locals, int nranks) override {
@@ -93,7 +94,8 @@ class ProxyTransport final : public Transport {
     const uint64_t ahead = (!capturing && last_b_ == b) ? 1 : 0;
     // the ipc transport's stream layout: per pair of faces the hi-side pull on a second stream,
     // concurrent with the lo-side pull on the halo stream
-    auto phase = [&](int s0, int ready) {
+    // (the ghost event after the last pair's pulls, as in the ipc transport)
+    auto phase = [&](int s0, int ready, bool last) {
       const bool both = halo_span(self_, b, s0, nranks_).peer >= 0 &&
                         halo_span(self_, b, s0 + 1, nranks_).peer >= 0;
       if (both) {
@@ -106,7 +108,14 @@ class ProxyTransport final : public Transport {
         hipStream_t ps = both && side == s0 + 1 ? aux_ : hs;
         hip_counter_wait(ctr_ + ready, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
         hip_face_copy(h.recv, h, h.send, h, ps, copy_);
-        hip_counter_signal(ctr_ + kPulled + side, ps);
+      }
+      if (last && self_.ghost_event) {  // (each pull's own stream: no join on the critical path)
+        HIPC(hipEventRecord((hipEvent_t)self_.ghost_event, hs));
+        HIPC(hipEventRecord((hipEvent_t)self_.ghost_event2, both ? aux_ : hs));
+      }
+      for (int side = s0; side < s0 + 2; ++side) {
+        if (halo_span(self_, b, side, nranks_).peer < 0) continue;
+        hip_counter_signal(ctr_ + kPulled + side, both && side == s0 + 1 ? aux_ : hs);
       }
       if (both) {
         HIPC(hipEventRecord(ev_join_, aux_));
@@ -132,11 +141,11 @@ class ProxyTransport final : public Transport {
       // pulls its y faces first and signals readyZ once they landed: its z faces carry those ghost rows
       hip_counter_signal(ctr_ + kReady, hs);
       if (pencil_) {
-        phase(2, kReady);
+        phase(2, kReady, false);
         hip_counter_signal(ctr_ + kReadyZ, hs);
-        phase(0, kReadyZ);
+        phase(0, kReadyZ, true);
       } else {
-        phase(0, kReady);
+        phase(0, kReady, true);
       }
       for (int side = 0; side < 4; ++side) {
         if (halo_span(self_, b, side, nranks_).peer < 0) continue;
@@ -165,6 +174,10 @@ class ProxyTransport final : public Transport {
       hip_counter_signal(ctr_ + kPulled + side, ps);
     }
     join();
+    if (self_.ghost_event) {
+      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event, hs));
+      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event2, hs));
+    }
     if (!capturing) last_b_ = b;
   }
   int last_parity() const override { return last_b_; }

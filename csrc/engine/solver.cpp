@@ -81,6 +81,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     s.ev_bnd = s.be->create_event();
     s.ev_int = s.be->create_event();
     s.ev_x = s.be->create_event();
+    s.ev_x2 = s.be->create_event();
     s.resid = (double*)s.be->alloc(2 * sizeof(double));
     if (s.be->kind() == DeviceKind::HIP && opt_.py == 1 && local_ranks.size() == 1) {
       s.be->activate();
@@ -133,6 +134,8 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     l.be = s.be.get();
     l.halo_stream = s.hs;
     l.bnd_event = s.ev_bnd;
+    l.ghost_event = s.ev_x;
+    l.ghost_event2 = s.ev_x2;
     l.lay = s.lay;
     l.buf[0] = s.buf[0];
     l.buf[1] = s.buf[1];
@@ -176,6 +179,7 @@ Solver::~Solver() {
     s.be->destroy_event(s.ev_bnd);
     s.be->destroy_event(s.ev_int);
     s.be->destroy_event(s.ev_x);
+    s.be->destroy_event(s.ev_x2);
     s.be->destroy_stream(s.hs);
     s.be->destroy_stream(s.cs);
   }
@@ -311,7 +315,10 @@ void Solver::exchange_ghosts() {
 // cross-stream event gap between them, measured 10-13 us each at the N = 8 slab shape, where a
 // 4-step sweep takes about 0.3 ms), and the exchange alone on the halo stream, after the boundary
 // kernels' event and overlapping the interior sweep. The next step's boundary kernels wait for that
-// exchange (ev_x): its ghosts are their input, and the faces it sent are what they overwrite.
+// exchange (ev_x): its ghosts are their input. (The ipc / proxy transports record ev_x / ev_x2 right
+// after their two pulls, ahead of their pulled signals and waits: 45 -> 26 -> ~20 us from the end of
+// the pulls to the next boundary launch at the N = 8 proxy, profiles/r05_session_{ad,ae}/. The faces
+// it sent are overwritten only by the sweep after next, after this exchange on the halo stream.)
 // Only for one slab per process (the production layout; 8 slabs in one process ran 1936 vs 2023
 // GCells/s with it, rank proxies N = 8 / 4 / 2 1850 / 2073 / 2284 vs 1824 / 2069 / 2259,
 // profiles/r03_session_x/) and transports whose exchange is pure stream work on the halo stream
@@ -445,7 +452,10 @@ void Solver::step(bool want_resid, int k) {
     // nothing; the cross-stream event wait alone put ~12 us between consecutive N = 1 sweeps,
     // profiles/r05_session_g2/prof_driver_kernel_trace.csv)
     if (bcs) {
-      if (nranks_ > 1) s.be->wait(s.cs, s.ev_x);
+      if (nranks_ > 1) {
+        s.be->wait(s.cs, s.ev_x);
+        if (transport_->records_ghost_event()) s.be->wait(s.cs, s.ev_x2);
+      }
     } else {
       s.be->wait(s.hs, s.ev_int);
     }
@@ -494,7 +504,7 @@ void Solver::step(bool want_resid, int k) {
   if (!slabs_.empty()) slabs_[0].be->trace_push("mdfx.exchange");
   transport_->exchange(nb);
   if (!slabs_.empty()) slabs_[0].be->trace_pop();
-  if (bcs && nranks_ > 1)
+  if (bcs && nranks_ > 1 && !transport_->records_ghost_event())
     for (auto& s : slabs_) s.be->record(s.ev_x, s.hs);
   if (prof_hip) {
     Slab& s0 = slabs_[0];
@@ -774,6 +784,7 @@ int Solver::prepare_graphs() {
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
     s.be->record(s.ev_x, s.hs);
+    s.be->record(s.ev_x2, s.hs);
   }
   return (graph_exec_[0] ? 1 : 0) + (graph_exec_[1] ? 1 : 0);
 }
@@ -841,6 +852,7 @@ void Solver::capture_graph(int parity, int k) {
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
     s.be->record(s.ev_x, s.hs);
+    s.be->record(s.ev_x2, s.hs);
   }
   const StepStats saved = stats_;
   GDBG("capture: steps");
@@ -895,6 +907,8 @@ void Solver::run_graph(int64_t pairs, int k) {
       s.be->record(s.ev_bnd, s.hs);
       s.be->record(s.ev_int, s.cs);
       s.be->record(s.ev_x, s.hs);
+      s.be->record(s.ev_x2, s.hs);
+    s.be->record(s.ev_x2, s.hs);
     }
   }
   GDBG("launch");
@@ -911,6 +925,7 @@ void Solver::run_graph(int64_t pairs, int k) {
     o.be->wait(o.hs, s.ev_bnd);
     o.be->wait(o.hs, s.ev_int);
     o.be->wait(o.hs, s.ev_x);
+    o.be->wait(o.hs, s.ev_x2);
   }
   o.be->wait(o.hs, o.ev_int);
   for (int64_t i = 0; i < pairs; ++i) HIPC(hipGraphLaunch((hipGraphExec_t)graph_exec_[cur_], (hipStream_t)o.hs));
@@ -927,6 +942,7 @@ void Solver::run_graph(int64_t pairs, int k) {
     s.be->record(s.ev_bnd, s.hs);
     s.be->record(s.ev_int, s.cs);
     s.be->record(s.ev_x, s.hs);
+    s.be->record(s.ev_x2, s.hs);
   }
   // a replayed cycle ends with the exchange of buffer cur_ (the parity is unchanged)
   transport_->set_last_parity(cur_);

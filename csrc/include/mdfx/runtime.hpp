@@ -54,6 +54,11 @@ struct LocalSlab {
   Backend* be = nullptr;
   void* halo_stream = nullptr;
   void* bnd_event = nullptr;  // recorded right after this step's boundary kernel(s)
+  // recorded by transports whose records_ghost_event() is true, the moment this slab's ghosts of
+  // the exchange have landed: ghost_event on the halo stream after its pull, ghost_event2 on the
+  // stream of the other pull (the halo stream too when there is one pull); the solver's ev_x / ev_x2
+  void* ghost_event = nullptr;
+  void* ghost_event2 = nullptr;
   FieldLayout lay;
   void* buf[2] = {nullptr, nullptr};
 };
@@ -117,6 +122,13 @@ class Transport {
   // Whether the loaded HIP runtime can also capture that stream work into a hipGraph that replays
   // it faithfully (stream_ordered() and capturable: RCCL's grouped send / recv only under HIP >= 7.2).
   virtual bool graph_capturable() const { return stream_ordered(); }
+  // Whether exchange() records every local slab's ghost_event / ghost_event2 as soon as that slab's
+  // ghosts have landed (each on the stream of the pull it follows), ahead of the exchange's
+  // remaining bookkeeping (the ipc protocol's pulled signals and waits for the neighbours to have
+  // pulled this slab's faces, which only the sweep after next, writing that buffer again, depends
+  // on; the halo stream orders it). The solver then orders the next sweep after those two events
+  // instead of after the whole exchange: no cross-stream join on the critical path.
+  virtual bool records_ghost_event() const { return false; }
   // Watchdog bound for blocking transport calls and device-side waits (seconds; 0 = default).
   virtual void set_timeout(double) {}
   // Watchdog escalation: make every outstanding transport operation return (ncclCommAbort, the

@@ -147,6 +147,7 @@ class Solver {
     void* ev_bnd = nullptr;
     void* ev_int = nullptr;
     void* ev_x = nullptr;  // the last exchange's stream work (boundary kernels on the compute stream wait for it)
+    void* ev_x2 = nullptr;  // (transports that record ghost events: the second pull stream's ghosts)
     double* resid = nullptr;  // 2 accumulators (halo-stream kernels, compute-stream kernels)
     int64_t lo_b = 0, lo_e = 0, hi_b = 0, hi_e = 0, in_b = 0, in_e = 0;  // storage-plane regions
     // pencils: storage-row regions of the interior planes (y-boundary strips and interior rows;
