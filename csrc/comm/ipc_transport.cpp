@@ -66,6 +66,7 @@
 #include <hip/hip_runtime_api.h>
 #include <unistd.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -103,6 +104,26 @@ struct IpcRecord {
   hipIpcMemHandle_t buf[2];  // the two field buffers (direct protocol)
   hipIpcMemHandle_t ctr;
 };
+
+// IPC export of a fresh allocation. When engines are built and closed in turn by several processes
+// on one GPU (bench.py's trial loop), the export of a new field buffer has failed with "invalid
+// argument" about once in three 8-process churn runs after the whole GPU tier (round 5,
+// profiles/r05_session_ag/), although every rank had unmapped its neighbours' exports before any
+// rank freed (~IpcTransport): the runtime evidently retires a closed import of the same address
+// range asynchronously. A bounded host-side retry (up to ~2 s) waits that out; any other error,
+// or one that persists, fails as before.
+void ipc_export(hipIpcMemHandle_t* h, void* p) {
+  for (int i = 0;; ++i) {
+    const hipError_t e = hipIpcGetMemHandle(h, p);
+    if (e == hipSuccess) {
+      if (i > 0) std::fprintf(stderr, "mdfx ipc: hipIpcGetMemHandle succeeded after %d retries\n", i);
+      return;
+    }
+    if (e != hipErrorInvalidValue || i >= 80) HIPC(e);
+    (void)hipGetLastError();
+    usleep(25000);
+  }
+}
 
 // This process's ordinal of the device with PCI bus id `pci` (-1 if it is not visible here).
 int local_device_of(const char* pci) {
@@ -194,14 +215,14 @@ class IpcTransport final : public Transport {
       (void)hipGetLastError();
       mine.pci[0] = 0;
     }
-    HIPC(hipIpcGetMemHandle(&mine.ctr, ctr_));
+    ipc_export(&mine.ctr, ctr_);
     if (want_direct) {
-      for (int b = 0; b < 2; ++b) HIPC(hipIpcGetMemHandle(&mine.buf[b], self_.buf[b]));
+      for (int b = 0; b < 2; ++b) ipc_export(&mine.buf[b], self_.buf[b]);
     }
     // the mailbox exists in both protocols (a rank that cannot go direct makes everyone fall back)
     HIPC(hipMalloc(&mbox_, 4 * face_));
     HIPC(hipMemset(mbox_, 0, 4 * face_));
-    HIPC(hipIpcGetMemHandle(&mine.mbox, mbox_));
+    ipc_export(&mine.mbox, mbox_);
     HIPC(hipDeviceSynchronize());
     const std::vector<std::string> all =
         f_.allgather(std::string((const char*)&mine, sizeof(mine)));  // also the setup barrier
