@@ -12,7 +12,7 @@ run c2_heat7_512_f32 --n 512 --steps 100 --warmup 10 || exit 1
 run c2_heat7_512_f32_t1 --n 512 --steps 100 --warmup 10 --temporal 1 || exit 1
 run c3_heat7_1024_f32 --n 1024 --steps 50 --warmup 10 --repeats 2 || exit 1
 run c3_heat7_1024_f32_driver --n 1024 --steps 20 --warmup 5 || exit 1
-for n in 2 4 8; do run c3_proxy$n --rank-proxy $n --steps 48 --warmup 12 || exit 1; done
+for n in 2 4 8; do run c3_proxy$n --rank-proxy $n --steps 50 --warmup 10 || exit 1; done  # (K = 5: whole sweeps)
 run c3_proxy8_pencil --rank-proxy 8 --py 2 --steps 48 --warmup 12 || exit 1
 run c4_box27_512_f32 --stencil box27 --n 512 --steps 100 --warmup 10 || exit 1
 run c4_box27_512_f64 --stencil box27 --n 512 --dtype f64 --steps 50 --warmup 5 || exit 1
@@ -25,9 +25,9 @@ run x_mdf2d_16k_f32_ref --stencil jacobi5 --nx 16384 --nz 16384 --steps 96 --war
 run x_mdf2d_16k_f64 --stencil jacobi5 --dtype f64 --nx 16384 --nz 16384 --steps 96 --warmup 16 || exit 1
 run x_life_32k --stencil life --dtype u8 --nx 32768 --nz 32768 --steps 96 --warmup 12 || exit 1
 run x_box27_1024_f32 --stencil box27 --n 1024 --steps 20 --warmup 4 || exit 1
-run x_heat7_3072_f32 --n 3072 --steps 12 --warmup 3 || exit 1
-run x_heat7_1024_f32_v8 --n 1024 --steps 48 --warmup 12 --virtual-ranks 8 || exit 1
-run x_heat7_1024_f32_ipc2 --n 1024 --steps 48 --warmup 12 --gpus 2 --share-gpu --transport ipc || exit 1
+run x_heat7_3072_f32 --n 3072 --steps 20 --warmup 5 || exit 1
+run x_heat7_1024_f32_v8 --n 1024 --steps 50 --warmup 10 --virtual-ranks 8 || exit 1
+run x_heat7_1024_f32_ipc2 --n 1024 --steps 50 --warmup 10 --gpus 2 --share-gpu --transport ipc || exit 1
 echo "== mdf dialogue (reference-compatible CLI, reference precision, fused)"
 printf '100\n16384\n16384\n' | timeout -k 10 300 ./build/bin/mdf --json > gpurun_out/baseline_mdf_dialogue.json 2>&1 || exit 1
 tail -1 gpurun_out/baseline_mdf_dialogue.json
