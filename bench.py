@@ -213,6 +213,16 @@ def make_problem(a, nx, ny, nz):
     return life2d(h=nz, w=nx)
 
 
+# the deepest fused sweep a (z, y) pencil layout has: heat7_wxk's pencil copies fuse 3 or 4 steps
+# (the 5-step sweep in rows of 2 cells per lane is for z slabs)
+PENCIL_MAX_DEPTH = 4
+
+
+def depth_for_layout(temporal, py, hip):
+    """Fused depth of a candidate with `py` ranks along y, given the slab depth `temporal`."""
+    return min(temporal, PENCIL_MAX_DEPTH) if (hip and py > 1) else temporal
+
+
 def pick_temporal(a, prob, nslab, hip):
     from mpi_cuda_process_amd import native
 
@@ -431,7 +441,7 @@ def run_proxy(a):
     py = max(1, a.py)
     temporal = pick_temporal(a, prob, max(1, n // py), True)
     if py > 1:
-        temporal = min(temporal, 4)  # (pencils fuse at most 4 steps)
+        temporal = depth_for_layout(temporal, py, True)
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True])
     overlaps = [True, False] if (n > 1 and not a.no_overlap and not a.overlap) else [not a.no_overlap]
     rounds = [int(a.rounds)] if a.rounds != "auto" else ([2, 1] if n > 1 else [0])
@@ -577,8 +587,7 @@ def main(argv=None):
     slab_depth = temporal
 
     def depth_for(q):
-        # pencils fuse at most 4 steps (heat7_wxk's pencil copies; the 5-step sweep is for slabs)
-        return min(slab_depth, 4) if (hip and q > 1) else slab_depth
+        return depth_for_layout(slab_depth, q, hip)
 
     # ---- transport / graph mode: correctness gate (N > 1), then short timed trials ---------
     # Every (transport, graph) candidate that passes the bitwise gate gets a short timed trial on

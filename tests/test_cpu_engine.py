@@ -577,6 +577,21 @@ def test_fused_depth_policy(mdfx):
     assert auto_temporal(m.heat3d(n=1024), 1, "cpu") == 1
 
 
+def test_bench_pencil_candidates_fuse_at_most_four_steps():
+    """bench.py gates and times (z, y) pencil candidates at their own depth: the slabs' fp32 depth 5
+    has no pencil kernel (heat7_wxk's pencil copies fuse 3 / 4 steps), so a pencil candidate run at
+    5 failed its gate (round-5 rehearsal, profiles/r05_session_y/)."""
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.depth_for_layout(5, 2, True) == 4 and bench.depth_for_layout(5, 1, True) == 5
+    assert bench.depth_for_layout(3, 2, True) == 3 and bench.depth_for_layout(4, 4, True) == 4
+    assert bench.depth_for_layout(5, 2, False) == 5  # (CPU pencils fuse any depth)
+
+
 def test_warm_kernels_is_a_noop_on_cpu():
     import mpi_cuda_process_amd as m
 
