@@ -451,9 +451,18 @@ void Solver::step(bool want_resid, int k) {
     // (a single slab has no neighbour: its exchange moves nothing and the compute stream waits on
     // nothing; the cross-stream event wait alone put ~12 us between consecutive N = 1 sweeps,
     // profiles/r05_session_g2/prof_driver_kernel_trace.csv)
+    // (never inside a capture: the folded exchange is ordered after the interior sweep's stores by a
+    // device spin wait alone, with no graph edge, so a replay that put the wait node on a queue ahead
+    // of the sweep could spin until the watchdog; captured cycles use the boundary launch + event)
+    const bool fold = bcs && !capturing_ && fold_ok(s, k);
+    // folded, with per-pull ghost events: the upper boundary launch reads only the upper ghosts
+    // (ev_x2, after the hi side's pull; a folded slab holds a lower region, an interior plane and
+    // the upper region, so that launch's inputs start above the lower ghosts) and the interior the
+    // lower ones (ev_x). (With one neighbour both events follow its pull.)
+    const bool split = fold && nranks_ > 1 && transport_->records_ghost_event();
     if (bcs) {
       if (nranks_ > 1) {
-        s.be->wait(s.cs, s.ev_x);
+        if (!split) s.be->wait(s.cs, s.ev_x);
         if (transport_->records_ghost_event()) s.be->wait(s.cs, s.ev_x2);
       }
     } else {
@@ -461,10 +470,6 @@ void Solver::step(bool want_resid, int k) {
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[0], (hipStream_t)bs));
     a.resid = want_resid ? s.resid : nullptr;
-    // (never inside a capture: the folded exchange is ordered after the interior sweep's stores by a
-    // device spin wait alone, with no graph edge, so a replay that put the wait node on a queue ahead
-    // of the sweep could spin until the watchdog; captured cycles use the boundary launch + event)
-    const bool fold = bcs && !capturing_ && fold_ok(s, k);
     if (fold) ++stats_.folded_sweeps;
     boundary_kernels(s, a, bs, fold);
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[1], (hipStream_t)bs));
@@ -481,6 +486,7 @@ void Solver::step(bool want_resid, int k) {
     }
     if (p0) HIPC(hipEventRecord((hipEvent_t)pev_[2], (hipStream_t)is));
     a.resid = want_resid ? s.resid + 1 : nullptr;
+    if (split) s.be->wait(is, s.ev_x);
     interior_kernel(s, a, is, fold);
     // the exchange sends the faces once the upper boundary launch and the interior sweep have
     // signalled them stored (in that order: both launches are on the compute stream). Folded steps
