@@ -458,7 +458,9 @@ void Solver::step(bool want_resid, int k) {
     // folded, with per-pull ghost events: the upper boundary launch reads only the upper ghosts
     // (ev_x2, after the hi side's pull; a folded slab holds a lower region, an interior plane and
     // the upper region, so that launch's inputs start above the lower ghosts) and the interior the
-    // lower ones (ev_x). (With one neighbour both events follow its pull.)
+    // lower ones (ev_x). (With one neighbour both events follow its pull.) At the N = 8 proxy, whose
+    // two pulls end together, this measured neutral (2,073-2,098 vs 2,050-2,128 GCells/s interleaved,
+    // profiles/r05_session_al/); it matters when one neighbour's face lands late.
     const bool split = fold && nranks_ > 1 && transport_->records_ghost_event();
     if (bcs) {
       if (nranks_ > 1) {
