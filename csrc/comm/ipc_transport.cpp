@@ -119,7 +119,9 @@ void ipc_export(hipIpcMemHandle_t* h, void* p) {
       if (i > 0) std::fprintf(stderr, "mdfx ipc: hipIpcGetMemHandle succeeded after %d retries\n", i);
       return;
     }
-    if (e != hipErrorInvalidValue || i >= 80) HIPC(e);
+    if (e != hipErrorInvalidValue || i >= 80)
+      throw_error(__FILE__, __LINE__,
+                  format("HIP: hipIpcGetMemHandle(%p) -> %s (after %d retries)", p, hipGetErrorString(e), i));
     (void)hipGetLastError();
     usleep(25000);
   }
