@@ -55,9 +55,12 @@ import argparse
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import time
+
+_T_START = time.time()  # (the JSON's wall_s: the whole process, torch import included)
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -112,9 +115,14 @@ def parse(argv=None):
                         "3D 7-point tries slabs and 2-along-y pencils on the ipc transports and times the faster)")
     p.add_argument("--variant", default="auto", choices=["auto", "tuned", "naive"])
     p.add_argument("--device", default="auto", choices=["auto", "hip", "cpu"])
-    p.add_argument("--repeats", type=int, default=0,
-                   help="timed repetitions of --steps steps each; the median is reported and every one is "
-                        "listed (0 = auto: 3 with several ranks, 1 on one GPU)")
+    p.add_argument("--repeats", type=int, default=3,
+                   help="timed repetitions of --steps steps each, back to back; the median is reported and "
+                        "every one is listed")
+    p.add_argument("--trial-budget", type=float, default=150.0,
+                   help="seconds the gate + trial phase may take before the second (interleaved) trial pass "
+                        "is skipped (all ranks agree on the slowest rank's clock)")
+    p.add_argument("--no-diagnose", action="store_true",
+                   help="N > 1: skip the profiled pass after verification (per-rank phases, face pull rates)")
     p.add_argument("--no-verify", action="store_true",
                    help="skip the check of the timed run against a full-grid naive run on each rank's device")
     p.add_argument("--timeout", type=float, default=120.0,
@@ -342,20 +350,27 @@ def verify_timed(a, sim, prob, hip, env, rank, world, seq):
 
     parts = [(sim.layout(i), _owned(sim, i, prob.nx)) for i in range(sim.num_local)]
     res_mine = sim.residual
-    diff, err = float("inf"), ""
+    diff, err, oom = float("inf"), "", False
     if hip:
         # the reference holds two full-grid buffers next to this rank's own: skip (and say so) where
         # they do not fit the device, e.g. 3072^3 fp32 or 2048^3 fp64 on ONE GPU
         from mpi_cuda_process_amd.ops import FieldLayout
 
-        need = 2 * FieldLayout.make(prob, halo=1).nbytes + (1 << 30)
+        # every rank on this device builds its own reference at once (--share-gpu: several per device)
+        dev = torch.cuda.current_device()
+        sharing = 1
+        if env:
+            devs = [None] * world
+            dist.all_gather_object(devs, (socket.gethostname(), dev))
+            sharing = sum(1 for d in devs if d == (socket.gethostname(), dev))
+        need = sharing * (2 * FieldLayout.make(prob, halo=1).nbytes + (1 << 30))
         free = torch.cuda.mem_get_info()[0]
         ok = torch.tensor([1.0 if free >= need else 0.0], dtype=torch.float64)
         if env:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if ok.item() == 0.0:
-            return {"ranks": world, "passed": True, "skipped": "the full-grid reference needs %.0f GB per device, "
-                    "%.0f GB free on rank %d" % (need / 1e9, free / 1e9, rank)}
+            return {"ranks": world, "passed": True, "skipped": "the full-grid reference needs %.0f GB per device "
+                    "(%d rank(s) on it), %.0f GB free on rank %d" % (need / 1e9, sharing, free / 1e9, rank)}
     if hip:
         native().set_kernel_variant("naive")
     try:
@@ -375,11 +390,23 @@ def verify_timed(a, sim, prob, hip, env, rank, world, seq):
                     diff = max(diff, float(d.nan_to_num(nan=float("inf")).max()))
             if res_mine >= 0 and abs(res_mine - ref.residual) > 1e-9 * max(1.0, abs(ref.residual)):
                 err = "residual %r vs %r" % (res_mine, ref.residual)
+    except torch.OutOfMemoryError as e:  # a resource limit, not a mismatch: reported as skipped below
+        err, oom = "%s: %s" % (type(e).__name__, e), True
     except Exception as e:  # noqa: BLE001 - reported and agreed on below
         err = "%s: %s" % (type(e).__name__, e)
+        oom = "out of memory" in str(e).lower() or "hipErrorOutOfMemory" in str(e)
     finally:
         if hip:
             native().set_kernel_variant(a.variant)
+    t = torch.tensor([1.0 if (err and oom) else 0.0], dtype=torch.float64)
+    if env:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if t.item() > 0:
+        if err and oom:
+            print("bench verify: rank %d could not allocate the full-grid reference: %s" % (rank, err),
+                  file=sys.stderr, flush=True)
+        return {"ranks": world, "passed": True, "skipped": "a rank could not allocate the full-grid reference "
+                "(out of memory)"}
     if err or diff != 0.0:
         print("bench verify: rank %d: owned cells differ from the full-grid run by up to %g %s" % (rank, diff, err),
               file=sys.stderr, flush=True)
@@ -390,6 +417,56 @@ def verify_timed(a, sim, prob, hip, env, rank, world, seq):
             "steps": [int(n) for n in seq],
             "reference": "full grid, one slab on each rank's own device, %s" % (
                 "naive single-step HIP kernels" if hip else "CPU oracle")}
+
+
+def diagnose(sim, temporal, env, world, rank, sweeps=4):
+    """N > 1, after the timed run and its verification (outside the timed region): where a rank's
+    time per sweep goes, and what its halo links deliver. Every rank runs `sweeps` profiled sweeps
+    (Solver phase timing: hipEvents on the boundary / compute / halo streams, one host sync per
+    sweep) and then times exchange_ghosts() alone (the current faces re-sent: the ghosts do not
+    change) five times. Returns (phases, links), one entry per rank, gathered on every rank.
+
+    phases (us per sweep): boundary = the boundary launch(es) before the interior sweep; interior =
+    the interior sweep (with the folded lower boundary when folded); exchange = from the end of the
+    boundary launch to the end of the exchange on the halo stream; exposed = how long the exchange
+    ran on after the sweep's last kernel ended (the part not hidden); step = the whole sweep.
+    links: the faces this rank pulls (peer rank, bytes), the best host-timed exchange of all of
+    them at once (an upper bound: it includes one host synchronisation), and bytes / time per face."""
+    import torch.distributed as dist
+
+    nat = sim.native
+    rec_p, rec_l = {"rank": rank}, {"rank": rank}
+    try:
+        sim.set_options(profile=True)
+        nat.reset_phases()
+        sim.run(sweeps * temporal)
+        sim.synchronize()
+        ph = nat.phase_times()
+        sim.set_options(profile=False)
+        n = max(1, int(ph["sweeps"]))
+        rec_p.update({k + "_us": round(ph[k + "_ms"] / n * 1e3, 1)
+                      for k in ("boundary", "interior", "exchange", "exposed", "step")})
+        rec_p["sweeps"] = n
+        faces = [sp for sp in nat.halo_spans(0, nat.current_index) if sp["peer"] >= 0]
+        ts = []
+        for _ in range(5):
+            if env:
+                dist.barrier()
+            t0 = time.perf_counter()
+            nat.exchange_ghosts()
+            ts.append(time.perf_counter() - t0)
+        best = min(ts)
+        rec_l.update({"peers": [int(sp["peer"]) for sp in faces], "face_bytes": [int(sp["bytes"]) for sp in faces],
+                      "exchange_us": round(best * 1e6, 1),
+                      "GBps_per_face": round(max([sp["bytes"] for sp in faces] or [0]) / best / 1e9, 2)})
+    except Exception as e:  # noqa: BLE001 - a diagnostic never fails the run
+        rec_p["error"] = rec_l["error"] = "%s: %s" % (type(e).__name__, e)
+    allp, alll = [rec_p], [rec_l]
+    if env:
+        allp, alll = [None] * world, [None] * world
+        dist.all_gather_object(allp, rec_p)
+        dist.all_gather_object(alll, rec_l)
+    return allp, alll
 
 
 def measure_copy_tbps(field_bytes):
@@ -484,10 +561,8 @@ def run_proxy(a):
     sim.run(a.warmup)
     timed(0)
     replays0, captures0 = sim.graph_replays, sim.graph_captures
-    best = None
-    for _ in range(max(1, a.repeats)):
-        dt = timed(a.steps)
-        best = dt if best is None else min(best, dt)
+    dts = [timed(a.steps) for _ in range(max(1, a.repeats))]
+    best = statistics.median(dts)  # (the median repetition, as the whole-node bench reports)
     per_gpu = slab_cells * a.steps / best / 1e9
     timed_vs_trial = (round(best / a.steps * 1e3 / min(t["ms_per_step"] for t in trials), 3) if trials else None)
     model = {"heat7": "3D 7-pt Jacobi", "box27": "3D 27-pt", "jacobi5": "2D 5-pt MDF", "life": "2D Game of Life"}[a.stencil]
@@ -518,7 +593,8 @@ def run_proxy(a):
                    "graph_replays_timed": sim.graph_replays - replays0,
                    "graph_captures_timed": sim.graph_captures - captures0,
                    "min_rounds": chosen[1], "overlap": chosen[2], "trials": trials,
-                   "timed_vs_trial": timed_vs_trial},
+                   "timed_vs_trial": timed_vs_trial,
+                   "repeats_ms_per_step": [round(d / a.steps * 1e3, 4) for d in dts]},
         "achieved_dram_TBps": round(dram_tbps, 3),
         "pct_of_hbm_copy_roof": round(100.0 * dram_tbps / HBM_MEASURED_TBPS, 1),
     }
@@ -596,27 +672,33 @@ def main(argv=None):
     if env and a.transport == "auto":
         # rccl (p2p kernels), ipc (pulls by the runtime's blit kernels), ipc_sdma (pulls by the
         # SDMA engines: no CUs taken from the interior sweep, lower bandwidth on one device)
-        transports = ["rccl", "ipc", "ipc_sdma"] if hip else ["torch"]
+        # (rccl_fold: rccl with the folded lower boundary, which rccl does not run by default; gated
+        # and verified like any other candidate, Transport::fold_by_default)
+        transports = ["rccl", "rccl_fold", "ipc", "ipc_sdma"] if hip else ["torch"]
     elif not env:
         transports = [a.transport if a.transport in ("loopback", "host") else "auto"]
     graphs = {"on": [True], "off": [False]}.get(a.graph, [False, True] if hip else [False])
-    cands = [(t, g, q) for t in transports for q in pys for g in graphs]
+    # (captured cycles never fold and pencils never fold, so rccl_fold is an eager z-slab candidate)
+    cands = [(t, g, q) for t in transports for q in pys for g in graphs if not (t == "rccl_fold" and (g or q > 1))]
     if hip and a.graph == "auto" and len(graphs) > 1:
         # rccl steps are captured only under HIP >= 7.2 (RcclTransport::graph_capturable); under the
         # runtime PyTorch bundles a graph candidate would just repeat the eager one
         from mpi_cuda_process_amd import native as _nat
         if not _nat().hip_runtime_version() >= 70200000:
-            cands = [(t, g, q) for t, g, q in cands if not (t == "rccl" and g)]
+            cands = [(t, g, q) for t, g, q in cands if not (t.startswith("rccl") and g)]
     if a.rounds != "auto":
         rounds = [int(a.rounds)]
     else:
         rounds = [2, 1] if (hip and env and world > 1) else [0]
     gate = None
+    t_sel0 = time.time()  # gate + trials start (the --trial-budget clock)
     if env and world > 1 and not a.no_gate:
         recs, ok = [], []
         for t, g, q in cands:
             if g and (t, False, q) in cands and (t, False, q) not in ok:
                 continue  # a transport whose eager run failed is not tried with graphs
+            if t == "rccl_fold" and ("rccl", False, q) in cands and ("rccl", False, q) not in ok:
+                continue  # nor rccl folded when plain rccl failed
             trace("gate %s graph=%s py=%d" % (t, g, q))
             passed, rec = run_gate(a, hip, t, depth_for(q), world, rank, graph=g, py=q)
             trace("gate %s graph=%s py=%d passed=%s" % (t, g, q, passed))
@@ -683,6 +765,7 @@ def main(argv=None):
         return dt
 
     trials = []
+    trial_passes = 0
     sim, sim_t = None, None
     if len(cands) > 1:
         # two interleaved passes over the candidates (sorted by transport, so each transport's engine
@@ -690,6 +773,16 @@ def main(argv=None):
         n_trial = max(2, a.trial_steps)
         best_t = {}
         for _pass in range(2):
+            if _pass > 0:
+                # the second (interleaved) pass only while the selection phase is inside its budget,
+                # judged by the slowest rank's clock so every rank takes the same branch
+                el = torch.tensor([time.time() - t_sel0], dtype=torch.float64)
+                if env:
+                    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                if el.item() > a.trial_budget:
+                    trace("trial budget spent after %.1f s: one pass" % el.item())
+                    break
+            trial_passes = _pass + 1
             for t, g, rr, ov, q in cands:
                 if sim is not None and sim_t != (t, q):
                     sim.close()
@@ -731,12 +824,12 @@ def main(argv=None):
     trace("warmup done")
     inject_timed_fault(sim, rank, world)
     replays0, captures0 = sim.graph_replays, sim.graph_captures
-    repeats = a.repeats if a.repeats > 0 else (3 if (env and world > 1) else 1)
+    repeats = max(1, a.repeats)
     dts = []
     for _ in range(repeats):
         dts.append(timed(sim, a.steps))
         trace("timed %.4f s" % dts[-1])
-    best = sorted(dts)[len(dts) // 2]  # the median repetition (the only one at N = 1)
+    best = statistics.median(dts)  # the median repetition (back to back, same engine)
     verified = None
     if not a.no_verify:
         trace("verifying the timed run")
@@ -753,6 +846,11 @@ def main(argv=None):
                 dist.barrier()
                 dist.destroy_process_group()
             return 4
+
+    phases = links = None
+    if env and world > 1 and not a.no_diagnose:
+        trace("diagnostic pass")
+        phases, links = diagnose(sim, temporal, env, world, rank)
 
     devices = [device_id]
     if env:
@@ -807,7 +905,7 @@ def main(argv=None):
                 "devices": devices,
                 "distinct_devices": len(set(devices)) if hip else 0,
                 "transport": sim_transport,
-                "comm_size": nproc if sim_transport == "rccl" else 0,
+                "comm_size": nproc if sim_transport.startswith("rccl") else 0,
                 "kernel_variant": native().kernel_variant(),
                 # effective mode: true only if captured cycles actually replayed in the timed region
                 "graph": (sim.graph_replays - replays0) > 0,
@@ -816,6 +914,7 @@ def main(argv=None):
                 "graph_captures_timed": sim.graph_captures - captures0,
                 "min_rounds": chosen[2] or ("2 (auto)" if nproc > 1 or a.virtual_ranks > 1 else "1 (auto)"),
                 "trials": trials,
+                "trial_passes": trial_passes,
                 "overlap": chosen[3],
                 "timed_vs_trial": timed_vs_trial,
                 "schedule": sim.schedule,
@@ -828,6 +927,8 @@ def main(argv=None):
                 "temporal_block": temporal,
                 "py": chosen[4],
                 "gate": gate,
+                "phases": phases,
+                "links": links,
             },
             "per_gpu_gcells": round(per_gpu, 3),
             "dram_bytes_per_step_per_gpu": int(cells / max(ngpu_phys, 1) * prob.bytes_per_cell_per_step / temporal),
@@ -839,6 +940,7 @@ def main(argv=None):
         copy_tbps = measure_copy_tbps(cells / max(ngpu_phys, 1) * prob.bytes_per_cell_per_step / 2) if hip else None
         rec["measured_copy_TBps"] = round(copy_tbps, 3) if copy_tbps else None
         rec["pct_of_measured_copy"] = round(100.0 * dram_tbps / copy_tbps, 1) if copy_tbps else None
+        rec["wall_s"] = round(time.time() - _T_START, 2)  # the whole bench process so far (gate, trials, timing, checks)
         print(json.dumps(rec), flush=True)
     sim.close()
     if env:

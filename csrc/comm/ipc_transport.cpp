@@ -69,6 +69,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <vector>
 
 #include "mdfx/devsync.hpp"
 #include "mdfx/runtime.hpp"
@@ -105,26 +107,102 @@ struct IpcRecord {
   hipIpcMemHandle_t ctr;
 };
 
+}  // namespace
+
 // IPC export of a fresh allocation. When engines are built and closed in turn by several processes
-// on one GPU (bench.py's trial loop), the export of a new field buffer has failed with "invalid
-// argument" about once in three 8-process churn runs after the whole GPU tier (round 5,
-// profiles/r05_session_ag/), although every rank had unmapped its neighbours' exports before any
-// rank freed (~IpcTransport): the runtime evidently retires a closed import of the same address
-// range asynchronously. A bounded host-side retry (up to ~2 s) waits that out; any other error,
-// or one that persists, fails as before.
-void ipc_export(hipIpcMemHandle_t* h, void* p) {
+// on one GPU (bench.py's trial loop), the export of a new field buffer failed with "invalid
+// argument" once in round 5 (8-process churn after the whole GPU tier, profiles/r05_session_ag/),
+// although every rank had unmapped its neighbours' exports before any rank freed (~IpcTransport).
+// Suspected cause, not confirmed: the runtime releases a closed import asynchronously, so a range
+// a neighbour still held could be handed out again before the release. ~IpcTransport now waits
+// for its closes (hipDeviceSynchronize) before the meeting that lets the neighbours free, and a
+// failing export logs what is known about the pointer (its attributes, its allocation's range, and
+// whether that range overlaps an import this process closed earlier) before a bounded retry (up to
+// ~2 s), so the next occurrence names its cause. MDFX_IPC_EXPORT_FAIL=n makes the first n exports
+// of the process fail with "invalid argument" (tests: the retry and logging path runs on demand).
+namespace {
+struct ClosedRange {
+  uintptr_t base = 0;
+  size_t size = 0;
+};
+std::vector<ClosedRange>& closed_imports() {
+  static std::vector<ClosedRange> v;
+  return v;
+}
+void note_closed_import(void* p) {
+  void* base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, p) != hipSuccess) {
+    (void)hipGetLastError();
+    base = p;
+    size = 1;
+  }
+  auto& v = closed_imports();
+  if (v.size() >= 64) v.erase(v.begin());
+  v.push_back(ClosedRange{(uintptr_t)base, size});
+}
+std::string export_diagnosis(void* p) {
+  if (!p) return "null pointer";
+  std::string out;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) == hipSuccess)
+    out += format("type %d device %d devicePointer %p", (int)at.type, at.device, at.devicePointer);
+  else {
+    (void)hipGetLastError();
+    out += "no pointer attributes";
+  }
+  void* base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, p) == hipSuccess) {
+    out += format("; allocation [%p, +%zu)", base, size);
+    int hits = 0;
+    for (const ClosedRange& c : closed_imports())
+      if ((uintptr_t)base < c.base + c.size && c.base < (uintptr_t)base + size) ++hits;
+    out += format("; overlaps %d import(s) this process closed earlier (of %zu recorded)", hits,
+                  closed_imports().size());
+  } else {
+    (void)hipGetLastError();
+    out += "; no allocation range";
+  }
+  return out;
+}
+int export_fail_budget() {
+  static int n = [] {
+    const char* v = std::getenv("MDFX_IPC_EXPORT_FAIL");
+    return v && *v ? std::atoi(v) : 0;
+  }();
+  return n;
+}
+}  // namespace
+
+int ipc_export_retry(const std::function<int()>& get, void* p, int max_retries, int sleep_us) {
+  static int injected = 0;
   for (int i = 0;; ++i) {
-    const hipError_t e = hipIpcGetMemHandle(h, p);
+    hipError_t e;
+    if (injected < export_fail_budget()) {
+      ++injected;
+      e = hipErrorInvalidValue;
+    } else {
+      e = (hipError_t)get();
+    }
     if (e == hipSuccess) {
       if (i > 0) std::fprintf(stderr, "mdfx ipc: hipIpcGetMemHandle succeeded after %d retries\n", i);
-      return;
+      return i;
     }
-    if (e != hipErrorInvalidValue || i >= 80)
+    if (i == 0) std::fprintf(stderr, "mdfx ipc: hipIpcGetMemHandle(%p) -> %s: %s; retrying\n", p,
+                             hipGetErrorString(e), export_diagnosis(p).c_str());
+    if (e != hipErrorInvalidValue || i >= max_retries)
       throw_error(__FILE__, __LINE__,
                   format("HIP: hipIpcGetMemHandle(%p) -> %s (after %d retries)", p, hipGetErrorString(e), i));
     (void)hipGetLastError();
-    usleep(25000);
+    if (sleep_us > 0) usleep(sleep_us);
   }
+}
+
+namespace {
+
+void ipc_export(hipIpcMemHandle_t* h, void* p) {
+  (void)ipc_export_retry([&]() { return (int)hipIpcGetMemHandle(h, p); }, p, 80, 25000);
 }
 
 // This process's ordinal of the device with PCI bus id `pci` (-1 if it is not visible here).
@@ -152,11 +230,14 @@ class IpcTransport final : public Transport {
     bool mapped = false;
     for (auto& p : peers_) {
       mapped = mapped || p.mbox || p.buf[0] || p.ctr;
-      if (p.mbox) (void)hipIpcCloseMemHandle(p.mbox);
-      for (void* b : p.buf)
-        if (b) (void)hipIpcCloseMemHandle(b);
-      if (p.ctr) (void)hipIpcCloseMemHandle(p.ctr);
+      for (void* q : {p.mbox, p.buf[0], p.buf[1], p.ctr}) {
+        if (!q) continue;
+        note_closed_import(q);
+        (void)hipIpcCloseMemHandle(q);
+      }
     }
+    // the closes complete before the meeting below lets the neighbours free what they exported
+    if (mapped) (void)hipDeviceSynchronize();
     // Every rank unmaps its neighbours' exports before any rank frees its own (the engine frees the
     // field buffers right after this destructor). Without this meeting a rank could free and
     // re-allocate memory a neighbour still had mapped, and the next engine's hipIpcGetMemHandle on

@@ -43,6 +43,10 @@ std::string rccl_unique_id() {
 
 // The grouped send / recv is pure stream work on the halo stream under every runtime
 bool rccl_stream_ordered() { return true; }
+// ... but the folded boundary is not the default with RCCL: no run has yet shown RCCL's p2p kernels
+// reading a face published by a mid-sweep device counter (Transport::fold_by_default); the bench
+// gates and verifies the folded schedule as its own candidate (`rccl_fold`) instead
+bool rccl_fold_by_default() { return false; }
 // ... but RCCL's group joins its own internal streams to the caller's with events, and the HIP 7.0
 // runtime PyTorch bundles segfaults in hipStreamEndCapture on such multi-stream captures
 // (profiles/r02_graph_runtime.txt): RCCL steps are captured only under HIP >= 7.2
@@ -79,9 +83,10 @@ class RcclTransport final : public Transport {
   }
   const char* name() const override { return "rccl"; }
   bool in_process_only() const override { return false; }
-  // RCCL gets the engine's folded single-stream boundary schedule under every runtime
-  // (stream_ordered), and graph capture only where the runtime supports it (eager otherwise)
+  // RCCL gets the engine's single-stream boundary schedule under every runtime (stream_ordered),
+  // folded only on request (fold_by_default), and graph capture only where the runtime supports it
   bool stream_ordered() const override { return rccl_stream_ordered(); }
+  bool fold_by_default() const override { return rccl_fold_by_default(); }
   bool graph_capturable() const override { return rccl_graph_capturable(); }
   void set_timeout(double s) override { timeout_s_ = s; }
   void abort() override {

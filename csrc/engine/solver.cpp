@@ -186,10 +186,11 @@ Solver::~Solver() {
 }
 
 void Solver::set_options(const SolverOptions& o) {
-  if (o.graph != opt_.graph || o.overlap != opt_.overlap || o.min_rounds != opt_.min_rounds) destroy_graph();
+  if (o.graph != opt_.graph || o.overlap != opt_.overlap || o.min_rounds != opt_.min_rounds || o.fold != opt_.fold)
+    destroy_graph();
   // a different overlap mode switches the schedule (boundary_on_cs), whose steps wait on events the
   // other schedule never records (ev_x) or stops recording (ev_int): drain the queued steps first
-  if (o.overlap != opt_.overlap) sync_all();
+  if (o.overlap != opt_.overlap || o.fold != opt_.fold) sync_all();
   MDFX_CHECK(o.temporal == opt_.temporal, "the temporal blocking depth is fixed at construction");
   opt_ = o;
   transport_->set_timeout(opt_.timeout_s);
@@ -334,7 +335,7 @@ void Solver::exchange_ghosts() {
 // keeps its launch (one round). (Round 4's switch back to two launches was removed in round 5; the
 // two-launch schedule measured 6-9 % slower at the N = 8 proxy, profiles/r04_session_{i,k}/.)
 bool Solver::fold_ok(const Slab& s, int k) const {
-  return s.sig && s.lo_e > s.lo_b && s.in_e > s.in_b && hip_region_signals(spec_, s.lay, k);
+  return fold_allowed(opt_.fold, transport_->fold_by_default()) && s.sig && s.lo_e > s.lo_b && s.in_e > s.in_b && hip_region_signals(spec_, s.lay, k);
 }
 
 int Solver::min_rounds() const { return opt_.min_rounds > 0 ? opt_.min_rounds : (nranks_ > 1 ? 2 : 1); }
@@ -530,6 +531,7 @@ void Solver::step(bool want_resid, int k) {
     phases_.interior_ms += i;
     phases_.exchange_ms += x;
     phases_.step_ms += std::max(t1, t2);
+    phases_.exposed_ms += std::max(0.0f, t1 - t2);
     ++phases_.steps;
   } else if (prof) {
     c3 = clk::now();
@@ -916,7 +918,6 @@ void Solver::run_graph(int64_t pairs, int k) {
       s.be->record(s.ev_int, s.cs);
       s.be->record(s.ev_x, s.hs);
       s.be->record(s.ev_x2, s.hs);
-    s.be->record(s.ev_x2, s.hs);
     }
   }
   GDBG("launch");

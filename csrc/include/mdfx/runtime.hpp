@@ -129,6 +129,14 @@ class Transport {
   // on; the halo stream orders it). The solver then orders the next sweep after those two events
   // instead of after the whole exchange: no cross-stream join on the critical path.
   virtual bool records_ghost_event() const { return false; }
+  // Whether the engine folds the lower boundary region into the interior sweep by default
+  // (SolverOptions::fold = -1). A folded face is published by a device counter from inside the
+  // sweep, not by a kernel boundary; its visibility to the exchange rests on the halo stream's
+  // counter-wait kernel ending with the dispatch's system-scope release (hip_region_signals,
+  // kernels.hpp). The ipc / proxy pulls are checked under it on one GPU (tests/test_gpu_ipc.py);
+  // RCCL's p2p kernels as readers are not, so rccl opts out and folds only when asked (bench.py's
+  // gated `rccl_fold` candidate).
+  virtual bool fold_by_default() const { return true; }
   // Watchdog bound for blocking transport calls and device-side waits (seconds; 0 = default).
   virtual void set_timeout(double) {}
   // Watchdog escalation: make every outstanding transport operation return (ncclCommAbort, the
@@ -155,6 +163,7 @@ std::unique_ptr<Transport> make_rccl_transport(const std::string& unique_id);
 // the engine schedule they select without constructing a communicator)
 bool rccl_stream_ordered();
 bool rccl_graph_capturable();
+bool rccl_fold_by_default();
 std::string rccl_unique_id();
 // Host callbacks (the Python layer plugs torch.distributed in here, e.g. gloo on CPU).
 struct CallbackFns {
@@ -177,6 +186,11 @@ std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode = -
 // copy per face) rather than through mailboxes (two): buffers of at most 1900 MiB, since torch's
 // HIP 7.0 runtime stalls mapping exported buffers of 2 GiB and more; MDFX_IPC_DIRECT=0 / 1 forces.
 bool ipc_direct_ok(size_t field_bytes);
+// The ipc transport's export with its bounded retry: calls get() (a hipError_t as int) until it
+// succeeds, retrying "invalid argument" up to max_retries times sleep_us apart (logging a diagnosis
+// of p on the first failure); returns the retries taken, throws on any other error or when they run
+// out. MDFX_IPC_EXPORT_FAIL=n injects n failures per process (tests).
+int ipc_export_retry(const std::function<int()>& get, void* p, int max_retries, int sleep_us);
 // Rank proxy (HIP): ONE slab of an N-way decomposition alone on a GPU, exchanging with itself
 // through the ipc transport's mailbox copies and device counters (csrc/comm/proxy_transport.cpp):
 // the per-GPU schedule of an N-GPU run, measurable on one GPU. Ghost values are the slab's own

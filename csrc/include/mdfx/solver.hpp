@@ -46,11 +46,22 @@ struct SolverOptions {
   // subdomains form a (nranks / py) x py grid of (z, y) pencils, each with `temporal` ghost rows
   // per split y side as well as ghost planes. 3D grids only; fixed at construction.
   int py = 1;
+  // Folded lower boundary (Solver::fold_ok): -1 = the transport's default (fold_by_default: ipc,
+  // proxy, loopback yes, rccl no), 0 = never, 1 = wherever the layout and kernels allow it.
+  int fold = -1;
 };
+
+// Whether a step may fold, given the fold option and the transport's default.
+inline bool fold_allowed(int fold_opt, bool transport_default) {
+  return fold_opt > 0 || (fold_opt < 0 && transport_default);
+}
 
 struct PhaseStats {
   int64_t steps = 0;  // sweeps profiled
   double boundary_ms = 0, interior_ms = 0, exchange_ms = 0, step_ms = 0;
+  // how long the halo stream (the exchange) ran on past the end of the sweep's last kernel: the
+  // part of the exchange the sweep did not hide (HIP profile only; 0 on the host clock)
+  double exposed_ms = 0;
 };
 
 struct StepStats {

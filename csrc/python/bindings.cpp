@@ -284,15 +284,24 @@ PYBIND11_MODULE(_mdfx, m) {
       "host-side check of an ipc neighbour record: '' if usable, else the reason");
   m.def("ipc_shared_gpu_problem", &ipc_shared_gpu_problem, py::arg("pid_pci"), py::arg("share_gpu") = false,
         "host-side check of every rank's (pid, GPU PCI bus id): '' unless engine processes share a GPU");
+  m.def("ipc_export_retry_selftest", [](int fail, int max_retries) {
+    // the export retry loop with a stand-in for hipIpcGetMemHandle that fails `fail` times with
+    // "invalid argument" (1), then succeeds (0); no device needed
+    int n = 0;
+    return ipc_export_retry([&]() { return n++ < fail ? 1 : 0; }, nullptr, max_retries, 0);
+  }, py::arg("fail"), py::arg("max_retries") = 80, "retries the ipc export loop takes for `fail` failures");
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_traits", []() {
     py::dict d;
     d["stream_ordered"] = rccl_stream_ordered();
     d["graph_capturable"] = rccl_graph_capturable();
+    d["fold_by_default"] = rccl_fold_by_default();
     return d;
   }, "what the rccl transport reports to the engine (it is never constructed for this)");
   m.def("step_schedule", &step_schedule, py::arg("overlap"), py::arg("local_slabs"), py::arg("stream_ordered"),
         py::arg("fold"), "the engine's per-step schedule for a layout and transport (Solver::schedule)");
+  m.def("fold_allowed", &fold_allowed, py::arg("fold_opt"), py::arg("transport_default"),
+        "whether a step may fold its lower boundary (SolverOptions::fold, Transport::fold_by_default)");
   m.def("set_kernel_variant", [](const std::string& v) { hip_set_kernel_variant(v.c_str()); });
   m.def("reload_knobs", &hip_reload_knobs, "re-read the MDFX_* kernel tuning knobs from the environment");
   m.def("poison_lds", &hip_poison_lds, "fill every CU's LDS with NaN (tests for stale-LDS reads)");
@@ -412,6 +421,7 @@ PYBIND11_MODULE(_mdfx, m) {
              d["interior_ms"] = ph.interior_ms;
              d["exchange_ms"] = ph.exchange_ms;
              d["step_ms"] = ph.step_ms;
+             d["exposed_ms"] = ph.exposed_ms;
              return d;
            })
       .def("reset_phases", [](PySolver& p) { p.chk().reset_phases(); })
@@ -453,6 +463,7 @@ PYBIND11_MODULE(_mdfx, m) {
                else if (k == "timeout_s") o.timeout_s = item.second.cast<double>();
                else if (k == "min_rounds") o.min_rounds = item.second.cast<int>();
                else if (k == "profile") o.profile = item.second.cast<bool>();
+               else if (k == "fold") o.fold = item.second.cast<int>();
                else throw py::key_error("unknown solver option " + k);
              }
              p.chk().set_options(o);
@@ -470,6 +481,7 @@ PYBIND11_MODULE(_mdfx, m) {
              d["temporal"] = o.temporal;
              d["min_rounds"] = o.min_rounds;
              d["py"] = o.py;
+             d["fold"] = o.fold;
              return d;
            })
       .def_property_readonly("num_local", [](PySolver& p) { return p.chk().num_local(); })

@@ -64,7 +64,8 @@ class Simulation:
 
     Parameters: ``device`` hip | cpu | auto; ``ranks`` P virtual slabs in this process (default:
     one per distributed rank, or 1); ``devices`` GPU ids for the local slabs; ``transport`` auto |
-    rccl | ipc | torch | staged | loopback | host; ``overlap`` interior sweep concurrent with boundary
+    rccl | rccl_fold (rccl with the folded lower boundary) | ipc | ipc_sdma | torch | staged |
+    loopback | host; ``overlap`` interior sweep concurrent with boundary
     planes + exchange; ``sync_debug`` serialise every phase (race screen); ``residual_every`` k:
     global L2 norm of the update every k steps (NaN/Inf guard); ``graph`` replay two-sweep cycles
     as hipGraphs; ``timeout_s`` watchdog; ``temporal`` fused steps per sweep (1 = none, 0 = auto,
@@ -92,6 +93,10 @@ class Simulation:
         self._control = None  # host control plane of the ipc transport (teardown barrier)
         self.group = group
 
+        fold_req = None
+        if transport == "rccl_fold":
+            # rccl with the folded lower boundary (not rccl's default: Transport::fold_by_default)
+            transport, fold_req = "rccl", 1
         if self.distributed:
             if transport in ("rccl", "ipc", "ipc_sdma") and device != "hip":
                 raise ValueError("%s transport needs HIP devices" % transport)
@@ -176,6 +181,9 @@ class Simulation:
         if self._torch_transport is not None:
             self._torch_transport.solver = self._s
         self.transport = self._s.transport_name if self._torch_transport is None else "torch"
+        if fold_req is not None:
+            self._s.set_options(fold=fold_req)
+            self.transport = "rccl_fold"
         self.bounds = slab_bounds(problem.nz, nranks // max(1, self.py))
 
     # ---- lifecycle -------------------------------------------------------------------------
@@ -226,8 +234,9 @@ class Simulation:
         self._s.synchronize()
 
     def set_options(self, **kw):
-        """Change run options (overlap, sync_debug, residual_every, graph, timeout_s, profile);
-        options not named keep their values."""
+        """Change run options (overlap, sync_debug, residual_every, graph, timeout_s, profile,
+        min_rounds, fold: -1 the transport's default, 0 never, 1 where possible); options not named
+        keep their values."""
         self._s.set_options(**kw)
 
     def warm_kernels(self, steps: int) -> None:

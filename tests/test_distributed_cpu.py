@@ -182,6 +182,47 @@ def test_bench_self_launches_8_ranks_cpu(mdfx):
     assert ver["passed"] and ver["ranks"] == 8 and ver["max_abs_diff"] == 0.0 and ver["steps"] == [1, 4, 4, 4]
     assert len(cfg["repeats_ms_per_step"]) == 3 and rec["ms_per_step"] == sorted(cfg["repeats_ms_per_step"])[1]
     assert cfg["schedule"] in cfg["parallelism"]
+    # self-diagnosis of the N > 1 run: every rank's phase split per sweep and its
+    # face pulls timed alone, the selection phase's passes, and the bench's wall time
+    ph, ln = cfg["phases"], cfg["links"]
+    assert [p["rank"] for p in ph] == list(range(8)) and [l["rank"] for l in ln] == list(range(8))
+    for p in ph:
+        assert "error" not in p, p
+        assert p["sweeps"] > 0 and p["step_us"] > 0 and p["interior_us"] >= 0
+        assert {"boundary_us", "exchange_us", "exposed_us"} <= set(p)
+    for r, l in enumerate(ln):
+        assert "error" not in l, l
+        npeer = 1 if r in (0, 7) else 2
+        if cfg["py"] == 1:
+            assert len(l["peers"]) == npeer and all(abs(q - r) == 1 for q in l["peers"])
+        assert l["exchange_us"] > 0 and l["GBps_per_face"] > 0 and all(b > 0 for b in l["face_bytes"])
+    assert cfg["trial_passes"] in (1, 2) and rec["wall_s"] > 0
+
+
+def test_bench_n1_times_three_repeats_and_reports_the_median(mdfx):
+    """At N = 1 too the timed window is three back-to-back repetitions; the median is reported
+    (one 8-ms shot is noisy), and no N > 1 diagnostics are attached."""
+    import json
+    import statistics
+
+    rc, out, err = _bench(["--device", "cpu", "--n", "24", "--steps", "3", "--warmup", "1"])
+    assert rc == 0, err
+    rec = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    cfg = rec["config"]
+    reps = cfg["repeats_ms_per_step"]
+    assert len(reps) == 3 and rec["ms_per_step"] == round(statistics.median(reps), 4)
+    assert cfg["verified"]["steps"] == [1, 3, 3, 3] and cfg["verified"]["passed"]
+    assert cfg["phases"] is None and cfg["links"] is None and rec["wall_s"] > 0
+
+
+def test_ipc_export_retry_loop_cpu(mdfx):
+    """The ipc transport's export retry: "invalid argument" is retried and the count
+    returned; one failure too many raises with the call named and the retries counted."""
+    nat = mdfx.native()
+    assert nat.ipc_export_retry_selftest(0) == 0
+    assert nat.ipc_export_retry_selftest(3) == 3
+    with pytest.raises(RuntimeError, match=r"hipIpcGetMemHandle.*after 2 retries"):
+        nat.ipc_export_retry_selftest(5, max_retries=2)
 
 
 def test_bench_json_reports_effective_graph_mode(mdfx):
@@ -225,14 +266,21 @@ def test_bench_verification_catches_a_fault_the_gate_missed(mdfx):
     assert not [l for l in out.splitlines() if l.startswith("{")]
 
 
-def test_rccl_gets_the_folded_single_stream_schedule(mdfx):
+def test_rccl_gets_the_single_stream_schedule_and_folds_only_on_request(mdfx):
     """RCCL's grouped send / recv is stream work on the halo stream under every HIP runtime, so one
-    slab per process gets the folded boundary-on-compute schedule with it, eager where the runtime
-    cannot capture it (it used to fall back to the two-stream schedule under HIP 7.0)."""
+    slab per process gets the boundary-on-compute schedule with it, eager where the runtime cannot
+    capture it (it used to fall back to the two-stream schedule under HIP 7.0). The
+    folded lower boundary is NOT rccl's default (no run has shown RCCL's p2p kernels
+    reading a face published by a mid-sweep counter); fold=1 (bench.py's gated `rccl_fold`
+    candidate) asks for it, fold=0 refuses it for every transport."""
     nat = mdfx.native()
     tr = nat.rccl_traits()
     assert tr["stream_ordered"] is True
     assert tr["graph_capturable"] == (nat.hip_runtime_version() >= 70200000)
+    assert tr["fold_by_default"] is False
+    assert nat.fold_allowed(-1, tr["fold_by_default"]) is False
+    assert nat.fold_allowed(1, tr["fold_by_default"]) is True
+    assert nat.fold_allowed(-1, True) is True and nat.fold_allowed(0, True) is False
     assert nat.step_schedule(True, 1, tr["stream_ordered"], True) == "folded"
     assert nat.step_schedule(True, 1, tr["stream_ordered"], False) == "boundary-on-compute"
     # several slabs in one process, or a host-side exchange (torch / staged callbacks): two streams

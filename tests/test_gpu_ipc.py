@@ -165,19 +165,23 @@ def test_ipc_fp64_fused_k4_folded(hip, tmp_path, graph):
         assert meta["folded"] > 0 and meta["captures"] == 0, meta
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_ipc_fp32_fused_k5_folded(hip, tmp_path, graph):
+@pytest.mark.parametrize("transport,direct,graph", [("ipc", "", False), ("ipc", "", True),
+                                                     ("ipc_sdma", "1", False), ("ipc_sdma", "0", False)])
+def test_ipc_fp32_fused_k5_folded(hip, tmp_path, transport, direct, graph):
     """fp32 K = 5 sweeps (the default depth of the 3D 7-point: heat7_wxk in rows of 2 cells per lane,
     the lower boundary folded into the interior sweep) over three processes: bitwise equal to one
-    process, residual included; eager runs fold, captured cycles never wait on a fold counter."""
+    process, residual included; eager runs fold, captured cycles never wait on a fold counter.
+    ipc_sdma: the folded face read by the SDMA engines, which bypass the L2 like a remote GPU's
+    pull over xGMI (direct pulls from the field buffers, and the mailbox protocol's local publish
+    copy): the face must have been written back by the time the halo stream's counter wait ends."""
     import mpi_cuda_process_amd as m
 
     prob_src = "m.heat3d(nx=300, ny=45, nz=66)"
     out = str(tmp_path / "g.npy")
     steps = 20  # (residual every 10 / 20: K = 5 sweeps throughout, the last residual step 20's as in _reference)
     code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=5, graph=graph, steps=steps,
-                         resid=20 if graph else 10, transport="ipc")
-    _spawn(3, lambda r: [sys.executable, "-c", code])
+                         resid=20 if graph else 10, transport=transport)
+    _spawn(3, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_IPC_DIRECT": direct} if direct else None)
     ref, rres = _reference(eval(prob_src), steps)
     assert np.array_equal(np.load(out), ref)
     meta = json.load(open(out + ".json"))
@@ -308,6 +312,24 @@ def test_ipc_direct_protocol_at_the_headline_size(hip):
     assert cfg["ipc_protocol"] == "direct" and cfg["face_copy"] == "blit"
     # the timed run itself was checked on all four ranks against a full-grid naive run
     assert cfg["verified"]["passed"] and cfg["verified"]["ranks"] == 4 and cfg["verified"]["max_abs_diff"] == 0.0
+
+
+def test_ipc_export_retry_path_runs_and_logs(hip, tmp_path):
+    """MDFX_IPC_EXPORT_FAIL=2: the first two IPC exports of every process fail with "invalid
+    argument"; the transport logs a diagnosis of the pointer (attributes, allocation range, overlap
+    with imports it closed), retries, and the run stays bitwise equal to one process."""
+    import mpi_cuda_process_amd as m
+
+    prob_src = "m.heat3d(nx=128, ny=32, nz=40)"
+    out = str(tmp_path / "g.npy")
+    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=2, graph=False, steps=6, resid=4,
+                         transport="ipc")
+    _, outs = _spawn(2, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_IPC_EXPORT_FAIL": "2"})
+    for o in outs:
+        assert "hipIpcGetMemHandle succeeded after 2 retries" in o, o[-2000:]
+        assert "allocation [" in o and "import(s) this process closed earlier" in o, o[-2000:]
+    ref, _ = _reference(eval(prob_src), 6)
+    assert np.array_equal(np.load(out), ref)
 
 
 def test_ipc_refuses_two_engine_processes_on_one_gpu(hip, tmp_path):
