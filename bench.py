@@ -101,7 +101,7 @@ def parse(argv=None):
                         "overlap (auto); every candidate is timed twice, interleaved, and its faster run counts")
     p.add_argument("--temporal", type=int, default=0,
                    help="time steps fused per memory sweep (temporal blocking); 0 = auto (native "
-                        "hip_fused_depth): 5 (fp32) / 4 (fp64) for the 3D 7-point where heat7_wxk's x segments "
+                        "hip_fused_depth): 5 (fp32; fp64 from 2048-cell rows, else 4) for the 3D 7-point where heat7_wxk's x segments "
                         "cover the row, 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 (2D "
                         "MDF) / 12 (Life)")
     p.add_argument("--ref-precision", action="store_true",
@@ -236,11 +236,11 @@ def pick_temporal(a, prob, nslab, hip):
 
     if a.temporal > 0:
         return a.temporal
-    # the deepest measured-win fused depth (native hip_fused_depth: 5 / 4 for the fp32 / fp64 3D
-    # 7-point through heat7_wxk where its x segments cover the row; 3 for the
-    # 27-point at 1024-cell rows
-    # and in fp64, else 2; 8 (MDF) / 12 (Life) for the 2D ones; profiles/r03_wxk/, r02_mdf2d/,
-    # r02_life.txt), made shallower until every slab is at least 4 sweeps deep
+    # the deepest measured-win fused depth (native hip_fused_depth: 5 for the fp32 3D 7-point and for
+    # fp64 rows of 2048+ cells, 4 for shorter fp64 rows, through heat7_wxk where its x segments cover
+    # the row; 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 (MDF) / 12 (Life) for the
+    # 2D ones; profiles/archive/r03_wxk/, r06_session_b/), made shallower until every slab is at
+    # least 4 sweeps deep
     want = native().hip_fused_depth(prob.kind, prob.dtype, prob.nx, prob.ref_precision) if hip else \
         {"jacobi5": 8, "life": 12}.get(a.stencil, 2)
     while want > 1 and prob.nz < 4 * want * nslab:

@@ -49,7 +49,7 @@ bool rccl_stream_ordered() { return true; }
 bool rccl_fold_by_default() { return false; }
 // ... but RCCL's group joins its own internal streams to the caller's with events, and the HIP 7.0
 // runtime PyTorch bundles segfaults in hipStreamEndCapture on such multi-stream captures
-// (profiles/r02_graph_runtime.txt): RCCL steps are captured only under HIP >= 7.2
+// (profiles/archive/r02_graph_runtime.txt): RCCL steps are captured only under HIP >= 7.2
 bool rccl_graph_capturable() {
   static const bool ok = [] {
     int v = 0;

@@ -94,7 +94,7 @@ Solver::Solver(const StencilSpec& spec, Extent3 global, int nranks, std::vector<
     if (opt_.temporal > 1 && s.be->kind() == DeviceKind::HIP)
       MDFX_CHECK(hip_supports_steps(spec_, s.lay, opt_.temporal),
                  format("no fused %d-step kernel for %s %s with nx=%lld (fused depths: 2 for every stencil "
-                        "(box27 rows up to 1024 fp32 / 512 fp64); 3, 4 for the 3D 7-point; 3, 4, 6, 8 for the 2D stencils, "
+                        "(box27 rows up to 1024 fp32 / 512 fp64); 3, 4, 5 for the 3D 7-point; 3, 4, 6, 8 for the 2D stencils, "
                         "also 12, 16 for Life; pencils: 3, 4 fp32 / 3 fp64 for the 3D 7-point only)",
                         opt_.temporal, stencil_name(spec_.kind), dtype_name(spec_.dtype), (long long)global_.nx));
     // regions (storage planes); owned = [halo, halo + nzl). The boundary regions are the `halo`
@@ -322,7 +322,7 @@ void Solver::exchange_ghosts() {
 // it sent are overwritten only by the sweep after next, after this exchange on the halo stream.)
 // Only for one slab per process (the production layout; 8 slabs in one process ran 1936 vs 2023
 // GCells/s with it, rank proxies N = 8 / 4 / 2 1850 / 2073 / 2284 vs 1824 / 2069 / 2259,
-// profiles/r03_session_x/) and transports whose exchange is pure stream work on the halo stream
+// profiles/archive/r03_session_x/) and transports whose exchange is pure stream work on the halo stream
 // (a host-side exchange synchronises the halo stream alone).
 // Rounds of resident blocks per streaming sweep: the option, else 2 with several slabs (exchange
 // kernels that need CUs find some mid-sweep) and 1 for a single slab. Passed with every launch
@@ -710,7 +710,7 @@ void Solver::run(int64_t steps) {
     // a HIP runtime >= 7.2: the 7.0 runtime PyTorch bundles segfaults in hipStreamEndCapture on the
     // multi-slab loopback capture (6 streams with cross-slab event waits), while the identical
     // binary and capture replay bitwise under 7.2 (csrc/tests/test_main.cpp test_graph run against
-    // both runtimes: profiles/r02_graph_runtime.txt). One slab per process (the production layout)
+    // both runtimes: profiles/archive/r02_graph_runtime.txt). One slab per process (the production layout)
     // replays under both.
     // A captured cycle's first exchange sends buffer 1 - cur_; it is replayed only when the exchange
     // before it sent the other parity (a repeated parity needs the ipc transport's eager look-ahead

@@ -65,7 +65,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
 // The deepest fused sweep that is a measured win for this stencil at row width nx (before any
 // cap by slab depth): 8 for the 2D MDF, 12 for Life, 4 for the 3D 7-point where heat7_wxk's x
 // segments cover the row efficiently, else 2
-// (profiles/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt, r04_session_o/).
+// (profiles/archive/r02_wtk/README.txt, r02_mdf2d/, r02_life.txt, r04_session_o/).
 int hip_fused_depth(const StencilSpec& spec, int64_t nx);
 // Relative time of one `steps`-step sweep on the device, in single-step sweeps of the same grid
 // (the engine's sweep plan minimises the sum over a residual stretch).

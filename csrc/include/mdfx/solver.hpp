@@ -205,7 +205,7 @@ class Solver {
   // overlapped schedule: the interior sweep of a step waits for the SAME step's boundary kernels
   // instead of the previous step's, so the short boundary launch gets the whole device before the
   // long interior sweep takes every CU; the exchange still runs under the interior (rank proxy
-  // N = 8 1,833 vs 1,759 GCells/s per GPU, N = 4 2,058 vs 1,816: profiles/r03_session_p/; the
+  // N = 8 1,833 vs 1,759 GCells/s per GPU, N = 4 2,058 vs 1,816: profiles/archive/r03_session_p/; the
   // other order was removed in round 4). With one slab per process and a transport whose exchange
   // is pure stream work, the boundary kernels run on the compute stream ahead of the interior and
   // only the exchange on the halo stream (boundary_on_cs).

@@ -58,18 +58,18 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
                       hipStream_t s);
 double heat7_wtk_xeff(int64_t nx, int esize, int steps);
 // 3D 7-point sweeps of K >= 3 steps run heat7_wtk (wave-independent tiles; 1024^3 fp32 K = 3:
-// 1443 vs 1081 GCells/s for heat7_tbk, profiles/r02_wtk/README.txt; heat7_tbk's K = 3 / 4 were
+// 1443 vs 1081 GCells/s for heat7_tbk, profiles/archive/r02_wtk/README.txt; heat7_tbk's K = 3 / 4 were
 // removed in round 5)
 static bool use_wxk(DType dt, int64_t nx, int steps);
 // (fp32 K = 5: heat7_wxk only, in rows of 2 cells per lane)
 static bool use_wtk(int steps, DType dt) {
-  return heat7_wtk_supported(steps) || (dt == DType::F32 && steps == 5);
+  return heat7_wtk_supported(steps) || ((dt == DType::F32 || dt == DType::F64) && steps == 5);
 }
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
-// 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/r03_wxk/). MDFX_H7_WXK =
+// 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/archive/r03_wxk/). MDFX_H7_WXK =
 // 0 / 1 forces it off / on. fp64 K = 3 takes it from 2048-cell rows on, in 3 + 1-row bands: 2048^3
 // fp64 + residual every 12 897 vs 796 GCells/s for heat7_wtk, while at 1024-cell rows heat7_wtk's
-// 3-row waves stay ahead (907 vs 874) (profiles/r03_session_p/). fp64 K = 4 always runs it, in
+// 3-row waves stay ahead (907 vs 874) (profiles/archive/r03_session_p/). fp64 K = 4 always runs it, in
 // 2 + 1-row bands (heat7_wtk's K = 4 needs 1-row waves: 1024^3 1112-1124 vs 418 GCells/s,
 // profiles/r04_session_o/)
 static bool use_wxk(DType dt, int64_t nx, int steps) {
@@ -271,7 +271,7 @@ bool hip_supports_steps(const StencilSpec& spec, const FieldLayout& lay, int ste
 
 bool hip_region_signals(const StencilSpec& spec, const FieldLayout& lay, int steps) {
   return !lay.pencil() && spec.kind == StencilKind::Heat7 &&
-         (steps == 3 || steps == 4 || (steps == 5 && spec.dtype == DType::F32)) && lay.halo >= steps &&
+         (steps == 3 || steps == 4 || steps == 5) && lay.halo >= steps &&
          dev::use_wtk(steps, spec.dtype) && dev::use_wxk(spec.dtype, lay.global.nx, steps);
 }
 
@@ -281,7 +281,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
     case StencilKind::Life: return 12;
     case StencilKind::Box27:
       // K = 3 through box27_wxk for fp64 (512^3: 663 vs 527 GCells/s for box27_tbk K = 2), for fp32
-      // rows of 1024 cells and more (1024^3: 1291 vs 1102, profiles/r03_wxk/) and, since round 5's
+      // rows of 1024 cells and more (1024^3: 1291 vs 1102, profiles/archive/r03_wxk/) and, since round 5's
       // whole-row blocks, for fp32 rows of 257..512 cells (512^3: 1332 vs 1092 for box27_tb2n K = 2,
       // profiles/r05_session_f/). MDFX_B27_WXK = 0 / 1 forces K = 2 / 3
       if (dev::knobs().b27_wxk == 1) return 3;
@@ -291,7 +291,7 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // K = 3 through heat7_wtk wherever its x segments cover at least 2/3 of the lane cells:
       // 1024^3 fp32 1617-1679 vs 1221-1232 GCells/s at K = 2 (round 2), 2048^3 fp32 1666 vs 1136,
       // 1024^3 fp64 823-825 vs 546, 2048^3 fp64 818 vs 556; since the natural-layout rows also
-      // 512^3 fp32 (3 segments of 256 for 512 cells): 1311 vs 1230 (profiles/r03_wtk/). K = 4
+      // 512^3 fp32 (3 segments of 256 for 512 cells): 1311 vs 1230 (profiles/archive/r03_wtk/). K = 4
       // where heat7_wxk runs: its per-wave rows no longer grow with K, so the fourth step per pass
       // costs less than the HBM pass it saves (fp32; fp64 in round 4: 512^3 983 vs 740 GCells/s at
       // K = 3, 1024^3 1121 vs 885, 2048^3 + residual every 12 953 vs 890, profiles/r04_session_{o,p}/)
@@ -299,8 +299,13 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
       // rows leave room for the fifth level: 1024^3 2689 vs 2426 GCells/s at K = 4 in one process,
       // 1024^2 x 256 2639 vs 2399, x 128 2536 vs 2384, 768^3 2349 vs 1954, 512^3 2187 vs 2039,
       // 2048^2 x 512 2166 vs 2144 (profiles/r05_session_t/, r05_session_u/)
+      // fp64 K = 5 (round 6): heat7_wxk in rows of 1 cell per lane (RowOps1d, the 2-cell fp32 rows'
+      // register footprint; 54 of 64 lanes own a column), from rows of 2048 cells: 2048^3 + residual
+      // every 20 1120 vs 1058 GCells/s at K = 4, while at 1024-cell rows its 19 x segments x 27 bands
+      // (513 tiles on 256 CUs) lose to K = 4 (1011-1035 vs 1062-1080) (profiles/r06_session_b/)
       if (nx >= 512 && dev::heat7_wtk_xeff(nx, (int)dtype_size(spec.dtype), 3) >= 0.66) {
         if (spec.dtype == DType::F32 && dev::knobs().h7_wxk != 0) return 5;
+        if (spec.dtype == DType::F64 && nx >= 2048 && dev::knobs().h7_wxk != 0) return 5;
         return dev::use_wxk(spec.dtype, nx, 4) ? 4 : 3;
       }
       return 2;
@@ -310,16 +315,18 @@ int hip_fused_depth(const StencilSpec& spec, int64_t nx) {
 
 // From the per-step rates of each fused depth on one MI355X (GCells/s; the time of a k-step sweep
 // is k / rate_k): 3D 7-point fp32 1024^3 694 / 1300 / 1896 / 2350 for K = 1..4, fp64 347 / 546 /
-// 885 / 1110 (profiles/r03_wxk/first_ab.txt, r04_session_o/). Elsewhere a
+// 885 / 1110 (profiles/archive/r03_wxk/first_ab.txt, r04_session_o/). Elsewhere a
 // deeper sweep is taken to cost 5 % more per pass than a single step, which makes the plan the
 // fewest sweeps with the deepest first.
 double hip_sweep_cost(const StencilSpec& spec, int64_t nx, int steps) {
   if (steps <= 1) return 1.0;
   if (spec.kind == StencilKind::Heat7 && steps <= 5 && nx >= 1024) {
     // (fp32 K = 5 from the round-5 rates 1929 / 2399 / 2639 GCells/s for K = 3 / 4 / 5 at 1024^2 x
-    // 256, scaled to the K = 4 entry; fp64 has no 5-step sweep)
+    // 256, scaled to the K = 4 entry; fp64 K = 5 from round 6's per-sweep times against K = 4: 2048^3
+    // 38.4 vs 32.5 ms (x 1.18), 1024^3 x 1.31, profiles/r06_session_b/)
     static const double f32[6] = {0.0, 1.0, 1.07, 1.10, 1.18, 1.34};
-    static const double f64[6] = {0.0, 1.0, 1.27, 1.18, 1.25, 1.6};
+    static const double f64[6] = {0.0, 1.0, 1.27, 1.18, 1.25, 1.64};
+    if (spec.dtype == DType::F64 && steps == 5 && nx >= 2048) return 1.48;
     return (spec.dtype == DType::F64 ? f64 : f32)[steps];
   }
   return 1.0 + 0.05 * (steps - 1);

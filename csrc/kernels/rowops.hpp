@@ -394,5 +394,34 @@ struct RowOps2f {
   static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.v)); }
 };
 
+// fp64 rows of 1 cell per lane (one 8-B value; heat7_wxk's fp64 5-step sweep): the register footprint
+// of RowOps2f, so a wave holds the same five levels of 5 + 4-row bands. Each x neighbour is two
+// v_mov_b32_dpp (64-bit VALU ops take no DPP operand on gfx9), and a 64-lane segment owns only
+// 64 - 2K columns (OV = K overlap lanes per side at one cell per lane)
+static constexpr int kRowOps1 = 1;
+struct RowOps1d {
+  typedef double V;
+  struct Row {
+    double v;
+  };
+  static __device__ __forceinline__ Row fromv(const V& v) { return Row{v}; }
+  static __device__ __forceinline__ Row zero() { return Row{0.0}; }
+  static __device__ __forceinline__ double first(const Row& c) { return c.v; }
+  static __device__ __forceinline__ double last(const Row& c) { return c.v; }
+  // (((xm + xp) + ym) + yp) + zm; l / rr are the neighbour lanes' cells
+  static __device__ __forceinline__ Row partial(const Row&, double l, double rr, const Row& ym, const Row& yp,
+                                                const Row& zm) {
+    return Row{(((l + rr) + ym.v) + yp.v) + zm.v};
+  }
+  static __device__ __forceinline__ Row fin(const Row& S, const Row& zp, const Row& c, const Row& rc) {
+    return Row{__builtin_fma(rc.v, __builtin_fma(-6.0, c.v, S.v + zp.v), c.v)};
+  }
+  static __device__ __forceinline__ Row coef(double r, const bool* held) { return Row{held[0] ? 0.0 : r}; }
+  static __device__ __forceinline__ Row scale(const Row& x, double s) { return Row{x.v * s}; }
+  static __device__ __forceinline__ double get(const Row& c, int) { return c.v; }
+  static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
+  static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.v)); }
+};
+
 }  // namespace dev
 }  // namespace mdfx

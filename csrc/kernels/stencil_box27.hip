@@ -674,7 +674,7 @@ static void launch_box27_tb2_w(const Geo& g, const T* in, T* out, const StencilC
   const T c0 = (T)c.c0, c1 = (T)c.c1, c2 = (T)c.c2, c3 = (T)c.c3;
   // the natural-layout kernel with the 2-plane unroll (box27_tb2n; round 2's pair-layout fp32
   // box27_tb2, 937-944 vs 1005-1013 GCells/s at 512^3, was removed in round 4,
-  // profiles/r03_wtk/b27f32_*; its fp64 instance, 491.8 GCells/s against box27_tbk's 553, in round 5)
+  // profiles/archive/r03_wtk/b27f32_*; its fp64 instance, 491.8 GCells/s against box27_tbk's 553, in round 5)
   static_assert(std::is_same<T, float>::value, "box27_tb2n: fp32 rows (fp64 runs box27_tbk)");
   if (resid)
     hipLaunchKernelGGL((box27_tb2n<RY, WXN, true>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, YT, resid);
@@ -699,7 +699,7 @@ void launch_box27_tb2(const Geo& g, const T* in, T* out, const StencilCoef& c, d
   if (g.lz_end <= g.lz_begin) return;
   // fp64: box27_tbk with 4 rows per tile, fp32: box27_tb2 (interleaved A/B on one MI355X, GCells/s,
   // tb2 / tbk RY 2 / tbk RY 4: 512^3 fp32 987 / 942 / 884, 1024^3 fp32 995 / 873 / 985, 512^3 fp64
-  // 492 / 468 / 553; profiles/r02_box27_tbk.txt). box27_tb2 exists for fp32 only (its pair-layout
+  // 492 / 468 / 553; profiles/archive/r02_box27_tbk.txt). box27_tb2 exists for fp32 only (its pair-layout
   // rows cost the fp64 instance occupancy: 489 -> 341). One row per tile on short columns. (The
   // switch to the other combinations, measured slower, was removed in round 5.)
   if constexpr (std::is_same<T, double>::value) {

@@ -363,7 +363,7 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
 // (Round 3 also had an x-pair variant for rows of 257..512 cells, box27_wxp: two 256-cell halves
 // side by side in one block with an LDS table of edge cells instead of overlapping lanes. Its
 // 6-row bands fetched twice the window rows per output row and it ran 909 vs 1017-1026 GCells/s
-// at 512^3 (profiles/r03_session_t/); removed in round 4.)
+// at 512^3 (profiles/archive/r03_session_t/); removed in round 4.)
 
 template <class T, int RY, int RE, int K, int WB, int XW = 0>
 static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf, double* resid, hipStream_t s) {

@@ -351,10 +351,10 @@ static void launch_heat7_ry(const Geo& g, const T* in, T* out, T r, double* resi
 template <class T>
 void launch_heat7(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  // defaults from bench/kernel_ab.py on MI355X, 1024^3 fp32 (profiles/r01_ab_heat7_f32.json):
+  // defaults from bench/kernel_ab.py on MI355X, 1024^3 fp32 (profiles/archive/r01_ab_heat7_f32.json):
   // RY=2 PF=1 1.546 ms (694.5 GCells/s) > RY=4 PF=1 1.584 > RY=4 PF=2 1.603 > RY=2 PF=2 1.662
   // fp64 1024^3: RY=4 PF=2 3.395 ms (316 GCells/s) > RY=4 PF=1 3.415 > RY=2 PF=1 3.479
-  // (profiles/r01_ab_heat7_f64.json).
+  // (profiles/archive/r01_ab_heat7_f64.json).
   // (short columns take the same tiles: a 1-row copy for ny < 8 was dropped in round 5 with the other
   // rarely reached instances, libmdfx.so size)
   constexpr int RY = sizeof(T) == 4 ? 2 : 4;

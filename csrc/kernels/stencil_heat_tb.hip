@@ -283,10 +283,10 @@ int64_t resident_blocks(const void* kfn) { return resident_blocks(kfn, 256); }
 // z-chunk of a fused sweep over `planes` planes and `tiles` xy tiles: balanced chunks of about 43
 // planes (equal up to one plane), shortened while the grid would not fill the device once.
 // Short chunks keep y-neighbour tiles at nearly the same z, so they share their halo rows in the
-// XCD's L2 (zc 128 fetched 2.00x the field, zc 32 1.25x: profiles/r01_tb2_zc_sweep.txt); balanced
+// XCD's L2 (zc 128 fetched 2.00x the field, zc 32 1.25x: profiles/archive/r01_tb2_zc_sweep.txt); balanced
 // ~43-plane chunks were the best or within 1% of it at every slab depth of the 1024^2 strong-
 // scaling shapes, e.g. 1024 x 1024 x 128 (the N = 8 slab): 876 GCells/s at zc 64 vs 1043 at zc 43
-// (profiles/r01_tb2_zc_slabs.txt).
+// (profiles/archive/r01_tb2_zc_slabs.txt).
 int tb2_zc(int64_t planes, int64_t tiles, int64_t resident) {
   if (planes <= 16) return (int)std::max<int64_t>(planes, 1);
   int64_t zt = (planes + 43) / 44;
@@ -321,7 +321,7 @@ void launch_heat7_tb2(const Geo& g, const T* in, T* out, T r, double* resid, hip
   if (g.lz_end <= g.lz_begin) return;
   MDFX_CHECK(g.pitch > 4 * 64 * VT<T>::N, "heat7_tb2 serves rows wider than one block (heat7_tbk covers the rest)");
   // RY = 2 (MDFX_TB_RY=1 for one row per tile): f64 2048^3 533 GCells/s vs 505 at RY = 4 and 429 at
-  // RY = 1, and the x-tiled heat7_tbk at 483 (profiles/r02_ab_f64_2048.txt)
+  // RY = 1, and the x-tiled heat7_tbk at 483 (profiles/archive/r02_ab_f64_2048.txt)
   if (knobs().tb_ry == 1 || g.ny < 8)
     launch_tb2_xt<T, 1>(g, in, out, r, resid, s);
   else
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void jacobi5_tbk(const T* __restrict__ in, T* 
   // MODE 2 / 3 keep PD rows in flight (u0 rows q + 1 .. q + PD load while row q is consumed): one
   // row of K-level work is far shorter than a loaded global-load round trip at 2-3 waves per SIMD
   // (16384^2 fp32 K = 8: 4487-4515 GCells/s with two rows in flight vs 4202-4208 with one,
-  // profiles/r03_session_aa/)
+  // profiles/archive/r03_session_aa/)
   Row nxr[PD];
   nxr[0] = nx;
 #pragma unroll
@@ -630,8 +630,8 @@ static void launch_jacobi5_tbk_km(const Geo& g, const T* in, T* out, T r, double
 // 4 waves per SIMD without the unroll (mode 1; 16384^2 K = 8: 3346-3368 GCells/s vs 3131-3145
 // unrolled at 2 waves per SIMD). fp64: the pair rows (RowOps<double>) with the 2-row unroll and two
 // u0 rows in flight (mode 2; 16384^2 K = 8: 2216-2219 vs 2005 GCells/s for mode 0,
-// profiles/r03_session_ac/). Round 2's fp32 pair layout and fp64 mode 0, and a 4-row unroll
-// (mode 3), measured slower and were removed in round 4 (profiles/r03_mdf2d/, r03_session_ac/).
+// profiles/archive/r03_session_ac/). Round 2's fp32 pair layout and fp64 mode 0, and a 4-row unroll
+// (mode 3), measured slower and were removed in round 4 (profiles/archive/r03_mdf2d/, r03_session_ac/).
 template <class T, int K, bool REF>
 static void launch_jacobi5_tbk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if constexpr (sizeof(T) == 4 && REF)

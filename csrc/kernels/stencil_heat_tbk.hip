@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
               // a compiler-visible store: hipcc drains this wave's in-flight DMA (vmcnt(0)) before
               // it. Measured faster here than lds_store() without the drain (1024^3 fp32 K=2 1274
               // vs 1125 GCells/s, K=3 1121 vs 1071); the occupancy-1 kernels (K=4, box27_tbk)
-              // gain from lds_store() instead (profiles/r02_lds_store_drain.txt)
+              // gain from lds_store() instead (profiles/archive/r02_lds_store_drain.txt)
               for (int j = 1; j < ROUT - 1; ++j) *(typename RO::T2*)(wp + j * TB_ROW) = RO::edges(Y[j]);
             }
             lds_barrier();
@@ -264,12 +264,12 @@ namespace dev {
 // so chunks are long: R whole rounds of resident blocks, R = planes-per-slot / 128 clamped to
 // [1, 4]. One single round has the best minimum but the worst mean sweep time (slow blocks are
 // never rebalanced); about 4 rounds are as fast on average with a small spread. Per-dispatch
-// means on 1024^3 fp32, K = 2 (profiles/r01_tbk/zc_dispatch_stats.txt): zc 512 / 256 / 171 /
+// means on 1024^3 fp32, K = 2 (profiles/archive/r01_tbk/zc_dispatch_stats.txt): zc 512 / 256 / 171 /
 // 128 / 86 -> 1.768 / 1.770 / 1.646 / 1.671 / 1.646 ms per sweep; the N = 8 slab (128 planes,
 // best of 3 x 20): zc 128 / 64 / 43 -> 1025 / 1358 / 1082 GCells/s.
 // Every chunk also pays 2K planes of pipeline fill, so a region is never split into chunks shorter
 // than 4K planes: under the 2-round policy of multi-slab runs the K-plane boundary regions were
-// split in two (8 slabs of 1024^2 x 128 at K = 3: 1369 vs 1491 GCells/s, profiles/r02_wtk/README.txt).
+// split in two (8 slabs of 1024^2 x 128 at K = 3: 1369 vs 1491 GCells/s, profiles/archive/r02_wtk/README.txt).
 int tbk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int min_rounds) {
   const double per_slot = (double)planes * (double)tiles / (double)resident;
   const int64_t rounds = std::max<int64_t>(min_rounds,
@@ -283,9 +283,9 @@ template <class T>
 bool heat7_tbk_supported(const Geo& g, int steps) {
   constexpr int WX = 64 * VT<T>::N;
   // the row in one block (wider rows at K = 2: heat7_tb2 x tiles, 533 vs 483 GCells/s for these
-  // kernels' x tiles at 2048^3 fp64, profiles/r02_ab_f64_2048.txt)
+  // kernels' x tiles at 2048^3 fp64, profiles/archive/r02_ab_f64_2048.txt)
   // (K = 3 / 4 run heat7_wtk / heat7_wxk: this kernel's deeper sweeps measured slower and were
-  // removed in round 5 with the switch that reached them, profiles/r01_tbk/, r02_wtk/README.txt)
+  // removed in round 5 with the switch that reached them, profiles/archive/r01_tbk/, r02_wtk/README.txt)
   return steps == 2 && g.pitch <= 4 * WX && g.nx >= 1 && g.ny >= 1;
 }
 template bool heat7_tbk_supported<float>(const Geo&, int);
@@ -318,7 +318,7 @@ static void launch_tbk_t(const Geo& g, const T* in, T* out, T r, double* resid, 
 }
 
 // Two fused steps. Rows per tile: 4 (1 on very short columns): RY 4 1351 GCells/s vs 3 1199, 2 1189
-// (profiles/r01_tbk/ab_1024_f32.log).
+// (profiles/archive/r01_tbk/ab_1024_f32.log).
 template <class T>
 void launch_heat7_tbk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;

@@ -48,7 +48,7 @@ int64_t resident_blocks(const void* kfn, int block);
 // sweep, where 6 or 4 chunks (171, 256 planes) end on a nearly empty round. (A balanced one-round
 // "split" schedule, block b marching the b-th equal share of the tile-major work, measured slower:
 // neighbouring y bands stop marching in lockstep and lose their L2 sharing of the y-halo rows, 1.59
-// instead of 1.20 fields fetched; removed in round 4, numbers in profiles/r03_wtk/.)
+// instead of 1.20 fields fetched; removed in round 4, numbers in profiles/archive/r03_wtk/.)
 static int wtk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int min_rounds) {
   const int64_t fill = 2 * K;
   const int64_t zmax = std::max<int64_t>(1, planes / (4 * K));
@@ -71,7 +71,7 @@ static int wtk_zc(int64_t planes, int64_t tiles, int64_t resident, int K, int mi
 // window, each row fetched once for the band instead of once per wave (9 rows per 3 output rows
 // -> 18 per 12 / 30 per 24), at one block barrier per plane. (The first version ran every wave as
 // an independent task with a private LDS slot and no barrier: 1.565 fields fetched per sweep
-// against 1.444 / 1.108 for bands of 4 / 8, and slower on every shape, profiles/r02_wtk/README.txt.)
+// against 1.444 / 1.108 for bands of 4 / 8, and slower on every shape, profiles/archive/r02_wtk/README.txt.)
 template <class T, int RY, int K, int WB, bool RES, int MODE>
 __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                  int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
@@ -299,7 +299,7 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
 // fp32 rows: the natural pair layout (RowOpsN) with the plane loop unrolled by two (mode 2); the
 // 3-row residual sweeps without the unroll (mode 1: the unrolled residual instance spills). fp64:
 // one layout (mode 0). (Round 2's regrouped fp32 layout, mode 0, measured slower and was removed
-// in round 4: 1.985 vs 1.736 ms per 3-step sweep, profiles/r03_pmc/.)
+// in round 4: 1.985 vs 1.736 ms per 3-step sweep, profiles/archive/r03_pmc/.)
 template <class T, int RY, int K, int WB>
 static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
   if constexpr (sizeof(T) == 4) {

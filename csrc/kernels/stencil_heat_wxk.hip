@@ -92,13 +92,16 @@ __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles,
 template <class T, int RY, int RE, int K, int WB, bool RES, bool PEN = false, bool SIG = false, int CN = 0>
 __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T* __restrict__ out, Geo g, T r,
                                                      int zc, int XT, int YT, int ntasks, double* __restrict__ resid) {
-  constexpr bool NAR = CN == kRowOps2;
-  static_assert(!NAR || sizeof(T) == 4, "heat7_wxk: 2-cell lanes are fp32");
-  using RO = typename std::conditional<NAR, RowOps2f,
-                                       typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type>::type;
+  constexpr bool NAR = CN != 0;  // narrow rows: 8 bytes per lane (fp32 2 cells, fp64 1 cell)
+  static_assert(CN != kRowOps2 || sizeof(T) == 4, "heat7_wxk: 2-cell lanes are fp32");
+  static_assert(CN != kRowOps1 || sizeof(T) == 8, "heat7_wxk: 1-cell lanes are fp64");
+  using RO = typename std::conditional<
+      CN == kRowOps2, RowOps2f,
+      typename std::conditional<CN == kRowOps1, RowOps1d,
+                                typename std::conditional<sizeof(T) == 4, RowOpsN, RowOps<T>>::type>::type>::type;
   using V = typename RO::V;
   using Row = typename RO::Row;
-  constexpr int N = NAR ? 2 : VT<T>::N;
+  constexpr int N = CN == kRowOps2 ? 2 : CN == kRowOps1 ? 1 : VT<T>::N;
   constexpr int OV = (K + N - 1) / N;     // overlap lanes per side
   constexpr int SEG = (64 - 2 * OV) * N;  // owned columns per wave
   constexpr int BR = 2 * RE + (WB - 2) * RY;  // output rows of a band
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
   __shared__ V seam[2][K - 1][WB - 1][2][64];
   // (A second plane in flight does not help this sweep: a third window buffer with one seam table
-  // and a second barrier lost in round 3 (profiles/r03_session_r/); an L2 prefetch of plane q + 2 by
+  // and a second barrier lost in round 3 (profiles/archive/r03_session_r/); an L2 prefetch of plane q + 2 by
   // 4-byte LDS DMAs lost 15-24 % in round 4 (profiles/r04_session_b/) and 15 % in round 5; the DMA
   // two planes ahead in these two buffers (a second barrier per step right after the window reads)
   // lost 4-6 %, non-temporal window DMAs 19 % (profiles/r05_session_b/, r05_session_c/).)
@@ -161,12 +164,16 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // u0 plane lz -> window buffer `buf` by LDS DMA; rows outside [0, ny) and lanes outside the row
   // read the nearest valid row / vector. Wave w fetches rows w, w + WB, ... of the window.
   const uint32_t xcb = (uint32_t)((x < 0 ? 0 : x >= pitch ? pitch - N : x) * (int64_t)sizeof(T));
-  // (2-cell lanes: the window row's two 64-cell halves, one cell per lane each)
+  // (narrow rows: the window row's 512 bytes as two halves of one dword per lane: fp32 2-cell lanes
+  // fetch cells xs + 64 h + lane, fp64 1-cell lanes dword 64 h + lane of the segment, i.e. half of
+  // cell xs + 32 h + lane / 2; cells outside the row clamp to the nearest valid one)
+  constexpr int DPC = (int)sizeof(T) / 4;  // dwords per cell
   uint32_t xch[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int64_t xh = xs + h * 64 + lane;
-    xch[h] = (uint32_t)((xh < 0 ? 0 : xh >= pitch ? pitch - 1 : xh) * (int64_t)sizeof(T));
+    const int d = h * 64 + lane;
+    const int64_t xh = xs + d / DPC;
+    xch[h] = (uint32_t)(((xh < 0 ? 0 : xh >= pitch ? pitch - 1 : xh) * DPC + d % DPC) * 4);
   }
   auto issue = [&](int lz, int buf) {
     const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
@@ -183,9 +190,9 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         if constexpr (NAR) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const T* a = (const T*)((const char*)(uintptr_t)rb + xch[h]);
-            dcheck(g, in, a, 1);
-            glds4(a, (T*)&win[buf][k][0] + h * 64);
+            const char* a = (const char*)(uintptr_t)rb + xch[h];
+            dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + (xch[h] & ~(uint32_t)(sizeof(T) - 1))), 1);
+            glds4(a, (char*)&win[buf][k][0] + h * 256);
           }
         } else {
           const T* a = (const T*)((const char*)(uintptr_t)rb + xcb);
@@ -398,7 +405,7 @@ struct WxGeo {
 };
 template <class T, int RY, int RE, int K, int WB, int CN = 0>
 static WxGeo wxk_geo(const Geo& g) {
-  constexpr int N = CN == kRowOps2 ? 2 : VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
+  constexpr int N = CN == kRowOps2 ? 2 : CN == kRowOps1 ? 1 : VT<T>::N, OV = (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   constexpr int BR = 2 * RE + (WB - 2) * RY;
   WxGeo w;
   const int64_t planes = g.lz_end - g.lz_begin;
@@ -440,7 +447,7 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
   };
   using F = std::false_type;
   using Tr = std::true_type;
-  if constexpr (CN != 0) {  // (the 5-step 2-cell-lane sweep: slabs, with or without the folded boundary)
+  if constexpr (CN != 0) {  // (the 5-step narrow-row sweeps: slabs, with or without the folded boundary)
     MDFX_CHECK(!pen, "heat7_wxk: the 5-step sweep is for slabs");
     if (g.sig) {
       MDFX_CHECK(g.lz2_end <= g.lz2_begin, "heat7_wxk: folded boundaries are for one-region slab sweeps");
@@ -478,7 +485,7 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 // waves): 1024^3 2387-2394 GCells/s on every box measured; 4-row inner waves ran 2415-2454 on one
 // box and 2095-2138 on two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row band also
 // fills one round of resident blocks best (N = 8 proxy: 1798 vs 1657 for 4 rows)
-// (profiles/r03_wxk/). fp32 K = 3 (step-count remainders): 4-row waves. fp64 K = 3: 3 + 1-row bands
+// (profiles/archive/r03_wxk/). fp32 K = 3 (step-count remainders): 4-row waves. fp64 K = 3: 3 + 1-row bands
 // (2048^3 + residual: 897 vs 861 for 3 + 2, 862 for 2 + 2); fp64 K = 4: 2 + 1-row bands (254 VGPRs;
 // the 2 + 2, 3 + 1 and 3 + 2-row bands spill), 1024^3 1112-1124 GCells/s against 418 for heat7_wtk's
 // 1-row K = 4 and 870-885 at K = 3 (profiles/r04_session_o/). fp32 K = 4 in 3 + 1 and 2 + 1-row
@@ -486,17 +493,22 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
 // 2372; profiles/r04_session_r/). Round 3's other shapes (4-wave bands, 2-row fp32 bands, the 5-step
 // sweep, 3 window buffers /
 // one seam table) measured slower and were removed in round 4; their numbers stay in
-// profiles/r03_wxk/ and profiles/r03_session_r/.
+// profiles/archive/r03_wxk/ and profiles/archive/r03_session_r/.
 // fp32 K = 5 (round 5): rows of 2 cells per lane (RowOps2f: half the registers per row, so a fifth
 // level fits), 5 + 4-row bands of 8 waves (38 rows; 9 x segments of 116 columns x 27 bands = 243
 // tiles at 1024 cells, one round; 245 VGPRs). 1024^3 kernel A/B 2689 vs 2426 GCells/s for K = 4,
 // 768^3 2349 vs 1954, 512^3 2187 vs 2039, 1024^2 x 128 2536 vs 2384 (profiles/r05_session_t/,
 // r05_session_u/); 6 + 1-row bands measured 3 % slower; K = 6 spills in every band that fits one
 // round.
+// fp64 K = 5 (round 6): rows of 1 cell per lane (RowOps1d: the register footprint of the fp32 2-cell
+// rows, 243 VGPRs in the same 5 + 4-row bands; each x neighbour costs two DPP moves, and a segment
+// owns 54 of its 64 lanes' columns at one cell per lane). 2048^3 + residual every 20 1120 vs 1058
+// GCells/s for K = 4; 1024^3 1011-1035 vs 1062-1080 (19 x 27 = 513 tiles on 256 CUs), so the auto
+// depth takes it from 2048-cell rows only (hip_fused_depth; profiles/r06_session_b/).
 template <class T>
 void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s) {
   if (g.lz_end <= g.lz_begin) return;
-  MDFX_CHECK((steps >= 3 && steps <= (sizeof(T) == 4 ? 5 : 4)) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
+  MDFX_CHECK((steps >= 3 && steps <= 5) && g.lz_begin >= steps && g.lz_end + steps <= g.lz_max,
              format("heat7_wxk: %d fused steps need %d valid planes around [%lld, %lld) of %lld", steps, steps,
                     (long long)g.lz_begin, (long long)g.lz_end, (long long)g.lz_max));
   MDFX_CHECK(g.lz2_end <= g.lz2_begin || (g.lz2_begin >= g.lz_end && g.lz2_end + steps <= g.lz_max),
@@ -523,6 +535,10 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
     if (steps == 3) launch_wxk<T, 4, 4, 3, 8>(g, in, out, r, resid, s);
     else launch_wxk<T, 3, 2, 4, 8>(g, in, out, r, resid, s);
   } else {
+    if (steps == 5) {  // (1 cell per lane: RowOps1d, the 2-cell fp32 sweep's register footprint)
+      launch_wxk<T, 5, 4, 5, 8, kRowOps1>(g, in, out, r, resid, s);
+      return;
+    }
     // (K = 4: 2 + 1-row bands, 254 VGPRs; 2 + 2, 3 + 1 and 3 + 2 rows spill)
     if (steps == 3) launch_wxk<T, 3, 1, 3, 8>(g, in, out, r, resid, s);
     else launch_wxk<T, 2, 1, 4, 8>(g, in, out, r, resid, s);

@@ -140,8 +140,8 @@ void launch_life(const Geo& g, const uint8_t* in, uint8_t* out, double* resid, h
   if (planes <= 0) return;
   constexpr int WX = 64 * 16;
   const int XT = (int)((g.nx + WX - 1) / WX);
-  // 32768^2: zc 64 beats 128 (profiles/r01_ab_life_u8.json), zc 32 beats 64 once the carry bytes
-  // moved to DPP (2414 vs 2351 GCells/s, profiles/r01_life_tb2.txt)
+  // 32768^2: zc 64 beats 128 (profiles/archive/r01_ab_life_u8.json), zc 32 beats 64 once the carry bytes
+  // moved to DPP (2414 vs 2351 GCells/s, profiles/archive/r01_life_tb2.txt)
   const int zc = pick_zc(planes, XT, 256, 4 * 8192);
   const int ZT = (int)((planes + zc - 1) / zc);
   const int ntasks = XT * ZT;
@@ -304,7 +304,7 @@ void launch_life_tb2(const Geo& g, const uint8_t* in, uint8_t* out, double* resi
 }
 
 // (Round 4's SWAR K-generation kernel, life_tbk: 7,656-7,960 GCells/s at 32768^2 against life_bits'
-// 21,268-22,430, profiles/r02_life.txt, reachable only through a switch, was removed in round 5.)
+// 21,268-22,430, profiles/archive/r02_life.txt, reachable only through a switch, was removed in round 5.)
 
 // ---- K generations per sweep, bit-sliced (life_bits) ---------------------------------------------
 //

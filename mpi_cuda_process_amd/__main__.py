@@ -39,7 +39,7 @@ def _parser() -> argparse.ArgumentParser:
                         "(one process); ipc pulls faces with blit kernels, ipc_sdma with the SDMA engines")
     p.add_argument("--residual-every", type=int, default=0)
     p.add_argument("--temporal", type=int, default=0,
-                   help="time steps fused per sweep: 0 = auto (as mdfx and bench.py: 5 / 4 for the fp32 / fp64 3D 7-point on "
+                   help="time steps fused per sweep: 0 = auto (as mdfx and bench.py: 5 for the fp32 3D 7-point (fp64: 5 from 2048-cell rows, else 4) on "
                         "the GPU, 3 for the 27-point at 1024-cell rows and in fp64, else 2; 8 for the 2D MDF, 12 "
                         "for Life), 1 = one step per sweep")
     p.add_argument("--graph", action="store_true")

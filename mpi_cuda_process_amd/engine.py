@@ -37,7 +37,7 @@ from .parallel.dist import ControlPlane, TorchP2PTransport, broadcast_bytes, gro
 
 def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1) -> int:
     """Fused steps per sweep chosen like the CLIs' auto mode: the deepest fused kernel that exists on
-    this device (``hip_fused_depth``: 5 / 4 for the fp32 / fp64 3D 7-point through heat7_wxk, 3 for the 27-point in fp64 or at rows of 1024+ cells, else 2 for the 3D stencils,
+    this device (``hip_fused_depth``: 5 for the fp32 3D 7-point through heat7_wxk, fp64 5 from rows of 2048 cells and 4 below, 3 for the 27-point in fp64 or at rows of 1024+ cells, else 2 for the 3D stencils,
     8 for the 2D MDF, 12 for Life), made shallower until every slab is at least 4 sweeps
     deep; 1 on the CPU, where fused sweeps bring nothing."""
     if device != "hip":

@@ -552,9 +552,10 @@ def test_mdf_ref_precision_at_power_of_two_rate_is_bitwise_fp32(mdfx, r):
 
 def test_fused_depth_policy(mdfx):
     """hip_fused_depth: the measured-win fused depth per stencil and row width (host-side policy,
-    profiles/r02_wtk/README.txt, r03_wtk/, r03_wxk/): for the 3D 7-point where the x segments cover
+    profiles/archive/r02_wtk/README.txt, r03_wtk/, r03_wxk/): for the 3D 7-point where the x segments cover
     at least 2/3 of the lane cells (rows of 512 cells and more) K = 5 through heat7_wxk in fp32
-    (2-cell lanes) and K = 4 in fp64, 2 below; the 27-point 3 (box27_wxk) in fp64, at fp32 rows of 257..512 cells (whole-row
+    (2-cell lanes), in fp64 K = 5 from rows of 2048 cells (1-cell lanes, round 6) and K = 4 below, 2
+    below 512; the 27-point 3 (box27_wxk) in fp64, at fp32 rows of 257..512 cells (whole-row
     blocks) and of 1024 cells and more, else 2;
     8 / 12 for the 2D stencils; auto_temporal makes it shallower for thin slabs (5 -> 4 -> 2 -> 1,
     3 -> 2 -> 1)."""
@@ -563,7 +564,12 @@ def test_fused_depth_policy(mdfx):
 
     d = m.native().hip_fused_depth
     assert d("heat7", "f32", 1024) == 5 and d("heat7", "f64", 1024) == 4
-    assert d("heat7", "f32", 2048) == 5 and d("heat7", "f64", 2048) == 4 and d("heat7", "f32", 3072) == 5
+    assert d("heat7", "f32", 2048) == 5 and d("heat7", "f64", 2048) == 5 and d("heat7", "f32", 3072) == 5
+    assert d("heat7", "f64", 2047) == 4 and d("heat7", "f64", 4096) == 5
+    # the sweep plan's cost of an fp64 5-step sweep follows the row width it is the default for
+    c = m.native().hip_sweep_cost
+    assert c("heat7", "f64", 2048, 5) < c("heat7", "f64", 1024, 5)
+    assert auto_temporal(m.heat3d(n=2048, dtype="f64"), 8, "hip") == 5   # config 5: 256-plane slabs
     assert d("heat7", "f32", 512) == 5 and d("heat7", "f32", 256) == 2 and d("heat7", "f64", 512) == 4
     assert d("box27", "f32", 512) == 3 and d("box27", "f32", 1024) == 3 and d("box27", "f64", 512) == 3
     assert d("box27", "f32", 256) == 2 and d("box27", "f32", 768) == 2

@@ -475,9 +475,7 @@ def test_heat7_wxk_bitwise(hip, prob, k, resid, knob):
     """heat7_wxk (y halo exchanged between the waves of a band through the LDS seam table, one
     barrier per plane) == K naive single steps, bitwise, with the residual of step K, for every
     shipped band and row count, including bands taller than the grid and waves wholly outside it
-    (K = 5: the fp32 sweep in rows of 2 cells per lane)."""
-    if k == 5 and prob.dtype != "f32":
-        pytest.skip("the 5-step sweep is fp32")
+    (K = 5: fp32 in rows of 2 cells per lane, fp64 in rows of 1 cell per lane)."""
     knob("MDFX_H7_WXK", 1)
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
@@ -503,11 +501,12 @@ def test_heat7_wxk_bitwise(hip, prob, k, resid, knob):
 
 
 @pytest.mark.parametrize("resid", [False, True])
-def test_heat7_fp64_wide_rows_default_path(hip, resid):
-    """fp64 rows of 1024 cells and more take heat7_wxk (2 + 1-row bands) at K = 4 by default: the
-    engine's default fused depth and kernel == 4 naive single steps, bitwise."""
-    prob = models.heat3d(nx=2048, ny=23, nz=11, dtype="f64")
-    k = 4
+@pytest.mark.parametrize("nx,k", [(1024, 4), (2048, 5)])
+def test_heat7_fp64_wide_rows_default_path(hip, resid, nx, k):
+    """fp64 rows of 1024 cells take heat7_wxk at K = 4 by default (2 + 1-row bands), rows of 2048
+    cells and more at K = 5 (1 cell per lane): the engine's default fused depth and kernel == K naive
+    single steps, bitwise."""
+    prob = models.heat3d(nx=nx, ny=23, nz=13, dtype="f64")
     assert native().hip_fused_depth(prob.kind, prob.dtype, prob.nx, False) == k
     lay = FieldLayout.make(prob, halo=k)
     src = alloc_field(lay, "cuda")
@@ -604,12 +603,12 @@ def test_box27_wxk_regions_and_engine(hip, knob, nx):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("k", [3, 4, 5])
-def test_heat7_wxk_regions_and_engine(hip, k, knob):
+@pytest.mark.parametrize("k,dtype", [(3, "f32"), (4, "f32"), (5, "f32"), (5, "f64")])
+def test_heat7_wxk_regions_and_engine(hip, k, dtype, knob):
     """heat7_wxk on a middle slab: both boundary regions in one launch + the interior == the whole
     grid; and an engine run over 3 slabs with the wxk sweeps == single steps."""
     knob("MDFX_H7_WXK", 1)
-    prob = models.heat3d(nx=1024, ny=20, nz=40)
+    prob = models.heat3d(nx=1024, ny=20, nz=40, dtype=dtype)
     full = FieldLayout.make(prob, halo=k)
     g = alloc_field(full, "cuda")
     init_field(prob, full, g)
@@ -633,7 +632,7 @@ def test_heat7_wxk_regions_and_engine(hip, k, knob):
         apply_stencil(prob, lay, src, out3, lo, hi, steps=k, resid=res3)
     torch.cuda.synchronize()
     assert res.item() > 0 and abs(res.item() - res3.item()) <= 1e-9 * res3.item()
-    p3 = models.heat3d(nx=600, ny=37, nz=45)
+    p3 = models.heat3d(nx=600, ny=37, nz=45, dtype=dtype)
     a, _ = _sim(p3, 2 * k, ranks=1)
     b, _ = _sim(p3, 2 * k, ranks=3, temporal=k)
     assert np.array_equal(a, b)

@@ -25,7 +25,7 @@ def recs():
 
 def test_no_kernel_spills_to_scratch(recs):
     # VGPR spills go to scratch memory (HBM round trips inside the z-march). SGPR spills land in
-    # VGPR lanes (v_writelane / v_readlane) and are tolerated; profiles/r01_kernel_resources.txt
+    # VGPR lanes (v_writelane / v_readlane) and are tolerated; profiles/archive/r01_kernel_resources.txt
     # lists them.
     bad = [n for n, r in recs.items() if r.get("private_segment_fixed_size", 0) or r.get("vgpr_spill_count", 0)]
     assert not bad, bad
@@ -68,6 +68,9 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, false, 0>", 2),       # fp64 K = 4 (the default from 1024-cell rows)
     ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, true, false, false, 0>", 2),
     ("mdfx::dev::heat7_wxk<double, 2, 1, 4, 8, false, false, true, 0>", 2),        # its folded-boundary copy
+    ("mdfx::dev::heat7_wxk<double, 5, 4, 5, 8, false, false, false, 1>", 2),       # fp64 K = 5 (1-cell lanes)
+    ("mdfx::dev::heat7_wxk<double, 5, 4, 5, 8, true, false, false, 1>", 2),
+    ("mdfx::dev::heat7_wxk<double, 5, 4, 5, 8, false, false, true, 1>", 2),        # its folded-boundary copy
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false, 0>", 2),              # 27-point K = 3 (1024-cell rows, fp64)
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, false, 2>", 2),              # fp32 rows <= 512: whole-row blocks
     ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, true, 2>", 2),
