@@ -89,6 +89,7 @@ static Knobs read_knobs() {
   k.h7_wxk = env_int("MDFX_H7_WXK", -1);
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
+  k.fold_release = env_int("MDFX_FOLD_RELEASE", 0);
   return k;
 }
 
@@ -365,6 +366,7 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
                "a folded boundary (RegionArgs::sig) needs a one-region slab sweep through heat7_wxk");
     g.sig = a.sig;
     g.sig_z = a.sig_z;
+    g.fold_release = dev::knobs().fold_release;
   }
   if (a.ly_end > a.ly_begin) {
     MDFX_CHECK(a.ly_begin >= a.lay.hy && a.ly_end <= a.lay.hy + a.lay.nyl(), "row range must lie inside the owned rows");

@@ -45,6 +45,7 @@ struct Geo {
   // sig[16] (sig[0] counts arrivals)
   unsigned long long* sig = nullptr;
   int64_t sig_z = 0;
+  int fold_release = 0;  // the signalling blocks write their XCD's L2 back first (Knobs::fold_release)
   unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };
 
@@ -222,6 +223,7 @@ struct Knobs {
   int h7_wxk = -1;     // MDFX_H7_WXK: K >= 3 sweeps of the 3D 7-point through heat7_wxk (-1: by dtype / width, 0: never, 1: always)
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64, fp32 rows of 257..512 or >= 1024 cells; 0 / 1)
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
+  int fold_release = 0;       // MDFX_FOLD_RELEASE: folded-boundary blocks release (L2 writeback) before they signal
 };
 const Knobs& knobs();
 

@@ -71,10 +71,18 @@ int64_t resident_blocks(const void* kfn, int block);
 // previous one on its stream, so no block of a launch arrives before the re-arm of the last one
 // that used its counters. (A monotonic count compared modulo `tiles` would need no re-arm, but
 // its 64-bit division around this out-of-line call makes the sweep spill.)
-__device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles, bool leader) {
+// fold_release (MDFX_FOLD_RELEASE=1, round 6 A/B): the leader first writes back its XCD's L2 with a
+// system-scope release fence (no invalidate), after every wave's stores of the block are in that L2,
+// so each signalling block publishes its own face tiles to memory instead of relying on the
+// halo stream's counter-wait dispatch to write every L2 back.
+__device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles, bool leader, bool release) {
   wait_vm0();
   lds_barrier();
   if (leader) {
+    if (release) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      wait_vm0();  // the writeback has completed before the arrival is counted
+    }
     const unsigned long long n = __hip_atomic_fetch_add(sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
     if (n == (unsigned long long)tiles) {
       __hip_atomic_store(sig, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -374,7 +382,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
           // block's arrival, and the last block of the launch to arrive bumps the sweep counter the
           // halo stream waits for. Visibility to the exchange rests on the counter-wait kernel's
           // end-of-dispatch release (hip_region_signals, kernels.hpp)
-          wxk_fold_signal(g.sig, tiles, w == 0 && lane == 0);
+          wxk_fold_signal(g.sig, tiles, w == 0 && lane == 0, g.fold_release != 0);
         }
       }
     };
