@@ -63,18 +63,28 @@ int64_t resident_blocks(const void* kfn, int block);
 // One block's arrival at the folded boundary (one out-of-line copy for every march variant): the
 // wave's stores of the lower planes complete (vmcnt 0: acknowledged by this XCD's L2), the block
 // barrier, then one lane counts the arrival; the block that completes the count re-arms it and bumps
-// the sweep counter sig[16]. No cache maintenance here: the halo stream's counter-wait kernel ends
-// with the dispatch packet's release, which writes back every XCD's L2 before the exchange reads the
-// face. (A per-block agent-scope release - an L2 writeback, and with acq_rel an L2 invalidate, by
+// the sweep counter sig[16]. No cache maintenance here by default (see fold_release below): the
+// halo stream's counter-wait kernel ends with the dispatch packet's release, which writes back
+// every XCD's L2 before the exchange reads the face. (A per-block agent-scope release - an L2 writeback, and with acq_rel an L2 invalidate, by
 // each of the 235 blocks - slowed the whole sweep by ~25 %.) The upper boundary launch and the
 // interior sweep count on separate counter blocks (Solver::Slab::sig), and each launch follows the
 // previous one on its stream, so no block of a launch arrives before the re-arm of the last one
 // that used its counters. (A monotonic count compared modulo `tiles` would need no re-arm, but
 // its 64-bit division around this out-of-line call makes the sweep spill.)
-// fold_release (MDFX_FOLD_RELEASE=1, round 6 A/B): the leader first writes back its XCD's L2 with a
+// fold_release (MDFX_FOLD_RELEASE=1, opt-in): the leader first writes back its XCD's L2 with a
 // system-scope release fence (no invalidate), after every wave's stores of the block are in that L2,
-// so each signalling block publishes its own face tiles to memory instead of relying on the
-// halo stream's counter-wait dispatch to write every L2 back.
+// so each signalling block publishes its own face tiles to memory instead of relying on the halo
+// stream's counter-wait dispatch to write every L2 back. (A release by the last-arriving block
+// alone would not do: buffer_wbl2 writes back only the L2 of the XCD that executes it.) Round 6
+// A/B, interleaved on one box: rank proxy N = 8 2,111 / 2,041 GCells/s without, 2,009 / 2,026 with
+// (-2.8 %), N = 4 2,449 vs 2,409 (-1.7 %); the K = 4 / 5 folded ipc and proxy tests pass with it
+// (profiles/r06_session_d/). Over the 1 % budget, so it stays opt-in.
+// What the default relies on: the counter-wait kernel on the halo stream ends with its dispatch
+// packet's system-scope release, which the HIP runtime implements as a writeback of every XCD's
+// L2 (the whole cache, not only that kernel's lines). The exchange's copies are dispatched after
+// it on the same stream. That whole-L2 writeback is an implementation property, not an HSA
+// guarantee; tests/test_gpu_ipc.py checks it for blit and SDMA readers (SDMA, like a peer GPU over
+// xGMI, reads memory without going through this device's L2).
 __device__ __noinline__ void wxk_fold_signal(unsigned long long* sig, int tiles, bool leader, bool release) {
   wait_vm0();
   lds_barrier();
@@ -157,6 +167,10 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int64_t pitch = g.pitch, plane = g.plane;
   const bool xin = x >= 0 && x < pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
+  // (store policy A/B, Geo::store_mode: the two owned lanes at each end of the segment write the
+  // 32-B sectors a neighbouring segment also writes)
+  const int smode = g.store_mode;
+  const bool seam_lane = lane <= OV + 1 || lane >= 62 - OV;
   bool xb[N];
 #pragma unroll
   for (int e = 0; e < N; ++e) xb[e] = (x + e == 0) || (x + e >= g.nx - 1);
@@ -345,7 +359,10 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
             if (valid && i >= 0 && i < SH::R && y0 + i < ly1 && own) {
               T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
               dcheck(g, (const T*)out, a, N);
-              store_nt((V*)a, RO::vec(cur));
+              if (smode == 2 || (smode == 1 && seam_lane))
+                *(V*)a = RO::vec(cur);
+              else
+                store_nt((V*)a, RO::vec(cur));
             }
             break;
           }

@@ -75,6 +75,15 @@ __global__ __launch_bounds__(64) void counter_signal_kernel(uint64_t* ctr) {
 // shared GPUs without share_gpu (ipc_shared_gpu_problem), captured graphs never containing a folded
 // wait (Solver::step), and the wall-clock bound below: a wait that cannot complete turns into an
 // error word the host watchdog reports, never into a hang.
+// Visibility guarantee relied on by the folded boundary: when this kernel, waiting for a fold
+// counter, completes, its dispatch packet's system-scope release is carried out by the runtime as
+// a writeback of every XCD's L2 (the whole cache), so the face tiles the still-running sweep stored
+// earlier (s_waitcnt vmcnt(0) before its arrival counted) are in memory before the exchange's
+// copies, dispatched after this kernel on the same stream, read them - blit kernels on other XCDs,
+// SDMA engines or a peer GPU over xGMI. An HSA release only promises the kernel's own writes; the
+// whole-L2 writeback is the implementation's behaviour, checked on one GPU with blit and SDMA
+// readers (tests/test_gpu_ipc.py::test_ipc_fp32_fused_k5_folded). MDFX_FOLD_RELEASE=1 makes every
+// signalling block write its own XCD's L2 back first instead (wxk_fold_signal; 1.7-2.8 % slower).
 __global__ __launch_bounds__(64) void counter_wait_kernel(const uint64_t* remote, uint64_t* expect, uint64_t ahead,
                                                           uint64_t ticks, const int* abort_w, int* err_w) {
   if (threadIdx.x != 0) return;
