@@ -66,14 +66,16 @@ static bool use_wtk(int steps, DType dt) {
   return heat7_wtk_supported(steps) || ((dt == DType::F32 || dt == DType::F64) && steps == 5);
 }
 // ... and among them heat7_wxk (y halo exchanged inside the band, stencil_heat_wxk.hip) for fp32:
-// 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/archive/r03_wxk/). MDFX_H7_WXK =
-// 0 / 1 forces it off / on. fp64 K = 3 takes it from 2048-cell rows on, in 3 + 1-row bands: 2048^3
+// 1024^3 K = 4 2262 GCells/s vs heat7_wtk K = 3 1868 on one box (profiles/archive/r03_wxk/); since
+// round 6 heat7_wtk is fp64 only (its fp32 instances ran only under MDFX_H7_WXK=0: 12 kernels,
+// ~290 KB of code object, removed). MDFX_H7_WXK = 0 / 1 forces fp64's choice off / on. fp64 K = 3
+// takes it from 2048-cell rows on, in 3 + 1-row bands: 2048^3
 // fp64 + residual every 12 897 vs 796 GCells/s for heat7_wtk, while at 1024-cell rows heat7_wtk's
 // 3-row waves stay ahead (907 vs 874) (profiles/archive/r03_session_p/). fp64 K = 4 always runs it, in
 // 2 + 1-row bands (heat7_wtk's K = 4 needs 1-row waves: 1024^3 1112-1124 vs 418 GCells/s,
 // profiles/r04_session_o/)
 static bool use_wxk(DType dt, int64_t nx, int steps) {
-  return steps >= 5 || knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (dt == DType::F32 || nx >= 2048 || steps == 4));
+  return steps >= 5 || dt == DType::F32 || knobs().h7_wxk == 1 || (knobs().h7_wxk < 0 && (nx >= 2048 || steps == 4));
 }
 
 static int env_int(const char* name, int dflt) {
@@ -440,11 +442,8 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
         dev::launch_heat7_wxk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
       else
         dev::launch_heat7_wxk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
-    } else if (dev::use_wtk(a.steps, spec.dtype)) {
-      if (spec.dtype == DType::F32)
-        dev::launch_heat7_wtk<float>(g, (const float*)a.in, (float*)a.out, (float)spec.rate(), a.steps, a.resid, s);
-      else
-        dev::launch_heat7_wtk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
+    } else if (dev::use_wtk(a.steps, spec.dtype)) {  // (fp64 only: use_wxk holds for every fp32 sweep)
+      dev::launch_heat7_wtk<double>(g, (const double*)a.in, (double*)a.out, spec.rate(), a.steps, a.resid, s);
     } else if (a.steps > 2 || (spec.dtype == DType::F32 ? dev::heat7_tbk_supported<float>(g, 2)
                                                         : dev::heat7_tbk_supported<double>(g, 2))) {
       // rows within one block: the streaming K-step kernel; wider rows (K = 2): heat7_tb2 x tiles

@@ -300,14 +300,13 @@ static void launch_wtk_kn(const Geo& g, const T* in, T* out, T r, double* resid,
 // 3-row residual sweeps without the unroll (mode 1: the unrolled residual instance spills). fp64:
 // one layout (mode 0). (Round 2's regrouped fp32 layout, mode 0, measured slower and was removed
 // in round 4: 1.985 vs 1.736 ms per 3-step sweep, profiles/archive/r03_pmc/.)
+// (Round 6: only the fp64 instances ship. Every fp32 3D 7-point sweep runs heat7_wxk, so the fp32
+// layouts of this kernel, modes 1 and 2, were reachable only through MDFX_H7_WXK=0; their 12
+// instances are no longer compiled. The numbers above stay as the record of why heat7_wxk won.)
 template <class T, int RY, int K, int WB>
 static void launch_wtk_k(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  if constexpr (sizeof(T) == 4) {
-    if (resid && RY == 3) launch_wtk_kn<T, RY, K, WB, 1>(g, in, out, r, resid, s);
-    else launch_wtk_kn<T, RY, K, WB, 2>(g, in, out, r, resid, s);
-  } else {
-    launch_wtk_kn<T, RY, K, WB, 0>(g, in, out, r, resid, s);
-  }
+  static_assert(sizeof(T) == 8, "heat7_wtk ships fp64 instances only");
+  launch_wtk_kn<T, RY, K, WB, 0>(g, in, out, r, resid, s);
 }
 
 bool heat7_wtk_supported(int steps) { return steps == 3 || steps == 4; }
@@ -357,7 +356,6 @@ void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double*
     launch_wtk_k<T, 1, 4, 4>(g, in, out, r, resid, s);
   }
 }
-template void launch_heat7_wtk<float>(const Geo&, const float*, float*, float, int, double*, hipStream_t);
 template void launch_heat7_wtk<double>(const Geo&, const double*, double*, double, int, double*, hipStream_t);
 
 }  // namespace dev

@@ -503,9 +503,6 @@ static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hi
 
 bool heat7_wxk_supported(int steps) { return steps == 3 || steps == 4; }
 
-template <class T>
-void launch_heat7_wtk(const Geo& g, const T* in, T* out, T r, int steps, double* resid, hipStream_t s);
-
 // Shipped bands of 8 waves: fp32 K = 4 in 2 + 6 x 3 + 2 rows (3-row inner waves, 2-row edge
 // waves): 1024^3 2387-2394 GCells/s on every box measured; 4-row inner waves ran 2415-2454 on one
 // box and 2095-2138 on two others (near the LDS limit, 156 KB), 2-row waves 2247-2253; on thin slabs the 3-row band also
@@ -547,10 +544,15 @@ void launch_heat7_wxk(const Geo& g, const T* in, T* out, T r, int steps, double*
   // 2 + 2 rows in 2-wave blocks instead of 22-row bands of 8 waves that would compute 4 useful rows
   // (and 4 blocks per CU, so the strip's few tiles split into many z chunks)
   const bool strip = g.ly_end - g.ly_begin <= 4 && (g.ly_begin != 0 || g.ly_end != g.ny);
-  if (strip) {
-    if (steps == 3) launch_wxk<T, 2, 2, 3, 2>(g, in, out, r, resid, s);
-    else launch_wxk<T, 2, 2, 4, 2>(g, in, out, r, resid, s);  // (fp64: 256 VGPRs, no spills)
-    return;
+  // (round 6: only the fp32 K = 4 strip, the pencils' default depth, keeps its 2-wave instance; the
+  // K = 3 strips (step-count tails) and fp64 strips run in the regular 8-wave bands, which compute
+  // more rows than the strip needs but are correct for any row range: 8 fewer kernel instances,
+  // ~320 KB of code object, and no more 322-VGPR fp64 K = 4 strip copy spilling into AGPRs)
+  if constexpr (sizeof(T) == 4) {
+    if (strip && steps == 4) {
+      launch_wxk<T, 2, 2, 4, 2>(g, in, out, r, resid, s);
+      return;
+    }
   }
   if constexpr (sizeof(T) == 4) {
     if (steps == 5) {

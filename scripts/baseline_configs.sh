@@ -10,7 +10,7 @@ run() { local tag=$1; shift; echo "== $tag: $*"; timeout -k 10 600 python bench.
 run c1_mdf2d_256_f32_cpu --device cpu --stencil jacobi5 --nx 256 --nz 256 --steps 200 --warmup 10 || exit 1
 run c2_heat7_512_f32 --n 512 --steps 100 --warmup 10 || exit 1
 run c2_heat7_512_f32_t1 --n 512 --steps 100 --warmup 10 --temporal 1 || exit 1
-run c3_heat7_1024_f32 --n 1024 --steps 50 --warmup 10 --repeats 2 || exit 1
+run c3_heat7_1024_f32 --n 1024 --steps 50 --warmup 10 || exit 1
 run c3_heat7_1024_f32_driver --n 1024 --steps 20 --warmup 5 || exit 1
 for n in 2 4 8; do run c3_proxy$n --rank-proxy $n --steps 50 --warmup 10 || exit 1; done  # (K = 5: whole sweeps)
 run c3_proxy8_pencil --rank-proxy 8 --py 2 --steps 48 --warmup 12 || exit 1
@@ -18,6 +18,8 @@ run c4_box27_512_f32 --stencil box27 --n 512 --steps 100 --warmup 10 || exit 1
 run c4_box27_512_f64 --stencil box27 --n 512 --dtype f64 --steps 50 --warmup 5 || exit 1
 run c5_heat7_2048_f64_resid --n 2048 --dtype f64 --steps 24 --warmup 12 --residual-every 12 || exit 1
 run c5_heat7_2048_f64_resid10 --n 2048 --dtype f64 --steps 20 --warmup 10 --residual-every 10 || exit 1
+run c5_heat7_2048_f64_resid20 --n 2048 --dtype f64 --steps 20 --warmup 20 --residual-every 20 || exit 1
+run c5_proxy8_2048_f64_resid10 --rank-proxy 8 --n 2048 --dtype f64 --steps 20 --warmup 10 --residual-every 10 || exit 1
 run c5_proxy8_2048_f64_resid --rank-proxy 8 --n 2048 --dtype f64 --steps 24 --warmup 12 --residual-every 12 || exit 1
 run x_heat7_1024_f64 --n 1024 --dtype f64 --steps 30 --warmup 5 || exit 1
 run x_mdf2d_16k_f32 --stencil jacobi5 --nx 16384 --nz 16384 --steps 96 --warmup 16 || exit 1

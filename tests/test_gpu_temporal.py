@@ -433,12 +433,14 @@ WTK3D = DEEP3D + [models.heat3d(nx=2048, ny=13, nz=11), models.heat3d(nx=1100, n
                   models.heat3d(nx=1030, ny=7, nz=8), models.heat3d(nx=8, ny=6, nz=9)]
 
 
-@pytest.mark.parametrize("prob", WTK3D, ids=lambda p: p.describe().replace(" ", "_"))
+@pytest.mark.parametrize("prob", [p for p in WTK3D if p.dtype == "f64"] + [models.heat3d(nx=300, ny=33, nz=9, dtype="f64")],
+                         ids=lambda p: p.describe().replace(" ", "_"))
 @pytest.mark.parametrize("k,wb", [(3, "4"), (3, "8"), (4, "4")])
 @pytest.mark.parametrize("resid", [False, True])
 def test_heat7_wtk_bitwise(hip, prob, k, wb, resid, knob):
-    """heat7_wtk's K fused steps (the 3D 7-point kernel for K >= 3 where heat7_wxk does not run:
-    fp64 rows below 2048 cells, MDFX_H7_WXK=0) == K naive single steps, bitwise, with or without the
+    """heat7_wtk's K fused steps (fp64 only since round 6: the 3D 7-point kernel for K = 3 where
+    heat7_wxk does not run, fp64 rows below 2048 cells, and any fp64 K = 3 / 4 under MDFX_H7_WXK=0)
+    == K naive single steps, bitwise, with or without the
     residual of step K, in bands of 4 or 8 waves."""
     knob("MDFX_H7_WXK", 0)
     knob("MDFX_WTK_WB", wb)
@@ -671,18 +673,20 @@ def test_heat7_wtk_regions_on_a_slab(hip, k):
     assert res2.item() > 0 and abs(res2.item() - res1.item()) <= 1e-9 * res1.item()
 
 
-@pytest.mark.parametrize("k,ranks,wxk", [(3, 1, "-1"), (3, 3, "-1"), (4, 2, "-1"), (3, 3, "0"), (4, 2, "0")])
-def test_engine_wtk_temporal_3d(hip, k, ranks, wxk, knob):
-    """The engine's K-step sweeps (heat7_wxk by default, heat7_wtk with MDFX_H7_WXK=0) over 1-3
-    slabs with a residual every 10 steps == single steps."""
+@pytest.mark.parametrize("k,ranks,wxk,dtype", [(3, 1, "-1", "f32"), (3, 3, "-1", "f32"), (4, 2, "-1", "f32"),
+                                              (3, 3, "-1", "f64"), (3, 3, "0", "f64"), (4, 2, "0", "f64")])
+def test_engine_wtk_temporal_3d(hip, k, ranks, wxk, dtype, knob):
+    """The engine's K-step sweeps (heat7_wxk by default; fp64 K = 3 at 1024-cell rows, and fp64 K =
+    3 / 4 with MDFX_H7_WXK=0, through heat7_wtk) over 1-3 slabs with a residual every 10 steps ==
+    single steps."""
     knob("MDFX_H7_WXK", wxk)
-    prob = mm.heat3d(nx=1024, ny=24, nz=60)
+    prob = mm.heat3d(nx=1024, ny=24, nz=60, dtype=dtype)
     ref, rr = _sim(prob, 23, ranks=1, temporal=1, residual_every=10)
     got, rg = _sim(prob, 23, ranks=ranks, temporal=k, residual_every=10)
     assert np.array_equal(ref, got) and abs(rr - rg) <= 1e-9 * rr
 
 
-@pytest.mark.parametrize("prob", [models.heat3d(nx=1024, ny=12, nz=11), models.heat3d(nx=500, ny=21, nz=11, dtype="f64")],
+@pytest.mark.parametrize("prob", [models.heat3d(nx=1024, ny=12, nz=11, dtype="f64"), models.heat3d(nx=500, ny=21, nz=11, dtype="f64")],
                          ids=lambda p: p.describe().replace(" ", "_"))
 def test_wtk_never_reads_stale_lds(hip, prob):
     """heat7_wtk reads only LDS its own DMA filled: NaN-poisoned LDS does not change the result."""

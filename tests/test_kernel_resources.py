@@ -55,7 +55,6 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, true, false, 0>", 2),   # its pencil copy
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, false, false, true, 0>", 2),   # folded-boundary copy (N > 1)
     ("mdfx::dev::heat7_wxk<float, 2, 2, 4, 2, false, true, false, 0>", 2),   # pencil y strips (2-wave bands)
-    ("mdfx::dev::heat7_wxk<double, 2, 2, 3, 2, false, true, false, 0>", 2),
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, true, 0>", 2),
     ("mdfx::dev::heat7_wxk<float, 3, 2, 4, 8, true, false, false, 0>", 2),         # its residual sweeps
     ("mdfx::dev::heat7_wxk<float, 5, 4, 5, 8, false, false, false, 2>", 2),        # fp32 K = 5 (2-cell lanes): the default
@@ -77,8 +76,6 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false, 0>", 2),
     ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true, 0>", 2),
     ("mdfx::dev::box27_tb2n<1, 1, false>", 3),                          # 27-point K = 2 fp32 (512^3)
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 8, false, 2>", 2),       # K = 3 where heat7_wxk does not run
-    ("mdfx::dev::heat7_wtk<float, 3, 3, 4, false, 2>", 2),       # (thin slabs: 4-wave bands)
     ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0>", 2),
     ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 2>", 3),           # 2D MDF, 8 steps per sweep
     ("mdfx::dev::jacobi5_tbk<float, 8, false, true, 1>", 4),            # reference precision (no unroll)
