@@ -307,6 +307,8 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
                     hip_supports_steps(spec, FieldLayout::make(g, 0, g.nz, want, spec.dtype), want))
                        ? want
                        : 1;
+      // (a depth one residual interval's plan never runs would only widen the halo)
+      if (hip && o.temporal > 2) o.temporal = hip_interval_depth(spec, g, o.temporal, o.residual_every);
     }
     SolverOptions so;
     so.overlap = o.overlap;

@@ -346,6 +346,18 @@ const char* step_schedule(bool overlap, size_t local_slabs, bool stream_ordered,
   return fold ? "folded" : "boundary-on-compute";
 }
 
+int hip_interval_depth(const StencilSpec& spec, Extent3 g, int want, int64_t residual_every) {
+  if (want <= 2 || residual_every <= 0) return want;
+  SweepCosts c;
+  c.T = std::min(want, 16);
+  const FieldLayout lay = FieldLayout::make(g, 0, g.nz, want, spec.dtype);
+  for (int k = 1; k <= c.T; ++k) {
+    c.cost[k] = hip_sweep_cost(spec, g.nx, k);
+    c.ok[k] = k == 1 || hip_supports_steps(spec, lay, k);
+  }
+  return interval_depth(c, residual_every);
+}
+
 bool Solver::boundary_on_cs() const {
   return opt_.overlap && slabs_.size() == 1 && transport_->stream_ordered();
 }

@@ -95,4 +95,28 @@ std::vector<std::pair<int, bool>> plan_sweeps(const SweepCosts& c, int64_t steps
   return out;
 }
 
+int interval_depth(const SweepCosts& c, int64_t residual_every) {
+  const int T0 = std::max(1, std::min(c.T, 16));
+  if (T0 <= 1 || residual_every <= 0) return T0;
+  int best_t = T0;
+  double best = -1.0;
+  for (int T = T0; T >= 1; --T) {
+    if (T > 1 && !c.ok[T]) continue;
+    SweepCosts cc = c;
+    cc.T = T;
+    double sum = 0.0;
+    bool uses = T == 1;
+    for (const auto& kr : plan_sweeps(cc, residual_every, 0, residual_every)) {
+      sum += kr.first <= 1 ? 1.0 : c.cost[kr.first];
+      uses = uses || kr.first == T;
+    }
+    // (a depth whose plan never sweeps it costs the same as the next one down, with a wider halo)
+    if (uses && (best < 0.0 || sum < best - 1e-9)) {
+      best = sum;
+      best_t = T;
+    }
+  }
+  return best_t;
+}
+
 }  // namespace mdfx

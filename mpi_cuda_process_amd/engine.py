@@ -35,7 +35,7 @@ from .parallel.decomp import slab_bounds
 from .parallel.dist import ControlPlane, TorchP2PTransport, broadcast_bytes, group_for, is_distributed
 
 
-def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1) -> int:
+def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1, residual_every: int = 0) -> int:
     """Fused steps per sweep chosen like the CLIs' auto mode: the deepest fused kernel that exists on
     this device (``hip_fused_depth``: 5 for the fp32 3D 7-point through heat7_wxk, fp64 5 from rows of 2048 cells and 4 below, 3 for the 27-point in fp64 or at rows of 1024+ cells, else 2 for the 3D stencils,
     8 for the 2D MDF, 12 for Life), made shallower until every slab is at least 4 sweeps
@@ -55,7 +55,9 @@ def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1) -> in
         want = {5: 4, 3: 2}.get(want, want // 2)
     if want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                                 want, want, problem.ref_precision):
-        return want
+        # a depth one residual interval never sweeps (every 12 at depth 5: 4 + 4 + 4) only widens the halo
+        return native().hip_auto_depth(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz, want,
+                                       residual_every, problem.ref_precision)
     return 1
 
 
@@ -172,7 +174,7 @@ class Simulation:
         self.nranks = nranks
         self.py = int(py)
         if temporal <= 0:
-            temporal = auto_temporal(problem, nranks, device, int(py))
+            temporal = auto_temporal(problem, nranks, device, int(py), int(residual_every))
         self._s = native().Solver(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                   nranks, local_ranks, dev_list, overlap=overlap,
                                   sync_debug=sync_debug, residual_every=residual_every, graph=graph,

@@ -583,6 +583,29 @@ def test_fused_depth_policy(mdfx):
     assert auto_temporal(m.heat3d(n=1024), 1, "cpu") == 1
 
 
+def test_interval_depth_drops_a_depth_the_residual_interval_never_sweeps(mdfx):
+    """The auto depth follows the residual interval (round 6): the depth whose one-interval sweep
+    plan costs least (2048^3 fp64, every 12 steps: depth 5 plans 5 + 4 + 3, depth 4 plans the
+    cheaper 4 + 4 + 4 and keeps a 4-plane halo; rank proxy N = 8 834.9 vs 900.5 GCells/s)."""
+    import mpi_cuda_process_amd as m
+    from mpi_cuda_process_amd.engine import auto_temporal
+
+    nat = m.native()
+    c = [0.0] + [nat.hip_sweep_cost("heat7", "f64", 2048, k) for k in range(1, 6)]
+    ok = [False] + [True] * 5
+    # depth 5 plans 5 + 4 + 3 for a 12-step interval; depth 4's 4 + 4 + 4 costs less
+    assert [k for k, _ in nat.plan_sweeps(12, 0, 12, 5, c, ok)] == [5, 4, 3]
+    assert [k for k, _ in nat.plan_sweeps(12, 0, 12, 4, c, ok)] == [4, 4, 4]
+    assert nat.interval_depth(12, 5, c, ok) == 4
+    assert nat.interval_depth(10, 5, c, ok) == 5 and nat.interval_depth(20, 5, c, ok) == 5
+    assert nat.interval_depth(0, 5, c, ok) == 5 and nat.interval_depth(7, 1, c, ok) == 1
+    assert nat.hip_auto_depth("heat7", "f64", 2048, 2048, 2048, 5, 12) == 4
+    assert nat.hip_auto_depth("heat7", "f64", 2048, 2048, 2048, 5, 10) == 5
+    assert nat.hip_auto_depth("heat7", "f32", 1024, 1024, 1024, 5, 0) == 5
+    assert auto_temporal(m.heat3d(n=2048, dtype="f64"), 8, "hip", residual_every=12) == 4
+    assert auto_temporal(m.heat3d(n=2048, dtype="f64"), 8, "hip", residual_every=10) == 5
+
+
 def test_bench_pencil_candidates_fuse_at_most_four_steps():
     """bench.py gates and times (z, y) pencil candidates at their own depth: the slabs' fp32 depth 5
     has no pencil kernel (heat7_wxk's pencil copies fuse 3 / 4 steps), so a pencil candidate run at
