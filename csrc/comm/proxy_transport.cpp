@@ -135,10 +135,53 @@ class ProxyTransport final : public Transport {
       HIPC(hipEventRecord(ev_join_, aux_));
       HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
     };
+    // the ipc transport's fused slab pulls (IpcTransport::fused_pulls): the aux stream forks first,
+    // the halo stream's ready signal and first wait are one dispatch
+    auto fused = [&](auto src) {
+      const bool two = both;
+      if (two) {
+        HIPC(hipEventRecord(ev_fork_, hs));
+        HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
+      }
+      bool signalled = false;
+      for (int side = 0; side < 2; ++side) {
+        const HaloSpan h = halo_span(self_, b, side, nranks_);
+        if (h.peer < 0) continue;
+        hipStream_t ps = two && side == 1 ? aux_ : hs;
+        if (ps == hs && !signalled) {
+          hip_counter_signal_wait(ctr_ + kReady, ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, hs, 0, &words_);
+          signalled = true;
+        } else {
+          hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
+        }
+        hip_face_copy(h.recv, h, src(side, h), h, ps, copy_);
+      }
+      if (!signalled) hip_counter_signal(ctr_ + kReady, hs);
+      if (self_.ghost_event) {
+        HIPC(hipEventRecord((hipEvent_t)self_.ghost_event, hs));
+        HIPC(hipEventRecord((hipEvent_t)self_.ghost_event2, two ? aux_ : hs));
+      }
+      for (int side = 0; side < 2; ++side)
+        if (halo_span(self_, b, side, nranks_).peer >= 0)
+          hip_counter_signal(ctr_ + kPulled + side, two && side == 1 ? aux_ : hs);
+      if (two) {
+        HIPC(hipEventRecord(ev_join_, aux_));
+        HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
+      }
+    };
     if (direct_) {
       // the ipc direct sequence: ready, then per face wait + pull from the (own) field buffer +
       // pulled, then the wait that frees the faces the next boundary kernels overwrite. A pencil
       // pulls its y faces first and signals readyZ once they landed: its z faces carry those ghost rows
+      if (fuse_ && !pencil_) {
+        fused([&](int, const HaloSpan& h) { return (const void*)h.send; });
+        for (int side = 0; side < 2; ++side) {
+          if (halo_span(self_, b, side, nranks_).peer < 0) continue;
+          hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, 0, &words_);
+        }
+        if (!capturing) last_b_ = b;
+        return;
+      }
       hip_counter_signal(ctr_ + kReady, hs);
       if (pencil_) {
         phase(2, kReady, false);
@@ -161,6 +204,11 @@ class ProxyTransport final : public Transport {
       MDFX_CHECK(h.bytes == face_, "proxy: face geometry mismatch");
       hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, ahead, &words_);
       hip_face_copy(slot(b, side), h.send, face_, hs, copy_);
+    }
+    if (fuse_) {
+      fused([&](int side, const HaloSpan&) { return (const void*)slot(b, side); });
+      if (!capturing) last_b_ = b;
+      return;
     }
     hip_counter_signal(ctr_ + kReady, hs);
     // pull
@@ -208,6 +256,7 @@ class ProxyTransport final : public Transport {
   bool ok_ = false;
   bool direct_ = false;
   bool pencil_ = false;  // (z, y) pencil: y faces first, then the z faces
+  bool fuse_ = xchg_fuse();
   int last_b_ = -1;
   double timeout_s_ = 300.0;
 };

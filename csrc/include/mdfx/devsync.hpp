@@ -45,6 +45,10 @@ void hip_words_free(HipWords& w);
 // `own` is given, else the process-wide one); a timeout raises the matching error word.
 void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s, void* stream,
                       uint64_t ahead = 0, const HipWords* own = nullptr);
+// hip_counter_signal(signal) and hip_counter_wait(remote, ...) in ONE dispatch: the signal first,
+// then the wait (the exchange's ready signal fused with its first pull's wait).
+void hip_counter_signal_wait(uint64_t* signal, const uint64_t* remote, uint64_t* expect, double timeout_s,
+                             void* stream, uint64_t ahead = 0, const HipWords* own = nullptr);
 // The wait's kernel (its first argument is `remote`): the engine finds its nodes in captured graphs.
 const void* hip_counter_wait_kernel();
 

@@ -84,9 +84,18 @@ __global__ __launch_bounds__(64) void counter_signal_kernel(uint64_t* ctr) {
 // whole-L2 writeback is the implementation's behaviour, checked on one GPU with blit and SDMA
 // readers (tests/test_gpu_ipc.py::test_ipc_fp32_fused_k5_folded). MDFX_FOLD_RELEASE=1 makes every
 // signalling block write its own XCD's L2 back first instead (wxk_fold_signal; 1.7-2.8 % slower).
+// `signal` (optional): bumped first, as counter_signal_kernel does, so one dispatch both publishes
+// this process's counter and waits for the neighbour's (the exchange's "ready" signal and its first
+// pull's wait: one kernel launch fewer ahead of the pull, hip_counter_signal_wait). The kernel
+// boundary before it has already made the stream's earlier work visible.
 __global__ __launch_bounds__(64) void counter_wait_kernel(const uint64_t* remote, uint64_t* expect, uint64_t ahead,
-                                                          uint64_t ticks, const int* abort_w, int* err_w) {
+                                                          uint64_t ticks, const int* abort_w, int* err_w,
+                                                          uint64_t* signal) {
   if (threadIdx.x != 0) return;
+  if (signal) {
+    const uint64_t v = __hip_atomic_load(signal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(signal, v + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   const uint64_t next = __hip_atomic_load(expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   __hip_atomic_store(expect, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t want = next + ahead;
@@ -156,8 +165,16 @@ void hip_counter_wait(const uint64_t* remote, uint64_t* expect, double timeout_s
                       const HipWords* own) {
   int* w = own ? own->dev : dev_words();
   hipLaunchKernelGGL(counter_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, remote, expect, ahead,
-                     ticks_for(timeout_s), (const int*)w, w + 16);
+                     ticks_for(timeout_s), (const int*)w, w + 16, (uint64_t*)nullptr);
   check_launch("counter_wait");
+}
+
+void hip_counter_signal_wait(uint64_t* signal, const uint64_t* remote, uint64_t* expect, double timeout_s,
+                             void* stream, uint64_t ahead, const HipWords* own) {
+  int* w = own ? own->dev : dev_words();
+  hipLaunchKernelGGL(counter_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, remote, expect, ahead,
+                     ticks_for(timeout_s), (const int*)w, w + 16, signal);
+  check_launch("counter_signal_wait");
 }
 
 HipWords hip_words_alloc() {
