@@ -247,9 +247,9 @@ def pick_temporal(a, prob, nslab, hip):
         want = {5: 4, 3: 2}.get(want, want // 2)
     if want > 1 and (not hip or native().hip_supports_steps(prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz,
                                                             want, want, prob.ref_precision)):
-        if hip:  # (a depth one residual interval's plan never runs would only widen the halo)
+        if hip:  # (the depth for the residual interval, native interval_depth)
             return native().hip_auto_depth(prob.kind, prob.dtype, prob.nx, prob.ny, prob.nz, want,
-                                           a.residual_every, prob.ref_precision)
+                                           a.residual_every, prob.ref_precision, nslab)
         return want
     return 1
 

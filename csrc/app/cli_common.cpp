@@ -308,7 +308,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
                        ? want
                        : 1;
       // (a depth one residual interval's plan never runs would only widen the halo)
-      if (hip && o.temporal > 2) o.temporal = hip_interval_depth(spec, g, o.temporal, o.residual_every);
+      if (hip && o.temporal > 2) o.temporal = hip_interval_depth(spec, g, o.temporal, o.residual_every, nranks);
     }
     SolverOptions so;
     so.overlap = o.overlap;

@@ -356,7 +356,7 @@ const char* step_schedule(bool overlap, size_t local_slabs, bool stream_ordered,
   return fold ? "folded" : "boundary-on-compute";
 }
 
-int hip_interval_depth(const StencilSpec& spec, Extent3 g, int want, int64_t residual_every) {
+int hip_interval_depth(const StencilSpec& spec, Extent3 g, int want, int64_t residual_every, int nranks) {
   if (want <= 2 || residual_every <= 0) return want;
   SweepCosts c;
   c.T = std::min(want, 16);
@@ -365,7 +365,7 @@ int hip_interval_depth(const StencilSpec& spec, Extent3 g, int want, int64_t res
     c.cost[k] = hip_sweep_cost(spec, g.nx, k);
     c.ok[k] = k == 1 || hip_supports_steps(spec, lay, k);
   }
-  return interval_depth(c, residual_every);
+  return interval_depth(c, residual_every, nranks > 1);
 }
 
 bool Solver::boundary_on_cs() const {

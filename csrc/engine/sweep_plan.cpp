@@ -95,9 +95,21 @@ std::vector<std::pair<int, bool>> plan_sweeps(const SweepCosts& c, int64_t steps
   return out;
 }
 
-int interval_depth(const SweepCosts& c, int64_t residual_every) {
+int interval_depth(const SweepCosts& c, int64_t residual_every, bool uniform) {
   const int T0 = std::max(1, std::min(c.T, 16));
   if (T0 <= 1 || residual_every <= 0) return T0;
+  if (uniform) {
+    // several ranks: the deepest depth whose interval is whole sweeps of that depth (a shallower
+    // sweep on a deeper layout exchanges and recomputes the deeper halo)
+    for (int T = T0; T > 1; --T) {
+      if (!c.ok[T]) continue;
+      SweepCosts cc = c;
+      cc.T = T;
+      bool all = true;
+      for (const auto& kr : plan_sweeps(cc, residual_every, 0, residual_every)) all = all && kr.first == T;
+      if (all) return T;
+    }
+  }
   int best_t = T0;
   double best = -1.0;
   for (int T = T0; T >= 1; --T) {

@@ -86,10 +86,10 @@ struct StepStats {
 // boundary region computed inside the interior sweep, heat7_wxk fused sweeps).
 const char* step_schedule(bool overlap, size_t local_slabs, bool stream_ordered, bool fold);
 
-// Auto fused depth for a residual interval on the device: `want` made shallower until one interval's
-// sweep plan (the hip_sweep_cost tables, depths hip_supports_steps has on a `want`-deep layout of
-// grid g) runs a sweep of that depth (interval_depth). want itself when residual_every <= 0.
-int hip_interval_depth(const StencilSpec& spec, Extent3 g, int want, int64_t residual_every);
+// Auto fused depth for a residual interval on the device: interval_depth over the hip_sweep_cost
+// tables and the depths hip_supports_steps has on a `want`-deep layout of grid g (uniform sweeps
+// with several ranks). want itself when residual_every <= 0.
+int hip_interval_depth(const StencilSpec& spec, Extent3 g, int want, int64_t residual_every, int nranks = 1);
 
 class Solver {
  public:

@@ -25,13 +25,15 @@ int plan_next_sweep(const SweepCosts& c, int64_t len, bool res_end, int64_t* gra
 std::vector<std::pair<int, bool>> plan_sweeps(const SweepCosts& c, int64_t steps, int64_t start,
                                               int64_t residual_every);
 
-// The maximum depth (at most c.T) whose sweep plan of one residual interval costs least, among the
-// depths whose plan runs a sweep of that depth (ties: the deeper; c.T itself without a residual).
-// The plan at depth T cuts the interval into T-step sweeps and a cheapest tail of < 2T steps, so
-// it can miss a cheaper all-shallower cut: a residual every 12 steps at depth 5 plans 5 + 4 + 3
-// (fp64 costs 3.91) where depth 4's 4 + 4 + 4 costs 3.75, and the depth-5 layout also exchanges
-// and recomputes 5-plane boundary regions every sweep (round 6: 2048^3 fp64 1,041.6 GCells/s and
-// rank proxy N = 8 834.9 at depth 5, against 1,057 / 900.5 at depth 4; profiles/r06_session_e/).
-int interval_depth(const SweepCosts& c, int64_t residual_every);
+// The fused depth (at most c.T) for a run with a residual every `residual_every` steps (c.T itself
+// without one). One rank: the depth whose sweep plan of one interval costs least, among the depths
+// whose plan runs a sweep of that depth (ties: the deeper) - the plan at depth T cuts the interval
+// into T-step sweeps and a cheapest tail of < 2T steps, so a shallower depth can plan a cheaper
+// cut. Several ranks (`uniform`): the deepest depth whose interval is whole sweeps of that depth,
+// else the one-rank rule - every sweep of a run exchanges and recomputes boundary regions as deep
+// as the layout's halo, so a 4- or 3-step sweep on a 5-plane halo pays for 5 planes (round 6,
+// 2048^3 fp64, residual every 12: one GPU 1022 GCells/s at depth 5 (5 + 4 + 3) against 961-985 at
+// depth 4 (4 + 4 + 4), but the N = 8 rank proxy 841-849 against 878-880; profiles/r06_session_g/).
+int interval_depth(const SweepCosts& c, int64_t residual_every, bool uniform = false);
 
 }  // namespace mdfx

@@ -334,10 +334,15 @@ double hip_sweep_cost(const StencilSpec& spec, int64_t nx, int steps) {
     // (fp32 K = 5 from the round-5 rates 1929 / 2399 / 2639 GCells/s for K = 3 / 4 / 5 at 1024^2 x
     // 256, scaled to the K = 4 entry; fp64 K = 5 from round 6's per-sweep times against K = 4: 2048^3
     // 38.4 vs 32.5 ms (x 1.18), 1024^3 x 1.31, profiles/r06_session_b/)
+    // fp64 rows of 2048+ cells have their own row (round 6, per-sweep times at 2048^3: K = 3 28.8 ms
+    // (heat7_wxk 3 + 1 rows, round 3's 897 GCells/s), K = 4 34.9, K = 5 38.4, against ~24.8 ms for a
+    // single step; a residual every 12 steps then plans 5 + 4 + 3, which measured 1022 vs 961-985
+    // GCells/s for depth 4's 4 + 4 + 4 on one box, profiles/r06_session_g/)
     static const double f32[6] = {0.0, 1.0, 1.07, 1.10, 1.18, 1.34};
     static const double f64[6] = {0.0, 1.0, 1.27, 1.18, 1.25, 1.64};
-    if (spec.dtype == DType::F64 && steps == 5 && nx >= 2048) return 1.48;
-    return (spec.dtype == DType::F64 ? f64 : f32)[steps];
+    static const double f64w[6] = {0.0, 1.0, 1.27, 1.16, 1.41, 1.55};
+    if (spec.dtype == DType::F64) return (nx >= 2048 ? f64w : f64)[steps];
+    return f32[steps];
   }
   return 1.0 + 0.05 * (steps - 1);
 }

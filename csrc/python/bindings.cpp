@@ -390,21 +390,22 @@ PYBIND11_MODULE(_mdfx, m) {
     return plan_sweeps(c, steps, start, residual_every);
   }, py::arg("steps"), py::arg("start"), py::arg("residual_every"), py::arg("temporal"), py::arg("cost"),
      py::arg("ok"), "the engine's sweep plan for given per-depth costs (cost[k], ok[k] indexed by depth)");
-  m.def("interval_depth", [](int64_t residual_every, int temporal, std::vector<double> cost, std::vector<bool> ok) {
+  m.def("interval_depth", [](int64_t residual_every, int temporal, std::vector<double> cost, std::vector<bool> ok,
+                             bool uniform) {
     SweepCosts c;
     c.T = temporal;
     for (size_t k = 0; k < cost.size() && k < 17; ++k) c.cost[k] = cost[k];
     for (size_t k = 0; k < ok.size() && k < 17; ++k) c.ok[k] = ok[k];
     c.ok[1] = true;
-    return interval_depth(c, residual_every);
-  }, py::arg("residual_every"), py::arg("temporal"), py::arg("cost"), py::arg("ok"),
+    return interval_depth(c, residual_every, uniform);
+  }, py::arg("residual_every"), py::arg("temporal"), py::arg("cost"), py::arg("ok"), py::arg("uniform") = false,
      "the deepest depth <= temporal that one residual interval's sweep plan runs (interval_depth)");
   m.def("hip_auto_depth", [](const std::string& kind, const std::string& dtype, int64_t nx, int64_t ny, int64_t nz,
-                             int want, int64_t residual_every, bool ref_precision) {
+                             int want, int64_t residual_every, bool ref_precision, int nranks) {
     StencilSpec s = make_spec(kind, dtype, -1, 0, 0, 0, 0, ref_precision);
-    return hip_interval_depth(s, Extent3{nx, ny, nz}, want, residual_every);
+    return hip_interval_depth(s, Extent3{nx, ny, nz}, want, residual_every, nranks);
   }, py::arg("kind"), py::arg("dtype"), py::arg("nx"), py::arg("ny"), py::arg("nz"), py::arg("want"),
-     py::arg("residual_every"), py::arg("ref_precision") = false,
+     py::arg("residual_every"), py::arg("ref_precision") = false, py::arg("nranks") = 1,
      "want, made shallower until one residual interval's plan runs a sweep of that depth (HIP cost tables)");
   m.def("hip_sweep_cost", [](const std::string& kind, const std::string& dtype, int64_t nx, int steps) {
     return hip_sweep_cost(make_spec(kind, dtype, -1, 0, 0, 0, 0, false), nx, steps);

@@ -55,9 +55,10 @@ def auto_temporal(problem: Problem, nranks: int, device: str, py: int = 1, resid
         want = {5: 4, 3: 2}.get(want, want // 2)
     if want > 1 and native().hip_supports_steps(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz,
                                                 want, want, problem.ref_precision):
-        # a depth one residual interval never sweeps (every 12 at depth 5: 4 + 4 + 4) only widens the halo
+        # the depth for the residual interval (native interval_depth: least plan cost on one rank,
+        # whole sweeps of the depth with several)
         return native().hip_auto_depth(problem.kind, problem.dtype, problem.nx, problem.ny, problem.nz, want,
-                                       residual_every, problem.ref_precision)
+                                       residual_every, problem.ref_precision, nranks)
     return 1
 
 

@@ -583,26 +583,33 @@ def test_fused_depth_policy(mdfx):
     assert auto_temporal(m.heat3d(n=1024), 1, "cpu") == 1
 
 
-def test_interval_depth_drops_a_depth_the_residual_interval_never_sweeps(mdfx):
-    """The auto depth follows the residual interval (round 6): the depth whose one-interval sweep
-    plan costs least (2048^3 fp64, every 12 steps: depth 5 plans 5 + 4 + 3, depth 4 plans the
-    cheaper 4 + 4 + 4 and keeps a 4-plane halo; rank proxy N = 8 834.9 vs 900.5 GCells/s)."""
+def test_interval_depth_follows_the_residual_interval(mdfx):
+    """The auto depth follows the residual interval (round 6, 2048^3 fp64, a residual every 12
+    steps): on one GPU depth 5's plan 5 + 4 + 3 (measured 1022 GCells/s) beats depth 4's 4 + 4 + 4
+    (961-985); with several ranks every sweep exchanges and recomputes halo-deep boundary regions, so
+    depth 4's whole 4-step sweeps win (N = 8 rank proxy 878-880 vs 841-849). Intervals that are
+    whole 5-step sweeps keep depth 5 either way."""
     import mpi_cuda_process_amd as m
     from mpi_cuda_process_amd.engine import auto_temporal
 
     nat = m.native()
     c = [0.0] + [nat.hip_sweep_cost("heat7", "f64", 2048, k) for k in range(1, 6)]
     ok = [False] + [True] * 5
-    # depth 5 plans 5 + 4 + 3 for a 12-step interval; depth 4's 4 + 4 + 4 costs less
     assert [k for k, _ in nat.plan_sweeps(12, 0, 12, 5, c, ok)] == [5, 4, 3]
     assert [k for k, _ in nat.plan_sweeps(12, 0, 12, 4, c, ok)] == [4, 4, 4]
-    assert nat.interval_depth(12, 5, c, ok) == 4
-    assert nat.interval_depth(10, 5, c, ok) == 5 and nat.interval_depth(20, 5, c, ok) == 5
-    assert nat.interval_depth(0, 5, c, ok) == 5 and nat.interval_depth(7, 1, c, ok) == 1
-    assert nat.hip_auto_depth("heat7", "f64", 2048, 2048, 2048, 5, 12) == 4
-    assert nat.hip_auto_depth("heat7", "f64", 2048, 2048, 2048, 5, 10) == 5
-    assert nat.hip_auto_depth("heat7", "f32", 1024, 1024, 1024, 5, 0) == 5
+    assert nat.interval_depth(12, 5, c, ok) == 5 and nat.interval_depth(12, 5, c, ok, True) == 4
+    for uniform in (False, True):
+        assert nat.interval_depth(10, 5, c, ok, uniform) == 5 and nat.interval_depth(20, 5, c, ok, uniform) == 5
+        assert nat.interval_depth(0, 5, c, ok, uniform) == 5 and nat.interval_depth(7, 1, c, ok, uniform) == 1
+    # a depth whose interval plan never runs it is never chosen on one rank either
+    c2 = [0.0, 1.0, 1.0, 1.0, 1.0, 9.0]
+    assert [k for k, _ in nat.plan_sweeps(8, 0, 8, 5, c2, ok)] == [4, 4] and nat.interval_depth(8, 5, c2, ok) == 4
+    assert nat.hip_auto_depth("heat7", "f64", 2048, 2048, 2048, 5, 12) == 5
+    assert nat.hip_auto_depth("heat7", "f64", 2048, 2048, 2048, 5, 12, nranks=8) == 4
+    assert nat.hip_auto_depth("heat7", "f64", 2048, 2048, 2048, 5, 10, nranks=8) == 5
+    assert nat.hip_auto_depth("heat7", "f32", 1024, 1024, 1024, 5, 0, nranks=8) == 5
     assert auto_temporal(m.heat3d(n=2048, dtype="f64"), 8, "hip", residual_every=12) == 4
+    assert auto_temporal(m.heat3d(n=2048, dtype="f64"), 1, "hip", residual_every=12) == 5
     assert auto_temporal(m.heat3d(n=2048, dtype="f64"), 8, "hip", residual_every=10) == 5
 
 
