@@ -69,11 +69,12 @@ void usage(const char* prog) {
       "  --print                   dump the final grid like the reference's print_array\n"
       "  --json                    one JSON metrics line ; --verbose per-rank detail ; --quiet\n"
       "  --no-overlap --sync-debug --graph --variant auto|tuned|naive --timeout S\n"
-      "  --temporal 0..16          time steps fused per memory sweep (0 = auto on GPUs: 5 / 4 for\n"
-      "                            the fp32 / fp64 3D 7-point where heat7_wxk covers the row, 3 for\n"
-      "                            the 27-point in fp64 or at rows of 1024+ cells, else 2 for 3D;\n"
-      "                            8 for the 2D MDF, 12 for Life; 1 on the CPU; shallower until\n"
-      "                            slabs are 4 sweeps deep)\n"
+      "  --temporal 0..16          time steps fused per memory sweep (0 = auto on GPUs: 5 for the\n"
+      "                            fp32 3D 7-point and fp64 rows of 2048+ cells (fp64 4 below) where\n"
+      "                            heat7_wxk covers the row, 3 for the 27-point in fp64 or at rows of\n"
+      "                            1024+ cells, else 2 for 3D; 8 for the 2D MDF, 12 for Life; 1 on the\n"
+      "                            CPU; shallower until slabs are 4 sweeps deep, and fitted to the\n"
+      "                            --residual-every interval)\n"
       "  --profile                 per-phase timing of rank 0 (boundary / interior / exchange)\n"
       "  --dim 2|3                 default stencil of that dimension (5 / 7) ; --bc V = --edge V ; --coef R = --r R\n"
       "  --dump DIR                write the final grid (per-slab raw + JSON header, checkpoint format)\n"

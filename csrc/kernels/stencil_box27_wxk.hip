@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "kcommon.hpp"
@@ -414,6 +415,11 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
   // box27_tb2n K = 2 (profiles/r05_session_f/)
   if constexpr (std::is_same<T, float>::value)
     if (g.nx <= 512) return launch_b27x<T, 2, 1, 3, 4, 2>(g, in, out, cf, resid, s);
+  // (fp64 at 512-cell rows fills only 185 of 256 CUs in one round (5 segments x 37 bands); round 6
+  // measured the shapes that fill more: 6-wave bands of 10 rows (255 tiles) 570-575, 1-row waves in
+  // 8-row bands 559-563, 4-wave bands in 2 blocks per CU (425 tiles) 659-683, against 705-707 GCells/s
+  // for these 14-row bands: the march is latency-bound per wave, so more waves per tile pay, more
+  // tiles do not (profiles/r06_session_h/))
   launch_b27x<T, 2, 1, 3, 8>(g, in, out, cf, resid, s);
 }
 template void launch_box27_wxk<float>(const Geo&, const float*, float*, const StencilCoef&, int, double*, hipStream_t);
