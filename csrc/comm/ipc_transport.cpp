@@ -381,20 +381,8 @@ class IpcTransport final : public Transport {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIPC(hipStreamIsCapturing(hs, &cap));
     const bool capturing = cap != hipStreamCaptureStatusNone;
-    // the two pulls: lo side on the halo stream, hi side on the aux stream (forked after the
-    // publish / ready signal, joined back before the exchange ends)
-    const bool both = peers_[0].rank >= 0 && peers_[1].rank >= 0;
-    auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
-    auto fork = [&]() {
-      if (!both) return;
-      HIPC(hipEventRecord(ev_fork_, hs));
-      HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
-    };
-    auto join = [&]() {
-      if (!both) return;
-      HIPC(hipEventRecord(ev_join_, aux_));
-      HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
-    };
+    // the two pulls: lo side on the halo stream, hi side on the aux stream (fused_pulls; pencils:
+    // phase below), joined back before the exchange ends
     if (direct_) {
       // one pair of faces: the lo side's pull on the halo stream, the hi side's on the aux stream.
       // After the last pair the ghosts are complete: the ghost event goes on the halo stream right
@@ -434,12 +422,9 @@ class IpcTransport final : public Transport {
         phase(2, kReady, false);
         hip_counter_signal(ctr_ + kReadyZ, hs);
         phase(0, kReadyZ, true);
-      } else if (fuse_) {
+      } else {
         fused_pulls(b, [&](int side) { return (const char*)peers_[side].buf[b] + peers_[side].face_off; },
                     [&](int side) { return peers_[side].face; });
-      } else {
-        hip_counter_signal(ctr_ + kReady, hs);
-        phase(0, kReady, true);
       }
       for (int side = 0; side < 4; ++side) {
         const Peer& p = peers_[side];
@@ -461,38 +446,17 @@ class IpcTransport final : public Transport {
                        ahead, &words_);
       hip_face_copy(slot(mbox_, b, side), mine.send, face_, hs, copy_);
     }
-    if (fuse_) {
-      fused_pulls(b, [&](int side) { return (const char*)slot(peers_[side].mbox, b, 1 - side); },
-                  [&](int side) { return halo_span(self_, b, side, nranks_); });
-      if (!capturing) last_b_ = b;
-      return;
-    }
-    hip_counter_signal(ctr_ + kReady, hs);
-    // pull: the neighbour on `side` published its (1 - side) face of exchange e
-    fork();
-    for (int side = 0; side < 2; ++side) {
-      const Peer& p = peers_[side];
-      if (p.rank < 0) continue;
-      const HaloSpan mine = halo_span(self_, b, side, nranks_);
-      hipStream_t ps = pull_stream(side);
-      hip_counter_wait((const uint64_t*)p.ctr + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
-      hip_face_copy(mine.recv, slot(p.mbox, b, 1 - side), face_, ps, copy_);
-      hip_counter_signal(ctr_ + kPulled + side, ps);
-    }
-    join();
-    if (self_.ghost_event) {
-      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event, hs));
-      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event2, hs));
-    }
+    fused_pulls(b, [&](int side) { return (const char*)slot(peers_[side].mbox, b, 1 - side); },
+                [&](int side) { return halo_span(self_, b, side, nranks_); });
     if (!capturing) last_b_ = b;
   }
-  // The slab pulls with the ready signal fused into the first halo-stream wait (MDFX_XCHG_FUSE,
-  // default on): the hi-side pull's stream forks off BEFORE the signal, so its wait for the upper
-  // neighbour runs beside the signal, and the halo stream's signal and lo-side wait are one
-  // dispatch. Round 6 rank-proxy trace (profiles/r06_session_f/): the fold wait's end -> signal
-  // (6 us) -> 8 us launch gap -> wait (9 us) -> pull put the pulls 22 us behind the face, and the
-  // pulls then outlasted the interior sweep by 12 us. src(side) / span(side): where the face comes
-  // from (the neighbour's field buffer or its mailbox slot) and its geometry.
+  // The slab pulls (both protocols) with the ready signal fused into the first halo-stream wait: the
+  // hi-side pull's stream forks off BEFORE the signal, so its wait for the upper neighbour runs
+  // beside the signal, and the halo stream's signal and lo-side wait are one dispatch. Round 6
+  // rank-proxy traces (profiles/r06_session_{f,g}/): signal (6 us) -> 8 us launch gap -> wait (9 us)
+  // -> pull put the pulls 22 us behind the fold wait's end, fused 16 us (N = 2 / 4 proxies +0.3-0.8
+  // %, N = 8 within noise). src(side) / span(side): where the face comes from (the neighbour's field
+  // buffer or its mailbox slot) and its geometry.
   template <class Src, class Span>
   void fused_pulls(int b, Src src, Span span) {
     hipStream_t hs = (hipStream_t)self_.halo_stream;
@@ -597,7 +561,6 @@ class IpcTransport final : public Transport {
   bool direct_ = false;
   bool pencil_ = false;  // (z, y) pencil: y faces first, then the z faces (which carry the y ghosts)
   bool setup_done_ = false, aborted_ = false, share_gpu_ = false;
-  bool fuse_ = xchg_fuse();  // fused_pulls (slabs)
   Peer peers_[4];
   double timeout_s_ = 300.0;
 };
@@ -637,11 +600,6 @@ void ipc_enable_peer(int mine, int peer, int peer_rank) {
 
 // The direct protocol maps the neighbours' field buffers; torch's HIP 7.0 runtime stalls in
 // hipIpcOpenMemHandle from 2 GiB up, so only buffers of at most 1900 MiB (probed good) go direct.
-
-bool xchg_fuse() {
-  const char* v = std::getenv("MDFX_XCHG_FUSE");
-  return !(v && *v == '0');
-}
 
 bool ipc_direct_ok(size_t field_bytes) {
   const char* v = std::getenv("MDFX_IPC_DIRECT");  // (read per call: tests switch it within a process)

@@ -124,17 +124,6 @@ class ProxyTransport final : public Transport {
     };
     const bool both = halo_span(self_, b, 0, nranks_).peer >= 0 &&
                       halo_span(self_, b, 1, nranks_).peer >= 0;
-    auto pull_stream = [&](int side) { return both && side == 1 ? aux_ : hs; };
-    auto fork = [&]() {
-      if (!both) return;
-      HIPC(hipEventRecord(ev_fork_, hs));
-      HIPC(hipStreamWaitEvent(aux_, ev_fork_, 0));
-    };
-    auto join = [&]() {
-      if (!both) return;
-      HIPC(hipEventRecord(ev_join_, aux_));
-      HIPC(hipStreamWaitEvent(hs, ev_join_, 0));
-    };
     // the ipc transport's fused slab pulls (IpcTransport::fused_pulls): the aux stream forks first,
     // the halo stream's ready signal and first wait are one dispatch
     auto fused = [&](auto src) {
@@ -173,7 +162,7 @@ class ProxyTransport final : public Transport {
       // the ipc direct sequence: ready, then per face wait + pull from the (own) field buffer +
       // pulled, then the wait that frees the faces the next boundary kernels overwrite. A pencil
       // pulls its y faces first and signals readyZ once they landed: its z faces carry those ghost rows
-      if (fuse_ && !pencil_) {
+      if (!pencil_) {
         fused([&](int, const HaloSpan& h) { return (const void*)h.send; });
         for (int side = 0; side < 2; ++side) {
           if (halo_span(self_, b, side, nranks_).peer < 0) continue;
@@ -183,13 +172,9 @@ class ProxyTransport final : public Transport {
         return;
       }
       hip_counter_signal(ctr_ + kReady, hs);
-      if (pencil_) {
-        phase(2, kReady, false);
-        hip_counter_signal(ctr_ + kReadyZ, hs);
-        phase(0, kReadyZ, true);
-      } else {
-        phase(0, kReady, true);
-      }
+      phase(2, kReady, false);
+      hip_counter_signal(ctr_ + kReadyZ, hs);
+      phase(0, kReadyZ, true);
       for (int side = 0; side < 4; ++side) {
         if (halo_span(self_, b, side, nranks_).peer < 0) continue;
         hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, 0, &words_);
@@ -205,27 +190,7 @@ class ProxyTransport final : public Transport {
       hip_counter_wait(ctr_ + kPulled + side, ctr_ + kExpPulled + side, timeout_s_, hs, ahead, &words_);
       hip_face_copy(slot(b, side), h.send, face_, hs, copy_);
     }
-    if (fuse_) {
-      fused([&](int side, const HaloSpan&) { return (const void*)slot(b, side); });
-      if (!capturing) last_b_ = b;
-      return;
-    }
-    hip_counter_signal(ctr_ + kReady, hs);
-    // pull
-    fork();
-    for (int side = 0; side < 2; ++side) {
-      const HaloSpan h = halo_span(self_, b, side, nranks_);
-      if (h.peer < 0) continue;
-      hipStream_t ps = pull_stream(side);
-      hip_counter_wait(ctr_ + kReady, ctr_ + kExpReady + side, timeout_s_, ps, 0, &words_);
-      hip_face_copy(h.recv, slot(b, side), face_, ps, copy_);
-      hip_counter_signal(ctr_ + kPulled + side, ps);
-    }
-    join();
-    if (self_.ghost_event) {
-      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event, hs));
-      HIPC(hipEventRecord((hipEvent_t)self_.ghost_event2, hs));
-    }
+    fused([&](int side, const HaloSpan&) { return (const void*)slot(b, side); });
     if (!capturing) last_b_ = b;
   }
   int last_parity() const override { return last_b_; }
@@ -256,7 +221,6 @@ class ProxyTransport final : public Transport {
   bool ok_ = false;
   bool direct_ = false;
   bool pencil_ = false;  // (z, y) pencil: y faces first, then the z faces
-  bool fuse_ = xchg_fuse();
   int last_b_ = -1;
   double timeout_s_ = 300.0;
 };

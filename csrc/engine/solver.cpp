@@ -334,16 +334,6 @@ void Solver::exchange_ghosts() {
 // once those planes are stored, and the halo stream waits for that counter; only the upper region
 // keeps its launch (one round). (Round 4's switch back to two launches was removed in round 5; the
 // two-launch schedule measured 6-9 % slower at the N = 8 proxy, profiles/r04_session_{i,k}/.)
-// MDFX_GHOST_SPLIT=0 / 1 (A/B): whether a folded step's upper boundary launch waits only for the
-// upper ghosts and the interior sweep for the lower ones (1), or the upper launch for both (0).
-static bool ghost_split() {
-  static const bool on = [] {
-    const char* v = std::getenv("MDFX_GHOST_SPLIT");
-    return !(v && *v == '0');
-  }();
-  return on;
-}
-
 bool Solver::fold_ok(const Slab& s, int k) const {
   return fold_allowed(opt_.fold, transport_->fold_by_default()) && s.sig && s.lo_e > s.lo_b && s.in_e > s.in_b && hip_region_signals(spec_, s.lay, k);
 }
@@ -483,8 +473,10 @@ void Solver::step(bool want_resid, int k) {
     // the upper region, so that launch's inputs start above the lower ghosts) and the interior the
     // lower ones (ev_x). (With one neighbour both events follow its pull.) At the N = 8 proxy, whose
     // two pulls end together, this measured neutral (2,073-2,098 vs 2,050-2,128 GCells/s interleaved,
-    // profiles/r05_session_al/); it matters when one neighbour's face lands late.
-    const bool split = fold && nranks_ > 1 && transport_->records_ghost_event() && ghost_split();
+    // profiles/r05_session_al/); it matters when one neighbour's face lands late. (Round 6: the upper
+    // launch waiting for both instead saves the 6-7 us between the two launches but lost 4 % at the
+    // N = 4 proxy, profiles/r06_session_g/.)
+    const bool split = fold && nranks_ > 1 && transport_->records_ghost_event();
     if (bcs) {
       if (nranks_ > 1) {
         if (!split) s.be->wait(s.cs, s.ev_x);

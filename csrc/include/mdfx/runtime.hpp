@@ -186,9 +186,6 @@ std::unique_ptr<Transport> make_ipc_transport(CallbackFns fns, int copy_mode = -
 // copy per face) rather than through mailboxes (two): buffers of at most 1900 MiB, since torch's
 // HIP 7.0 runtime stalls mapping exported buffers of 2 GiB and more; MDFX_IPC_DIRECT=0 / 1 forces.
 bool ipc_direct_ok(size_t field_bytes);
-// Whether the ipc / proxy slab exchange fuses its ready signal into the first pull's wait and forks
-// the second pull's stream first (MDFX_XCHG_FUSE=0 / 1, read per transport; default 1).
-bool xchg_fuse();
 // The ipc transport's export with its bounded retry: calls get() (a hipError_t as int) until it
 // succeeds, retrying "invalid argument" up to max_retries times sleep_us apart (logging a diagnosis
 // of p on the first failure); returns the retries taken, throws on any other error or when they run

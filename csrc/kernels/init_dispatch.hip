@@ -92,13 +92,6 @@ static Knobs read_knobs() {
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   k.fold_release = env_int("MDFX_FOLD_RELEASE", 0);
-  // heat7_wxk stores: plain (not non-temporal) in the two owned lanes at each end of an x segment.
-  // The 116-column segments split a 32-B sector at every other seam; non-temporal partial-sector
-  // writes from the two neighbouring blocks reached memory separately (K = 5 sweep: 1.066 fields
-  // written, 6.1 M 32-B requests), plain ones merge in the L2 first: 1.009 fields (round 6,
-  // profiles/r06_session_d/; kernel A/B +0.9 %, driver form within noise). 0 = all non-temporal,
-  // 2 = all plain (same bytes as 1)
-  k.wxk_store = env_int("MDFX_WXK_STORE", 1);
   return k;
 }
 
@@ -374,7 +367,6 @@ void hip_stencil(const StencilSpec& spec, const RegionArgs& a, void* stream) {
   g.lz2_begin = a.lz2_begin;
   g.lz2_end = a.lz2_end;
   g.min_rounds = std::max(1, std::min(4, a.min_rounds));
-  g.store_mode = dev::knobs().wxk_store;
   if (a.sig) {
     MDFX_CHECK(hip_region_signals(spec, a.lay, a.steps) && a.lz2_end <= a.lz2_begin && a.sig_z > a.lz_begin &&
                    a.sig_z <= a.lz_end,

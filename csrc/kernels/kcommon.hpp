@@ -46,7 +46,6 @@ struct Geo {
   unsigned long long* sig = nullptr;
   int64_t sig_z = 0;
   int fold_release = 0;  // the signalling blocks write their XCD's L2 back first (Knobs::fold_release)
-  int store_mode = 0;    // heat7_wxk output stores: 0 non-temporal, 1 plain at segment seams, 2 plain (Knobs::wxk_store)
   unsigned long long* oob = nullptr;  // device-check violation counter (debug builds only)
 };
 
@@ -225,7 +224,6 @@ struct Knobs {
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64, fp32 rows of 257..512 or >= 1024 cells; 0 / 1)
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
   int fold_release = 0;       // MDFX_FOLD_RELEASE: folded-boundary blocks release (L2 writeback) before they signal
-  int wxk_store = 0;          // MDFX_WXK_STORE: heat7_wxk store policy A/B (Geo::store_mode)
 };
 const Knobs& knobs();
 

@@ -167,9 +167,11 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int64_t pitch = g.pitch, plane = g.plane;
   const bool xin = x >= 0 && x < pitch;
   const bool own = lane >= OV && lane <= 63 - OV && xin;
-  // (store policy A/B, Geo::store_mode: the two owned lanes at each end of the segment write the
-  // 32-B sectors a neighbouring segment also writes)
-  const int smode = g.store_mode;
+  // Output stores are non-temporal except in the two owned lanes at each end of the x segment: the
+  // 116-column segments of the 5-step sweep split a 32-B sector at every other seam, and the two
+  // blocks' non-temporal partial-sector writes reached memory separately (1.066 fields written per
+  // K = 5 sweep, 6.1 M 32-B requests); plain stores merge in the L2 first: 1.009 fields, kernel A/B
+  // +0.9 % (round 6, profiles/r06_session_d/; all-plain stores write the same bytes)
   const bool seam_lane = lane <= OV + 1 || lane >= 62 - OV;
   bool xb[N];
 #pragma unroll
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
             if (valid && i >= 0 && i < SH::R && y0 + i < ly1 && own) {
               T* a = (T*)((char*)(ob + (int64_t)lz * plane + (int64_t)i * pitch) + xob);
               dcheck(g, (const T*)out, a, N);
-              if (smode == 2 || (smode == 1 && seam_lane))
+              if (seam_lane)
                 *(V*)a = RO::vec(cur);
               else
                 store_nt((V*)a, RO::vec(cur));
