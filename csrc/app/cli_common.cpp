@@ -32,6 +32,7 @@ struct Opts {
   int residual_every = 0;
   bool print = false, json = false, sync_debug = false, overlap = true, graph = false;
   bool verbose = false, quiet = false, share_gpu = false;
+  int fold = -1;  // --fold auto|on|off (SolverOptions::fold)
   std::string variant = "auto";
   double timeout = 0;
   int64_t ckpt_every = 0;
@@ -60,6 +61,8 @@ void usage(const char* prog) {
       "  --transport auto|rccl|ipc|ipc_sdma|loopback|host|tcp\n"
       "                            multi-process runs (mpirun / torchrun): rccl on GPUs, tcp on CPUs\n"
       "  --share-gpu               ipc: allow several processes on one GPU (tests; one per GPU otherwise)\n"
+      "  --fold auto|on|off        fold the lower boundary into the interior sweep (auto: the transport's\n"
+      "                            default - ipc yes, rccl no)\n"
       "  --init random|dirichlet|constant|life|compat  --seed --lo --hi --value --edge --interior --density\n"
       "  --r R | --c0 --c1 --c2 --c3   update coefficients\n"
       "  --ref-precision           2D MDF: the reference's fp32-sum / fp64-scale evaluation of the update\n"
@@ -108,6 +111,11 @@ Opts parse(int argc, char** argv, const char* prog) {
     else if (a == "--ranks") o.ranks = std::atoi(need(i));
     else if (a == "--transport") o.transport = need(i);
     else if (a == "--share-gpu") o.share_gpu = true;
+    else if (a == "--fold") {
+      const std::string v = need(i);
+      MDFX_CHECK(v == "auto" || v == "on" || v == "off", "--fold takes auto, on or off");
+      o.fold = v == "on" ? 1 : v == "off" ? 0 : -1;
+    }
     else if (a == "--init") o.init = need(i);
     else if (a == "--seed") o.seed = std::strtoull(need(i), nullptr, 10);
     else if (a == "--lo") o.lo = std::atof(need(i));
@@ -319,6 +327,7 @@ int run_cli(int argc, char** argv, const char* default_stencil, const char* prog
     so.timeout_s = o.timeout;
     so.temporal = o.temporal;
     so.py = o.py;
+    so.fold = o.fold;
     Solver solver(spec, g, nranks, local_ranks, std::move(bes), std::move(tr), so);
 
     // ---- initial condition ----------------------------------------------------------------

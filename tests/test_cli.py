@@ -96,6 +96,16 @@ def test_checkpoint_resume_cli(tmp_path):
     assert full == resumed
 
 
+def test_fold_option():
+    """--fold auto|on|off sets SolverOptions::fold (the RCCL transport folds only with `on`); other
+    values are refused; the option does not change results (CPU ranks never fold)."""
+    base = [os.path.join(BIN, "mdfx"), "--backend", "cpu", "--stencil", "7", "--n", "12", "--steps", "3", "--print",
+            "--quiet", "--ranks", "2"]
+    assert run(base + ["--fold", "off"]) == run(base + ["--fold", "on"]) == run(base)
+    p = subprocess.run(base + ["--fold", "maybe"], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    assert p.returncode != 0 and b"--fold takes auto, on or off" in p.stderr
+
+
 def test_bad_option_fails():
     p = subprocess.run([os.path.join(BIN, "mdfx"), "--bogus"], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
     assert p.returncode != 0 and b"unknown option" in p.stderr
