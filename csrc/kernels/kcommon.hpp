@@ -106,6 +106,22 @@ __device__ __forceinline__ void glds4(const void* g, void* l) {
                                    (__attribute__((address_space(3))) void*)l, 4, 0, 0);
 }
 
+// The same copies through a buffer descriptor (buffer_load_dword{,x4} ... lds) whose base is a
+// wave-uniform row address in SGPRs, `off` the lane's byte offset from it. hipcc's waitcnt pass
+// counts a global_load_lds in flight as a possible LDS access by a flat instruction, whose lgkm
+// completion is out of order, so every LDS read issued while one is in flight waits for ALL
+// outstanding LDS reads (lgkmcnt(0)) at its first use; a buffer DMA leaves those waits partial
+// (lgkmcnt(n): the reads return in order). Offsets past the descriptor's range read 0, never fault.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t off, void* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, off, 0, 0, 0);
+}
+__device__ __forceinline__ void blds4(__amdgpu_buffer_rsrc_t r, uint32_t off, void* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 4, off, 0, 0, 0);
+}
+
 // Raw waits: s_waitcnt encodings for gfx9 (vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8]).
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 // vmcnt(n) for a wave-uniform n in 0..15 (an immediate per case): wait until at most the wave's n
@@ -224,6 +240,7 @@ struct Knobs {
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64, fp32 rows of 257..512 or >= 1024 cells; 0 / 1)
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
   int fold_release = 0;       // MDFX_FOLD_RELEASE: folded-boundary blocks release (L2 writeback) before they signal
+  int b27_shape = 0;          // MDFX_B27_SHAPE: box27_wxk band shape A/B (0: shipped)
 };
 const Knobs& knobs();
 

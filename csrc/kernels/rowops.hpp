@@ -392,6 +392,19 @@ struct RowOps2f {
   // adds as DPP operands; a non-volatile pin that lets rows interleave measured the same, +0.4-0.8 %
   // in the kernel A/B, profiles/r05_session_w/)
   static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.v)); }
+  // ---- 27-point with per-cell coefficients (box27_wxk narrow rows; RowOpsN's arithmetic) ----
+  static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.v + y.v}; }
+  static __device__ __forceinline__ Row hsum(const Row& c, float l, float rr) { return Row{T2{l + c.v.y, c.v.x + rr}}; }
+  static __device__ __forceinline__ Row lin3r(const Row& c, const Row& x, const Row& d, const Row& k0, const Row& k1,
+                                              const Row& k2) {
+    return Row{__builtin_elementwise_fma(k2.v, d.v, __builtin_elementwise_fma(k1.v, x.v, k0.v * c.v))};
+  }
+  static __device__ __forceinline__ Row fmaz(float z, const Row& a, const Row& s) {
+    return Row{__builtin_elementwise_fma(T2{z, z}, a.v, s.v)};
+  }
+  static __device__ __forceinline__ Row coefv(float v, float h, const bool* held) {
+    return Row{T2{held[0] ? h : v, held[1] ? h : v}};
+  }
 };
 
 // fp64 rows of 1 cell per lane (one 8-B value; heat7_wxk's fp64 5-step sweep): the register footprint
@@ -421,6 +434,15 @@ struct RowOps1d {
   static __device__ __forceinline__ double get(const Row& c, int) { return c.v; }
   static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
   static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.v)); }
+  // ---- 27-point with per-cell coefficients (box27_wxk narrow rows) ----
+  static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.v + y.v}; }
+  static __device__ __forceinline__ Row hsum(const Row&, double l, double rr) { return Row{l + rr}; }
+  static __device__ __forceinline__ Row lin3r(const Row& c, const Row& x, const Row& d, const Row& k0, const Row& k1,
+                                              const Row& k2) {
+    return Row{__builtin_fma(k2.v, d.v, __builtin_fma(k1.v, x.v, k0.v * c.v))};
+  }
+  static __device__ __forceinline__ Row fmaz(double z, const Row& a, const Row& s) { return Row{__builtin_fma(z, a.v, s.v)}; }
+  static __device__ __forceinline__ Row coefv(double v, double h, const bool* held) { return Row{held[0] ? h : v}; }
 };
 
 }  // namespace dev

@@ -538,7 +538,8 @@ B27X = [models.box27(n=40), models.box27(n=24, dtype="f64"), models.box27(nx=700
         models.box27(nx=8, ny=5, nz=9),
         # rows of 257..512 cells (3 overlapping x segments; round 3's x-pair kernel was removed)
         models.box27(nx=512, ny=29, nz=14), models.box27(nx=300, ny=17, nz=11), models.box27(nx=257, ny=9, nz=8),
-        models.box27(nx=512, ny=5, nz=9), models.box27(nx=448, ny=40, nz=23)]
+        models.box27(nx=512, ny=5, nz=9), models.box27(nx=448, ny=40, nz=23),
+        models.box27(nx=512, ny=13, nz=9, dtype="f64"), models.box27(nx=130, ny=21, nz=7, dtype="f64")]
 
 
 @pytest.mark.parametrize("prob", B27X, ids=lambda p: p.describe().replace(" ", "_"))
