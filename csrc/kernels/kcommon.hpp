@@ -118,6 +118,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
 __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t off, void* l) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, off, 0, 0, 0);
 }
+// (`soff`: a wave-uniform byte offset added in the instruction's SGPR offset field)
+__device__ __forceinline__ void blds16s(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff, void* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, off, (int)soff, 0, 0);
+}
 __device__ __forceinline__ void blds4(__amdgpu_buffer_rsrc_t r, uint32_t off, void* l) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 4, off, 0, 0, 0);
 }
@@ -240,7 +244,6 @@ struct Knobs {
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64, fp32 rows of 257..512 or >= 1024 cells; 0 / 1)
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
   int fold_release = 0;       // MDFX_FOLD_RELEASE: folded-boundary blocks release (L2 writeback) before they signal
-  int b27_shape = 0;          // MDFX_B27_SHAPE: box27_wxk band shape A/B (0: shipped)
 };
 const Knobs& knobs();
 

@@ -434,15 +434,6 @@ struct RowOps1d {
   static __device__ __forceinline__ double get(const Row& c, int) { return c.v; }
   static __device__ __forceinline__ V vec(const Row& c) { return c.v; }
   static __device__ __forceinline__ void pin(Row& r) { asm volatile("" : "+v"(r.v)); }
-  // ---- 27-point with per-cell coefficients (box27_wxk narrow rows) ----
-  static __device__ __forceinline__ Row add(const Row& x, const Row& y) { return Row{x.v + y.v}; }
-  static __device__ __forceinline__ Row hsum(const Row&, double l, double rr) { return Row{l + rr}; }
-  static __device__ __forceinline__ Row lin3r(const Row& c, const Row& x, const Row& d, const Row& k0, const Row& k1,
-                                              const Row& k2) {
-    return Row{__builtin_fma(k2.v, d.v, __builtin_fma(k1.v, x.v, k0.v * c.v))};
-  }
-  static __device__ __forceinline__ Row fmaz(double z, const Row& a, const Row& s) { return Row{__builtin_fma(z, a.v, s.v)}; }
-  static __device__ __forceinline__ Row coefv(double v, double h, const bool* held) { return Row{held[0] ? h : v}; }
 };
 
 }  // namespace dev

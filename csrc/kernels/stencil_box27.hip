@@ -481,18 +481,22 @@ __global__ __launch_bounds__(256) void box27_tbk(const T* __restrict__ in, T* __
     return (y < 0 ? 0 : y >= g.ny ? g.ny - 1 : y) - (y0 - K);
   };
   const int64_t srowc = rowc(srow < R0 ? srow : 0);
+  // (buffer-descriptor DMAs as heat7_tbk's: partial lgkmcnt waits for the LDS reads that follow)
   auto issue = [&](int64_t lz) {
-    const T* pb = ib0 + lz * plane;
+    uint64_t pbs = (uint64_t)(uintptr_t)(ib0 + lz * plane);
+    asm volatile("" : "+s"(pbs));
+    const char* pb = (const char*)(uintptr_t)pbs;
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(pb);
 #pragma unroll
     for (int k = 0; k < R0; ++k) {
-      const T* a = (const T*)((const char*)(pb + rowc(k) * pitch) + xcb);
-      dcheck(g, in, a, N);
-      glds16(a, &slot[w][k][0]);
+      const uint32_t ro = (uint32_t)(rowc(k) * pitch * (int64_t)sizeof(T));
+      dcheck(g, in, (const T*)(pb + ro + xcb), N);
+      blds16s(rs, xcb, ro, &slot[w][k][0]);
     }
     if (WXN > 1) {
-      const T* a = (const T*)((const char*)(pb + srowc * pitch) + socb);
-      dcheck(g, in, a, N);
-      glds16(a, &slot[w][R0][0]);
+      const uint32_t o = (uint32_t)(srowc * pitch * (int64_t)sizeof(T)) + socb;
+      dcheck(g, in, (const T*)(pb + o), N);
+      blds16(rs, o, &slot[w][R0][0]);
     }
   };
   const int wl = wx > 0 ? w - 1 : w, wr = wx < WXN - 1 ? w + 1 : w;

@@ -54,18 +54,23 @@ int64_t resident_blocks(const void* kfn, int block);
 // the neighbour's window row, level l > 1 from an edge table in which every wave leaves the first
 // and last cell of each row it finishes at levels 1..K-1 (written one step before it is read, like
 // the y seams). A block is then XW x WB waves.
-// CN = kRowOps2 / kRowOps1: narrow rows of 8 bytes per lane (fp32 2 cells, RowOps2f; fp64 1 cell,
-// RowOps1d): half the registers per row, so the same band takes twice the waves. The window is then
-// filled with row PAIRS per 16-byte LDS DMA in whole-row blocks (a wave's 512-byte row is 32 DMA
-// lanes; rows of one x wave are adjacent in the window), 4-byte DMA halves in overlapping segments
-// (their start is not 16-byte aligned), as heat7_wxk's narrow rows.
-template <class T, int RY, int RE, int K, int WB, bool RES, int XW = 0, int CN = 0, int NB = 2, int XL = 0>
+// CN = kRowOps2 (XW = 0 only): fp32 rows of 2 cells per lane (RowOps2f), half the registers per
+// row, so a CU holds two 8-wave bands (rows of 1024 cells: 1641 vs 1582 GCells/s in 4-cell lanes,
+// profiles/r06_session_n/). The window is then filled by 4-byte DMA halves (a segment's start is
+// not 16-byte aligned), as heat7_wxk's narrow rows.
+// Round 6 also measured (profiles/r06_session_{j,k,m}/): 2-cell lanes in whole-row blocks of 16 /
+// 12 / 8 waves at 512-cell rows (1235 / 957 / 1129 vs 1379), 1-cell fp64 lanes (554-638 vs 692-830),
+// a third window buffer with the DMA two planes ahead (-4.4 % fp32, -2.6 % fp64), level 1's x
+// neighbours read from the window instead of lane shifts (10 % fewer VALU slots, -3 %): the march is
+// set by the plane step's latency chain, not by occupancy, HBM latency or VALU count.
+template <class T, int RY, int RE, int K, int WB, bool RES, int XW = 0, int CN = 0>
 __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T* __restrict__ in, T* __restrict__ out,
                                                                          Geo g, T c0, T c1, T c2, T c3, int zc, int XT,
                                                                          int YT, int ntasks, double* __restrict__ resid) {
   constexpr bool NAR = CN != 0;
   static_assert(CN != kRowOps2 || sizeof(T) == 4, "box27_wxk: 2-cell lanes are fp32");
   static_assert(CN != kRowOps1 || sizeof(T) == 8, "box27_wxk: 1-cell lanes are fp64");
+  static_assert(CN == 0 || XW == 0, "box27_wxk: narrow rows in overlapping segments only");
   using RO = typename std::conditional<
       CN == kRowOps2, RowOps2f,
       typename std::conditional<CN == kRowOps1, RowOps1d,
@@ -87,8 +92,7 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
   const int w = wid / XN, wx = wid % XN;  // y wave of the band, x wave of the row
   const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
   if (b >= ntasks) return;
-  static_assert(NB == 2 || NB == 3, "box27_wxk: two or three window buffers");
-  __shared__ V win[NB][XN][RB][64];
+  __shared__ V win[2][XN][RB][64];
   __shared__ V seam[2][XN][K - 1][WB - 1][2][64];
   // x-edge table (XW >= 1) and the slots the other 62 lanes of an edge store write into
   constexpr int XE = XW > 0 ? 2 * (K - 1) * XN * RX * 2 : 1;
@@ -137,40 +141,23 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
     return (uint32_t)((xx < 0 ? 0 : xx >= pitch ? pitch - N : xx) * (int64_t)sizeof(T));
   };
   const uint32_t xcb = xcb_of(0);
-  // narrow rows in segments: dword d = 64 h + lane of the segment's row (heat7_wxk's layout)
+  // narrow rows: dword d = 64 h + lane of the segment's row (heat7_wxk's layout)
   constexpr int DPC = (int)sizeof(T) / 4;
   uint32_t xch[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int d = h * 64 + lane;
-    const int64_t xh = (XW > 0 ? 0 : (int64_t)xt * SEG - OV * N) + d / DPC;
+    const int64_t xh = (int64_t)xt * SEG - OV * N + d / DPC;
     xch[h] = (uint32_t)(((xh < 0 ? 0 : xh >= pitch ? pitch - 1 : xh) * DPC + d % DPC) * 4);
   }
-  // narrow whole-row blocks: DMA lane j of a pair loads cells 16 / sizeof(T) * (j % 32) of x wave kx
-  // of window row 2 p + j / 32 (flattened [kx][row]); cells past the pitch clamp to the last vector
-  constexpr int CPD = 16 / (int)sizeof(T);
+  // u0 plane lz -> window buffer `buf`. Buffer-descriptor DMAs on the wave-uniform row base (blds16 /
+  // blds4): with a global_load_lds in flight hipcc made every LDS read of the plane step wait for
+  // all of them (lgkmcnt(0)) before the first use; with these the waits are partial, so level K starts
+  // on its seam rows while level 1's window rows are still arriving (512^3 fp32 1440 vs 1402, fp64
+  // 735 vs 696 GCells/s with the read order and level barriers below, profiles/r06_session_n/)
   auto issue = [&](int lz, int buf) {
     const int lzc = lz < 0 ? 0 : lz >= lzmax ? lzmax - 1 : lz;
     constexpr int NW = XN * WB, NR = XN * RB;
-    if constexpr (NAR && XW > 0) {
-      static_assert(NR % 2 == 0 && 32 * CPD == 64 * N, "box27_wxk: narrow window rows go by pairs");
-      constexpr int NP = NR / 2;
-#pragma unroll
-      for (int j = 0; j < (NP + NW - 1) / NW; ++j) {
-        const int pr = wid + j * NW;
-        if (pr < NP) {
-          const int k = 2 * pr + (lane >> 5);
-          const int kx = k / RB, kr = k - kx * RB;
-          const int y = yb - K + kr;
-          const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-          const int64_t xx = (int64_t)kx * 64 * N + (int64_t)(lane & 31) * CPD;
-          const T* a = in + (int64_t)lzc * plane + (int64_t)yc * pitch + (xx >= pitch ? pitch - CPD : xx);
-          dcheck(g, in, a, CPD);
-          glds16(a, (char*)&win[buf][0][0][0] + pr * 1024);
-        }
-      }
-      return;
-    }
 #pragma unroll
     for (int j = 0; j < (NR + NW - 1) / NW; ++j) {
       const int k = wid + j * NW;
@@ -178,30 +165,19 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
         const int kx = k / RB, kr = k - kx * RB;
         const int y = yb - K + kr;
         const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-        if constexpr ((XL & 16) != 0) {
-          // (buffer DMA: see blds16; the row base is wave-uniform)
-          uint64_t rb = (uint64_t)(uintptr_t)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
-          asm volatile("" : "+s"(rb));
-          const __amdgpu_buffer_rsrc_t rs = row_rsrc((const void*)(uintptr_t)rb);
-          if constexpr (NAR) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) blds4(rs, xch[h], (char*)&win[buf][kx][kr][0] + h * 256);
-          } else {
-            blds16(rs, XW > 1 ? xcb_of(kx) : xcb, &win[buf][kx][kr][0]);
-          }
-        } else if constexpr (NAR) {
+        uint64_t rb = (uint64_t)(uintptr_t)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
+        asm volatile("" : "+s"(rb));
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc((const void*)(uintptr_t)rb);
+        if constexpr (NAR) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const char* a = (const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xch[h];
-            dcheck(g, in, (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) +
-                                     (xch[h] & ~(uint32_t)(sizeof(T) - 1))), 1);
-            glds4(a, (char*)&win[buf][kx][kr][0] + h * 256);
+            dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + (xch[h] & ~(uint32_t)(sizeof(T) - 1))), 1);
+            blds4(rs, xch[h], (char*)&win[buf][kx][kr][0] + h * 256);
           }
         } else {
-          const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) +
-                                  (XW > 1 ? xcb_of(kx) : xcb));
-          dcheck(g, in, a, N);
-          glds16(a, &win[buf][kx][kr][0]);
+          const uint32_t o = XW > 1 ? xcb_of(kx) : xcb;
+          dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + o), N);
+          blds16(rs, o, &win[buf][kx][kr][0]);
         }
       }
     }
@@ -210,15 +186,6 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
   const int qdma = ze - 1 + K;    // last u0 plane any valid output needs
   const int qend = ze - 1 + LAG;  // the step that finishes the chunk's last output plane
   issue(zs - K, 0);
-  // NB = 3: the DMA runs two planes ahead. Before the barrier of step q a wave waits until DMA(q) has
-  // landed: the operations it issued after that DMA may stay in flight - the stores of step q - 2,
-  // DMA(q + 1) (ndma_w instructions, issued at step q - 1) and the stores of step q - 1.
-  const int ndma_w = NAR && XW > 0 ? (XN * RB / 2 - wid + XN * WB - 1) / (XN * WB) : (XN * RB - wid + XN * WB - 1) / (XN * WB);
-  int s1 = 0, s2 = 0, d1 = 0, wb = 0;
-  if constexpr (NB == 3) {
-    issue(zs - K + 1, 1);
-    d1 = NAR && XW == 0 ? 2 * ndma_w : ndma_w;
-  }
   T* ob = out + (int64_t)y0 * pitch;
   const uint32_t xob = (uint32_t)((xin ? x : 0) * (int64_t)sizeof(T));
   double acc = 0.0;
@@ -259,22 +226,6 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
     else
       asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)p), "v"(v) : "memory");
   };
-  // XL & 1: level 1's x neighbours (cells x - 1 and x + N of a lane) read from the window like its
-  // rows, so its x sums take no lane shift and no edge select (the row ends read a finite cell of
-  // their own; an overlap lane's value is never stored). XL & 2 (XW > 1): the upper levels' left and
-  // right edges loaded into separate registers, so each lane shift's `old` operand is its own
-  // register (one edge register feeding both shifts cost a copy per row).
-  LT* const l_win = lds_vptr(lane > 0 ? cell(&win[0][wx][y0 - yb][lane - 1], N - 1)
-                                      : (XW > 1 && wx > 0 ? cell(&win[0][wx - 1][y0 - yb][63], N - 1)
-                                                          : cell(&win[0][wx][y0 - yb][0], 0)));
-  LT* const r_win = lds_vptr(lane < 63 ? cell(&win[0][wx][y0 - yb][lane + 1], 0)
-                                       : (XW > 1 && wx < XN - 1 ? cell(&win[0][wx + 1][y0 - yb][0], 0)
-                                                                : cell(&win[0][wx][y0 - yb][63], N - 1)));
-  LT* const e_tabl = lds_vptr(&xe[(wl * RX) * 2 + xrow0 + (wx > 0 ? 1 : 0)]);
-  LT* const e_tabr = lds_vptr(&xe[(wr * RX) * 2 + xrow0 + (wx < XN - 1 ? 0 : 1)]);
-  auto hsx2 = [](const Row& v, T el, T er) -> Row {
-    return RO::hsum(v, lane_up1_or(el, RO::last(v)), lane_down1_or(er, RO::first(v)));
-  };
   auto hs = [](const Row& v) -> Row { return RO::hsum(v, lane_up1(RO::last(v)), lane_down1(RO::first(v))); };
   auto hsx = [](const Row& v, T e) -> Row {
     return RO::hsum(v, lane_up1_or(e, RO::last(v)), lane_down1_or(e, RO::first(v)));
@@ -298,88 +249,45 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
       constexpr bool GEN = decltype(gen_c)::value;  // held rows / planes may occur in this step
       constexpr int P = decltype(par_c)::value;
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NB == 2) {
-        wait_vm_le(nst);
-        lds_barrier();
-        if constexpr ((XL & 8) == 0 || (XL & 16) != 0)
-          if (q < qdma) issue(q + 1, P ^ 1);
-      } else {
-        wait_vm_le(s2 + d1 + s1);
-        lds_barrier();
-        const bool dq = q + 2 <= qdma;
-        if (dq) issue(q + 2, wb == 0 ? 2 : wb - 1);
-        s2 = s1;
-        d1 = dq ? (NAR && XW == 0 ? 2 * ndma_w : ndma_w) : 0;
-      }
-      const int WO = (NB == 2 ? P : wb) * WIN_BUF;
+      wait_vm_le(nst);
+      lds_barrier();
+      if (q < qdma) issue(q + 1, P ^ 1);
+      constexpr int WO = P * WIN_BUF;
       const int lzo = q - LAG;  // level K's output plane
       const bool valid = lzo >= zs && lzo < ze;
-      // the step's LDS rows (level 1's u0 window rows, every upper level's two seam rows) are read up
-      // front, so the reads overlap each other instead of each waiting out a round trip right before
-      // its use (round 5: 512^3 fp64 678 vs 640 GCells/s, fp32 1056 vs 971, profiles/r05_session_a/)
+      // the step's LDS rows (every upper level's two seam rows and x edges, level 1's u0 window rows)
+      // are read up front, so the reads overlap each other instead of each waiting out a round trip
+      // right before its use (round 5: 512^3 fp64 678 vs 640 GCells/s, profiles/r05_session_a/), in
+      // the order the levels use them (top-down): the waits before each level are partial
       constexpr int NU = SH::n(1) + 2;
       Row U[NU], SU[K], SD[K];
-      T E1[NU], EX[K][NM + 2], EXr[K][NM + 2], L1[NU], R1[NU];
-      // level 1's u0 window rows (and their x edges / neighbours)
-      auto rd_win = [&]() __attribute__((always_inline)) {
+      T E1[NU], EX[K][NM + 2];
 #pragma unroll
-        for (int k = 0; k < NU; ++k) U[k] = RO::fromv(V(wrow[WO + (SH::lo(1) - 1 + k + K) * 64]));
-        if constexpr ((XL & 1) != 0) {
-#pragma unroll
-          for (int k = 0; k < NU; ++k) {
-            L1[k] = l_win[(WO + (SH::lo(1) - 1 + k + K) * 64) * N];
-            R1[k] = r_win[(WO + (SH::lo(1) - 1 + k + K) * 64) * N];
-          }
-        } else if constexpr (XW > 1) {
-#pragma unroll
-          for (int k = 0; k < NU; ++k) E1[k] = e_win[(WO + (SH::lo(1) - 1 + k + K) * 64) * N];
-        }
-      };
-      // level j's two seam rows (the neighbour waves' rows level j + 1 reads) and, XW > 1, the x
-      // edges of level j + 1's input rows from the table level j filled in the previous step
-      auto rd_lvl = [&](int j) __attribute__((always_inline)) {
+      for (int j = K - 1; j >= 1; --j) {
+        // level j's two seam rows (the neighbour waves' rows level j + 1 reads) and, XW > 1, the x
+        // edges of level j + 1's input rows from the table level j filled in the previous step
         SU[j] = SD[j] = RO::zero();
         if (SH::lo(j + 1) - 1 < SH::lo(j)) SU[j] = RO::fromv(V(s_rdu[(P ^ 1) * SEAM_PAR + (j - 1) * SEAM_LVL]));
         if (SH::hi(j + 1) >= SH::hi(j)) SD[j] = RO::fromv(V(s_rdd[(P ^ 1) * SEAM_PAR + (j - 1) * SEAM_LVL]));
         if constexpr (XW > 1) {
 #pragma unroll
-          for (int k = 0; k < SH::n(j + 1) + 2; ++k) {
-            const int o = (P ^ 1) * XE_PAR + (j - 1) * XE_LVL + (SH::lo(j + 1) - 1 + k + K - 1) * 2;
-            if constexpr ((XL & 2) != 0) {
-              EX[j][k] = e_tabl[o];
-              EXr[j][k] = e_tabr[o];
-            } else {
-              EX[j][k] = e_tab[o];
-            }
-          }
+          for (int k = 0; k < SH::n(j + 1) + 2; ++k)
+            EX[j][k] = e_tab[(P ^ 1) * XE_PAR + (j - 1) * XE_LVL + (SH::lo(j + 1) - 1 + k + K - 1) * 2];
         }
-      };
-      if constexpr ((XL & 4) != 0) {
-        // in the order the levels use them (top-down), so level K starts once its own rows are in
-#pragma unroll
-        for (int j = K - 1; j >= 1; --j) rd_lvl(j);
-        rd_win();
-      } else {
-        rd_win();
-#pragma unroll
-        for (int j = 1; j < K; ++j) rd_lvl(j);
       }
-      // XL & 8: the window DMA after the step's LDS reads. hipcc's waitcnt pass counts an LDS DMA as
-      // a possible LDS access through a flat instruction, whose lgkm completion is out of order, so
-      // a DMA in flight made it wait for ALL of the step's LDS reads (lgkmcnt(0)) before the first use
-      if constexpr (NB == 2 && (XL & 8) != 0 && (XL & 16) == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (q < qdma) issue(q + 1, P ^ 1);
-        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < NU; ++k) U[k] = RO::fromv(V(wrow[WO + (SH::lo(1) - 1 + k + K) * 64]));
+      if constexpr (XW > 1) {
+#pragma unroll
+        for (int k = 0; k < NU; ++k) E1[k] = e_win[(WO + (SH::lo(1) - 1 + k + K) * 64) * N];
       }
       // levels top-down: level l reads its inputs (the level below's plane from the previous step)
       // before that level overwrites its other stored plane
 #pragma unroll
       for (int l = K; l >= 1; --l) {
-        // XL & 8: no level's arithmetic moves ahead of the level above, so level K starts on its own
-        // LDS rows while the lower levels' rows are still in flight (partial lgkmcnt waits)
-        if constexpr ((XL & 8) != 0)
-          if (l < K) __builtin_amdgcn_sched_barrier(0);
+        // no level's arithmetic moves ahead of the level above (it would pull that level's waits
+        // for the later LDS reads forward)
+        if (l < K) __builtin_amdgcn_sched_barrier(0);
         const int m = q - (2 * l - 1);  // output plane of level l; its inputs are plane p = m + 1
         T zm = T(1), zp = T(1);
         bool zhp = false;
@@ -398,15 +306,8 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
           return H[j - 1][P ^ 1][i - SH::lo(j)];
         };
         auto hsi = [&](const Row& v, int i) -> Row {
-          if constexpr ((XL & 1) != 0)
-            if (l == 1) return RO::hsum(v, L1[i - (SH::lo(1) - 1)], R1[i - (SH::lo(1) - 1)]);
-          if constexpr (XW > 1) {
-            if constexpr ((XL & 2) != 0)
-              if (l > 1) return hsx2(v, EX[l - 1][i - (SH::lo(l) - 1)], EXr[l - 1][i - (SH::lo(l) - 1)]);
-            return hsx(v, l == 1 ? E1[i - (SH::lo(1) - 1)] : EX[l - 1][i - (SH::lo(l) - 1)]);
-          } else {
-            return hs(v);
-          }
+          if constexpr (XW > 1) return hsx(v, l == 1 ? E1[i - (SH::lo(1) - 1)] : EX[l - 1][i - (SH::lo(l) - 1)]);
+          else return hs(v);
         };
         Row vm = vin(SH::lo(l) - 1), vc = vin(SH::lo(l));
         Row hm = hsi(vm, SH::lo(l) - 1), hc = hsi(vc, SH::lo(l));
@@ -460,7 +361,6 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
         }
       }
       nst = valid ? nsto : 0;
-      if constexpr (NB == 3) wb = wb == 2 ? 0 : wb + 1;
       if constexpr (GEN && ROLE != 1) {
         if ((ROLE == 0 ? held0 : held1) && q >= zs && q < ze) {  // u0 plane q is output plane q there
           constexpr int ih = ROLE == 0 ? -1 : SH::R;
@@ -472,7 +372,6 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
           ++nst;
         }
       }
-      if constexpr (NB == 3) s1 = nst;
     };
     // in a y-interior band, the step pairs whose levels all finish and read z-interior planes take
     // the copy without the held-row / held-plane tests (at 512^3 two of the three z chunks touch a
@@ -480,9 +379,6 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
     using Tr = std::true_type;
     using F = std::false_type;
     int q = zs - K;
-    // XL & 8: every scalar load (kernel arguments) completes before the march, so the waitcnt pass
-    // does not carry a pending scalar load into the loop, which forces lgkmcnt(0) at each LDS use
-    if constexpr ((XL & 8) != 0) wait_lgkm0();
     if constexpr (!YGEN) {
       auto zfree = [&](int qq) { return qq - LAG + gzoff >= 1 && qq + 1 + gzoff <= gnz - 2; };  // qq and qq + 1
       for (; q <= qend && !zfree(q); q += 2) {
@@ -518,7 +414,7 @@ __global__ __launch_bounds__((XW > 0 ? XW : 1) * WB * 64) void box27_wxk(const T
 // 6-row bands fetched twice the window rows per output row and it ran 909 vs 1017-1026 GCells/s
 // at 512^3 (profiles/archive/r03_session_t/); removed in round 4.)
 
-template <class T, int RY, int RE, int K, int WB, int XW = 0, int CN = 0, int NB = 2, int XL = 0>
+template <class T, int RY, int RE, int K, int WB, int XW = 0, int CN = 0>
 static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf, double* resid, hipStream_t s) {
   constexpr int N = CN == kRowOps2 ? 2 : CN == kRowOps1 ? 1 : VT<T>::N, OV = XW > 0 ? 0 : (K + N - 1) / N, SEG = (64 - 2 * OV) * N;
   constexpr int BR = 2 * RE + (WB - 2) * RY, NT = 64 * WB * (XW > 0 ? XW : 1);
@@ -528,7 +424,7 @@ static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf
   const int XT = XW > 0 ? 1 : (int)((g.nx + SEG - 1) / SEG);
   const int YT = (int)std::max<int64_t>(1, (g.ny - 2 + BR - 1) / BR);  // bands over rows 1 .. ny-2
   const int64_t tiles = (int64_t)XT * YT;
-  const void* kfn = (const void*)&box27_wxk<T, RY, RE, K, WB, false, XW, CN, NB, XL>;
+  const void* kfn = (const void*)&box27_wxk<T, RY, RE, K, WB, false, XW, CN>;
   const int64_t resident = resident_blocks(kfn, NT);
   int zc = wx_zc(planes, tiles, resident, K, 3 * K - 1, g.min_rounds);
   if (planes2 > 0) zc = (int)std::max(planes, planes2);
@@ -538,10 +434,10 @@ static void launch_b27x(const Geo& g, const T* in, T* out, const StencilCoef& cf
   const dim3 grd((unsigned)ntasks), blk(NT);
   const T c0 = (T)cf.c0, c1 = (T)cf.c1, c2 = (T)cf.c2, c3 = (T)cf.c3;
   if (resid)
-    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, true, XW, CN, NB, XL>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
+    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, true, XW, CN>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT, YT,
                        (int)ntasks, resid);
   else
-    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false, XW, CN, NB, XL>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT,
+    hipLaunchKernelGGL((box27_wxk<T, RY, RE, K, WB, false, XW, CN>), grd, blk, 0, s, in, out, g, c0, c1, c2, c3, zc, XT,
                        YT, (int)ntasks, resid);
 }
 
@@ -565,31 +461,17 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
   // the LDS (no lane of a 512-cell row computed twice; bands over rows 1..ny-2 fill 255 blocks in
   // three z chunks): 512^3 1332 GCells/s against 1009 in three overlapping segments and 1092 for
   // box27_tb2n K = 2 (profiles/r05_session_f/)
-  const int shape = knobs().b27_shape;
   if constexpr (std::is_same<T, float>::value) {
-    if (g.nx <= 512) {
-      if (shape == 7) return launch_b27x<T, 2, 1, 3, 4, 2, 0, 2, 2>(g, in, out, cf, resid, s);
-      if (shape == 10) return launch_b27x<T, 2, 1, 3, 4, 2, 0, 2, 16>(g, in, out, cf, resid, s);
-      if (shape == 11) return launch_b27x<T, 2, 1, 3, 4, 2, 0, 2, 18>(g, in, out, cf, resid, s);
-      if (shape == 12) return launch_b27x<T, 2, 1, 3, 4, 2, 0, 2, 28>(g, in, out, cf, resid, s);
-      if (shape == 13) return launch_b27x<T, 2, 1, 3, 4, 2, 0, 2, 30>(g, in, out, cf, resid, s);
-      return launch_b27x<T, 2, 1, 3, 4, 2>(g, in, out, cf, resid, s);
-    }
-    if (shape == 1) return launch_b27x<T, 2, 1, 3, 8, 0, kRowOps2>(g, in, out, cf, resid, s);
-    if (shape == 10) return launch_b27x<T, 2, 1, 3, 8, 0, 0, 2, 16>(g, in, out, cf, resid, s);
-    if (shape == 11) return launch_b27x<T, 2, 1, 3, 8, 0, kRowOps2, 2, 16>(g, in, out, cf, resid, s);
-    if (shape == 12) return launch_b27x<T, 2, 1, 3, 8, 0, 0, 2, 28>(g, in, out, cf, resid, s);
-    if (shape == 13) return launch_b27x<T, 2, 1, 3, 8, 0, kRowOps2, 2, 28>(g, in, out, cf, resid, s);
+    if (g.nx <= 512) return launch_b27x<T, 2, 1, 3, 4, 2>(g, in, out, cf, resid, s);
+    return launch_b27x<T, 2, 1, 3, 8, 0, kRowOps2>(g, in, out, cf, resid, s);
   } else {
-    if (shape == 10) return launch_b27x<T, 2, 1, 3, 8, 0, 0, 2, 16>(g, in, out, cf, resid, s);
-    if (shape == 12) return launch_b27x<T, 2, 1, 3, 8, 0, 0, 2, 28>(g, in, out, cf, resid, s);
+    // (fp64 at 512-cell rows fills only 185 of 256 CUs in one round (5 segments x 37 bands); round 6
+    // measured the shapes that fill more: 6-wave bands of 10 rows (255 tiles) 570-575, 1-row waves
+    // in 8-row bands 559-563, 4-wave bands in 2 blocks per CU (425 tiles) 659-683, against 705-707
+    // GCells/s for these 14-row bands: the march is latency-bound per wave, so more waves per tile
+    // pay, more tiles do not (profiles/r06_session_h/))
+    launch_b27x<T, 2, 1, 3, 8>(g, in, out, cf, resid, s);
   }
-  // (fp64 at 512-cell rows fills only 185 of 256 CUs in one round (5 segments x 37 bands); round 6
-  // measured the shapes that fill more: 6-wave bands of 10 rows (255 tiles) 570-575, 1-row waves in
-  // 8-row bands 559-563, 4-wave bands in 2 blocks per CU (425 tiles) 659-683, against 705-707 GCells/s
-  // for these 14-row bands: the march is latency-bound per wave, so more waves per tile pay, more
-  // tiles do not (profiles/r06_session_h/))
-  launch_b27x<T, 2, 1, 3, 8>(g, in, out, cf, resid, s);
 }
 template void launch_box27_wxk<float>(const Geo&, const float*, float*, const StencilCoef&, int, double*, hipStream_t);
 template void launch_box27_wxk<double>(const Geo&, const double*, double*, const StencilCoef&, int, double*, hipStream_t);

@@ -113,18 +113,23 @@ __global__ __launch_bounds__(256) void heat7_tbk(const T* __restrict__ in, T* __
     return (y < 0 ? 0 : y >= ny ? ny - 1 : y) - (y0 - K);
   };
   const int srowc = rowc(srow < R0 ? srow : 0);
+  // buffer-descriptor DMAs on the wave-uniform plane base (blds16s: row offset in the SGPR field,
+  // the lane's column in the VGPR one), so the LDS reads that follow get partial lgkmcnt waits
   auto issue = [&](int lz) {
-    const T* pb = ib0 + (int64_t)lz * plane;
+    uint64_t pbs = (uint64_t)(uintptr_t)(ib0 + (int64_t)lz * plane);
+    asm volatile("" : "+s"(pbs));
+    const char* pb = (const char*)(uintptr_t)pbs;
+    const __amdgpu_buffer_rsrc_t rs = row_rsrc(pb);
 #pragma unroll
     for (int k = 0; k < R0; ++k) {
-      const T* a = (const T*)((const char*)(pb + (int64_t)rowc(k) * pitch) + xcb);
-      dcheck(g, in, a, N);
-      glds16(a, &slot[w][k][0]);
+      const uint32_t ro = (uint32_t)((int64_t)rowc(k) * pitch * (int64_t)sizeof(T));
+      dcheck(g, in, (const T*)(pb + ro + xcb), N);
+      blds16s(rs, xcb, ro, &slot[w][k][0]);
     }
-    if (WXN > 1) {  // srowc is per lane: the row term stays in the 64-bit address
-      const T* a = (const T*)((const char*)(pb + (int64_t)srowc * pitch) + socb);
-      dcheck(g, in, a, N);
-      glds16(a, &slot[w][R0][0]);
+    if (WXN > 1) {  // srowc is per lane: its row term goes in the VGPR offset
+      const uint32_t o = (uint32_t)((int64_t)srowc * pitch * (int64_t)sizeof(T)) + socb;
+      dcheck(g, in, (const T*)(pb + o), N);
+      blds16(rs, o, &slot[w][R0][0]);
     }
   };
   // Seam reads: ONE ds_read2 per row gives lane 0 the left neighbour's last cell in `lo` and lane

@@ -136,9 +136,12 @@ __global__ __launch_bounds__(WB == 8 ? 512 : 256) void heat7_wtk(const T* __rest
         if (k < RB) {
           const int y = yb - K + k;
           const int yc = y < 0 ? 0 : y >= ny ? ny - 1 : y;
-          const T* a = (const T*)((const char*)(in + (int64_t)lzc * plane + (int64_t)yc * pitch) + xcb);
-          dcheck(g, in, a, N);
-          glds16(a, &slot[buf][k][0]);
+          // buffer-descriptor DMA on the wave-uniform row base: partial lgkmcnt waits for the LDS
+          // reads that follow (blds16)
+          uint64_t rb = (uint64_t)(uintptr_t)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
+          asm volatile("" : "+s"(rb));
+          dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + xcb), N);
+          blds16(row_rsrc((const void*)(uintptr_t)rb), xcb, &slot[buf][k][0]);
         }
       }
   };

@@ -211,17 +211,17 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         // 32-bit lane-offset form instead of a 64-bit VGPR address per row held across the loop
         uint64_t rb = (uint64_t)(uintptr_t)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
         asm volatile("" : "+s"(rb));
+        // buffer-descriptor DMA (blds16 / blds4): the step's LDS reads then get partial lgkmcnt waits
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc((const void*)(uintptr_t)rb);
         if constexpr (NAR) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const char* a = (const char*)(uintptr_t)rb + xch[h];
             dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + (xch[h] & ~(uint32_t)(sizeof(T) - 1))), 1);
-            glds4(a, (char*)&win[buf][k][0] + h * 256);
+            blds4(rs, xch[h], (char*)&win[buf][k][0] + h * 256);
           }
         } else {
-          const T* a = (const T*)((const char*)(uintptr_t)rb + xcb);
-          dcheck(g, in, a, N);
-          glds16(a, &win[buf][k][0]);
+          dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + xcb), N);
+          blds16(rs, xcb, &win[buf][k][0]);
         }
       }
     }
@@ -327,7 +327,10 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
           RO::pin(a);
         }
       }
-      // (2) level 1 row by row from the u0 window, each new row cascading up through the levels
+      // (2) level 1 row by row from the u0 window, each new row cascading up through the levels.
+      // (The scheduling barrier keeps (1), which needs only the seam rows read first, ahead of the
+      // window rows' waits: the buffer-descriptor DMA (issue) leaves those waits partial.)
+      __builtin_amdgcn_sched_barrier(0);
       Row X[3];
       auto urow = [&](int i) -> Row {
         if constexpr (LAZY) return RO::fromv(V(wbuf[(i + K) * 64]));

@@ -70,11 +70,12 @@ def test_lds_never_limits_occupancy(recs):
     ("mdfx::dev::heat7_wxk<double, 5, 4, 5, 8, false, false, false, 1>", 2),       # fp64 K = 5 (1-cell lanes)
     ("mdfx::dev::heat7_wxk<double, 5, 4, 5, 8, true, false, false, 1>", 2),
     ("mdfx::dev::heat7_wxk<double, 5, 4, 5, 8, false, false, true, 1>", 2),        # its folded-boundary copy
-    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false, 0, 0, 2, 0>", 2),              # 27-point K = 3 (1024-cell rows, fp64)
-    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, false, 2, 0, 2, 0>", 2),              # fp32 rows <= 512: whole-row blocks
-    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, true, 2, 0, 2, 0>", 2),
-    ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false, 0, 0, 2, 0>", 2),
-    ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true, 0, 0, 2, 0>", 2),
+    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, false, 0, 2>", 4),       # 27-point K = 3 fp32 rows > 512: 2-cell lanes, 2 bands per CU
+    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 8, true, 0, 2>", 3),
+    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, false, 2, 0>", 2),       # fp32 rows <= 512: whole-row blocks
+    ("mdfx::dev::box27_wxk<float, 2, 1, 3, 4, true, 2, 0>", 2),
+    ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, false, 0, 0>", 2),
+    ("mdfx::dev::box27_wxk<double, 2, 1, 3, 8, true, 0, 0>", 2),
     ("mdfx::dev::box27_tb2n<1, 1, false>", 3),                          # 27-point K = 2 fp32 (512^3)
     ("mdfx::dev::heat7_wtk<double, 2, 3, 8, false, 0>", 2),
     ("mdfx::dev::jacobi5_tbk<float, 8, false, false, 2>", 3),           # 2D MDF, 8 steps per sweep
