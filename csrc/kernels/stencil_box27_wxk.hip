@@ -462,7 +462,9 @@ void launch_box27_wxk(const Geo& g, const T* in, T* out, const StencilCoef& cf, 
   // three z chunks): 512^3 1332 GCells/s against 1009 in three overlapping segments and 1092 for
   // box27_tb2n K = 2 (profiles/r05_session_f/)
   if constexpr (std::is_same<T, float>::value) {
-    if (g.nx <= 512 && knobs().b27_shape == 0) return launch_b27x<T, 2, 1, 3, 4, 2>(g, in, out, cf, resid, s);
+    // (2-cell lanes in 5 overlapping segments at 512-cell rows: 1262-1266 vs 1397-1401 GCells/s,
+    // profiles/r06_session_q/)
+    if (g.nx <= 512) return launch_b27x<T, 2, 1, 3, 4, 2>(g, in, out, cf, resid, s);
     return launch_b27x<T, 2, 1, 3, 8, 0, kRowOps2>(g, in, out, cf, resid, s);
   } else {
     // (fp64 at 512-cell rows fills only 185 of 256 CUs in one round (5 segments x 37 bands); round 6
