@@ -211,17 +211,33 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
         // 32-bit lane-offset form instead of a 64-bit VGPR address per row held across the loop
         uint64_t rb = (uint64_t)(uintptr_t)(in + (int64_t)lzc * plane + (int64_t)yc * pitch);
         asm volatile("" : "+s"(rb));
-        // buffer-descriptor DMA (blds16 / blds4): the step's LDS reads then get partial lgkmcnt waits
-        const __amdgpu_buffer_rsrc_t rs = row_rsrc((const void*)(uintptr_t)rb);
-        if constexpr (NAR) {
+        // fp64: buffer-descriptor DMA (blds16 / blds4), so the step's LDS reads get partial lgkmcnt
+        // waits (2048^3 + residual every 12 / 20: 1048 / 1160 vs 1031 / 1138 GCells/s); fp32 keeps
+        // global_load_lds: 1024^3 within +-1 %, 3072^3 2272-2310 vs 2450-2493 with the buffer form
+        // (profiles/r06_session_{p,s}/)
+        if constexpr (sizeof(T) == 8) {
+          const __amdgpu_buffer_rsrc_t rs = row_rsrc((const void*)(uintptr_t)rb);
+          if constexpr (NAR) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + (xch[h] & ~(uint32_t)(sizeof(T) - 1))), 1);
+              blds4(rs, xch[h], (char*)&win[buf][k][0] + h * 256);
+            }
+          } else {
+            dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + xcb), N);
+            blds16(rs, xcb, &win[buf][k][0]);
+          }
+        } else if constexpr (NAR) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
+            const char* a = (const char*)(uintptr_t)rb + xch[h];
             dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + (xch[h] & ~(uint32_t)(sizeof(T) - 1))), 1);
-            blds4(rs, xch[h], (char*)&win[buf][k][0] + h * 256);
+            glds4(a, (char*)&win[buf][k][0] + h * 256);
           }
         } else {
-          dcheck(g, in, (const T*)((const char*)(uintptr_t)rb + xcb), N);
-          blds16(rs, xcb, &win[buf][k][0]);
+          const T* a = (const T*)((const char*)(uintptr_t)rb + xcb);
+          dcheck(g, in, a, N);
+          glds16(a, &win[buf][k][0]);
         }
       }
     }
