@@ -23,7 +23,7 @@ import mpi_cuda_process_amd as m  # noqa: E402
 from mpi_cuda_process_amd.ops import (FieldLayout, alloc_field, apply_stencil, init_field,  # noqa: E402
                                       set_kernel_variant)
 
-KEYS = {"TBRY": "MDFX_TB_RY", "WB": "MDFX_WTK_WB", "WXK": "MDFX_H7_WXK", "B27WXK": "MDFX_B27_WXK", "WXSPLIT": "MDFX_WX_SPLIT"}
+KEYS = {"TBRY": "MDFX_TB_RY", "WB": "MDFX_WTK_WB", "WXK": "MDFX_H7_WXK", "B27WXK": "MDFX_B27_WXK"}
 
 
 def parse_variant(s):

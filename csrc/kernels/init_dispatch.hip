@@ -92,7 +92,6 @@ static Knobs read_knobs() {
   k.b27_wxk = env_int("MDFX_B27_WXK", -1);
   k.devcheck_selftest = env_int("MDFX_DEVCHECK_SELFTEST", 0);
   k.fold_release = env_int("MDFX_FOLD_RELEASE", 0);
-  k.wx_split = env_int("MDFX_WX_SPLIT", 0);
   return k;
 }
 

@@ -36,7 +36,6 @@ struct Geo {
   int64_t lz2_begin = 0, lz2_end = 0;  // optional second region of the same launch (heat7_wtk)
   int64_t alloc = 0;                 // elements allocated (planes + slack), for device checks
   int min_rounds = 1;                // whole rounds of resident blocks a streaming sweep spans at least (RegionArgs)
-  int zfull = 0;                     // heat7_wxk remainder split: tasks that sweep a whole tile (0: uniform chunks)
   // pencil layouts (a y split with ghost rows): global rows, global y = storage row + gy_off, and the
   // storage rows [ly_begin, ly_end) to write (slabs: gny = ny, gy_off = 0, every row). Kernels
   // without pencil support only ever see slab geometry (hip_stencil routes pencils to naive / wxk)
@@ -245,7 +244,6 @@ struct Knobs {
   int b27_wxk = -1;    // MDFX_B27_WXK: the 27-point's fused depth 3 through box27_wxk (-1: fp64, fp32 rows of 257..512 or >= 1024 cells; 0 / 1)
   int devcheck_selftest = 0;  // MDFX_DEVCHECK_SELFTEST (make devcheck builds)
   int fold_release = 0;       // MDFX_FOLD_RELEASE: folded-boundary blocks release (L2 writeback) before they signal
-  int wx_split = 0;           // MDFX_WX_SPLIT=1: heat7_wxk splits the tiles of a partial last round finely in z
 };
 const Knobs& knobs();
 

@@ -130,40 +130,8 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // work: block-uniform task = one z chunk of one (x segment, y band) tile; x segments fastest, then
   // y bands, then z chunks (the first region's chunks, then the second region's)
-  const int tiles = XT * YT;
-  // task -> (tile, z chunk). Uniform chunks of zc planes (the first region's, then the second's), or,
-  // g.zfull > 0 (one region, wxk_geo's remainder split): the first zfull blocks in dispatch order
-  // sweep whole tiles (whole rounds of resident blocks), the rest split the remaining tiles into
-  // chunks of zc planes that share the last round
-  int t, zs, ze;
-  if (g.zfull > 0) {
-    const int bi = (int)blockIdx.x;
-    if (bi < g.zfull) {
-      t = (int)xcd_remap((unsigned)bi, (unsigned)g.zfull);
-      zs = (int)g.lz_begin;
-      ze = (int)g.lz_end;
-    } else {
-      const int tr = tiles - g.zfull, j = bi - g.zfull;
-      if (bi >= ntasks) return;
-      t = g.zfull + j % tr;
-      zs = (int)g.lz_begin + (j / tr) * zc;
-      ze = min((int)g.lz_end, zs + zc);
-    }
-  } else {
-    const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
-    if (b >= ntasks) return;
-    t = b % tiles;
-    const int zt = b / tiles;
-    const int P0 = (int)(g.lz_end - g.lz_begin);
-    const int zt1 = (P0 + zc - 1) / zc;
-    if (zt < zt1) {
-      zs = (int)g.lz_begin + zt * zc;
-      ze = min((int)g.lz_end, zs + zc);
-    } else {
-      zs = (int)g.lz2_begin + (zt - zt1) * zc;
-      ze = min((int)g.lz2_end, zs + zc);
-    }
-  }
+  const int b = (int)xcd_remap(blockIdx.x, gridDim.x);
+  if (b >= ntasks) return;
   // two window buffers: the u0 plane DMA runs one plane ahead of the plane being computed
   __shared__ V win[2][RB][64];
   // seam[parity][level-1][boundary between waves s and s+1][0: first row of wave s+1, 1: last row of wave s]
@@ -173,6 +141,18 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
   // 4-byte LDS DMAs lost 15-24 % in round 4 (profiles/r04_session_b/) and 15 % in round 5; the DMA
   // two planes ahead in these two buffers (a second barrier per step right after the window reads)
   // lost 4-6 %, non-temporal window DMAs 19 % (profiles/r05_session_b/, r05_session_c/).)
+  const int tiles = XT * YT;
+  const int t = b % tiles, zt = b / tiles;
+  const int P0 = (int)(g.lz_end - g.lz_begin);
+  const int zt1 = (P0 + zc - 1) / zc;
+  int zs, ze;
+  if (zt < zt1) {
+    zs = (int)g.lz_begin + zt * zc;
+    ze = min((int)g.lz_end, zs + zc);
+  } else {
+    zs = (int)g.lz2_begin + (zt - zt1) * zc;
+    ze = min((int)g.lz2_end, zs + zc);
+  }
   const int xt = t % XT, yt = t / XT;
   const int64_t xs = (int64_t)xt * SEG - OV * N;  // column of lane 0
   const int64_t x = xs + (int64_t)lane * N;
@@ -465,7 +445,7 @@ __global__ __launch_bounds__(WB * 64) void heat7_wxk(const T* __restrict__ in, T
 
 // launch geometry of one shape: tiles, z chunks, and the rounds of resident blocks they take
 struct WxGeo {
-  int XT = 0, YT = 0, zc = 0, zfull = 0;
+  int XT = 0, YT = 0, zc = 0;
   int64_t ntasks = 0, resident = 0, rounds = 0;
 };
 template <class T, int RY, int RE, int K, int WB, int CN = 0>
@@ -485,31 +465,6 @@ static WxGeo wxk_geo(const Geo& g) {
   if (planes2 > 0) w.zc = (int)std::max(planes, planes2);
   const int ZT = (int)((planes + w.zc - 1) / w.zc) + (planes2 > 0 ? (int)((planes2 + w.zc - 1) / w.zc) : 0);
   w.ntasks = tiles * ZT;
-  // Remainder split (one region, T >= R tiles): uniform chunks leave the tiles beyond the last whole
-  // round of resident blocks (2048^2 fp64 K = 5: 2052 tiles = 8 x 256 + 4) to a round of their own, or
-  // shorten every chunk and pay its fill again. Instead the first F = R floor(T / R) tiles sweep whole,
-  // and the T - F others split into m chunks of c planes that together fill one more round:
-  // F / R (P + f) + (c + f) plane steps against the uniform plan's rounds x (zc + f). Each tile still
-  // has exactly one chunk at lz_begin (the folded boundary's signalling blocks), of c >= the signal's
-  // planes.
-  const int64_t R = w.resident, f = 2 * K;
-  if (planes2 == 0 && WB != 2 && tiles >= R && tiles % R != 0 && knobs().wx_split != 0) {
-    const int64_t F = tiles / R * R, tr = tiles - F;
-    const int64_t cmin = std::max<int64_t>(K, g.sig ? g.sig_z - g.lz_begin : 0);
-    int64_t m = std::max<int64_t>(1, R / tr);
-    int64_t c = (planes + m - 1) / m;
-    if (c < cmin) {
-      c = cmin;
-      m = (planes + c - 1) / c;
-    }
-    const double t_split = (double)(F / R) * (double)(planes + f) + (double)(c + f);
-    const double t_uni = (double)((w.ntasks + R - 1) / R) * (double)(w.zc + f);
-    if (c < planes && tr * m <= R && t_split < 0.98 * t_uni) {
-      w.zfull = (int)F;
-      w.zc = (int)c;
-      w.ntasks = F + tr * m;
-    }
-  }
   w.rounds = (w.ntasks + w.resident - 1) / w.resident;
   return w;
 }
@@ -517,10 +472,8 @@ static WxGeo wxk_geo(const Geo& g) {
 static bool pen_geo(const Geo& g) { return g.ly_begin != 0 || g.ly_end != g.ny || g.gy_off != 0 || g.gny != g.ny; }
 
 template <class T, int RY, int RE, int K, int WB, int CN = 0>
-static void launch_wxk(const Geo& g0, const T* in, T* out, T r, double* resid, hipStream_t s) {
-  const WxGeo wg = wxk_geo<T, RY, RE, K, WB, CN>(g0);
-  Geo g = g0;
-  g.zfull = wg.zfull;
+static void launch_wxk(const Geo& g, const T* in, T* out, T r, double* resid, hipStream_t s) {
+  const WxGeo wg = wxk_geo<T, RY, RE, K, WB, CN>(g);
   const int XT = wg.XT, YT = wg.YT, zc = wg.zc;
   // only the blocks of the first z chunk signal: it must hold every plane the signal covers (a
   // chunk shorter than that would leave the halo stream waiting for a signal never sent)

@@ -192,26 +192,6 @@ def test_ipc_fp32_fused_k5_folded(hip, tmp_path, transport, direct, graph):
         assert meta["folded"] > 0 and meta["captures"] == 0, meta
 
 
-def test_ipc_fp64_k5_folded_remainder_split(hip, tmp_path):
-    """2048 x 2048 fp64 slabs at K = 5 over three processes: 2052 tiles per sweep, so the interior
-    sweep (lower boundary folded) runs the remainder split (wxk_geo: 2048 whole-tile chunks plus 4
-    tiles in short chunks, each tile's first chunk signalling the fold): bitwise equal to one
-    process, residual included."""
-    import mpi_cuda_process_amd as m
-
-    prob_src = "m.heat3d(nx=2048, ny=2048, nz=66, dtype='f64')"
-    out = str(tmp_path / "g.npy")
-    steps = 20
-    code = WORKER % dict(py=1, root=ROOT, prob=prob_src, out=out, temporal=5, graph=False, steps=steps,
-                         resid=10, transport="ipc")
-    _spawn(3, lambda r: [sys.executable, "-c", code], env_extra={"MDFX_WX_SPLIT": "1"})
-    ref, rres = _reference(eval(prob_src), steps)
-    assert np.array_equal(np.load(out), ref)
-    meta = json.load(open(out + ".json"))
-    assert abs(meta["residual"] - rres) <= 1e-9 * rres
-    assert meta["folded"] > 0, meta
-
-
 @pytest.mark.parametrize("world,py,temporal,graph,transport,prob_src", [
     (4, 2, 4, False, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),   # 2 x 2 pencils, the fused K = 4 sweep
     (4, 2, 3, True, "ipc", "m.heat3d(nx=256, ny=70, nz=47)"),    # ... K = 3, replayed

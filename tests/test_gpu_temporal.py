@@ -503,44 +503,6 @@ def test_heat7_wxk_bitwise(hip, prob, k, resid, knob):
 
 
 @pytest.mark.parametrize("resid", [False, True])
-def test_heat7_wxk_remainder_split(hip, resid, knob):
-    """2048 x 2048 x 40 fp64 at K = 5: 2052 tiles, 4 more than 8 whole rounds of resident blocks, so
-    heat7_wxk sweeps 2048 tiles whole and splits the other 4 into short z chunks sharing one more
-    round (wxk_geo) == 5 naive single steps, bitwise, and == the uniform-chunk sweep
-    (MDFX_WX_SPLIT=0), residual included."""
-    k = 5
-    prob = models.heat3d(nx=2048, ny=2048, nz=40, dtype="f64")
-    lay = FieldLayout.make(prob, halo=k)
-    src = alloc_field(lay, "cuda")
-    init_field(prob, lay, src)
-    outs, ress = [], []
-    for split in (1, 0):
-        knob("MDFX_WX_SPLIT", split)
-        out = alloc_field(lay, "cuda")
-        res = torch.zeros((), dtype=torch.float64, device="cuda")
-        apply_stencil(prob, lay, src, out, steps=k, resid=res if resid else None)
-        outs.append(out)
-        ress.append(res)
-    set_kernel_variant("naive")
-    try:
-        cur = src.clone()
-        ref_res = torch.zeros((), dtype=torch.float64, device="cuda")
-        for i in range(k):
-            nxt = cur.clone()
-            apply_stencil(prob, lay, cur, nxt, resid=ref_res if i == k - 1 else None)
-            cur = nxt
-    finally:
-        set_kernel_variant("auto")
-    torch.cuda.synchronize()
-    o = lay.owned
-    assert torch.equal(outs[0][o, :, :lay.nx], cur[o, :, :lay.nx])
-    assert torch.equal(outs[1][o, :, :lay.nx], cur[o, :, :lay.nx])
-    if resid:
-        for r in ress:
-            assert r.item() > 0 and abs(r.item() - ref_res.item()) <= 1e-9 * ref_res.item()
-
-
-@pytest.mark.parametrize("resid", [False, True])
 @pytest.mark.parametrize("nx,k", [(1024, 4), (2048, 5)])
 def test_heat7_fp64_wide_rows_default_path(hip, resid, nx, k):
     """fp64 rows of 1024 cells take heat7_wxk at K = 4 by default (2 + 1-row bands), rows of 2048
